@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): char-tokens/sec of a full GRU training step
+(forward + softmax-xent + BPTT + gradient all-reduce + Adam), 1-layer GRU hidden=512,
+256 sequences x 32 chars per GPU (weak scaling: global batch = 256 * N), bf16 MFMA compute
+with fp32 master weights, synthetic name sequences, random-init weights.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line; `value` is the whole-job aggregate (tokens/s over all ranks),
+timed over exactly K steps bracketed by barrier + device synchronize, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+METRIC = "char-tokens/sec (whole node) for GRU hidden=512 at 1/2/4/8 MI355X"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--preset", default="h512")
+    ap.add_argument("--per-gpu-batch", type=int, default=None,
+                    help="override per-GPU batch (default: preset batch, 256 for h512)")
+    ap.add_argument("--impl", choices=["hip", "torch"], default="hip",
+                    help="hip = this engine; torch = torch.nn.GRU (MIOpen) comparator")
+    ap.add_argument("--chunks", type=int, default=None)
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from gru_mpi_cuda_amd.config import preset
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.utils.data import NameStream
+
+    ctx = gdist.init(use_gpu=torch.cuda.is_available())
+    world = ctx.world
+    base = preset(args.preset)
+    per_gpu = args.per_gpu_batch or base.batch
+    cfg = base.replace(batch=per_gpu * world)
+    if args.chunks:
+        cfg = cfg.replace(time_chunks=args.chunks)
+
+    stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
+    pool = [stream.next() for _ in range(8)]
+
+    if args.impl == "hip":
+        from gru_mpi_cuda_amd.engine.trainer import make_trainer
+        from gru_mpi_cuda_amd.parallel.rccl import make_comm
+        comm = make_comm(ctx) if ctx.device.type == "cuda" else None
+        tr = make_trainer(cfg, ctx, comm=comm)
+        if args.no_graph and hasattr(tr, "t"):
+            tr.t.set_use_graph(False)
+        step = lambda i: tr.step(*pool[i % len(pool)])  # noqa: E731
+        final_loss = lambda: tr.loss()                  # noqa: E731
+    else:
+        step, final_loss = _torch_gru_step(cfg, ctx, pool)
+
+    def sync():
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize(ctx.device)
+        gdist.barrier()
+
+    for i in range(args.warmup):
+        step(i)
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = final_loss()
+    tokens = cfg.batch * cfg.seq * args.steps
+    value = tokens / el
+    if ctx.is_main:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "char-tokens/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000 * el / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic name sequences (seeded syllable generator), random-init weights",
+            "config": {"model": f"GRU L={cfg.layers} H={cfg.hidden} E={cfg.embed} V={cfg.vocab}",
+                       "global_batch": cfg.batch, "seq_len": cfg.seq,
+                       "parallelism": f"dp{world}", "impl": args.impl,
+                       "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks},
+            "final_loss": round(float(loss), 4),
+        }
+        print(json.dumps(out), flush=True)
+    gdist.shutdown()
+    return 0
+
+
+def _torch_gru_step(cfg, ctx, pool):
+    """torch.nn.GRU (MIOpen) comparator with the same model, loss and optimiser, bf16 autocast."""
+    import torch
+    import torch.nn as nn
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    class Model(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.emb = nn.Embedding(cfg.vocab, cfg.embed)
+            self.gru = nn.GRU(cfg.embed, cfg.hidden, cfg.layers, batch_first=True)
+            self.fc = nn.Linear(cfg.hidden, cfg.vocab)
+
+        def forward(self, x):
+            h, _ = self.gru(self.emb(x))
+            return self.fc(h)
+
+    dev = ctx.device
+    m = Model().to(dev)
+    model = DDP(m, device_ids=[dev.index]) if ctx.world > 1 else m
+    opt = torch.optim.Adam(model.parameters(), lr=cfg.lr)
+    dpool = [(torch.from_numpy(x).long().to(dev), torch.from_numpy(y).long().to(dev)) for x, y in pool]
+    state = {"loss": None}
+
+    def step(i):
+        x, y = dpool[i % len(dpool)]
+        with torch.autocast(device_type=dev.type, dtype=torch.bfloat16):
+            logits = model(x)
+            loss = nn.functional.cross_entropy(logits.float().reshape(-1, cfg.vocab), y.reshape(-1))
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        state["loss"] = loss.detach()
+
+    return step, lambda: float(state["loss"])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,115 @@
+"""In-tree build of the native engine with hipcc for gfx950 only.
+
+No torch.utils.cpp_extension (its ROCm path hipifies sources; this code is written for
+CDNA4 directly) and no torch headers: the extension is pybind11 + HIP, linked into
+``gru_mpi_cuda_amd/_C.<abi>.so`` next to this file, so it ships with the repo snapshot to
+the GPU box.  Also builds ``libnamegen.so`` (the reference's 3-call C API, no Python) and
+the ``namegen`` driver executable under ``gru_mpi_cuda_amd/bin``.
+
+    python -m gru_mpi_cuda_amd.build_ext [--force] [--jobs N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build", "obj")
+ARCH = os.environ.get("GK_OFFLOAD_ARCH", "gfx950")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+KERNELS = ["kernels/gru_step.hip", "kernels/fc.hip", "kernels/gemm.hip", "kernels/misc.hip"]
+ENGINE = ["engine/trainer.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp"]
+PYBIND = ["bindings.cpp"]
+CAPI = ["capi/namegen_api.cpp", "capi/ckpt_reader.cpp"]
+DRIVER = ["capi/namegen_main.cpp"]
+
+
+def ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(HERE, "_C" + suffix)
+
+
+def _headers():
+    for root, _, files in os.walk(CSRC):
+        for f in files:
+            if f.endswith((".h", ".hpp")):
+                yield os.path.join(root, f)
+
+
+def _newest_header() -> float:
+    return max((os.path.getmtime(h) for h in _headers()), default=0.0)
+
+
+def _flags(extra=()):
+    import pybind11
+    return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+            f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+            "-I/opt/rocm/include", *extra]
+
+
+def _compile(src: str, force: bool, hdr_time: float) -> str:
+    out = os.path.join(OBJ, src.replace("/", "_") + ".o")
+    path = os.path.join(CSRC, src)
+    if not force and os.path.exists(out):
+        t = os.path.getmtime(out)
+        if t >= os.path.getmtime(path) and t >= hdr_time:
+            return out
+    cmd = [HIPCC, *_flags(), "-c", path, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def _link(objs, out, shared=True, libs=()):
+    newest = max(os.path.getmtime(o) for o in objs)
+    if os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *(["-shared"] if shared else []), "-fPIC", *objs, "-o", out,
+           "-L/opt/rocm/lib", *libs, "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
+    hdr = _newest_header()
+    srcs = KERNELS + ENGINE + PYBIND + [s for s in CAPI + DRIVER if os.path.exists(os.path.join(CSRC, s))]
+    jobs = jobs or min(8, os.cpu_count() or 4, 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = dict(zip(srcs, ex.map(lambda s: _compile(s, force, hdr), srcs)))
+    core = [objs[s] for s in KERNELS + ENGINE]
+    _link(core + [objs[s] for s in PYBIND], ext_path(), libs=["-lrccl"])
+    capi_objs = [objs[s] for s in CAPI if s in objs]
+    if capi_objs:
+        lib = os.path.join(HERE, "bin", "libnamegen.so")
+        _link(core + capi_objs, lib, libs=["-lrccl"])
+        drv = [objs[s] for s in DRIVER if s in objs]
+        if drv:
+            _link(drv, os.path.join(HERE, "bin", "namegen"), shared=False,
+                  libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl",
+                        f"-Wl,-rpath,{os.path.join(HERE, 'bin')}", "-Wl,-rpath,$ORIGIN"])
+    if verbose:
+        print(f"[build_ext] {ext_path()} ({len(srcs)} sources, arch {ARCH})")
+    return ext_path()
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,192 @@
+// Thin pybind11 layer over the native engine.  No torch headers: device memory is passed as
+// integer addresses (tensor.data_ptr()) and streams as integer handles
+// (torch.cuda.current_stream().cuda_stream), so this TU compiles in seconds and the
+// extension binds to whichever libamdhip64 the process already loaded (torch's).
+#include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+
+#include "engine/trainer.h"
+#include "engine/generator.h"
+#include "comm/rccl_comm.h"
+
+namespace py = pybind11;
+using namespace gk;
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T> static T* Pp(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+template <class T>
+static T get(const py::dict& d, const char* k, T dflt) {
+  if (!d.contains(k)) return dflt;
+  return d[k].cast<T>();
+}
+#define GP(T, d, k) reinterpret_cast<T*>(get<uintptr_t>(d, k, 0))
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "gru_mpi_cuda_amd native engine (HIP/CDNA4 kernels, hipGraph executor, RCCL comm)";
+
+  m.def("set_rank", [](int r) { global_rank() = r; });
+  m.def("device_info", []() {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["arch"] = std::string(p.gcnArchName);
+    d["cus"] = p.multiProcessorCount;
+    d["lds_per_cu"] = (long)p.maxSharedMemoryPerMultiProcessor;
+    d["hbm_bytes"] = (long)p.totalGlobalMem;
+    return d;
+  });
+  m.def("device_synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+
+  py::class_<Trainer>(m, "Trainer")
+      .def(py::init([](py::dict dims, py::dict opt, uintptr_t params, uintptr_t grads, uintptr_t mm, uintptr_t vv,
+                       long nflat, std::map<std::string, long> offsets) {
+        Dims d;
+        d.V = get<int>(dims, "V", 256); d.E = get<int>(dims, "E", 512); d.H = get<int>(dims, "H", 512);
+        d.L = get<int>(dims, "L", 1); d.B = get<int>(dims, "B", 256); d.T = get<int>(dims, "T", 32);
+        d.chunks = get<int>(dims, "chunks", 4);
+        OptCfg o;
+        o.lr = get<float>(opt, "lr", 1e-3f); o.b1 = get<float>(opt, "beta1", 0.9f); o.b2 = get<float>(opt, "beta2", 0.999f);
+        o.eps = get<float>(opt, "eps", 1e-8f); o.wd = get<float>(opt, "weight_decay", 0.f);
+        o.clip = get<float>(opt, "clip_norm", 0.f); o.sgd = get<int>(opt, "sgd", 0);
+        return new Trainer(d, o, Pp<float>(params), Pp<float>(grads), Pp<float>(mm), Pp<float>(vv), nflat, offsets);
+      }))
+      .def("refresh_weights", [](Trainer& t, uintptr_t s) { t.refresh_weights(S(s)); })
+      .def("set_batch", [](Trainer& t, py::array_t<int, py::array::c_style | py::array::forcecast> x,
+                           py::array_t<int, py::array::c_style | py::array::forcecast> y, uintptr_t s) {
+        if (x.ndim() != 2 || y.ndim() != 2 || x.shape(0) != y.shape(0) || x.shape(1) != y.shape(1))
+          throw std::runtime_error("set_batch: x and y must both be [B, T]");
+        t.set_batch(x.data(), y.data(), (int)x.shape(0), S(s));
+      })
+      .def("forward_backward", [](Trainer& t, uintptr_t s) { t.forward_backward(S(s)); })
+      .def("optimizer_step", [](Trainer& t, uintptr_t s) { t.optimizer_step(S(s)); })
+      .def("read_loss", &Trainer::read_loss)
+      .def("read_grad_norm", &Trainer::read_grad_norm)
+      .def("set_lr", &Trainer::set_lr)
+      .def("set_use_graph", &Trainer::set_use_graph)
+      .def("padded_batch", &Trainer::padded_batch)
+      .def("workspace_bytes", &Trainer::workspace_bytes)
+      .def("buffer", &Trainer::buffer);
+
+  py::class_<Generator>(m, "Generator")
+      .def(py::init([](py::dict dims, uintptr_t params, std::map<std::string, long> offsets) {
+        GenDims d;
+        d.V = get<int>(dims, "V", 256); d.E = get<int>(dims, "E", 512); d.H = get<int>(dims, "H", 1024);
+        d.L = get<int>(dims, "L", 2); d.max_len = get<int>(dims, "max_len", 10); d.sos = get<int>(dims, "sos", 0);
+        d.eos = get<int>(dims, "eos", 0); d.max_batch = get<int>(dims, "max_batch", 4096);
+        return new Generator(d, Pp<const float>(params), offsets);
+      }))
+      .def("refresh_weights", [](Generator& g, uintptr_t s) { g.refresh_weights(S(s)); })
+      .def("generate", [](Generator& g, uintptr_t rf, int N, uintptr_t out, uintptr_t s) {
+        g.generate(Pp<const float>(rf), N, Pp<unsigned char>(out), S(s));
+      })
+      .def("set_use_graph", &Generator::set_use_graph)
+      .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); });
+
+  // ---------------------------------------------------------------- raw kernels (tests, bench)
+  m.def("gemm_nt", [](py::dict d, uintptr_t s) {
+    GemmArgs a;
+    a.A = GP(const u16, d, "A"); a.lda = get<int>(d, "lda", 0);
+    a.onehot_ids = GP(const int, d, "onehot_ids");
+    a.B = GP(const u16, d, "B"); a.ldb = get<int>(d, "ldb", 0);
+    a.C = GP(float, d, "C"); a.ldc = get<int>(d, "ldc", 0);
+    a.bias = GP(const float, d, "bias"); a.rowsumA = GP(float, d, "rowsumA");
+    a.M = get<int>(d, "M", 0); a.N = get<int>(d, "N", 0); a.K = get<int>(d, "K", 0);
+    a.splits = get<int>(d, "splits", 1); a.accumulate = get<int>(d, "accumulate", 0);
+    if (a.M % 64 || a.N % 64 || (a.K / a.splits) % 32 || a.K % a.splits)
+      throw std::runtime_error("gemm_nt: M, N must be multiples of 64 and K/splits a multiple of 32");
+    gemm_nt(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fwd_step", [](py::dict d, uintptr_t s) {
+    FwdStepArgs a;
+    a.hprev_bf = GP(const u16, d, "hprev_bf"); a.hprev_f = GP(const float, d, "hprev_f");
+    a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
+    a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
+    a.x_bf = GP(const u16, d, "x_bf"); a.Wih = GP(const u16, d, "Wih"); a.bih = GP(const float, d, "bih");
+    a.Kin = get<int>(d, "Kin", 0);
+    a.h_f = GP(float, d, "h_f"); a.h_bf = GP(u16, d, "h_bf"); a.hT = GP(u16, d, "hT");
+    a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
+    a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
+    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    if (a.Bp % 32 || a.H % 64) throw std::runtime_error("fwd_step: Bp % 32 and H % 64 required");
+    gru_fwd_step(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("bwd_step", [](py::dict d, uintptr_t s) {
+    BwdStepArgs a;
+    a.dgh_next = GP(const u16, d, "dgh_next"); a.WhhT = GP(const u16, d, "WhhT");
+    a.carry_in = GP(const float, d, "carry_in"); a.dy = GP(const float, d, "dy");
+    a.r = GP(const float, d, "r"); a.z = GP(const float, d, "z"); a.n = GP(const float, d, "n");
+    a.ghn = GP(const float, d, "ghn"); a.hprev = GP(const float, d, "hprev");
+    a.carry_out = GP(float, d, "carry_out"); a.dgh = GP(u16, d, "dgh"); a.dghT = GP(u16, d, "dghT");
+    a.dgiT = GP(u16, d, "dgiT"); a.dgi = GP(u16, d, "dgi");
+    a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
+    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    if (a.Bp % 32 || a.H % 64) throw std::runtime_error("bwd_step: Bp % 32 and H % 64 required");
+    gru_bwd_step(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fc_xent", [](py::dict d, uintptr_t s) {
+    FcXentArgs a;
+    a.X = GP(const u16, d, "X"); a.W = GP(const u16, d, "W"); a.b = GP(const float, d, "b");
+    a.labels = GP(const int, d, "labels"); a.inv_count = GP(const float, d, "inv_count");
+    a.dl = GP(u16, d, "dl"); a.dlT = GP(u16, d, "dlT"); a.loss_part = GP(float, d, "loss_part");
+    a.M = get<int>(d, "M", 0); a.H = get<int>(d, "H", 0); a.V = get<int>(d, "V", 0);
+    a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
+    if (a.M % 32 || a.V % 64 || a.V > 512 || a.H % 32) throw std::runtime_error("fc_xent: bad shape");
+    fc_xent(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fc_sample", [](py::dict d, uintptr_t s) {
+    FcSampleArgs a;
+    a.X = GP(const u16, d, "X"); a.W = GP(const u16, d, "W"); a.b = GP(const float, d, "b");
+    a.rf = GP(const float, d, "rf"); a.ids = GP(int, d, "ids"); a.out = GP(unsigned char, d, "out");
+    a.alive = GP(int, d, "alive"); a.probs = GP(float, d, "probs");
+    a.N = get<int>(d, "N", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0); a.V = get<int>(d, "V", 0);
+    a.step = get<int>(d, "step", 0); a.max_len = get<int>(d, "max_len", 0); a.eos = get<int>(d, "eos", 0);
+    if (a.Bp % 32 || a.V % 64 || a.V > 512 || a.H % 32) throw std::runtime_error("fc_sample: bad shape");
+    fc_sample(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("reduce_slabs", [](uintptr_t src, int splits, long n, uintptr_t dst, uintptr_t s) {
+    reduce_slabs(Pp<const float>(src), splits, n, Pp<float>(dst), S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("cast_bf16", [](uintptr_t in, long n, uintptr_t out, uintptr_t s) {
+    cast_bf16(Pp<const float>(in), n, Pp<u16>(out), S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("transpose_bf16", [](uintptr_t in, int R, int C, uintptr_t out, uintptr_t s) {
+    transpose_bf16(Pp<const float>(in), R, C, Pp<u16>(out), S(s));
+    HIP_LAUNCH_CHECK();
+  });
+
+  // ---------------------------------------------------------------- RCCL communicator
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int rank, int world) {
+        std::string s = uid;
+        return new RcclComm(s, rank, world);
+      }))
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def("allreduce_avg_f32", [](RcclComm& c, uintptr_t p, long n, uintptr_t s) {
+        c.allreduce_avg_f32(Pp<float>(p), n, S(s));
+      })
+      .def("allreduce_sum_f32", [](RcclComm& c, uintptr_t p, long n, uintptr_t s) {
+        c.allreduce_sum_f32(Pp<float>(p), n, S(s));
+      })
+      .def("broadcast_f32", [](RcclComm& c, uintptr_t p, long n, int root, uintptr_t s) {
+        c.broadcast_f32(Pp<float>(p), n, root, S(s));
+      })
+      .def("allgather_u8", [](RcclComm& c, uintptr_t send, uintptr_t recv, long n, uintptr_t s) {
+        c.allgather_u8(Pp<const unsigned char>(send), Pp<unsigned char>(recv), n, S(s));
+      })
+      .def("check_async_error", &RcclComm::check_async_error)
+      .def("abort", &RcclComm::abort)
+      .def("rank", &RcclComm::rank)
+      .def("world", &RcclComm::world);
+}

@@ -1,0 +1,62 @@
+#include "rccl_comm.h"
+
+#include <rccl/rccl.h>
+#include <stdexcept>
+#include <cstring>
+#include "../runtime/runtime.h"
+
+namespace gk {
+
+#define RCCL_CHECK(x)                                                                          \
+  do {                                                                                         \
+    ncclResult_t _r = (x);                                                                     \
+    if (_r != ncclSuccess)                                                                     \
+      throw std::runtime_error("[rank " + std::to_string(global_rank()) + "] RCCL error '" +   \
+                               ncclGetErrorString(_r) + "' at " + __FILE__ + ":" +             \
+                               std::to_string(__LINE__) + ": " #x);                            \
+  } while (0)
+
+static ncclComm_t C(void* p) { return reinterpret_cast<ncclComm_t>(p); }
+
+std::string RcclComm::unique_id() {
+  ncclUniqueId id;
+  RCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+RcclComm::RcclComm(const std::string& uid, int rank, int world) : rank_(rank), world_(world) {
+  if (uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("RcclComm: bad unique id size");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t c;
+  RCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+  comm_ = c;
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) (void)ncclCommDestroy(C(comm_));
+}
+
+void RcclComm::allreduce_avg_f32(float* p, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclAvg, C(comm_), s));
+}
+void RcclComm::allreduce_sum_f32(float* p, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclSum, C(comm_), s));
+}
+void RcclComm::broadcast_f32(float* p, long n, int root, hipStream_t s) {
+  RCCL_CHECK(ncclBroadcast(p, p, (size_t)n, ncclFloat32, root, C(comm_), s));
+}
+void RcclComm::allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclUint8, C(comm_), s));
+}
+void RcclComm::check_async_error() {
+  ncclResult_t r = ncclSuccess;
+  RCCL_CHECK(ncclCommGetAsyncError(C(comm_), &r));
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error("[rank " + std::to_string(rank_) + "] RCCL async error: " + ncclGetErrorString(r));
+}
+void RcclComm::abort() {
+  if (comm_) { (void)ncclCommAbort(C(comm_)); comm_ = nullptr; }
+}
+
+}  // namespace gk

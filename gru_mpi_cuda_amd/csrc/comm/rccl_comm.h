@@ -1,0 +1,35 @@
+// RCCL communicator over xGMI: one per process/GPU.
+//
+// Replaces the reference's MPI layer (MPI_Comm_rank/size, MPI_Barrier, MPI_Scatter,
+// MPI_Gather on host buffers: /root/reference/namegensf.cu:360-366,615,636,889) with
+// device-buffer collectives on HIP streams.  Bootstrap: rank 0 makes an ncclUniqueId, the
+// Python side ships its 128 bytes through the torch.distributed TCP store, every rank calls
+// ncclCommInitRank.  Collectives issued on a stream that is being captured become graph
+// nodes, so gradient all-reduce can live inside the training step's hipGraph.
+#pragma once
+#include <string>
+#include <hip/hip_runtime.h>
+
+namespace gk {
+
+class RcclComm {
+ public:
+  static std::string unique_id();
+  RcclComm(const std::string& uid, int rank, int world);
+  ~RcclComm();
+  void allreduce_avg_f32(float* p, long n, hipStream_t s);
+  void allreduce_sum_f32(float* p, long n, hipStream_t s);
+  void broadcast_f32(float* p, long n, int root, hipStream_t s);
+  void allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s);
+  // watchdog hook: raises if the communicator reported an asynchronous error
+  void check_async_error();
+  void abort();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+ private:
+  void* comm_ = nullptr;   // ncclComm_t
+  int rank_ = 0, world_ = 1;
+};
+
+}  // namespace gk

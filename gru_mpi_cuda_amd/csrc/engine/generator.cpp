@@ -1,0 +1,111 @@
+#include "generator.h"
+
+#include <algorithm>
+
+namespace gk {
+
+static int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+Generator::Generator(const GenDims& d, const float* params, const std::map<std::string, long>& offsets)
+    : d_(d), params_(params), off_(offsets) {
+  if (d_.V % 64 || d_.E % 64 || d_.H % 64)
+    throw std::runtime_error("HIP generator needs vocab, embed and hidden to be multiples of 64");
+  Bmax_ = rup(std::max(32, d_.max_batch), 64);
+  const int V = d_.V, E = d_.E, H = d_.H, L = d_.L, B = Bmax_;
+  std::vector<size_t> ohf, ohb, oWhh, oWih;
+  for (int i = 0; i < 2 * L; ++i) { ohf.push_back(arena_.reserve((size_t)B * H * 4)); ohb.push_back(arena_.reserve((size_t)B * H * 2)); }
+  for (int l = 0; l < L; ++l) {
+    oWhh.push_back(arena_.reserve((size_t)3 * H * H * 2));
+    oWih.push_back(arena_.reserve((size_t)3 * H * (l == 0 ? E : H) * 2));
+  }
+  size_t oEmb = arena_.reserve((size_t)V * E * 2), oWfc = arena_.reserve((size_t)V * H * 2);
+  size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
+  size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
+  size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
+  arena_.commit();
+  for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
+  for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
+  Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); Ptab_ = arena_.get<float>(oP);
+  rf_ = arena_.get<float>(orf); ids_ = arena_.get<int>(oids); alive_ = arena_.get<int>(oal);
+  out_ = arena_.get<unsigned char>(oout);
+  HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
+  const char* ng = std::getenv("GK_NO_GRAPH");
+  if (ng && ng[0] == '1') use_graph_ = false;
+}
+
+Generator::~Generator() {
+  graphs_.clear();
+  if (cap_) (void)hipStreamDestroy(cap_);
+}
+
+void Generator::refresh_weights(hipStream_t s) {
+  const int V = d_.V, E = d_.E, H = d_.H;
+  cast_bf16(P("embedding"), (long)V * E, Emb_, s);
+  for (int l = 0; l < d_.L; ++l) {
+    const std::string k = std::to_string(l);
+    cast_bf16(P("weight_hh_l" + k), 3L * H * H, Whh_[l], s);
+    cast_bf16(P("weight_ih_l" + k), 3L * H * (l == 0 ? E : H), Wih_[l], s);
+  }
+  cast_bf16(P("fc.weight"), (long)V * H, Wfc_, s);
+  GemmArgs g;   // layer-0 input projection table P = Emb · W_ih0^T + b_ih0  ([V][3H])
+  g.A = Emb_; g.lda = E; g.B = Wih_[0]; g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
+  g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;
+  gemm_nt(g, s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Generator::record_steps(int n, hipStream_t s) {
+  const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
+  const int Bp = rup(n, 32);
+  // per-batch init (part of the graph): h = 0, input = SOS, alive = 1, output rows = NUL
+  for (int l = 0; l < L; ++l) {
+    HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * H * 4, s));
+    HIP_CHECK(hipMemsetAsync(hb_[2 * l], 0, (size_t)Bp * H * 2, s));
+  }
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
+  HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (ML + 1), s));
+  for (int st = 0; st < ML; ++st) {
+    const int cur = st & 1, nxt = cur ^ 1;
+    for (int l = 0; l < L; ++l) {
+      const std::string k = std::to_string(l);
+      FwdStepArgs a;
+      a.hprev_bf = hb_[2 * l + cur]; a.hprev_f = hf_[2 * l + cur];
+      a.Whh = Whh_[l]; a.bhh = P("bias_hh_l" + k);
+      if (l == 0) { a.P = Ptab_; a.ids = ids_; }
+      else { a.x_bf = hb_[2 * (l - 1) + nxt]; a.Wih = Wih_[l]; a.bih = P("bias_ih_l" + k); a.Kin = H; }
+      a.h_f = hf_[2 * l + nxt]; a.h_bf = hb_[2 * l + nxt];
+      a.Bp = Bp; a.H = H;
+      gru_fwd_step(a, s);
+    }
+    FcSampleArgs f;
+    f.X = hb_[2 * (L - 1) + nxt]; f.W = Wfc_; f.b = P("fc.bias"); f.rf = rf_;
+    f.ids = ids_; f.out = out_; f.alive = alive_; f.probs = (st == ML - 1) ? probe_ : nullptr;
+    f.N = n; f.Bp = Bp; f.H = H; f.V = V; f.step = st; f.max_len = ML; f.eos = d_.eos;
+    fc_sample(f, s);
+  }
+  HIP_LAUNCH_CHECK();
+}
+
+void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t s) {
+  const int ML = d_.max_len;
+  for (int start = 0; start < N; start += Bmax_) {
+    const int n = std::min(Bmax_, N - start);
+    HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
+    if (use_graph_) {
+      auto& g = graphs_[n];
+      if (!g) {
+        g.reset(new Graph());
+        g->begin(cap_);
+        record_steps(n, cap_);
+        g->end(cap_);
+      }
+      g->launch(s);
+    } else {
+      record_steps(n, s);
+    }
+    HIP_CHECK(hipMemcpyAsync(out + (size_t)start * (ML + 1), out_, (size_t)n * (ML + 1), hipMemcpyDeviceToDevice, s));
+  }
+}
+
+}  // namespace gk

@@ -1,0 +1,58 @@
+// Device-resident batched name generator (reference parity half).
+//
+// The reference generates ONE name at a time with 51 launches + 2 blocking memcpys +
+// host sampling per character (/root/reference/namegensf.cu:649-884).  Here all local
+// names advance together: per character, one fused step launch per layer (layer >= 1 fuses
+// its input projection W_ih·h_below as a second MFMA product) and one FC+softmax+sample
+// launch that writes the chosen char straight into the next step's input ids and into the
+// output rows.  The MAX_LEN loop is captured once into a hipGraph; the host touches the
+// device only to upload the uniforms and to read the finished names.
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+#include "../runtime/runtime.h"
+#include "../kernels/kernels.h"
+
+namespace gk {
+
+struct GenDims {
+  int V = 256, E = 512, H = 1024, L = 2, max_len = 10, sos = 0, eos = 0, max_batch = 4096;
+};
+
+class Generator {
+ public:
+  Generator(const GenDims& d, const float* params, const std::map<std::string, long>& offsets);
+  ~Generator();
+  void refresh_weights(hipStream_t s);   // bf16 weights + layer-0 table (call after params change)
+  // rf: device [N][max_len] uniforms of THIS rank's names; out: device [N][max_len+1]
+  void generate(const float* rf, int N, unsigned char* out, hipStream_t s);
+  void set_use_graph(bool g) { use_graph_ = g; }
+  // optional: device [Bp][V] softmax of the last generated step (tests)
+  void set_probe(float* probs) { probe_ = probs; graphs_.clear(); }
+
+ private:
+  void record_steps(int n_active, hipStream_t s);
+  const float* P(const std::string& n) const { return params_ + off_.at(n); }
+
+  GenDims d_;
+  int Bmax_;
+  const float* params_;
+  std::map<std::string, long> off_;
+  Arena arena_;
+  hipStream_t cap_ = nullptr;
+  bool use_graph_ = true;
+  float* probe_ = nullptr;
+  std::map<int, std::unique_ptr<Graph>> graphs_;   // keyed by active-name count
+  // buffers
+  std::vector<float*> hf_;             // [L*2][Bmax][H]
+  std::vector<u16*> hb_;
+  std::vector<u16*> Whh_, Wih_;
+  u16 *Emb_, *Wfc_;
+  float *Ptab_, *rf_;
+  int *ids_, *alive_;
+  unsigned char* out_;
+};
+
+}  // namespace gk

@@ -1,0 +1,389 @@
+#include "trainer.h"
+
+#include <cstring>
+#include <algorithm>
+
+namespace gk {
+
+static int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, float* m, float* v, long nflat,
+                 const std::map<std::string, long>& offsets)
+    : d_(d), o_(o), params_(params), grads_(grads), m_(m), v_(v), nflat_(nflat), off_(offsets) {
+  if (d_.V % 64 || d_.E % 64 || d_.H % 64)
+    throw std::runtime_error("HIP engine needs vocab, embed and hidden to be multiples of 64");
+  Bp_ = round_up(std::max(d_.B, 1), 64);
+  C_ = std::max(1, d_.chunks);
+  while (C_ > 1 && d_.T % C_) --C_;
+  Tc_ = d_.T / C_;
+  const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
+  const size_t tok = (size_t)T * B;
+
+  // ---- size the arena
+  struct Pend { size_t off; };
+  std::vector<size_t> lo;
+  auto R = [&](size_t bytes) { return arena_.reserve(bytes); };
+  size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4);
+  size_t o_lp = R(tok / 32 * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
+  size_t o_sP = R((size_t)C_ * V * 3 * H * 4), o_dP = R((size_t)V * 3 * H * 4);
+  size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
+  size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
+  size_t o_dl = R(tok * V * 2), o_dlT = R(tok * V * 2), o_dPb = R((size_t)V * 3 * H * 2), o_dPTb = R((size_t)V * 3 * H * 2);
+  struct LO { size_t HSf, sr, sz, sn, sghn, dy, Gi, c0, c1, HSb, HT, g0, g1, dghT, dgiT, dgi, Whh, WhhT, Wih, WihT, shh, rhh, sih, rih; };
+  std::vector<LO> los(L);
+  for (int l = 0; l < L; ++l) {
+    const int K = in_dim(l);
+    LO& x = los[l];
+    x.HSf = R((tok + B) * H * 4);
+    x.sr = R(tok * H * 4); x.sz = R(tok * H * 4); x.sn = R(tok * H * 4); x.sghn = R(tok * H * 4);
+    x.dy = R(tok * H * 4);
+    x.Gi = l > 0 ? R(tok * 3 * H * 4) : 0;
+    x.c0 = R((size_t)B * H * 4); x.c1 = R((size_t)B * H * 4);
+    x.HSb = R((tok + B) * H * 2); x.HT = R((tok + B) * H * 2);
+    x.g0 = R((size_t)B * 3 * H * 2); x.g1 = R((size_t)B * 3 * H * 2);
+    x.dghT = R(tok * 3 * H * 2); x.dgiT = R(tok * 3 * H * 2);
+    x.dgi = l > 0 ? R(tok * 3 * H * 2) : 0;
+    x.Whh = R((size_t)3 * H * H * 2); x.WhhT = R((size_t)3 * H * H * 2);
+    x.Wih = R((size_t)3 * H * K * 2); x.WihT = R((size_t)3 * H * K * 2);
+    x.shh = R((size_t)C_ * 3 * H * H * 4); x.rhh = R((size_t)C_ * 3 * H * 4);
+    x.sih = l > 0 ? R((size_t)C_ * 3 * H * K * 4) : 0; x.rih = l > 0 ? R((size_t)C_ * 3 * H * 4) : 0;
+  }
+  arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
+
+  ids_ = arena_.get<int>(o_ids); labels_ = arena_.get<int>(o_lab); inv_count_ = arena_.get<float>(o_inv);
+  Ptab_ = arena_.get<float>(o_P); loss_part_ = arena_.get<float>(o_lp); loss_ = arena_.get<float>(o_loss);
+  slab_fc_ = arena_.get<float>(o_sfc); rs_fc_ = arena_.get<float>(o_rfc); slab_P_ = arena_.get<float>(o_sP);
+  dP_ = arena_.get<float>(o_dP); norm_parts_ = arena_.get<float>(o_np); gscale_ = arena_.get<float>(o_gs);
+  step_ = arena_.get<int>(o_step);
+  Emb = arena_.get<u16>(o_Emb); EmbT = arena_.get<u16>(o_EmbT); Wfc = arena_.get<u16>(o_Wfc); WfcT = arena_.get<u16>(o_WfcT);
+  dl_ = arena_.get<u16>(o_dl); dlT_ = arena_.get<u16>(o_dlT); dP_bf_ = arena_.get<u16>(o_dPb); dPT_bf_ = arena_.get<u16>(o_dPTb);
+  Ls_.resize(L);
+  for (int l = 0; l < L; ++l) {
+    const LO& x = los[l];
+    Layer& y = Ls_[l];
+    y.HSf = arena_.get<float>(x.HSf); y.sr = arena_.get<float>(x.sr); y.sz = arena_.get<float>(x.sz);
+    y.sn = arena_.get<float>(x.sn); y.sghn = arena_.get<float>(x.sghn); y.dy = arena_.get<float>(x.dy);
+    y.Gi = l > 0 ? arena_.get<float>(x.Gi) : nullptr;
+    y.carry[0] = arena_.get<float>(x.c0); y.carry[1] = arena_.get<float>(x.c1);
+    y.HSb = arena_.get<u16>(x.HSb); y.HT = arena_.get<u16>(x.HT);
+    y.dgh[0] = arena_.get<u16>(x.g0); y.dgh[1] = arena_.get<u16>(x.g1);
+    y.dghT = arena_.get<u16>(x.dghT); y.dgiT = arena_.get<u16>(x.dgiT);
+    y.dgi = l > 0 ? arena_.get<u16>(x.dgi) : nullptr;
+    y.Whh = arena_.get<u16>(x.Whh); y.WhhT = arena_.get<u16>(x.WhhT);
+    y.Wih = arena_.get<u16>(x.Wih); y.WihT = arena_.get<u16>(x.WihT);
+    y.slab_hh = arena_.get<float>(x.shh); y.rs_hh = arena_.get<float>(x.rhh);
+    y.slab_ih = l > 0 ? arena_.get<float>(x.sih) : nullptr; y.rs_ih = l > 0 ? arena_.get<float>(x.rih) : nullptr;
+  }
+
+  HIP_CHECK(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+  events_.resize(64 + 8 * C_ * L);
+  for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_CHECK(hipHostMalloc(&h_stage_, (2 * tok + 4) * sizeof(int)));
+  HIP_CHECK(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(stage_done_, s0_));
+  const char* ng = std::getenv("GK_NO_GRAPH");
+  if (ng && ng[0] == '1') use_graph_ = false;
+}
+
+Trainer::~Trainer() {
+  g_fb_.reset();
+  g_opt_.reset();
+  for (auto& e : events_) (void)hipEventDestroy(e);
+  if (stage_done_) (void)hipEventDestroy(stage_done_);
+  if (h_stage_) (void)hipHostFree(h_stage_);
+  if (s0_) (void)hipStreamDestroy(s0_);
+  if (s1_) (void)hipStreamDestroy(s1_);
+}
+
+hipEvent_t Trainer::ev() {
+  if (ev_next_ >= events_.size()) throw std::runtime_error("trainer: event pool exhausted");
+  return events_[ev_next_++];
+}
+
+void Trainer::set_lr(float lr) {
+  o_.lr = lr;
+  g_opt_.reset();   // lr is a kernel argument frozen into the captured graph
+}
+
+void Trainer::refresh_weights(hipStream_t s) {
+  const int V = d_.V, E = d_.E, H = d_.H;
+  cast_bf16(P("embedding"), (long)V * E, Emb, s);
+  transpose_bf16(P("embedding"), V, E, EmbT, s);
+  for (int l = 0; l < d_.L; ++l) {
+    const std::string k = std::to_string(l);
+    const int K = in_dim(l);
+    cast_bf16(P("weight_hh_l" + k), 3L * H * H, Ls_[l].Whh, s);
+    transpose_bf16(P("weight_hh_l" + k), 3 * H, H, Ls_[l].WhhT, s);
+    cast_bf16(P("weight_ih_l" + k), 3L * H * K, Ls_[l].Wih, s);
+    transpose_bf16(P("weight_ih_l" + k), 3 * H, K, Ls_[l].WihT, s);
+  }
+  cast_bf16(P("fc.weight"), (long)V * H, Wfc, s);
+  transpose_bf16(P("fc.weight"), V, H, WfcT, s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::set_batch(const int* x, const int* y, int B, hipStream_t s) {
+  if (B > Bp_ || B <= 0) throw std::runtime_error("set_batch: batch larger than the trainer was built for");
+  const int T = d_.T;
+  HIP_CHECK(hipEventSynchronize(stage_done_));       // previous upload finished with the staging buffer
+  int* ids = h_stage_;
+  int* lab = h_stage_ + (size_t)T * Bp_;
+  long valid = 0;
+  for (int t = 0; t < T; ++t) {
+    for (int b = 0; b < B; ++b) {
+      ids[(size_t)t * Bp_ + b] = x[(size_t)b * T + t];
+      const int yy = y[(size_t)b * T + t];
+      lab[(size_t)t * Bp_ + b] = yy;
+      valid += yy >= 0;
+    }
+    for (int b = B; b < Bp_; ++b) { ids[(size_t)t * Bp_ + b] = 0; lab[(size_t)t * Bp_ + b] = -1; }
+  }
+  float inv = 1.0f / (float)std::max(1L, valid);
+  std::memcpy(h_stage_ + 2 * (size_t)T * Bp_, &inv, 4);
+  // ids_, labels_, inv_count_ are consecutive 256-B aligned arena regions: copy the pieces
+  HIP_CHECK(hipMemcpyAsync(ids_, ids, (size_t)T * Bp_ * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(labels_, lab, (size_t)T * Bp_ * 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(inv_count_, h_stage_ + 2 * (size_t)T * Bp_, 4, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipEventRecord(stage_done_, s));
+}
+
+void Trainer::fwd_step(int l, int t, hipStream_t s) {
+  const int H = d_.H, B = Bp_;
+  Layer& y = Ls_[l];
+  FwdStepArgs a;
+  a.hprev_bf = y.HSb + (size_t)t * B * H;
+  a.hprev_f = y.HSf + (size_t)t * B * H;
+  a.Whh = y.Whh;
+  a.bhh = P("bias_hh_l" + std::to_string(l));
+  if (l == 0) { a.P = Ptab_; a.ids = ids_ + (size_t)t * B; }
+  else a.Gi = y.Gi + (size_t)t * B * 3 * H;
+  a.h_f = y.HSf + (size_t)(t + 1) * B * H;
+  a.h_bf = y.HSb + (size_t)(t + 1) * B * H;
+  a.hT = y.HT; a.ldT = (d_.T + 1) * B; a.colT = (t + 1) * B;
+  const size_t so = (size_t)t * B * H;
+  a.sr = y.sr + so; a.sz = y.sz + so; a.sn = y.sn + so; a.sghn = y.sghn + so;
+  a.Bp = B; a.H = H;
+  gru_fwd_step(a, s);
+}
+
+void Trainer::bwd_step(int l, int t, hipStream_t s) {
+  const int H = d_.H, B = Bp_, T = d_.T;
+  Layer& y = Ls_[l];
+  BwdStepArgs a;
+  const bool last = (t == T - 1);
+  a.dgh_next = last ? nullptr : y.dgh[(t + 1) & 1];
+  a.WhhT = y.WhhT;
+  a.carry_in = last ? nullptr : y.carry[(t + 1) & 1];
+  const size_t so = (size_t)t * B * H;
+  a.dy = y.dy + so;
+  a.r = y.sr + so; a.z = y.sz + so; a.n = y.sn + so; a.ghn = y.sghn + so;
+  a.hprev = y.HSf + so;
+  a.carry_out = y.carry[t & 1];
+  a.dgh = y.dgh[t & 1];
+  a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = T * B; a.colT = t * B;
+  a.dgi = y.dgi ? y.dgi + (size_t)t * B * 3 * H : nullptr;
+  a.Bp = B; a.H = H;
+  gru_bwd_step(a, s);
+}
+
+void Trainer::record_fb(hipStream_t s0) {
+  const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_, C = C_, Tc = Tc_;
+  const int H3 = 3 * H;
+  hipStream_t s1 = s1_;
+  ev_next_ = 0;
+  std::vector<std::vector<hipEvent_t>> evDy(L, std::vector<hipEvent_t>(C, nullptr));
+  auto edge = [&](hipStream_t from, hipStream_t to) {
+    hipEvent_t e = ev();
+    HIP_CHECK(hipEventRecord(e, from));
+    HIP_CHECK(hipStreamWaitEvent(to, e, 0));
+  };
+  edge(s0, s1);   // fork
+
+  // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]  (exact: Emb[x]·W^T)
+  {
+    GemmArgs g;
+    g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
+    g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
+    gemm_nt(g, s0);
+  }
+  // ------------------------------------------------------------------ forward
+  for (int l = 0; l < L; ++l) {
+    Layer& y = Ls_[l];
+    std::vector<hipEvent_t> evF(C);
+    for (int c = 0; c < C; ++c) {
+      if (l > 0) {
+        // Gi for this chunk from the layer below (already complete: layers run in order on s0)
+        GemmArgs g;
+        g.A = Ls_[l - 1].HSb + (size_t)(1 + c * Tc) * B * H; g.lda = H;
+        g.B = y.Wih; g.ldb = H;
+        g.C = y.Gi + (size_t)c * Tc * B * H3; g.ldc = H3;
+        g.bias = P("bias_ih_l" + std::to_string(l));
+        g.M = Tc * B; g.N = H3; g.K = H;
+        gemm_nt(g, s0);
+      }
+      for (int t = c * Tc; t < (c + 1) * Tc; ++t) fwd_step(l, t, s0);
+      if (l == L - 1) {
+        edge(s0, s1);
+        const size_t t0 = (size_t)c * Tc * B;   // first token of the chunk
+        FcXentArgs f;
+        f.X = y.HSb + (t0 + B) * H; f.W = Wfc; f.b = P("fc.bias");
+        f.labels = labels_ + t0; f.inv_count = inv_count_;
+        f.dl = dl_ + t0 * V; f.dlT = dlT_; f.ldT = T * B; f.colT = (int)t0;
+        f.loss_part = loss_part_ + t0 / 32;
+        f.M = Tc * B; f.H = H; f.V = V;
+        fc_xent(f, s1);
+        GemmArgs g;   // dy_top = dlogits · W_fc
+        g.A = dl_ + t0 * V; g.lda = V; g.B = WfcT; g.ldb = V;
+        g.C = y.dy + t0 * H; g.ldc = H; g.M = Tc * B; g.N = H; g.K = V;
+        gemm_nt(g, s1);
+        GemmArgs w;   // dW_fc slab c (+ db_fc as row sums of dlogits^T)
+        w.A = dlT_ + t0; w.lda = T * B; w.B = y.HT + t0 + B; w.ldb = (T + 1) * B;
+        w.C = slab_fc_ + (size_t)c * V * H; w.ldc = H; w.rowsumA = rs_fc_ + (size_t)c * V;
+        w.M = V; w.N = H; w.K = Tc * B;
+        gemm_nt(w, s1);
+        hipEvent_t e = ev();
+        HIP_CHECK(hipEventRecord(e, s1));
+        evDy[l][c] = e;
+      }
+    }
+  }
+  // ------------------------------------------------------------------ backward (BPTT)
+  for (int l = L - 1; l >= 0; --l) {
+    Layer& y = Ls_[l];
+    const int K = in_dim(l);
+    for (int c = C - 1; c >= 0; --c) {
+      HIP_CHECK(hipStreamWaitEvent(s0, evDy[l][c], 0));
+      for (int t = (c + 1) * Tc - 1; t >= c * Tc; --t) bwd_step(l, t, s0);
+      edge(s0, s1);
+      const size_t t0 = (size_t)c * Tc * B;
+      GemmArgs w;   // dW_hh slab c = dGh^T · h_{t-1}, db_hh = row sums of dGh^T
+      w.A = y.dghT + t0; w.lda = T * B; w.B = y.HT + t0; w.ldb = (T + 1) * B;
+      w.C = y.slab_hh + (size_t)c * H3 * H; w.ldc = H; w.rowsumA = y.rs_hh + (size_t)c * H3;
+      w.M = H3; w.N = H; w.K = Tc * B;
+      gemm_nt(w, s1);
+      if (l == 0) {
+        GemmArgs p;   // dP slab c = onehot(x)^T · dGi   ([V][3H]; gives dEmb, dW_ih0, db_ih0)
+        p.onehot_ids = ids_ + t0; p.B = y.dgiT + t0; p.ldb = T * B;
+        p.C = slab_P_ + (size_t)c * V * H3; p.ldc = H3; p.M = V; p.N = H3; p.K = Tc * B;
+        gemm_nt(p, s1);
+      } else {
+        GemmArgs wi;  // dW_ih slab c = dGi^T · h_below
+        wi.A = y.dgiT + t0; wi.lda = T * B; wi.B = Ls_[l - 1].HT + t0 + B; wi.ldb = (T + 1) * B;
+        wi.C = y.slab_ih + (size_t)c * H3 * K; wi.ldc = K; wi.rowsumA = y.rs_ih + (size_t)c * H3;
+        wi.M = H3; wi.N = K; wi.K = Tc * B;
+        gemm_nt(wi, s1);
+        GemmArgs dx;  // dy of the layer below = dGi · W_ih
+        dx.A = y.dgi + t0 * H3; dx.lda = H3; dx.B = y.WihT; dx.ldb = H3;
+        dx.C = Ls_[l - 1].dy + t0 * H; dx.ldc = H; dx.M = Tc * B; dx.N = H; dx.K = H3;
+        gemm_nt(dx, s1);
+        hipEvent_t e = ev();
+        HIP_CHECK(hipEventRecord(e, s1));
+        evDy[l - 1][c] = e;
+      }
+    }
+  }
+  // ------------------------------------------------------------------ finalize gradients (s1)
+  reduce_slabs(slab_fc_, C, (long)V * H, G("fc.weight"), s1);
+  reduce_slabs(rs_fc_, C, V, G("fc.bias"), s1);
+  for (int l = 0; l < L; ++l) {
+    const std::string k = std::to_string(l);
+    const int K = in_dim(l);
+    reduce_slabs(Ls_[l].slab_hh, C, (long)H3 * H, G("weight_hh_l" + k), s1);
+    reduce_slabs(Ls_[l].rs_hh, C, H3, G("bias_hh_l" + k), s1);
+    if (l > 0) {
+      reduce_slabs(Ls_[l].slab_ih, C, (long)H3 * K, G("weight_ih_l" + k), s1);
+      reduce_slabs(Ls_[l].rs_ih, C, H3, G("bias_ih_l" + k), s1);
+    }
+  }
+  reduce_slabs(slab_P_, C, (long)V * H3, dP_, s1);
+  cast_bf16(dP_, (long)V * H3, dP_bf_, s1);
+  transpose_bf16(dP_, V, H3, dPT_bf_, s1);
+  colsum(dP_, V, H3, G("bias_ih_l0"), s1);
+  {
+    GemmArgs g;   // dW_ih0 = dP^T · Emb
+    g.A = dPT_bf_; g.lda = V; g.B = EmbT; g.ldb = V; g.C = G("weight_ih_l0"); g.ldc = E;
+    g.M = H3; g.N = E; g.K = V;
+    gemm_nt(g, s1);
+    GemmArgs e;   // dEmb = dP · W_ih0
+    e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = G("embedding"); e.ldc = E;
+    e.M = V; e.N = E; e.K = H3;
+    gemm_nt(e, s1);
+  }
+  sum_partials(loss_part_, (int)((size_t)T * B / 32), loss_, s1);
+  edge(s1, s0);   // join
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::record_opt(hipStream_t s) {
+  if (o_.clip > 0.f) {
+    sumsq_partials(grads_, nflat_, norm_parts_, 256, s);
+    clip_scale_finalize(norm_parts_, 256, o_.clip, gscale_, s);
+  }
+  bump_step(step_, s);
+  OptimArgs a;
+  a.p = params_; a.g = grads_; a.m = m_; a.v = v_; a.n = nflat_; a.step = step_;
+  a.gscale = o_.clip > 0.f ? gscale_ : nullptr;
+  a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
+  adam_step(a, s);
+  refresh_weights(s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::forward_backward(hipStream_t s) {
+  if (!use_graph_) {
+    // eager: run on the internal streams, ordered after / before the caller's stream
+    hipEvent_t a = events_.back();
+    HIP_CHECK(hipEventRecord(a, s));
+    HIP_CHECK(hipStreamWaitEvent(s0_, a, 0));
+    record_fb(s0_);
+    HIP_CHECK(hipEventRecord(a, s0_));
+    HIP_CHECK(hipStreamWaitEvent(s, a, 0));
+    return;
+  }
+  if (!g_fb_.ready()) {
+    g_fb_.begin(s0_);
+    record_fb(s0_);
+    g_fb_.end(s0_);
+  }
+  g_fb_.launch(s);
+}
+
+void Trainer::optimizer_step(hipStream_t s) {
+  if (!use_graph_) { record_opt(s); return; }
+  if (!g_opt_.ready()) {
+    g_opt_.begin(s0_);
+    record_opt(s0_);
+    g_opt_.end(s0_);
+  }
+  g_opt_.launch(s);
+}
+
+float Trainer::read_loss() {
+  float v = 0.f;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(&v, loss_, 4, hipMemcpyDeviceToHost));
+  return v;
+}
+
+float Trainer::read_grad_norm() {
+  float v[2] = {0.f, 0.f};
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(v, gscale_, 8, hipMemcpyDeviceToHost));
+  return v[1];
+}
+
+uintptr_t Trainer::buffer(const std::string& n) const {
+  auto u = [](const void* p) { return reinterpret_cast<uintptr_t>(p); };
+  if (n == "ids") return u(ids_);
+  if (n == "labels") return u(labels_);
+  if (n == "P") return u(Ptab_);
+  if (n == "loss") return u(loss_);
+  if (n == "dl") return u(dl_);
+  if (n == "step") return u(step_);
+  if (n.rfind("HSf", 0) == 0) return u(Ls_.at(std::stoi(n.substr(3))).HSf);
+  if (n.rfind("dy", 0) == 0) return u(Ls_.at(std::stoi(n.substr(2))).dy);
+  throw std::runtime_error("unknown buffer " + n);
+}
+
+}  // namespace gk

@@ -1,0 +1,89 @@
+// Native training-step executor (SURVEY §3.5 train_step, §7.1 engine/trainer).
+//
+// One Trainer per process/GPU.  It owns the whole BPTT working set in one device arena and
+// records a full forward + loss + backward + weight-gradient step as ONE hipGraph over two
+// HIP streams:
+//   s0  the serial critical path: per-timestep recurrent kernels, forward then backward;
+//   s1  everything that only *consumes* a finished time chunk: FC + softmax-xent + dH for
+//       chunk c while s0 is still stepping chunk c+1 forward, and the split-K weight-gradient
+//       GEMMs of chunk c while s0 steps chunk c-1 backward.
+// The latency-bound recurrence leaves most of the chip idle; the side stream fills it.
+// Parameters / gradients / Adam moments live in caller-owned flat fp32 buffers (the Python
+// side keeps them as torch tensors so RCCL all-reduce and checkpointing work on them directly).
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+#include "../runtime/runtime.h"
+#include "../kernels/kernels.h"
+
+namespace gk {
+
+struct Dims {
+  int V = 256, E = 512, H = 512, L = 1, B = 256, T = 32, chunks = 4;
+};
+struct OptCfg {
+  float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f, clip = 0.f;
+  int sgd = 0;
+};
+
+class Trainer {
+ public:
+  Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, float* m, float* v, long nflat,
+          const std::map<std::string, long>& offsets);
+  ~Trainer();
+
+  void refresh_weights(hipStream_t s);                  // bf16 / transposed copies of the master weights
+  void set_batch(const int* x_bt, const int* y_bt, int B, hipStream_t s);  // host [B][T] ids/labels
+  void forward_backward(hipStream_t s);                 // graph replay (captured on first call)
+  void optimizer_step(hipStream_t s);                   // clip + Adam/SGD + refresh (graph)
+  float read_loss();                                    // blocking
+  float read_grad_norm();                               // blocking (valid when clip > 0)
+  void set_lr(float lr);
+  void set_use_graph(bool g) { use_graph_ = g; }
+  int padded_batch() const { return Bp_; }
+  long workspace_bytes() const { return (long)arena_.bytes(); }
+  // test/debug access to internal buffers by name
+  uintptr_t buffer(const std::string& name) const;
+
+ private:
+  void record_fb(hipStream_t s0);
+  void record_opt(hipStream_t s0);
+  void fwd_step(int l, int t, hipStream_t s);
+  void bwd_step(int l, int t, hipStream_t s);
+  hipEvent_t ev();
+  float* P(const std::string& name) const { return params_ + off_.at(name); }
+  float* G(const std::string& name) const { return grads_ + off_.at(name); }
+  int in_dim(int l) const { return l == 0 ? d_.E : d_.H; }
+
+  Dims d_;
+  OptCfg o_;
+  int Bp_ = 0, Tc_ = 0, C_ = 1;
+  float* params_; float* grads_; float* m_; float* v_;
+  long nflat_;
+  std::map<std::string, long> off_;
+
+  Arena arena_;
+  hipStream_t s0_ = nullptr, s1_ = nullptr;
+  std::vector<hipEvent_t> events_;
+  size_t ev_next_ = 0;
+  Graph g_fb_, g_opt_;
+  bool use_graph_ = true;
+  int* h_stage_ = nullptr;      // pinned [T*Bp ids][T*Bp labels][1 float]
+  hipEvent_t stage_done_ = nullptr;
+
+  struct Layer {
+    float *HSf, *sr, *sz, *sn, *sghn, *dy, *Gi, *carry[2];
+    u16 *HSb, *HT, *dgh[2], *dghT, *dgiT, *dgi;
+    u16 *Whh, *WhhT, *Wih, *WihT;
+    float *slab_hh, *rs_hh, *slab_ih, *rs_ih;
+  };
+  std::vector<Layer> Ls_;
+  int *ids_, *labels_;
+  float *inv_count_, *Ptab_, *loss_part_, *loss_, *slab_fc_, *rs_fc_, *slab_P_, *dP_;
+  float *norm_parts_, *gscale_;
+  int* step_;
+  u16 *Emb, *EmbT, *Wfc, *WfcT, *dl_, *dlT_, *dP_bf_, *dPT_bf_;
+};
+
+}  // namespace gk

@@ -1,0 +1,73 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+//
+// Everything here is written for wave64 + MFMA 16x16x32 bf16:
+//   A fragment: lane l holds A[row l&15][k = 8*(l>>4) + j], j = 0..7   (16 contiguous bytes)
+//   B fragment: lane l holds B[k = 8*(l>>4) + j][col l&15]              (stored [N][K]: 16 contiguous bytes)
+//   C/D:        lane l, reg i  ->  C[row (l>>4)*4 + i][col l&15]
+// so every operand of the "NT" products used by the engine (both operands K-contiguous)
+// is a single 16-byte load per lane per 32-deep k-step.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define DEV __device__ __forceinline__
+
+namespace gk {
+
+DEV float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (hipcc lowers the plain cast to v_cvt_pk_bf16_f32, NaN-safe)
+DEV u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(u16, b);
+}
+
+DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+DEV bf16x8 ld8(const u16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+DEV bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.0f;
+  return z;
+}
+
+DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+DEV float tanhf_(float x) {
+  // tanh via exp of a non-positive argument: no overflow, ~1 ulp-level agreement with tanhf
+  float e = __expf(-2.0f * fabsf(x));
+  float t = (1.0f - e) / (1.0f + e);
+  return copysignf(t, x);
+}
+
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// reduce across the 16 lanes that share (l>>4) -- i.e. across the 16 columns of a C tile
+DEV float max16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DEV float sum16(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace gk

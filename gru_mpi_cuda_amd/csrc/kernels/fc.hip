@@ -1,0 +1,217 @@
+// Fused FC head: logits = X·W_fc^T + b_fc on MFMA, then in the same launch either
+//   * fc_xent  : max-subtracted softmax + cross-entropy + dL/dlogits (training), or
+//   * fc_sample: softmax + on-device inverse-CDF sampling (generation).
+//
+// Replaces the reference's FC matvec + add + set_zero + racy atomic softmax and the
+// per-char D2H copy + host `random_select` (/root/reference/namegensf.cu:861-876,
+// kernels K7/K2/K8/K9 of SURVEY §2.2, sampler H7 at namegensf.cu:322-333).
+// A workgroup owns 32 full rows (all V columns) so the row reductions stay on chip:
+// each of the V/64 waves holds a 32x64 slab in 8 MFMA accumulators, rows are reduced
+// across the 16 column lanes with DPP-able xor shuffles and across waves through LDS.
+#include "kernels.h"
+#include "mma_tile.h"
+
+namespace gk {
+
+static constexpr int FROWS = 32;
+
+// Computes the wave's 32x64 logits slab (bias added) into acc.
+template <int KB>
+DEV void fc_logits(f32x4 (&acc)[2][4], const u16* X, const u16* W, const float* bias, int H, int m0,
+                   int lane, int w) {
+  zero_acc(acc);
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const u16* A = X + (size_t)(m0 + lr) * H + lk;
+  const u16* B = W + (size_t)(w * 64 + lr) * H + lk;
+  MmaLoop<2, 4, KB>::run(acc, A, H, B, 16 * H, H / 32);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float bb = bias[w * 64 + c * 16 + lr];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[r][c][i] += bb;
+  }
+}
+
+// Row max and sum-of-exp over all V columns; results broadcast per (rb, reg) to every lane.
+DEV void row_stats(const f32x4 (&acc)[2][4], float* red /*[2][NW][32]*/, int NW, int lane, int w,
+                   float (&mx)[2][4], float (&se)[2][4]) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float m = fmaxf(fmaxf(acc[r][0][i], acc[r][1][i]), fmaxf(acc[r][2][i], acc[r][3][i]));
+      m = max16(m);
+      if ((lane & 15) == 0) red[w * 32 + r * 16 + (lane >> 4) * 4 + i] = m;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + (lane >> 4) * 4 + i;
+      float m = red[row];
+      for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+      mx[r][i] = m;
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += __expf(acc[r][c][i] - m);
+      s = sum16(s);
+      if ((lane & 15) == 0) red[NW * 32 + w * 32 + row] = s;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + (lane >> 4) * 4 + i;
+      float s = 0.f;
+      for (int ww = 0; ww < NW; ++ww) s += red[NW * 32 + ww * 32 + row];
+      se[r][i] = s;
+    }
+}
+
+template <int KB>
+__global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int m0 = blockIdx.x * FROWS;
+  const int V = a.V;
+  f32x4 acc[2][4];
+  fc_logits<KB>(acc, a.X, a.W, a.b, a.H, m0, lane, w);
+
+  float* red = smem;                               // [2][NW][32]
+  float* lab = smem + 2 * NW * 32;                 // [32] label logit
+  float* lrow = lab + 32;                          // [32] per-row loss
+  u16* st = reinterpret_cast<u16*>(lrow + 32);     // [V][32] bf16 dl^T staging
+  float mx[2][4], se[2][4];
+  row_stats(acc, red, NW, lane, w, mx, se);
+  const float inv = a.inv_count[0];
+  const int lr = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + (lane >> 4) * 4 + i;
+      const int y = a.labels[m0 + row];
+      const float scale = (y >= 0) ? inv : 0.f;
+      const float rs = 1.f / se[r][i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = w * 64 + c * 16 + lr;
+        const float x = acc[r][c][i];
+        if (col == y) lab[row] = x;
+        const float p = __expf(x - mx[r][i]) * rs;
+        const float d = (p - (col == y ? 1.f : 0.f)) * scale;
+        const u16 db = f2bf(d);
+        a.dl[(size_t)(m0 + row) * V + col] = db;
+        st[col * FROWS + row] = db;
+      }
+    }
+  __syncthreads();
+  // per-row nll (one thread per row), then the block partial
+  if (threadIdx.x < FROWS) {
+    const int row = threadIdx.x;
+    const int y = a.labels[m0 + row];
+    // recompute this row's max / sum from wave-level partials
+    float m = red[row];
+    for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+    float s = 0.f;
+    for (int ww = 0; ww < NW; ++ww) s += red[NW * 32 + ww * 32 + row];
+    lrow[row] = (y >= 0) ? (logf(s) + m - lab[row]) * inv : 0.f;
+  }
+  for (int q = threadIdx.x; q < V * FROWS; q += blockDim.x) {
+    const int col = q >> 5, row = q & 31;
+    a.dlT[(size_t)col * a.ldT + a.colT + m0 + row] = st[col * FROWS + row];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < FROWS; ++i) t += lrow[i];
+    a.loss_part[blockIdx.x] = t;
+  }
+}
+
+template <int KB>
+__global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
+  const int m0 = blockIdx.x * FROWS;
+  const int V = a.V;
+  f32x4 acc[2][4];
+  fc_logits<KB>(acc, a.X, a.W, a.b, a.H, m0, lane, w);
+  float* red = smem;                   // [2][NW][32]
+  float* prob = smem + 2 * NW * 32;    // [32][V]
+  float mx[2][4], se[2][4];
+  row_stats(acc, red, NW, lane, w, mx, se);
+  const int lr = lane & 15;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + (lane >> 4) * 4 + i;
+      const float rs = 1.f / se[r][i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = w * 64 + c * 16 + lr;
+        const float p = __expf(acc[r][c][i] - mx[r][i]) * rs;
+        prob[row * V + col] = p;
+        if (a.probs) a.probs[(size_t)(m0 + row) * V + col] = p;
+      }
+    }
+  __syncthreads();
+  // inverse CDF: first index with running fp32 sum > r (namegensf.cu:326-331), else V-1.
+  // One wave per row: lane holds V/64 consecutive probabilities, sums them in index order,
+  // an exclusive wave scan gives its prefix, and the lowest hitting index wins.
+  const int per = V / 64;
+  for (int row = w; row < FROWS; row += NW) {
+    const int b = m0 + row;
+    if (b >= a.N) continue;                              // padding rows (wave-uniform)
+    const float rnd = a.rf[(size_t)b * a.max_len + a.step];
+    float loc = 0.f;
+    for (int e = 0; e < per; ++e) loc += prob[row * V + lane * per + e];
+    float inc = loc;                                     // inclusive scan of lane totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    float psum = inc - loc;
+    int hit = V;                                         // V = "no hit in this lane"
+    for (int e = 0; e < per; ++e) {
+      psum += prob[row * V + lane * per + e];
+      if (psum > rnd) { hit = lane * per + e; break; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hit = min(hit, __shfl_xor(hit, o, 64));
+    if (lane == 0) {
+      const int sel = (hit >= V) ? V - 1 : hit;
+      if (a.alive[b]) {
+        a.out[(size_t)b * (a.max_len + 1) + a.step] = (unsigned char)sel;
+        if (sel == a.eos) a.alive[b] = 0;
+      }
+      a.ids[b] = sel;
+    }
+  }
+}
+
+void fc_xent(const FcXentArgs& a, hipStream_t s) {
+  const int NW = a.V / 64;
+  const size_t shm = (2 * NW * 32 + 64) * 4 + (size_t)a.V * FROWS * 2;
+  const int nks = a.H / 32;
+  dim3 grid(a.M / FROWS), block(64 * NW);
+  if (nks % 2 == 0) hipLaunchKernelGGL(fc_xent_kernel<2>, grid, block, shm, s, a);
+  else hipLaunchKernelGGL(fc_xent_kernel<1>, grid, block, shm, s, a);
+}
+
+void fc_sample(const FcSampleArgs& a, hipStream_t s) {
+  const int NW = a.V / 64;
+  const size_t shm = (2 * NW * 32) * 4 + (size_t)a.V * FROWS * 4;
+  const int nks = a.H / 32;
+  dim3 grid(a.Bp / FROWS), block(64 * NW);
+  if (nks % 2 == 0) hipLaunchKernelGGL(fc_sample_kernel<2>, grid, block, shm, s, a);
+  else hipLaunchKernelGGL(fc_sample_kernel<1>, grid, block, shm, s, a);
+}
+
+}  // namespace gk

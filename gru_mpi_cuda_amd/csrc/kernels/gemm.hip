@@ -1,0 +1,129 @@
+// Generic bf16 "NT" MFMA GEMM  C[M][N] = A[M][K] · B[N][K]^T  with fp32 accumulate.
+//
+// Used for every non-recurrent product of the engine:
+//   * P = Emb·W_ih0^T + b_ih0        (the layer-0 input projection folded into a V x 3H table)
+//   * Gi = H_below·W_ih^T + b_ih      (hoisted input projection, layers >= 1)
+//   * dH = dlogits·W_fc,  dX = dGi·W_ih
+//   * weight gradients  dW = dG^T·H  over all B·T tokens (split-K partial slabs, one slab per
+//     time chunk so they run on a side stream while the serial recurrence continues), with the
+//     bias gradient as the fused row sum of A, and the one-hot A of the embedding gradient
+//     generated from the char ids on the fly (no gather/scatter, no float atomics:
+//     bitwise-deterministic).
+// Tile 64x64 per 4-wave workgroup (2x2 waves of 32x32 = 2x2 MFMA 16x16x32 tiles), operands
+// straight to VGPRs with a two-batch software pipeline (mma_tile.h), XCD-aware bijective
+// block remap so tiles sharing an operand panel share an L2 (cdna_hip_programming.md T1).
+#include "kernels.h"
+#include "mma_tile.h"
+
+namespace gk {
+
+DEV float sum8(const bf16x8& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += (float)v[i];
+  return s;
+}
+
+DEV int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <int KB, bool ONEHOT, bool ROWSUM>
+__global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  const int nwg = gridDim.x;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  const int tn = id % ntn;
+  const int tm = (id / ntn) % ntm;
+  const int sp = id / (ntn * ntm);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const int m0 = tm * 64 + wm * 32, n0 = tn * 64 + wn * 32;
+  const int kbeg = sp * kper;
+  const int nks = kper / 32;
+
+  f32x4 acc[2][2];
+  zero_acc(acc);
+  float rs[2] = {0.f, 0.f};
+  const u16* B = a.B + (size_t)(n0 + lr) * a.ldb + kbeg + lk;
+  if constexpr (ONEHOT) {
+    // A[m][k] = (ids[k] == m): 8 ids per lane per k-step, compare against the lane's two rows
+    const int* ids = a.onehot_ids + kbeg + lk;
+    for (int ks = 0; ks < nks; ++ks) {
+      const int4 i0 = *reinterpret_cast<const int4*>(ids + ks * 32);
+      const int4 i1 = *reinterpret_cast<const int4*>(ids + ks * 32 + 4);
+      const int idv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+      bf16x8 af[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int row = m0 + r * 16 + lr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) af[r][e] = (__bf16)(idv[e] == row ? 1.0f : 0.0f);
+      }
+      bf16x8 bf[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bf[c] = ld8(B + (size_t)c * 16 * a.ldb + ks * 32);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[r][c] = mfma16(af[r], bf[c], acc[r][c]);
+    }
+  } else {
+    const u16* A = a.A + (size_t)(m0 + lr) * a.lda + kbeg + lk;
+    MmaLoop<2, 2, KB>::run(acc, A, a.lda, B, 16 * a.ldb, nks);
+    if constexpr (ROWSUM) {
+      // bias gradient = row sums of A; only the tn == 0 column of workgroups, wave column 0
+      if (tn == 0 && wn == 0) {
+        for (int ks = 0; ks < nks; ++ks)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) rs[r] += sum8(ld8(A + (size_t)r * 16 * a.lda + ks * 32));
+      }
+    }
+  }
+
+  // epilogue: lane (l&15) = column, rows (l>>4)*4 + i
+  float* C = a.C + (size_t)sp * a.M * a.ldc;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = n0 + c * 16 + lr;
+      const float bb = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + r * 16 + (lane >> 4) * 4 + i;
+        float* dst = C + (size_t)row * a.ldc + col;
+        const float v = acc[r][c][i] + bb;
+        if (a.accumulate) *dst += v; else *dst = v;
+      }
+    }
+  if constexpr (ROWSUM && !ONEHOT) {
+    if (tn == 0 && wn == 0) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        float v = rs[r];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) a.rowsumA[(size_t)sp * a.M + m0 + r * 16 + lane] = v;
+      }
+    }
+  }
+}
+
+void gemm_nt(const GemmArgs& a, hipStream_t s) {
+  const int ntn = a.N / 64, ntm = a.M / 64;
+  const int kper = a.K / a.splits;
+  const int nks = kper / 32;
+  const int nwg = ntn * ntm * a.splits;
+  const bool rsum = a.rowsumA != nullptr;
+  dim3 grid(nwg), block(256);
+#define GL(KBV, OH, RS) hipLaunchKernelGGL((gemm_nt_kernel<KBV, OH, RS>), grid, block, 0, s, a, ntn, ntm, kper)
+  if (a.onehot_ids) { GL(1, true, false); return; }
+  if (nks % 4 == 0) { if (rsum) GL(4, false, true); else GL(4, false, false); }
+  else if (nks % 2 == 0) { if (rsum) GL(2, false, true); else GL(2, false, false); }
+  else { if (rsum) GL(1, false, true); else GL(1, false, false); }
+#undef GL
+}
+
+}  // namespace gk

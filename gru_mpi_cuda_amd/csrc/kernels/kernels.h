@@ -1,0 +1,125 @@
+// Host-side launch API of every HIP kernel in the engine (gfx950 only).
+//
+// Reference mapping: the reference's nine kernels K1..K9
+// (/root/reference/namegensf.cu:112-300) -- embedding, five element-wise ops, matvec,
+// set_zero, softmax -- are replaced by *fused* kernels: one launch per GRU timestep
+// (all three gate GEMMs + sigmoid/tanh/Hadamard epilogue), one fused FC+softmax(+xent or
+// +sampling) launch, and MFMA GEMMs for the hoisted / weight-gradient products.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short u16;
+
+namespace gk {
+
+// ------------------------------------------------------------------ recurrent steps
+struct FwdStepArgs {
+  const u16* hprev_bf = nullptr;   // [Bp][H]   h_{t-1} (bf16 MFMA operand)
+  const float* hprev_f = nullptr;  // [Bp][H]   h_{t-1} fp32 (blend operand)
+  const u16* Whh = nullptr;        // [3H][H]
+  const float* bhh = nullptr;      // [3H]
+  // input projection source (exactly one):
+  const float* P = nullptr;        //   [V][3H] table  Emb·W_ih^T + b_ih, gathered by ids
+  const int* ids = nullptr;        //   [Bp]
+  const float* Gi = nullptr;       //   [Bp][3H] precomputed (incl. b_ih)
+  const u16* x_bf = nullptr;       //   fused: Gi = x_bf[Bp][Kin] · Wih[3H][Kin]^T + bih
+  const u16* Wih = nullptr;
+  const float* bih = nullptr;
+  int Kin = 0;
+  // outputs
+  float* h_f = nullptr;            // [Bp][H]
+  u16* h_bf = nullptr;             // [Bp][H]
+  u16* hT = nullptr;               // transposed copy: hT[j*ldT + colT + b]  (nullable)
+  int ldT = 0, colT = 0;
+  float* sr = nullptr; float* sz = nullptr; float* sn = nullptr; float* sghn = nullptr;  // saves (nullable)
+  int Bp = 0, H = 0;
+};
+void gru_fwd_step(const FwdStepArgs& a, hipStream_t s);
+
+struct BwdStepArgs {
+  const u16* dgh_next = nullptr;   // [Bp][3H] dGh_{t+1} (null at t = T-1)
+  const u16* WhhT = nullptr;       // [H][3H]
+  const float* carry_in = nullptr; // [Bp][H]  z_{t+1} ⊙ dh_{t+1}    (null at t = T-1)
+  const float* dy = nullptr;       // [Bp][H]  dL/dh_t from above (FC or next layer)
+  const float *r = nullptr, *z = nullptr, *n = nullptr, *ghn = nullptr;  // saves at t
+  const float* hprev = nullptr;    // [Bp][H]  h_{t-1}
+  float* carry_out = nullptr;      // [Bp][H]
+  u16* dgh = nullptr;              // [Bp][3H]
+  u16* dghT = nullptr;             // [3H][ldT] at column colT + b
+  u16* dgiT = nullptr;             // [3H][ldT]
+  u16* dgi = nullptr;              // [Bp][3H] row-major dGi (nullable; needed below layer 0 only)
+  int ldT = 0, colT = 0, Bp = 0, H = 0;
+};
+void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ FC + softmax
+struct FcXentArgs {
+  const u16* X = nullptr;          // [M][H] top-layer hidden states (bf16)
+  const u16* W = nullptr;          // [V][H]
+  const float* b = nullptr;        // [V]
+  const int* labels = nullptr;     // [M], -1 = ignore
+  const float* inv_count = nullptr;// device scalar 1 / #valid tokens
+  u16* dl = nullptr;               // [M][V] bf16 dL/dlogits
+  u16* dlT = nullptr;              // [V][ldT] at column colT + row
+  float* loss_part = nullptr;      // [M/32] per-block partial (already scaled)
+  int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
+};
+void fc_xent(const FcXentArgs& a, hipStream_t s);
+
+struct FcSampleArgs {              // generation: logits -> softmax -> inverse-CDF sample
+  const u16* X = nullptr;          // [Bp][H]
+  const u16* W = nullptr;          // [V][H]
+  const float* b = nullptr;        // [V]
+  const float* rf = nullptr;       // [N][max_len] uniforms (global name index)
+  int* ids = nullptr;              // [Bp] in: unused / out: sampled char (next input)
+  unsigned char* out = nullptr;    // [N][max_len+1]
+  int* alive = nullptr;            // [Bp]
+  float* probs = nullptr;          // optional [Bp][V] softmax output (debug / tests)
+  int N = 0, Bp = 0, H = 0, V = 0, step = 0, max_len = 0, eos = 0;
+};
+void fc_sample(const FcSampleArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ generic GEMM
+// C[M][N] (+)= A[M][K] · B[N][K]^T  (bf16 in, fp32 accumulate), both operands K-contiguous.
+struct GemmArgs {
+  const u16* A = nullptr; int lda = 0;
+  const int* onehot_ids = nullptr; // if set, A[m][k] = (ids[k] == m) generated on the fly
+  const u16* B = nullptr; int ldb = 0;
+  float* C = nullptr; int ldc = 0;
+  const float* bias = nullptr;     // [N] added in the epilogue (non-split only)
+  float* rowsumA = nullptr;        // [splits][M] partial row sums of A (nullable)
+  int M = 0, N = 0, K = 0;
+  int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
+  int accumulate = 0;              // C += result instead of C = result
+};
+void gemm_nt(const GemmArgs& a, hipStream_t s);
+
+// sum `splits` slabs [splits][n] -> dst[n] (optionally also as bf16 and/or accumulate)
+void reduce_slabs(const float* src, int splits, long n, float* dst, hipStream_t s);
+
+// out = bf16 of in [R][C] (row-major) and/or its transpose [C][R]
+void cast_bf16(const float* in, long n, u16* out, hipStream_t s);
+void transpose_bf16(const float* in, int R, int C, u16* outT, hipStream_t s);
+// column sums of a [R][C] fp32 matrix -> out[C]
+void colsum(const float* in, int R, int C, float* out, hipStream_t s);
+
+// ------------------------------------------------------------------ optimiser / misc
+struct OptimArgs {
+  float* p = nullptr; const float* g = nullptr; float* m = nullptr; float* v = nullptr;
+  long n = 0;
+  int* step = nullptr;             // device step counter (graph-replay safe), incremented by caller kernel
+  const float* gscale = nullptr;   // device scalar gradient scale (clip); nullable = 1
+  float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f;
+  int sgd = 0;
+};
+void adam_step(const OptimArgs& a, hipStream_t s);
+void bump_step(int* step, hipStream_t s);
+// sum of squares of x[n] -> partials; finalize computes clip scale = min(1, clip/(sqrt(sum)+1e-6))
+void sumsq_partials(const float* x, long n, float* partials, int nparts, hipStream_t s);
+void clip_scale_finalize(const float* partials, int nparts, float clip, float* scale, hipStream_t s);
+// deterministic sum of partials -> out[0]
+void sum_partials(const float* partials, int n, float* out, hipStream_t s);
+void fill_f32(float* p, long n, float v, hipStream_t s);
+
+}  // namespace gk

@@ -1,0 +1,174 @@
+// Memory-bound helpers: split-K slab reduction, bf16 cast / transpose of the fp32 master
+// weights, column sums, fused Adam/SGD, gradient-norm clipping and deterministic scalar
+// reductions.  All vectorised 16 B per lane (cdna_hip_programming.md Guideline 13) and free
+// of float atomics, so a training step is bitwise reproducible run to run.
+#include "kernels.h"
+#include "common.h"
+
+namespace gk {
+
+static int nblocks(long n, int per_block, int cap = 4096) {
+  long b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return (int)(b > cap ? cap : b);
+}
+
+__global__ void reduce_slabs_kernel(const float* __restrict__ src, int splits, long n, float* __restrict__ dst) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(src)[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(src + (size_t)s * n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(dst)[i] = acc;
+  }
+  // tail
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += src[(size_t)s * n + i];
+    dst[i] = acc;
+  }
+}
+void reduce_slabs(const float* src, int splits, long n, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(nblocks(n / 4 + 1, 256, 2048)), dim3(256), 0, s, src, splits, n, dst);
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ in, long n, u16* __restrict__ out) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(in)[i];
+    ushort4 o;
+    o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+    reinterpret_cast<ushort4*>(out)[i] = o;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = f2bf(in[i]);
+}
+void cast_bf16(const float* in, long n, u16* out, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(nblocks(n / 4 + 1, 256, 2048)), dim3(256), 0, s, in, n, out);
+}
+
+// [R][C] fp32 -> [C][R] bf16 through a padded 64x64 LDS tile
+__global__ void transpose_bf16_kernel(const float* __restrict__ in, int R, int C, u16* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 256 threads: 4 rows per pass
+  for (int y = ty; y < 64; y += 4) {
+    const int r = r0 + y, c = c0 + tx;
+    tile[y][tx] = (r < R && c < C) ? in[(size_t)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 64; y += 4) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < C && r < R) out[(size_t)c * R + r] = f2bf(tile[tx][y]);
+  }
+}
+void transpose_bf16(const float* in, int R, int C, u16* outT, hipStream_t s) {
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, in, R, C, outT);
+}
+
+__global__ void colsum_kernel(const float* __restrict__ in, int R, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += in[(size_t)r * C + c];
+  out[c] = s;
+}
+void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, in, R, C, out);
+}
+
+__global__ void adam_kernel(OptimArgs a) {
+  const int t = *a.step;
+  const float sc = a.gscale ? *a.gscale : 1.f;
+  const float bc1 = 1.f - powf(a.b1, (float)t), bc2 = 1.f - powf(a.b2, (float)t);
+  const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
+  const long n4 = a.n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    const float4 g4 = reinterpret_cast<const float4*>(a.g)[i];
+    float pv[4] = {p.x, p.y, p.z, p.w};
+    const float gv[4] = {g4.x * sc, g4.y * sc, g4.z * sc, g4.w * sc};
+    if (a.sgd) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+    } else {
+      float4 m = reinterpret_cast<float4*>(a.m)[i];
+      float4 v = reinterpret_cast<float4*>(a.v)[i];
+      float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mv[e] = a.b1 * mv[e] + (1.f - a.b1) * gv[e];
+        vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
+        float u = (mv[e] * ib1) / (sqrtf(vv[e] * ib2) + a.eps);
+        if (a.wd != 0.f) u += a.wd * pv[e];
+        pv[e] -= a.lr * u;
+      }
+      reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    reinterpret_cast<float4*>(a.p)[i] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  }
+}
+void adam_step(const OptimArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks(a.n / 4, 256, 2048)), dim3(256), 0, s, a);
+}
+
+__global__ void bump_kernel(int* step) { *step += 1; }
+void bump_step(int* step, hipStream_t s) { hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step); }
+
+__global__ void sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ parts) {
+  __shared__ float red[16];
+  float acc = 0.f;
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    acc += x[i] * x[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    parts[blockIdx.x] = t;
+  }
+}
+void sumsq_partials(const float* x, long n, float* partials, int nparts, hipStream_t s) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(256), 0, s, x, n, partials);
+}
+
+__global__ void clip_final_kernel(const float* parts, int n, float clip, float* scale) {
+  float t = 0.f;
+  for (int i = 0; i < n; ++i) t += parts[i];
+  const float norm = sqrtf(t);
+  scale[0] = fminf(1.f, clip / (norm + 1e-6f));
+  scale[1] = norm;
+}
+void clip_scale_finalize(const float* partials, int nparts, float clip, float* scale, hipStream_t s) {
+  hipLaunchKernelGGL(clip_final_kernel, dim3(1), dim3(1), 0, s, partials, nparts, clip, scale);
+}
+
+__global__ void sum_partials_kernel(const float* p, int n, float* out) {
+  // one wave, fixed order: deterministic
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += 64) acc += p[i];
+  acc = wave_sum(acc);
+  if (threadIdx.x == 0) out[0] = acc;
+}
+void sum_partials(const float* partials, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out);
+}
+
+__global__ void fill_kernel(float* p, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+void fill_f32(float* p, long n, float v, hipStream_t s) {
+  hipLaunchKernelGGL(fill_kernel, dim3(nblocks(n, 256, 1024)), dim3(256), 0, s, p, n, v);
+}
+
+}  // namespace gk

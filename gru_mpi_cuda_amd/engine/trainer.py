@@ -1,0 +1,156 @@
+"""Training engines.
+
+``HipTrainer``  -- the MI355X path: the native executor (csrc/engine/trainer.cpp) runs the
+whole forward + softmax-xent + BPTT + weight-gradient step as one hipGraph over two HIP
+streams; gradients are then averaged with bucketed RCCL all-reduce on the device (native
+communicator) and a fused Adam + bf16-weight-refresh graph finishes the step.
+
+``CpuTrainer``  -- the CPU reference path (BASELINE config #1): same math in PyTorch
+(models/cpu_ref.manual_backward), gloo all-reduce for multi-process tests.
+
+Neither has a reference counterpart: the reference is inference-only.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..config import GRUConfig
+from ..models import cpu_ref
+from ..models.params import flat_layout, from_flat, init_params, to_flat
+from ..parallel.dist import DistCtx, allreduce_mean_buckets, bucket_bounds
+
+
+def _bucket_list(cfg: GRUConfig, total: int):
+    lay = flat_layout(cfg)
+    bounds = [s.offset for s in lay.segments]
+    return bucket_bounds(total, max(1024, int(cfg.bucket_mb * (1 << 20) / 4)), bounds)
+
+
+class HipTrainer:
+    def __init__(self, cfg: GRUConfig, ctx: Optional[DistCtx] = None,
+                 params: Optional[Dict[str, torch.Tensor]] = None, comm=None, use_graph: bool = True):
+        from ..ops import load_ext
+        self.C = load_ext()
+        self.cfg = cfg
+        self.ctx = ctx or DistCtx(device=torch.device("cuda", torch.cuda.current_device()))
+        self.dev = self.ctx.device
+        if cfg.batch % self.ctx.world:
+            raise ValueError(f"global batch {cfg.batch} not divisible by world size {self.ctx.world}")
+        self.local_batch = cfg.batch // self.ctx.world
+        self.layout = flat_layout(cfg)
+        self.params = to_flat(cfg, params if params is not None else init_params(cfg)).to(self.dev)
+        self.grads = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.comm = comm
+        self.buckets = _bucket_list(cfg, self.layout.total)
+        offsets = {s.name: s.offset for s in self.layout.segments}
+        dims = dict(V=cfg.vocab, E=cfg.embed, H=cfg.hidden, L=cfg.layers, B=self.local_batch,
+                    T=cfg.seq, chunks=cfg.time_chunks)
+        opt = dict(lr=cfg.lr, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps,
+                   weight_decay=cfg.weight_decay, clip_norm=cfg.clip_norm,
+                   sgd=int(cfg.optimizer == "sgd"))
+        self.t = self.C.Trainer(dims, opt, self.params.data_ptr(), self.grads.data_ptr(),
+                                self.m.data_ptr(), self.v.data_ptr(), self.layout.total, offsets)
+        self.t.set_use_graph(use_graph)
+        if self.comm is not None:     # identical replicas: rank 0's weights everywhere
+            self.comm.broadcast_f32(self.params.data_ptr(), self.layout.total, 0, self._stream())
+        self.t.refresh_weights(self._stream())
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def forward_backward(self, x: np.ndarray, y: np.ndarray) -> None:
+        s = self._stream()
+        self.t.set_batch(x, y, s)
+        self.t.forward_backward(s)
+
+    def allreduce_grads(self) -> None:
+        if self.comm is None:
+            return
+        s = self._stream()
+        base = self.grads.data_ptr()
+        for a, b in self.buckets:
+            self.comm.allreduce_avg_f32(base + 4 * a, b - a, s)
+
+    def optimizer_step(self) -> None:
+        self.t.optimizer_step(self._stream())
+
+    def step(self, x: np.ndarray, y: np.ndarray) -> None:
+        self.forward_backward(x, y)
+        self.allreduce_grads()
+        self.optimizer_step()
+
+    def loss(self) -> float:
+        return self.t.read_loss()
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        torch.cuda.synchronize(self.dev)
+        return {k: v.cpu() for k, v in from_flat(self.cfg, self.params).items()}
+
+    def grad_dict(self) -> Dict[str, torch.Tensor]:
+        torch.cuda.synchronize(self.dev)
+        return {k: v.cpu() for k, v in from_flat(self.cfg, self.grads).items()}
+
+    def load_state(self, params: Dict[str, torch.Tensor]) -> None:
+        self.params.copy_(to_flat(self.cfg, params).to(self.dev))
+        self.t.refresh_weights(self._stream())
+
+
+class CpuTrainer:
+    def __init__(self, cfg: GRUConfig, ctx: Optional[DistCtx] = None,
+                 params: Optional[Dict[str, torch.Tensor]] = None, dtype=torch.float32):
+        self.cfg = cfg
+        self.ctx = ctx or DistCtx()
+        if cfg.batch % self.ctx.world:
+            raise ValueError(f"global batch {cfg.batch} not divisible by world size {self.ctx.world}")
+        self.local_batch = cfg.batch // self.ctx.world
+        p = params if params is not None else init_params(cfg)
+        self.layout = flat_layout(cfg)
+        self.flat_p = to_flat(cfg, p).to(dtype)
+        self.flat_g = torch.zeros_like(self.flat_p)
+        self.params = self.layout.views(self.flat_p)
+        self.gviews = self.layout.views(self.flat_g)
+        if self.ctx.world > 1:          # identical replicas
+            import torch.distributed as dist
+            dist.broadcast(self.flat_p, 0)
+        self.opt = cpu_ref.Adam(cfg, self.params)
+        self.buckets = _bucket_list(cfg, self.layout.total)
+        self._loss = float("nan")
+
+    def forward_backward(self, x: np.ndarray, y: np.ndarray) -> None:
+        loss, grads = cpu_ref.manual_backward(self.params, self.cfg, torch.from_numpy(np.asarray(x)),
+                                              torch.from_numpy(np.asarray(y)))
+        for k, g in grads.items():
+            self.gviews[k].copy_(g)
+        self._loss = float(loss)
+
+    def allreduce_grads(self) -> None:
+        allreduce_mean_buckets(self.flat_g, self.buckets, self.ctx.world)
+
+    def optimizer_step(self) -> None:
+        self.opt.step(self.params, self.gviews)
+
+    def step(self, x, y) -> None:
+        self.forward_backward(x, y)
+        self.allreduce_grads()
+        self.optimizer_step()
+
+    def loss(self) -> float:
+        return self._loss
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v.detach().clone() for k, v in self.params.items()}
+
+    def grad_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v.detach().clone() for k, v in self.gviews.items()}
+
+
+def make_trainer(cfg: GRUConfig, ctx: DistCtx, comm=None, params=None):
+    if ctx.device.type == "cuda":
+        return HipTrainer(cfg, ctx, params=params, comm=comm)
+    return CpuTrainer(cfg, ctx, params=params)

@@ -1,0 +1,36 @@
+"""Loads the in-tree native extension ``gru_mpi_cuda_amd/_C``.
+
+torch is imported first so the extension binds to torch's already-loaded HIP runtime
+(same soname ``libamdhip64.so.7``).  On a machine with a GPU a missing or broken extension
+is an ERROR, never a silent fallback to eager PyTorch: the HIP path is the product.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_EXT = None
+
+
+def ext_available() -> bool:
+    from ..build_ext import ext_path
+    return os.path.exists(ext_path())
+
+
+def load_ext(build_if_missing: bool = True):
+    global _EXT
+    if _EXT is not None:
+        return _EXT
+    import torch  # noqa: F401  (load torch's libamdhip64 first)
+    from ..build_ext import build, ext_path
+    if not os.path.exists(ext_path()):
+        if not build_if_missing:
+            raise ImportError(f"native extension missing at {ext_path()}; run "
+                              "`python -m gru_mpi_cuda_amd.build_ext`")
+        build()
+    try:
+        _EXT = importlib.import_module("gru_mpi_cuda_amd._C")
+    except ImportError as e:
+        raise ImportError(f"failed to load native extension {ext_path()}: {e}. "
+                          "Rebuild with `python -m gru_mpi_cuda_amd.build_ext --force`") from e
+    return _EXT

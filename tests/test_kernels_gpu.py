@@ -1,0 +1,205 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Operands are rounded to bf16 first (the kernels' input precision) so the comparison
+isolates the kernel: fp32-accumulated MFMA vs fp32 torch matmul of the same bf16 values.
+Asymmetric operands everywhere (an A = I / symmetric-B test would hide a transposed C-write,
+cdna_hip_programming.md §3).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def bf(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(64, 64, 32, 1), (128, 192, 256, 1), (256, 512, 1024, 4), (192, 128, 512, 2)])
+def test_gemm_nt(ext, M, N, K, splits):
+    A, B = bf(rnd(M, K, seed=1)), bf(rnd(N, K, seed=2) + 0.1 * torch.arange(K, device=DEV) / K)
+    bias = rnd(N, seed=3) if splits == 1 else None
+    C = torch.full((splits, M, N), float("nan"), device=DEV)
+    rs = torch.full((splits, M), float("nan"), device=DEV)
+    d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=M, N=N, K=K,
+             splits=splits, rowsumA=rs.data_ptr())
+    if bias is not None:
+        d["bias"] = bias.data_ptr()
+    ext.gemm_nt(d, S())
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().T + (bias if bias is not None else 0)
+    got = C.sum(0)
+    torch.testing.assert_close(got, ref, atol=2e-3 * K ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(rs.sum(0), A.float().sum(1), atol=1e-2, rtol=1e-3)
+
+
+def test_gemm_onehot(ext):
+    V, N, K = 256, 192, 512
+    ids = torch.randint(0, V, (K,), device=DEV, dtype=torch.int32)
+    B = bf(rnd(N, K, seed=5))
+    C = torch.zeros(V, N, device=DEV)
+    ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=V, N=N, K=K), S())
+    torch.cuda.synchronize()
+    oh = torch.nn.functional.one_hot(ids.long(), V).float()      # [K][V]
+    ref = oh.T @ B.float().T
+    torch.testing.assert_close(C, ref, atol=1e-3, rtol=1e-3)
+
+
+def _gates_ref(gi, gh, hp):
+    H = hp.shape[1]
+    r = torch.sigmoid(gi[:, :H] + gh[:, :H])
+    z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+    n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+    return n + z * (hp - n), r, z, n, gh[:, 2 * H:]
+
+
+@pytest.mark.parametrize("mode", ["table", "gi", "fused"])
+@pytest.mark.parametrize("H", [128, 512])
+def test_fwd_step(ext, mode, H):
+    Bp, V, Kin = 64, 256, 256
+    hp = rnd(Bp, H, scale=0.5, seed=1).clamp(-1, 1)
+    hpb = bf(hp)
+    Whh = bf(rnd(3 * H, H, scale=H ** -0.5, seed=2))
+    bhh = rnd(3 * H, scale=0.1, seed=3)
+    d = dict(hprev_bf=hpb.data_ptr(), hprev_f=hp.data_ptr(), Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), Bp=Bp, H=H)
+    keep = []
+    if mode == "table":
+        P = rnd(V, 3 * H, seed=4)
+        ids = torch.randint(0, V, (Bp,), device=DEV, dtype=torch.int32)
+        d.update(P=P.data_ptr(), ids=ids.data_ptr())
+        gi = P[ids.long()]
+        keep += [P, ids]
+    elif mode == "gi":
+        Gi = rnd(Bp, 3 * H, seed=5)
+        d.update(Gi=Gi.data_ptr())
+        gi = Gi
+        keep.append(Gi)
+    else:
+        x = bf(rnd(Bp, Kin, seed=6))
+        Wih = bf(rnd(3 * H, Kin, scale=Kin ** -0.5, seed=7))
+        bih = rnd(3 * H, scale=0.1, seed=8)
+        d.update(x_bf=x.data_ptr(), Wih=Wih.data_ptr(), bih=bih.data_ptr(), Kin=Kin)
+        gi = x.float() @ Wih.float().T + bih
+        keep += [x, Wih, bih]
+    T = 3
+    h_f = torch.empty(Bp, H, device=DEV)
+    h_b = torch.empty(Bp, H, device=DEV, dtype=torch.bfloat16)
+    hT = torch.zeros(H, (T + 1) * Bp, device=DEV, dtype=torch.bfloat16)
+    sv = [torch.empty(Bp, H, device=DEV) for _ in range(4)]
+    d.update(h_f=h_f.data_ptr(), h_bf=h_b.data_ptr(), hT=hT.data_ptr(), ldT=(T + 1) * Bp, colT=2 * Bp,
+             sr=sv[0].data_ptr(), sz=sv[1].data_ptr(), sn=sv[2].data_ptr(), sghn=sv[3].data_ptr())
+    ext.fwd_step(d, S())
+    torch.cuda.synchronize()
+    gh = hpb.float() @ Whh.float().T + bhh
+    h, r, z, n, ghn = _gates_ref(gi, gh, hp)
+    tol = dict(atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(h_f, h, **tol)
+    torch.testing.assert_close(h_b.float(), h, atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(hT[:, 2 * Bp:3 * Bp].T.float(), h_b.float(), atol=0, rtol=0)
+    for got, ref in zip(sv, (r, z, n, ghn)):
+        torch.testing.assert_close(got, ref, **tol)
+
+
+@pytest.mark.parametrize("first", [False, True])
+def test_bwd_step(ext, first):
+    Bp, H, T = 64, 128, 4
+    t = 1
+    dgn = bf(rnd(Bp, 3 * H, scale=0.1, seed=1))
+    Whh = rnd(3 * H, H, scale=H ** -0.5, seed=2)
+    WhhT = bf(Whh.T)
+    carry = rnd(Bp, H, scale=0.1, seed=3)
+    dy = rnd(Bp, H, scale=0.1, seed=4)
+    r, z, n = torch.sigmoid(rnd(Bp, H, seed=5)), torch.sigmoid(rnd(Bp, H, seed=6)), torch.tanh(rnd(Bp, H, seed=7))
+    ghn, hp = rnd(Bp, H, seed=8), torch.tanh(rnd(Bp, H, seed=9))
+    cout = torch.empty(Bp, H, device=DEV)
+    dgh = torch.empty(Bp, 3 * H, device=DEV, dtype=torch.bfloat16)
+    dgi = torch.empty(Bp, 3 * H, device=DEV, dtype=torch.bfloat16)
+    dghT = torch.zeros(3 * H, T * Bp, device=DEV, dtype=torch.bfloat16)
+    dgiT = torch.zeros(3 * H, T * Bp, device=DEV, dtype=torch.bfloat16)
+    d = dict(WhhT=WhhT.data_ptr(), dy=dy.data_ptr(), r=r.data_ptr(), z=z.data_ptr(), n=n.data_ptr(),
+             ghn=ghn.data_ptr(), hprev=hp.data_ptr(), carry_out=cout.data_ptr(), dgh=dgh.data_ptr(),
+             dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), dgi=dgi.data_ptr(), ldT=T * Bp, colT=t * Bp, Bp=Bp, H=H)
+    if not first:
+        d.update(dgh_next=dgn.data_ptr(), carry_in=carry.data_ptr())
+    ext.bwd_step(d, S())
+    torch.cuda.synchronize()
+    dh = dy.clone()
+    if not first:
+        dh += dgn.float() @ WhhT.float().T + carry
+    dn = dh * (1 - z)
+    dz = dh * (hp - n)
+    dan = dn * (1 - n * n)
+    dar = dan * ghn * r * (1 - r)
+    daz = dz * z * (1 - z)
+    ref_h = torch.cat([dar, daz, dan * r], 1)
+    ref_i = torch.cat([dar, daz, dan], 1)
+    torch.testing.assert_close(cout, z * dh, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(dgh.float(), ref_h, atol=2e-3, rtol=1e-2)
+    torch.testing.assert_close(dgi.float(), ref_i, atol=2e-3, rtol=1e-2)
+    torch.testing.assert_close(dghT[:, t * Bp:(t + 1) * Bp].T, dgh, atol=0, rtol=0)
+    torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
+
+
+def test_fc_xent(ext):
+    M, H, V = 128, 256, 256
+    X = bf(rnd(M, H, seed=1))
+    W = bf(rnd(V, H, scale=H ** -0.5, seed=2))
+    b = rnd(V, scale=0.5, seed=3)
+    y = torch.randint(0, V, (M,), device=DEV, dtype=torch.int32)
+    y[::7] = -1
+    inv = torch.tensor([1.0 / int((y >= 0).sum())], device=DEV)
+    dl = torch.empty(M, V, device=DEV, dtype=torch.bfloat16)
+    dlT = torch.zeros(V, 2 * M, device=DEV, dtype=torch.bfloat16)
+    lp = torch.empty(M // 32, device=DEV)
+    ext.fc_xent(dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), labels=y.data_ptr(), inv_count=inv.data_ptr(),
+                     dl=dl.data_ptr(), dlT=dlT.data_ptr(), loss_part=lp.data_ptr(), M=M, H=H, V=V, ldT=2 * M, colT=M), S())
+    torch.cuda.synchronize()
+    logits = X.float() @ W.float().T + b
+    valid = y >= 0
+    loss = torch.nn.functional.cross_entropy(logits[valid], y[valid].long())
+    p = torch.softmax(logits, -1)
+    oh = torch.nn.functional.one_hot(y.clamp_min(0).long(), V).float()
+    ref = (p - oh) * valid[:, None] * inv
+    torch.testing.assert_close(lp.sum(), loss, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dl.float(), ref, atol=1e-4, rtol=1e-2)
+    torch.testing.assert_close(dlT[:, M:].T, dl, atol=0, rtol=0)
+
+
+def test_fc_sample(ext):
+    from gru_mpi_cuda_amd.models.cpu_ref import sample_inverse_cdf
+    N, Bp, H, V, ML = 50, 64, 128, 256, 6
+    X = bf(rnd(Bp, H, seed=1))
+    W = bf(rnd(V, H, scale=3 * H ** -0.5, seed=2))
+    b = rnd(V, seed=3)
+    rf = torch.rand(N, ML, device=DEV)
+    ids = torch.zeros(Bp, device=DEV, dtype=torch.int32)
+    alive = torch.ones(Bp, device=DEV, dtype=torch.int32)
+    alive[3] = 0
+    out = torch.zeros(N, ML + 1, device=DEV, dtype=torch.uint8)
+    probs = torch.zeros(Bp, V, device=DEV)
+    step = 2
+    ext.fc_sample(dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), rf=rf.data_ptr(), ids=ids.data_ptr(),
+                       out=out.data_ptr(), alive=alive.data_ptr(), probs=probs.data_ptr(), N=N, Bp=Bp, H=H, V=V,
+                       step=step, max_len=ML, eos=0), S())
+    torch.cuda.synchronize()
+    ref_p = torch.softmax(X.float() @ W.float().T + b, -1)
+    torch.testing.assert_close(probs, ref_p, atol=1e-5, rtol=1e-4)
+    sel = sample_inverse_cdf(probs[:N].double().cpu(), rf[:, step].double().cpu())
+    got = ids[:N].long().cpu()
+    assert (got == sel).float().mean() >= 0.98
+    o = out.cpu()
+    assert o[3, step] == 0                       # dead row untouched
+    live = [i for i in range(N) if i != 3]
+    assert torch.equal(o[live, step].long(), got[live])
