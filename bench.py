@@ -35,6 +35,7 @@ def main() -> int:
                     help="hip = this engine; torch = torch.nn.GRU (MIOpen) comparator")
     ap.add_argument("--chunks", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--serial", action="store_true", help="single HIP stream (no side-stream overlap)")
     args = ap.parse_args()
 
     import torch
@@ -50,6 +51,8 @@ def main() -> int:
     cfg = base.replace(batch=per_gpu * world)
     if args.chunks:
         cfg = cfg.replace(time_chunks=args.chunks)
+    if args.serial:
+        cfg = cfg.replace(overlap=False)
 
     stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
     pool = [stream.next() for _ in range(8)]
@@ -96,7 +99,8 @@ def main() -> int:
             "config": {"model": f"GRU L={cfg.layers} H={cfg.hidden} E={cfg.embed} V={cfg.vocab}",
                        "global_batch": cfg.batch, "seq_len": cfg.seq,
                        "parallelism": f"dp{world}", "impl": args.impl,
-                       "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks},
+                       "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
+                       "overlap": cfg.overlap},
             "final_loss": round(float(loss), 4),
         }
         print(json.dumps(out), flush=True)

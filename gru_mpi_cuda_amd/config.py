@@ -40,6 +40,7 @@ class GRUConfig:
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
+    overlap: bool = True        # run chunk consumers (FC, weight grads) on a side HIP stream
 
     def __post_init__(self):
         if self.layers < 1:

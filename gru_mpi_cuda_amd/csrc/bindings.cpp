@@ -48,7 +48,7 @@ PYBIND11_MODULE(_C, m) {
         Dims d;
         d.V = get<int>(dims, "V", 256); d.E = get<int>(dims, "E", 512); d.H = get<int>(dims, "H", 512);
         d.L = get<int>(dims, "L", 1); d.B = get<int>(dims, "B", 256); d.T = get<int>(dims, "T", 32);
-        d.chunks = get<int>(dims, "chunks", 4);
+        d.chunks = get<int>(dims, "chunks", 4); d.overlap = get<int>(dims, "overlap", 1);
         OptCfg o;
         o.lr = get<float>(opt, "lr", 1e-3f); o.b1 = get<float>(opt, "beta1", 0.9f); o.b2 = get<float>(opt, "beta2", 0.999f);
         o.eps = get<float>(opt, "eps", 1e-8f); o.wd = get<float>(opt, "weight_decay", 0.f);

@@ -40,13 +40,15 @@ Generator::~Generator() {
 
 void Generator::refresh_weights(hipStream_t s) {
   const int V = d_.V, E = d_.E, H = d_.H;
-  cast_bf16(P("embedding"), (long)V * E, Emb_, s);
+  CastJobs j;
+  j.add(P("embedding"), V, E, Emb_, nullptr);
   for (int l = 0; l < d_.L; ++l) {
     const std::string k = std::to_string(l);
-    cast_bf16(P("weight_hh_l" + k), 3L * H * H, Whh_[l], s);
-    cast_bf16(P("weight_ih_l" + k), 3L * H * (l == 0 ? E : H), Wih_[l], s);
+    j.add(P("weight_hh_l" + k), 3 * H, H, Whh_[l], nullptr);
+    j.add(P("weight_ih_l" + k), 3 * H, l == 0 ? E : H, Wih_[l], nullptr);
   }
-  cast_bf16(P("fc.weight"), (long)V * H, Wfc_, s);
+  j.add(P("fc.weight"), V, H, Wfc_, nullptr);
+  cast_multi(j, s);
   GemmArgs g;   // layer-0 input projection table P = Emb · W_ih0^T + b_ih0  ([V][3H])
   g.A = Emb_; g.lda = E; g.B = Wih_[0]; g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
   g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;

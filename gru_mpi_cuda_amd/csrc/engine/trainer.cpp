@@ -84,6 +84,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   HIP_CHECK(hipEventRecord(stage_done_, s0_));
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
+  overlap_ = d_.overlap != 0;
 }
 
 Trainer::~Trainer() {
@@ -107,19 +108,17 @@ void Trainer::set_lr(float lr) {
 }
 
 void Trainer::refresh_weights(hipStream_t s) {
+  // one launch: every master weight -> bf16 copy (+ transposed bf16 copy where a kernel needs it)
   const int V = d_.V, E = d_.E, H = d_.H;
-  cast_bf16(P("embedding"), (long)V * E, Emb, s);
-  transpose_bf16(P("embedding"), V, E, EmbT, s);
+  CastJobs j;
+  j.add(P("embedding"), V, E, Emb, EmbT);
   for (int l = 0; l < d_.L; ++l) {
     const std::string k = std::to_string(l);
-    const int K = in_dim(l);
-    cast_bf16(P("weight_hh_l" + k), 3L * H * H, Ls_[l].Whh, s);
-    transpose_bf16(P("weight_hh_l" + k), 3 * H, H, Ls_[l].WhhT, s);
-    cast_bf16(P("weight_ih_l" + k), 3L * H * K, Ls_[l].Wih, s);
-    transpose_bf16(P("weight_ih_l" + k), 3 * H, K, Ls_[l].WihT, s);
+    j.add(P("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
+    j.add(P("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
   }
-  cast_bf16(P("fc.weight"), (long)V * H, Wfc, s);
-  transpose_bf16(P("fc.weight"), V, H, WfcT, s);
+  j.add(P("fc.weight"), V, H, Wfc, WfcT);
+  cast_multi(j, s);
   HIP_LAUNCH_CHECK();
 }
 
@@ -190,10 +189,11 @@ void Trainer::bwd_step(int l, int t, hipStream_t s) {
 void Trainer::record_fb(hipStream_t s0) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_, C = C_, Tc = Tc_;
   const int H3 = 3 * H;
-  hipStream_t s1 = s1_;
+  hipStream_t s1 = overlap_ ? s1_ : s0;   // serial mode: one stream, edges become no-ops
   ev_next_ = 0;
   std::vector<std::vector<hipEvent_t>> evDy(L, std::vector<hipEvent_t>(C, nullptr));
   auto edge = [&](hipStream_t from, hipStream_t to) {
+    if (from == to) return;
     hipEvent_t e = ev();
     HIP_CHECK(hipEventRecord(e, from));
     HIP_CHECK(hipStreamWaitEvent(to, e, 0));
@@ -244,7 +244,7 @@ void Trainer::record_fb(hipStream_t s0) {
         gemm_nt(w, s1);
         hipEvent_t e = ev();
         HIP_CHECK(hipEventRecord(e, s1));
-        evDy[l][c] = e;
+        evDy[l][c] = e;   // (serial mode: recorded on s0 itself, the wait is a no-op)
       }
     }
   }
@@ -284,21 +284,27 @@ void Trainer::record_fb(hipStream_t s0) {
     }
   }
   // ------------------------------------------------------------------ finalize gradients (s1)
-  reduce_slabs(slab_fc_, C, (long)V * H, G("fc.weight"), s1);
-  reduce_slabs(rs_fc_, C, V, G("fc.bias"), s1);
-  for (int l = 0; l < L; ++l) {
-    const std::string k = std::to_string(l);
-    const int K = in_dim(l);
-    reduce_slabs(Ls_[l].slab_hh, C, (long)H3 * H, G("weight_hh_l" + k), s1);
-    reduce_slabs(Ls_[l].rs_hh, C, H3, G("bias_hh_l" + k), s1);
-    if (l > 0) {
-      reduce_slabs(Ls_[l].slab_ih, C, (long)H3 * K, G("weight_ih_l" + k), s1);
-      reduce_slabs(Ls_[l].rs_ih, C, H3, G("bias_ih_l" + k), s1);
+  {
+    SlabJobs j;   // every split-K slab set -> its gradient segment, one launch
+    j.add(slab_fc_, C, (long)V * H, G("fc.weight"));
+    j.add(rs_fc_, C, V, G("fc.bias"));
+    for (int l = 0; l < L; ++l) {
+      const std::string k = std::to_string(l);
+      j.add(Ls_[l].slab_hh, C, (long)H3 * H, G("weight_hh_l" + k));
+      j.add(Ls_[l].rs_hh, C, H3, G("bias_hh_l" + k));
+      if (l > 0) {
+        j.add(Ls_[l].slab_ih, C, (long)H3 * in_dim(l), G("weight_ih_l" + k));
+        j.add(Ls_[l].rs_ih, C, H3, G("bias_ih_l" + k));
+      }
     }
+    j.add(slab_P_, C, (long)V * H3, dP_);
+    reduce_slabs_multi(j, s1);
   }
-  reduce_slabs(slab_P_, C, (long)V * H3, dP_, s1);
-  cast_bf16(dP_, (long)V * H3, dP_bf_, s1);
-  transpose_bf16(dP_, V, H3, dPT_bf_, s1);
+  {
+    CastJobs j;
+    j.add(dP_, V, H3, dP_bf_, dPT_bf_);
+    cast_multi(j, s1);
+  }
   colsum(dP_, V, H3, G("bias_ih_l0"), s1);
   {
     GemmArgs g;   // dW_ih0 = dP^T · Emb
@@ -310,7 +316,8 @@ void Trainer::record_fb(hipStream_t s0) {
     e.M = V; e.N = E; e.K = H3;
     gemm_nt(e, s1);
   }
-  sum_partials(loss_part_, (int)((size_t)T * B / 32), loss_, s1);
+  // loss = Σ partials (fixed order); also advances the optimiser's device step counter
+  sum_partials(loss_part_, (int)((size_t)T * B / 32), loss_, s1, step_);
   edge(s1, s0);   // join
   HIP_LAUNCH_CHECK();
 }
@@ -320,7 +327,6 @@ void Trainer::record_opt(hipStream_t s) {
     sumsq_partials(grads_, nflat_, norm_parts_, 256, s);
     clip_scale_finalize(norm_parts_, 256, o_.clip, gscale_, s);
   }
-  bump_step(step_, s);
   OptimArgs a;
   a.p = params_; a.g = grads_; a.m = m_; a.v = v_; a.n = nflat_; a.step = step_;
   a.gscale = o_.clip > 0.f ? gscale_ : nullptr;

@@ -21,6 +21,7 @@ namespace gk {
 
 struct Dims {
   int V = 256, E = 512, H = 512, L = 1, B = 256, T = 32, chunks = 4;
+  int overlap = 1;   // side stream for chunk-consumers (0 = everything on one stream)
 };
 struct OptCfg {
   float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f, clip = 0.f;
@@ -69,6 +70,7 @@ class Trainer {
   size_t ev_next_ = 0;
   Graph g_fb_, g_opt_;
   bool use_graph_ = true;
+  bool overlap_ = true;
   int* h_stage_ = nullptr;      // pinned [T*Bp ids][T*Bp labels][1 float]
   hipEvent_t stage_done_ = nullptr;
 

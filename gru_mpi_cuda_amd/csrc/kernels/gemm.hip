@@ -17,13 +17,6 @@
 
 namespace gk {
 
-DEV float sum8(const bf16x8& v) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s += (float)v[i];
-  return s;
-}
-
 DEV int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
@@ -48,38 +41,45 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs a, int ntn, int n
   float rs[2] = {0.f, 0.f};
   const u16* B = a.B + (size_t)(n0 + lr) * a.ldb + kbeg + lk;
   if constexpr (ONEHOT) {
-    // A[m][k] = (ids[k] == m): 8 ids per lane per k-step, compare against the lane's two rows
+    // A[m][k] = (ids[k] == m): 8 ids per lane per k-step compared against the lane's two rows.
+    // ids and B fragments for k-step ks+1 are in flight while k-step ks computes.
     const int* ids = a.onehot_ids + kbeg + lk;
-    for (int ks = 0; ks < nks; ++ks) {
-      const int4 i0 = *reinterpret_cast<const int4*>(ids + ks * 32);
-      const int4 i1 = *reinterpret_cast<const int4*>(ids + ks * 32 + 4);
+    auto ldids = [&](int ks, int4& i0, int4& i1) {
+      i0 = *reinterpret_cast<const int4*>(ids + ks * 32);
+      i1 = *reinterpret_cast<const int4*>(ids + ks * 32 + 4);
+    };
+    auto ldb = [&](int ks, bf16x8 (&bf)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) bf[c] = ld8(B + (size_t)c * 16 * a.ldb + ks * 32);
+    };
+    auto step = [&](const int4& i0, const int4& i1, const bf16x8 (&bf)[2]) {
       const int idv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
-      bf16x8 af[2];
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         const int row = m0 + r * 16 + lr;
+        bf16x8 af;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) af[r][e] = (__bf16)(idv[e] == row ? 1.0f : 0.0f);
+        for (int e = 0; e < 8; ++e) af[e] = (__bf16)(idv[e] == row ? 1.0f : 0.0f);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) acc[r][c] = mfma16(af, bf[c], acc[r][c]);
       }
-      bf16x8 bf[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) bf[c] = ld8(B + (size_t)c * 16 * a.ldb + ks * 32);
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int c = 0; c < 2; ++c) acc[r][c] = mfma16(af[r], bf[c], acc[r][c]);
+    };
+    int4 x0, x1, y0, y1;
+    bf16x8 b0[2], b1[2];
+    ldids(0, x0, x1); ldb(0, b0);
+    int ks = 0;
+    for (; ks + 2 <= nks; ks += 2) {
+      ldids(ks + 1, y0, y1); ldb(ks + 1, b1);
+      step(x0, x1, b0);
+      if (ks + 2 < nks) { ldids(ks + 2, x0, x1); ldb(ks + 2, b0); }
+      step(y0, y1, b1);
     }
+    if (ks < nks) step(x0, x1, b0);
   } else {
     const u16* A = a.A + (size_t)(m0 + lr) * a.lda + kbeg + lk;
-    MmaLoop<2, 2, KB>::run(acc, A, a.lda, B, 16 * a.ldb, nks);
-    if constexpr (ROWSUM) {
-      // bias gradient = row sums of A; only the tn == 0 column of workgroups, wave column 0
-      if (tn == 0 && wn == 0) {
-        for (int ks = 0; ks < nks; ++ks)
-#pragma unroll
-          for (int r = 0; r < 2; ++r) rs[r] += sum8(ld8(A + (size_t)r * 16 * a.lda + ks * 32));
-      }
-    }
+    // bias gradient = row sums of A, from the fragments already loaded (tn == 0 tiles, wave column 0)
+    const bool do_rs = ROWSUM && tn == 0 && wn == 0;
+    MmaLoop<2, 2, KB>::run(acc, A, a.lda, B, 16 * a.ldb, nks, rs, do_rs);
   }
 
   // epilogue: lane (l&15) = column, rows (l>>4)*4 + i

@@ -20,6 +20,27 @@ static constexpr int TROWS = 32;   // batch rows per workgroup (2 MFMA row block
 static constexpr int TUNITS = 16;  // hidden units per workgroup (x3 gates)
 
 // LDS: partial tiles [KS][NT][4][64] fp32, then transposed staging.
+struct FwdEpi { float gi[3], bh[3], hp; };
+
+template <bool FUSE_IN>
+DEV void fwd_epi_load(const FwdStepArgs& a, int p, int b0, int j0, FwdEpi& e) {
+  const int H = a.H;
+  const int rb = p >> 8, reg = (p >> 6) & 3, ln = p & 63;
+  const int b = b0 + rb * 16 + (ln >> 4) * 4 + reg, j = j0 + (ln & 15);
+#pragma unroll
+  for (int g = 0; g < 3; ++g) e.bh[g] = a.bhh[g * H + j];
+  if constexpr (FUSE_IN) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) e.gi[g] = a.bih[g * H + j];
+  } else {
+    const float* src = a.ids ? a.P + (size_t)a.ids[b] * 3 * H : a.Gi + (size_t)b * 3 * H;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) e.gi[g] = src[g * H + j];
+  }
+  e.hp = a.hprev_f[(size_t)b * H + j];
+}
+
+// LDS: partial tiles [KS][NT][4][64] fp32, then transposed staging.
 template <int KB, bool FUSE_IN>
 __global__ void __launch_bounds__(512) gru_fwd_step_kernel(FwdStepArgs a, int nks_h, int nks_i) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -31,6 +52,11 @@ __global__ void __launch_bounds__(512) gru_fwd_step_kernel(FwdStepArgs a, int nk
   const int j0 = blockIdx.x * TUNITS;
   const int b0 = blockIdx.y * TROWS;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
+
+  // epilogue operands of this thread's first item are fetched before the MMA so their
+  // latency (a dependent ids -> P gather for layer 0) hides under the recurrent GEMM
+  FwdEpi pre;
+  fwd_epi_load<FUSE_IN>(a, threadIdx.x, b0, j0, pre);
 
   f32x4 acc[2][3];
   zero_acc(acc);
@@ -67,6 +93,8 @@ __global__ void __launch_bounds__(512) gru_fwd_step_kernel(FwdStepArgs a, int nk
   // epilogue: 512 (row, unit) pairs; item p = rb*256 + reg*64 + lane
   u16* stage = reinterpret_cast<u16*>(smem + (size_t)KS * NT * 256);   // [16 units][32 rows]
   for (int p = threadIdx.x; p < TROWS * TUNITS; p += blockDim.x) {
+    FwdEpi e;
+    if (p == (int)threadIdx.x) e = pre; else fwd_epi_load<FUSE_IN>(a, p, b0, j0, e);
     const int rb = p >> 8, reg = (p >> 6) & 3, ln = p & 63;
     const int row = rb * 16 + (ln >> 4) * 4 + reg;
     const int col = ln & 15;
@@ -79,20 +107,14 @@ __global__ void __launch_bounds__(512) gru_fwd_step_kernel(FwdStepArgs a, int nk
         s += smem[(size_t)ww * NT * 256 + ((rb * 3 + g) * 4 + reg) * 64 + ln];
         if constexpr (FUSE_IN) si += smem[(size_t)ww * NT * 256 + ((6 + rb * 3 + g) * 4 + reg) * 64 + ln];
       }
-      gh[g] = s + a.bhh[g * H + j];
-      if constexpr (FUSE_IN) gi[g] = si + a.bih[g * H + j];
-    }
-    if constexpr (!FUSE_IN) {
-      const float* src = a.ids ? a.P + (size_t)a.ids[b] * 3 * H : a.Gi + (size_t)b * 3 * H;
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+      gh[g] = s + e.bh[g];
+      gi[g] = FUSE_IN ? si + e.gi[g] : e.gi[g];
     }
     const float r = sigmoidf_(gi[0] + gh[0]);
     const float z = sigmoidf_(gi[1] + gh[1]);
     const float n = tanhf_(gi[2] + r * gh[2]);
     const size_t o = (size_t)b * H + j;
-    const float hp = a.hprev_f[o];
-    const float h = n + z * (hp - n);
+    const float h = n + z * (e.hp - n);
     a.h_f[o] = h;
     const u16 hb = f2bf(h);
     a.h_bf[o] = hb;
@@ -108,6 +130,17 @@ __global__ void __launch_bounds__(512) gru_fwd_step_kernel(FwdStepArgs a, int nk
   }
 }
 
+struct BwdEpi { float dy, carry, r, z, n, ghn, hp; };
+
+DEV void bwd_epi_load(const BwdStepArgs& a, int p, int b0, int j0, BwdEpi& e) {
+  const int rb = p >> 8, reg = (p >> 6) & 3, ln = p & 63;
+  const int b = b0 + rb * 16 + (ln >> 4) * 4 + reg, j = j0 + (ln & 15);
+  const size_t o = (size_t)b * a.H + j;
+  e.dy = a.dy[o];
+  e.carry = a.carry_in ? a.carry_in[o] : 0.f;
+  e.r = a.r[o]; e.z = a.z[o]; e.n = a.n[o]; e.ghn = a.ghn[o]; e.hp = a.hprev[o];
+}
+
 template <int KB>
 __global__ void __launch_bounds__(512) gru_bwd_step_kernel(BwdStepArgs a, int nks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -120,6 +153,8 @@ __global__ void __launch_bounds__(512) gru_bwd_step_kernel(BwdStepArgs a, int nk
   const int b0 = blockIdx.y * TROWS;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
 
+  BwdEpi pre;
+  bwd_epi_load(a, threadIdx.x, b0, j0, pre);
   if (a.dgh_next) {
     f32x4 acc[2][1];
     zero_acc(acc);
@@ -137,22 +172,24 @@ __global__ void __launch_bounds__(512) gru_bwd_step_kernel(BwdStepArgs a, int nk
   // staging for transposed stores: dGh [3][16][32] and dGi_n [16][32]
   u16* st = reinterpret_cast<u16*>(smem + (size_t)KS * NT * 256);
   for (int p = threadIdx.x; p < TROWS * TUNITS; p += blockDim.x) {
+    BwdEpi e;
+    if (p == (int)threadIdx.x) e = pre; else bwd_epi_load(a, p, b0, j0, e);
     const int rb = p >> 8, reg = (p >> 6) & 3, ln = p & 63;
     const int row = rb * 16 + (ln >> 4) * 4 + reg;
     const int col = ln & 15;
     const int b = b0 + row, j = j0 + col;
     const size_t o = (size_t)b * H + j;
-    float dh = a.dy[o];
+    float dh = e.dy;
     if (a.dgh_next) {
       float s = 0.f;
       for (int ww = 0; ww < KS; ++ww) s += smem[(size_t)ww * NT * 256 + (rb * 4 + reg) * 64 + ln];
-      dh += s + a.carry_in[o];
+      dh += s + e.carry;
     }
-    const float r = a.r[o], z = a.z[o], n = a.n[o], ghn = a.ghn[o], hp = a.hprev[o];
+    const float r = e.r, z = e.z, n = e.n;
     const float dn = dh * (1.f - z);
-    const float dz = dh * (hp - n);
+    const float dz = dh * (e.hp - n);
     const float dan = dn * (1.f - n * n);
-    const float dar = dan * ghn * r * (1.f - r);
+    const float dar = dan * e.ghn * r * (1.f - r);
     const float daz = dz * z * (1.f - z);
     a.carry_out[o] = z * dh;
     const u16 br = f2bf(dar), bz = f2bf(daz), bnh = f2bf(dan * r), bni = f2bf(dan);

@@ -118,8 +118,18 @@ void bump_step(int* step, hipStream_t s);
 // sum of squares of x[n] -> partials; finalize computes clip scale = min(1, clip/(sqrt(sum)+1e-6))
 void sumsq_partials(const float* x, long n, float* partials, int nparts, hipStream_t s);
 void clip_scale_finalize(const float* partials, int nparts, float clip, float* scale, hipStream_t s);
-// deterministic sum of partials -> out[0]
-void sum_partials(const float* partials, int n, float* out, hipStream_t s);
+// deterministic sum of partials -> out[0]; optionally also ++(*bump) (the optimiser step counter)
+void sum_partials(const float* partials, int n, float* out, hipStream_t s, int* bump = nullptr);
+
+// multi-tensor launches (one kernel for the whole list)
+struct SlabJob { const float* src; float* dst; long n; int splits; };
+struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0;
+  void add(const float* s, int splits, long n_, float* d) { job[n++] = SlabJob{s, d, n_, splits}; } };
+void reduce_slabs_multi(SlabJobs& j, hipStream_t s);
+struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; };
+struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
+  void add(const float* s, int R, int C, u16* d, u16* dT) { job[n++] = CastJob{s, d, dT, R, C}; } };
+void cast_multi(CastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
 
 }  // namespace gk

@@ -69,15 +69,88 @@ void transpose_bf16(const float* in, int R, int C, u16* outT, hipStream_t s) {
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, s, in, R, C, outT);
 }
 
+// [R][C] -> [C]: 64 columns x 4 row groups per block, independent loads, LDS combine (fixed order)
 __global__ void colsum_kernel(const float* __restrict__ in, int R, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   float s = 0.f;
-  for (int r = 0; r < R; ++r) s += in[(size_t)r * C + c];
-  out[c] = s;
+  if (c < C)
+    for (int r = g; r < R; r += 4) s += in[(size_t)r * C + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < C) out[c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, in, R, C, out);
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64), dim3(256), 0, s, in, R, C, out);
+}
+
+// ---------------------------------------------------------------- multi-tensor launches
+// One launch for many independent jobs (the tail of a training step is otherwise a chain of
+// tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
+// prefix sum over their block counts.
+__global__ void reduce_multi_kernel(SlabJobs j) {
+  int b = blockIdx.x, k = 0;
+  while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
+  const SlabJob& J = j.job[k];
+  const long n4 = J.n / 4;
+  const long nb = j.blk_start[k + 1] - j.blk_start[k];
+  for (long i = (b - j.blk_start[k]) * (long)blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(J.src)[i];
+    for (int s = 1; s < J.splits; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(J.src + (size_t)s * J.n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(J.dst)[i] = acc;
+  }
+  if (b == j.blk_start[k])
+    for (long i = n4 * 4 + threadIdx.x; i < J.n; i += blockDim.x) {
+      float acc = 0.f;
+      for (int s = 0; s < J.splits; ++s) acc += J.src[(size_t)s * J.n + i];
+      J.dst[i] = acc;
+    }
+}
+void reduce_slabs_multi(SlabJobs& j, hipStream_t s) {
+  int tot = 0;
+  for (int k = 0; k < j.n; ++k) {
+    j.blk_start[k] = tot;
+    long b = (j.job[k].n / 4 + 255) / 256;
+    tot += (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
+  }
+  j.blk_start[j.n] = tot;
+  hipLaunchKernelGGL(reduce_multi_kernel, dim3(tot), dim3(256), 0, s, j);
+}
+
+// fp32 [R][C] -> bf16 [R][C] and/or bf16 [C][R], 64x64 tiles through LDS, many tensors per launch
+__global__ void cast_multi_kernel(CastJobs j) {
+  __shared__ float tile[64][65];
+  int b = blockIdx.x, k = 0;
+  while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
+  const CastJob& J = j.job[k];
+  const int tiles_c = (J.C + 63) / 64;
+  const int t = b - j.blk_start[k];
+  const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int y = ty; y < 64; y += 4) {
+    const int r = r0 + y, c = c0 + tx;
+    const float v = (r < J.R && c < J.C) ? J.src[(size_t)r * J.C + c] : 0.f;
+    tile[y][tx] = v;
+    if (J.dst && r < J.R && c < J.C) J.dst[(size_t)r * J.C + c] = f2bf(v);
+  }
+  if (!J.dstT) return;
+  __syncthreads();
+  for (int y = ty; y < 64; y += 4) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < J.C && r < J.R) J.dstT[(size_t)c * J.R + r] = f2bf(tile[tx][y]);
+  }
+}
+void cast_multi(CastJobs& j, hipStream_t s) {
+  int tot = 0;
+  for (int k = 0; k < j.n; ++k) {
+    j.blk_start[k] = tot;
+    tot += ((j.job[k].R + 63) / 64) * ((j.job[k].C + 63) / 64);
+  }
+  j.blk_start[j.n] = tot;
+  hipLaunchKernelGGL(cast_multi_kernel, dim3(tot), dim3(256), 0, s, j);
 }
 
 __global__ void adam_kernel(OptimArgs a) {
@@ -153,15 +226,18 @@ void clip_scale_finalize(const float* partials, int nparts, float clip, float* s
   hipLaunchKernelGGL(clip_final_kernel, dim3(1), dim3(1), 0, s, partials, nparts, clip, scale);
 }
 
-__global__ void sum_partials_kernel(const float* p, int n, float* out) {
+__global__ void sum_partials_kernel(const float* p, int n, float* out, int* step) {
   // one wave, fixed order: deterministic
   float acc = 0.f;
   for (int i = threadIdx.x; i < n; i += 64) acc += p[i];
   acc = wave_sum(acc);
-  if (threadIdx.x == 0) out[0] = acc;
+  if (threadIdx.x == 0) {
+    out[0] = acc;
+    if (step) *step += 1;
+  }
 }
-void sum_partials(const float* partials, int n, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out);
+void sum_partials(const float* partials, int n, float* out, hipStream_t s, int* bump) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out, bump);
 }
 
 __global__ void fill_kernel(float* p, long n, float v) {

@@ -11,8 +11,17 @@
 
 namespace gk {
 
+DEV float sum8(const bf16x8& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += (float)v[i];
+  return s;
+}
+
 // A: pointer at (row0 + (lane&15)) * lda + k0 + 8*(lane>>4); row-block stride 16*lda.
 // B: pointer at (col0 + (lane&15)) * ldb + k0 + 8*(lane>>4); col-tile c starts at B + c*bts.
+// With `rs` non-null the row sums of A are accumulated from the fragments already in registers
+// (lane partials; reduce over lane>>4 afterwards) -- no second pass over A.
 template <int RB, int CT, int KB>
 struct MmaLoop {
   static DEV void load(bf16x8 (&a)[KB][RB], bf16x8 (&b)[KB][CT], const u16* A, int lda,
@@ -26,16 +35,24 @@ struct MmaLoop {
       for (int c = 0; c < CT; ++c) b[kk][c] = ld8(B + (size_t)c * bts + ko);
     }
   }
-  static DEV void mma(f32x4 (&acc)[RB][CT], const bf16x8 (&a)[KB][RB], const bf16x8 (&b)[KB][CT]) {
+  static DEV void mma(f32x4 (&acc)[RB][CT], const bf16x8 (&a)[KB][RB], const bf16x8 (&b)[KB][CT],
+                      float (&rs)[RB], bool do_rs) {
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk)
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int c = 0; c < CT; ++c) acc[r][c] = mfma16(a[kk][r], b[kk][c], acc[r][c]);
+    if (do_rs) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) rs[r] += sum8(a[kk][r]);
+    }
   }
   // nks must be a multiple of KB
-  static DEV void run(f32x4 (&acc)[RB][CT], const u16* A, int lda, const u16* B, int bts, int nks) {
+  static DEV void run(f32x4 (&acc)[RB][CT], const u16* A, int lda, const u16* B, int bts, int nks,
+                      float (&rs)[RB], bool do_rs) {
     const int nb = nks / KB;
     if (nb <= 0) return;
     bf16x8 a0[KB][RB], b0[KB][CT], a1[KB][RB], b1[KB][CT];
@@ -43,11 +60,15 @@ struct MmaLoop {
     int bt = 0;
     for (; bt + 2 <= nb; bt += 2) {
       load(a1, b1, A, lda, B, bts, (bt + 1) * KB);
-      mma(acc, a0, b0);
+      mma(acc, a0, b0, rs, do_rs);
       if (bt + 2 < nb) load(a0, b0, A, lda, B, bts, (bt + 2) * KB);
-      mma(acc, a1, b1);
+      mma(acc, a1, b1, rs, do_rs);
     }
-    if (bt < nb) mma(acc, a0, b0);
+    if (bt < nb) mma(acc, a0, b0, rs, do_rs);
+  }
+  static DEV void run(f32x4 (&acc)[RB][CT], const u16* A, int lda, const u16* B, int bts, int nks) {
+    float rs[RB];
+    run(acc, A, lda, B, bts, nks, rs, false);
   }
 };
 

@@ -50,7 +50,7 @@ class HipTrainer:
         self.buckets = _bucket_list(cfg, self.layout.total)
         offsets = {s.name: s.offset for s in self.layout.segments}
         dims = dict(V=cfg.vocab, E=cfg.embed, H=cfg.hidden, L=cfg.layers, B=self.local_batch,
-                    T=cfg.seq, chunks=cfg.time_chunks)
+                    T=cfg.seq, chunks=cfg.time_chunks, overlap=int(cfg.overlap))
         opt = dict(lr=cfg.lr, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps,
                    weight_decay=cfg.weight_decay, clip_norm=cfg.clip_norm,
                    sgd=int(cfg.optimizer == "sgd"))

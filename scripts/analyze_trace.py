@@ -1,0 +1,18 @@
+"""Summarise one training step from a rocprofv3 kernel trace: per-kernel time, gaps, span."""
+import csv, sys, collections
+path = sys.argv[1]
+rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+marks = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
+a, b = marks[-2], marks[-1]
+seg = rows[a + 1:b + 1]
+t0 = int(seg[0]["Start_Timestamp"]); t1 = int(seg[-1]["End_Timestamp"])
+agg = collections.defaultdict(lambda: [0, 0.0])
+busy = 0.0; last_end = t0
+for r in seg:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:60]
+    agg[k][0] += 1; agg[k][1] += (e - s) / 1e3
+    busy += max(0, e - max(s, last_end)) / 1e3; last_end = max(last_end, e)
+print(f"step span {(t1 - t0) / 1e3:.1f} us, kernels {len(seg)}, union-busy {busy:.1f} us")
+for k, (n, us) in sorted(agg.items(), key=lambda x: -x[1][1]):
+    print(f"  {k:60s} n={n:4d} total={us:8.1f} us avg={us / n:7.2f}")
