@@ -35,7 +35,8 @@ def main() -> int:
                     help="hip = this engine; torch = torch.nn.GRU (MIOpen) comparator")
     ap.add_argument("--chunks", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--serial", action="store_true", help="single HIP stream (no side-stream overlap)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="chunked two-stream schedule instead of the persistent single-stream one")
     args = ap.parse_args()
 
     import torch
@@ -51,8 +52,8 @@ def main() -> int:
     cfg = base.replace(batch=per_gpu * world)
     if args.chunks:
         cfg = cfg.replace(time_chunks=args.chunks)
-    if args.serial:
-        cfg = cfg.replace(overlap=False)
+    if args.overlap:
+        cfg = cfg.replace(overlap=True)
 
     stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
     pool = [stream.next() for _ in range(8)]
@@ -66,8 +67,10 @@ def main() -> int:
             tr.t.set_use_graph(False)
         step = lambda i: tr.step(*pool[i % len(pool)])  # noqa: E731
         final_loss = lambda: tr.loss()                  # noqa: E731
+        plan = tr.t.plan() if hasattr(tr, "t") else "cpu"
     else:
         step, final_loss = _torch_gru_step(cfg, ctx, pool)
+        plan = "torch.nn.GRU (MIOpen)"
 
     def sync():
         if ctx.device.type == "cuda":
@@ -100,7 +103,7 @@ def main() -> int:
                        "global_batch": cfg.batch, "seq_len": cfg.seq,
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
-                       "overlap": cfg.overlap},
+                       "overlap": cfg.overlap, "plan": plan},
             "final_loss": round(float(loss), 4),
         }
         print(json.dumps(out), flush=True)

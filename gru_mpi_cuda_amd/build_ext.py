@@ -24,8 +24,9 @@ OBJ = os.path.join(HERE, "build", "obj")
 ARCH = os.environ.get("GK_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
-KERNELS = ["kernels/gru_step.hip", "kernels/fc.hip", "kernels/gemm.hip", "kernels/misc.hip"]
-ENGINE = ["engine/trainer.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp"]
+KERNELS = ["kernels/gru_step.hip", "kernels/gru_seq.hip", "kernels/fc.hip", "kernels/gemm.hip",
+           "kernels/misc.hip"]
+ENGINE = ["engine/trainer.cpp", "engine/trainer_seq.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp"]
 PYBIND = ["bindings.cpp"]
 CAPI = ["capi/namegen_api.cpp", "capi/ckpt_reader.cpp"]
 DRIVER = ["capi/namegen_main.cpp"]

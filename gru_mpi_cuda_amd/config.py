@@ -40,7 +40,8 @@ class GRUConfig:
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
-    overlap: bool = True        # run chunk consumers (FC, weight grads) on a side HIP stream
+    overlap: bool = False       # True: chunked side-stream schedule; False: single stream built on
+                                # the persistent sequence kernels (faster on MI355X, profiles/)
 
     def __post_init__(self):
         if self.layers < 1:

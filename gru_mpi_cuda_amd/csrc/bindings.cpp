@@ -70,6 +70,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_use_graph", &Trainer::set_use_graph)
       .def("padded_batch", &Trainer::padded_batch)
       .def("workspace_bytes", &Trainer::workspace_bytes)
+      .def("plan", &Trainer::plan)
+      .def("uses_persistent", &Trainer::uses_persistent)
+      .def("read_error", &Trainer::read_error)
       .def("buffer", &Trainer::buffer);
 
   py::class_<Generator>(m, "Generator")
@@ -129,6 +132,22 @@ PYBIND11_MODULE(_C, m) {
     a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (a.Bp % 32 || a.H % 64) throw std::runtime_error("bwd_step: Bp % 32 and H % 64 required");
     gru_bwd_step(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fwd_seq_supported", &gru_fwd_seq_supported);
+  m.def("bwd_seq_supported", &gru_bwd_seq_supported);
+  m.def("fwd_seq", [](py::dict d, uintptr_t s) {
+    SeqFwdArgs a;
+    a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+    a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
+    a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
+    a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
+    a.h0 = GP(const float, d, "h0");
+    a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
+    a.dbg = GP(unsigned long long, d, "dbg");
+    a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
+    gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
   m.def("fc_xent", [](py::dict d, uintptr_t s) {

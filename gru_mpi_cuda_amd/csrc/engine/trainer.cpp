@@ -48,7 +48,43 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     x.shh = R((size_t)C_ * 3 * H * H * 4); x.rhh = R((size_t)C_ * 3 * H * 4);
     x.sih = l > 0 ? R((size_t)C_ * 3 * H * K * 4) : 0; x.rih = l > 0 ? R((size_t)C_ * 3 * H * 4) : 0;
   }
+  // ---- persistent-sequence path (gru_seq.hip): decided per layer from the occupancy query
+  const int nrb = B / 32;
+  const char* pe = std::getenv("GK_PERSIST");
+  const bool allow = !(pe && pe[0] == '0');
+  persist_fwd_ = allow && gru_fwd_seq_supported(H, B);
+  seq_.resize(L);
+  bool any_bwd = false;
+  for (int l = 0; l < L; ++l) {
+    SeqPlan& q = seq_[l];
+    q.fuse_p = (l == 0) && V == 256 && allow && gru_bwd_seq_supported(H, B, H <= 512, true);
+    q.fuse_w = allow && H <= 512 && gru_bwd_seq_supported(H, B, true, q.fuse_p);
+    q.bwd = allow && gru_bwd_seq_supported(H, B, q.fuse_w, q.fuse_p);
+    if (!q.bwd) q.fuse_w = q.fuse_p = false;
+    any_bwd |= q.bwd;
+  }
+  splits_ = 8;
+  size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)2 * B * 3 * H * 2);
+  // split-K slab: large enough for every weight-gradient product it serves
+  const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
+  size_t o_sw = R((size_t)splits_ * wmax * 4);
+  size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
+  std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0);
+  for (int l = 0; l < L; ++l) {
+    if (seq_[l].fuse_w) o_pw[l] = R((size_t)nrb * 3 * H * H * 4);
+    if (seq_[l].bwd) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
+  }
+  size_t o_pP = seq_[0].fuse_p ? R((size_t)nrb * V * 3 * H * 4) : 0;
+  (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
+  cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
+  slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
+  for (int l = 0; l < L; ++l) {
+    seq_[l].dWhh_part = seq_[l].fuse_w ? arena_.get<float>(o_pw[l]) : nullptr;
+    seq_[l].dbhh_part = seq_[l].bwd ? arena_.get<float>(o_pbh[l]) : nullptr;
+    seq_[l].dbih_part = seq_[l].bwd ? arena_.get<float>(o_pbi[l]) : nullptr;
+  }
+  dP_part_ = seq_[0].fuse_p ? arena_.get<float>(o_pP) : nullptr;
 
   ids_ = arena_.get<int>(o_ids); labels_ = arena_.get<int>(o_lab); inv_count_ = arena_.get<float>(o_inv);
   Ptab_ = arena_.get<float>(o_P); loss_part_ = arena_.get<float>(o_lp); loss_ = arena_.get<float>(o_loss);
@@ -342,14 +378,14 @@ void Trainer::forward_backward(hipStream_t s) {
     hipEvent_t a = events_.back();
     HIP_CHECK(hipEventRecord(a, s));
     HIP_CHECK(hipStreamWaitEvent(s0_, a, 0));
-    record_fb(s0_);
+    if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     HIP_CHECK(hipEventRecord(a, s0_));
     HIP_CHECK(hipStreamWaitEvent(s, a, 0));
     return;
   }
   if (!g_fb_.ready()) {
     g_fb_.begin(s0_);
-    record_fb(s0_);
+    if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     g_fb_.end(s0_);
   }
   g_fb_.launch(s);
@@ -367,7 +403,9 @@ void Trainer::optimizer_step(hipStream_t s) {
 
 float Trainer::read_loss() {
   float v = 0.f;
-  HIP_CHECK(hipDeviceSynchronize());
+  if (read_error())
+    throw std::runtime_error("[rank " + std::to_string(global_rank()) +
+                             "] persistent sequence kernel hit its spin limit (workgroups not co-resident?)");
   HIP_CHECK(hipMemcpy(&v, loss_, 4, hipMemcpyDeviceToHost));
   return v;
 }

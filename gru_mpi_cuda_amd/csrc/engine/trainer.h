@@ -81,6 +81,25 @@ class Trainer {
     float *slab_hh, *rs_hh, *slab_ih, *rs_ih;
   };
   std::vector<Layer> Ls_;
+  // persistent-sequence path
+  struct SeqPlan {
+    bool bwd = false, fuse_w = false, fuse_p = false;
+    float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
+  };
+  void record_fb_seq(hipStream_t s0);
+  void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
+                  float* rowsum, hipStream_t s);
+  bool persist_fwd_ = false;
+  std::vector<SeqPlan> seq_;
+  int splits_ = 8;
+  unsigned *cnt_ = nullptr, *err_ = nullptr;
+  u16* xbuf_ = nullptr;
+  float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
+ public:
+  bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }
+  std::string plan() const;
+  unsigned read_error();
+ private:
   int *ids_, *labels_;
   float *inv_count_, *Ptab_, *loss_part_, *loss_, *slab_fc_, *rs_fc_, *slab_P_, *dP_;
   float *norm_parts_, *gscale_;

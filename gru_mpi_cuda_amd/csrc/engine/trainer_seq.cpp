@@ -1,0 +1,171 @@
+// Single-stream training step built around the persistent sequence kernels (gru_seq.hip):
+//
+//   P-table GEMM -> [per layer: Gi GEMM (l>0) -> forward sequence kernel]
+//   -> fused FC + softmax-xent over all B*T tokens -> dH GEMM -> dW_fc split-K GEMM
+//   -> [per layer, top-down: backward sequence kernel with fused dW_hh / dP / bias partials
+//       -> (l>0) dW_ih GEMM + dX GEMM]
+//   -> one multi-tensor reduction of all partial slabs -> dW_ih0 / dEmb GEMMs -> loss.
+//
+// Every layer falls back to the per-timestep kernels when its shape cannot be made
+// co-resident (gru_*_seq_supported), so any config still runs -- just slower.
+#include "trainer.h"
+
+namespace gk {
+
+void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
+                         float* rowsum_dst, hipStream_t s) {
+  // split-K into slab_w_ / rs_w_, then reduce straight into the gradient segment(s)
+  int sp = splits_;
+  while (sp > 1 && (K % sp || (K / sp) % 128)) sp >>= 1;
+  GemmArgs w;
+  w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb;
+  w.C = slab_w_; w.ldc = N; w.rowsumA = rowsum_dst ? rs_w_ : nullptr;
+  w.M = M; w.N = N; w.K = K; w.splits = sp;
+  gemm_nt(w, s);
+  SlabJobs j;
+  j.add(slab_w_, sp, (long)M * N, dst);
+  if (rowsum_dst) j.add(rs_w_, sp, M, rowsum_dst);
+  reduce_slabs_multi(j, s);
+}
+
+void Trainer::record_fb_seq(hipStream_t s) {
+  const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
+  const int H3 = 3 * H, nrb = B / 32;
+  const long tok = (long)T * B;
+  const long fw = seq_flag_words(H, B);
+  HIP_CHECK(hipMemsetAsync(cnt_, 0, (size_t)2 * L * fw * 4 + 64, s));   // re-initialise every call
+
+  {   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]
+    GemmArgs g;
+    g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
+    g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
+    gemm_nt(g, s);
+  }
+  // ------------------------------------------------------------------ forward
+  for (int l = 0; l < L; ++l) {
+    Layer& y = Ls_[l];
+    if (l > 0) {
+      GemmArgs g;   // hoisted input projection over all B*T tokens
+      g.A = Ls_[l - 1].HSb + (size_t)B * H; g.lda = H; g.B = y.Wih; g.ldb = H;
+      g.C = y.Gi; g.ldc = H3; g.bias = P("bias_ih_l" + std::to_string(l));
+      g.M = (int)tok; g.N = H3; g.K = H;
+      gemm_nt(g, s);
+    }
+    if (persist_fwd_) {
+      SeqFwdArgs a;
+      a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B;
+      a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+      a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
+      if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
+      a.cnt = cnt_ + (size_t)l * fw; a.err = err_;
+      a.T = T; a.Bp = B; a.H = H;
+      gru_fwd_seq(a, s);
+    } else {
+      for (int t = 0; t < T; ++t) fwd_step(l, t, s);
+    }
+  }
+  // ------------------------------------------------------------------ FC + loss + dH
+  Layer& top = Ls_[L - 1];
+  {
+    FcXentArgs f;
+    f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
+    f.labels = labels_; f.inv_count = inv_count_;
+    f.dl = dl_; f.dlT = dlT_; f.ldT = (int)tok; f.colT = 0;
+    f.loss_part = loss_part_; f.M = (int)tok; f.H = H; f.V = V;
+    fc_xent(f, s);
+    GemmArgs g;   // dy_top = dlogits · W_fc
+    g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
+    g.M = (int)tok; g.N = H; g.K = V;
+    gemm_nt(g, s);
+    // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T
+    wgrad_gemm(dlT_, (int)tok, top.HT + B, (T + 1) * B, V, H, (int)tok, G("fc.weight"), G("fc.bias"), s);
+  }
+  // ------------------------------------------------------------------ backward (BPTT)
+  for (int l = L - 1; l >= 0; --l) {
+    Layer& y = Ls_[l];
+    const SeqPlan& q = seq_[l];
+    const std::string k = std::to_string(l);
+    if (q.bwd) {
+      SeqBwdArgs a;
+      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+      a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.WhhT = y.WhhT; a.xbuf = xbuf_;
+      const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
+      a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;
+      a.dgi = y.dgi;
+      a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
+      if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
+      a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
+      a.T = T; a.Bp = B; a.H = H;
+      gru_bwd_seq(a, s);
+    } else {
+      for (int t = T - 1; t >= 0; --t) bwd_step(l, t, s);
+    }
+    // weight gradients not accumulated inside the sequence kernel
+    SlabJobs j;
+    if (q.fuse_w) j.add(q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
+    if (q.bwd) j.add(q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
+    if (l == 0 && q.fuse_p) j.add(dP_part_, nrb, (long)V * H3, dP_);
+    if (l == 0 && q.bwd) j.add(q.dbih_part, nrb, H3, G("bias_ih_l0"));
+    if (j.n) reduce_slabs_multi(j, s);
+    if (!q.fuse_w)
+      wgrad_gemm(y.dghT, (int)tok, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
+                 q.bwd ? nullptr : G("bias_hh_l" + k), s);
+    if (l == 0) {
+      if (!q.fuse_p) {
+        GemmArgs p;   // dP = onehot(x)^T · dGi, split-K then reduce
+        int sp = splits_;
+        while (sp > 1 && (tok % sp || (tok / sp) % 128)) sp >>= 1;
+        p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)tok;
+        p.C = slab_w_; p.ldc = H3; p.M = V; p.N = H3; p.K = (int)tok; p.splits = sp;
+        gemm_nt(p, s);
+        reduce_slabs(slab_w_, sp, (long)V * H3, dP_, s);
+        if (!q.bwd) colsum(dP_, V, H3, G("bias_ih_l0"), s);
+      }
+    } else {
+      const int K = in_dim(l);
+      // dW_ih = dGi^T · h_below, db_ih = row sums of dGi^T
+      wgrad_gemm(y.dgiT, (int)tok, Ls_[l - 1].HT + B, (T + 1) * B, H3, K, (int)tok, G("weight_ih_l" + k),
+                 G("bias_ih_l" + k), s);
+      GemmArgs dx;  // dy of the layer below = dGi · W_ih
+      dx.A = y.dgi; dx.lda = H3; dx.B = y.WihT; dx.ldb = H3;
+      dx.C = Ls_[l - 1].dy; dx.ldc = H; dx.M = (int)tok; dx.N = H; dx.K = H3;
+      gemm_nt(dx, s);
+    }
+  }
+  // ------------------------------------------------------------------ embedding-side gradients
+  {
+    CastJobs j;
+    j.add(dP_, V, H3, dP_bf_, dPT_bf_);
+    cast_multi(j, s);
+    GemmArgs g;   // dW_ih0 = dP^T · Emb
+    g.A = dPT_bf_; g.lda = V; g.B = EmbT; g.ldb = V; g.C = G("weight_ih_l0"); g.ldc = E;
+    g.M = H3; g.N = E; g.K = V;
+    gemm_nt(g, s);
+    GemmArgs e;   // dEmb = dP · W_ih0
+    e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = G("embedding"); e.ldc = E;
+    e.M = V; e.N = E; e.K = H3;
+    gemm_nt(e, s);
+  }
+  sum_partials(loss_part_, (int)(tok / 32), loss_, s, step_);
+  HIP_LAUNCH_CHECK();
+}
+
+std::string Trainer::plan() const {
+  std::string p = std::string("fwd=") + (persist_fwd_ ? "persistent" : "per-step");
+  for (size_t l = 0; l < seq_.size(); ++l) {
+    p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
+    if (seq_[l].fuse_w) p += "+dWhh";
+    if (seq_[l].fuse_p) p += "+dP";
+  }
+  p += overlap_ ? " overlap(chunks=" + std::to_string(C_) + ")" : " serial";
+  return p;
+}
+
+unsigned Trainer::read_error() {
+  unsigned e = 0;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(&e, err_, 4, hipMemcpyDeviceToHost));
+  return e;
+}
+
+}  // namespace gk

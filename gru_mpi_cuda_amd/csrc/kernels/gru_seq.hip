@@ -1,0 +1,427 @@
+// Persistent (whole-sequence) GRU recurrence kernels for gfx950: ONE launch runs all T
+// timesteps of one layer, forward or backward.
+//
+// Why: at the headline shape (B = 256 per GPU, H = 512) one timestep's recurrent GEMM is
+// 0.4 GFLOP -- a few hundred ns of MFMA work spread over 256 CUs -- so a per-step launch is
+// dominated by the launch/drain floor (profiles/: ~1.6 us graph node + ~1 us store drain +
+// ~1 us of load latency).  Here:
+//   * grid = (H/16 unit tiles) x (Bp/32 row blocks), one 512-thread workgroup per CU, all
+//     co-resident (checked on the host against the occupancy query);
+//   * each wave keeps its K-slice of the recurrent weights in VGPRs for the whole sequence
+//     (W_hh never re-read from memory);
+//   * step t+1 of row block rb needs h_t of those 32 rows from all H/16 unit-tile workgroups:
+//     the 1 KB tile each workgroup produces is stored write-through (sc1) by one wave, that
+//     wave drains (s_waitcnt vmcnt(0)) and bumps the row block's counter (agent-scope atomic);
+//     consumers poll the counter with sc1 loads and read the tiles with sc1 buffer loads
+//     (cdna_hip_programming.md §6 Guideline 16, MI355X_MICROARCH.md 'Valid forms' row 1).
+//     Every spin is bounded: on timeout an error word is set and the kernel runs to completion.
+//   * backward additionally accumulates the weight gradients dW_hh = Σ_t dGh_t^T h_{t-1} and
+//     the embedding-side dP = Σ_t onehot(x_t)^T dGi_t (layer 0) plus both bias gradients in
+//     registers, using the MFMA pipe that the latency-bound recurrence leaves idle; partial
+//     sums per row block are reduced by one small kernel afterwards (no float atomics).
+// Reference mapping: this is the whole per-char hot loop of /root/reference/namegensf.cu:661-872
+// (for all names at once), plus the BPTT half the reference does not have.
+#include "kernels.h"
+#include "mma_tile.h"
+
+namespace gk {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+DEV rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+DEV bf16x8 ld8_sc1(rsrc_t r, unsigned off) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);   // aux 16 = sc1
+  return __builtin_bit_cast(bf16x8, v);
+}
+DEV void st16_sc1(rsrc_t r, unsigned off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16); }
+
+static constexpr unsigned kSpinLimit = 1u << 21;   // x s_sleep(2): ~0.3 s, >> any real wait
+
+// Per-producer epoch flags: producer p of a row block owns flags[p * kFlagStride] (its own 64-B
+// line, no read-modify-write contention); after its payload drained it stores the epoch with a
+// relaxed agent-scope (sc1) store.  The consumer's wave 0 sweeps all producers' flags -- lane p
+// reads flag p with an sc1 load -- until every one has reached the epoch (wave vote), then the
+// workgroup barrier releases the other waves.  A single shared counter instead measured ~6.7 us
+// per hop (32 atomic adders + 256 pollers on one line; scripts/probe_seq.py).
+static constexpr int kFlagStride = 16;   // uints (64 B)
+
+DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* err) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    for (;;) {
+      bool ok = true;
+      if (lane < nprod) ok = __hip_atomic_load(flags + lane * kFlagStride, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+DEV void signal_flag(unsigned* flag, unsigned epoch) {
+  __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Diagnostic phase stamps (100 MHz wall clock) for the first and last workgroup, thread 0 only.
+// Only written when the caller passes a dbg buffer; nothing reads them inside the kernel.
+DEV void stamp(unsigned long long* dbg, int t, int k) {
+  if (!dbg || threadIdx.x != 0) return;
+  const bool first = blockIdx.x == 0 && blockIdx.y == 0;
+  const bool last = blockIdx.x == gridDim.x - 1 && blockIdx.y == gridDim.y - 1;
+  if (!first && !last) return;
+  const unsigned long long v = __builtin_amdgcn_s_memrealtime();
+  dbg[((last ? 1 : 0) * 4096 + t) * 8 + k] = v;
+}
+
+// ==================================================================== forward
+template <int NKW>
+__global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[8][6][256];
+  __shared__ __attribute__((aligned(16))) u16 stg[32][16];
+  __shared__ __attribute__((aligned(16))) u16 stgT[16][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = a.H, Bp = a.Bp, T = a.T;
+  const int j0 = blockIdx.x * 16, rbk = blockIdx.y, b0 = rbk * 32;
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const int k0 = w * NKW * 32;
+  const unsigned nunit = (unsigned)(H / 16);
+
+  bf16x8 bw[NKW][3];   // this wave's K-slice of W_h{r,z,n} for the 16 units, resident all sequence
+#pragma unroll
+  for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
+
+  // this thread's epilogue item (row, unit) -- one per thread with 512 threads
+  const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
+  const int row = rb * 16 + (ln >> 4) * 4 + reg, col = ln & 15;
+  const int b = b0 + row, j = j0 + col;
+  float bh[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + j];
+  float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
+  const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+
+  for (int t = 0; t < T; ++t) {
+    stamp(a.dbg, t, 0);
+    float gi[3];
+    {
+      const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H
+                               : a.Gi + ((size_t)t * Bp + b) * 3 * H;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    }
+    f32x4 acc[2][3];
+    zero_acc(acc);
+    if (t > 0 || a.h0) {
+      if (t > 0) wait_flags(a.cnt + (size_t)rbk * nunit * kFlagStride, (int)nunit, (unsigned)t, a.err);
+      stamp(a.dbg, t, 1);
+      bf16x8 af[NKW][2];
+      const unsigned base = (unsigned)((((size_t)t * Bp + b0 + lr) * H + k0 + lk) * 2);
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rH, base + (unsigned)(r * 16 * H * 2 + kk * 64));
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc[r][g] = mfma16(af[kk][r], bw[kk][g], acc[r][g]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[w][r * 3 + g][i * 64 + lane] = acc[r][g][i];
+    __syncthreads();
+    stamp(a.dbg, t, 2);
+    float gh[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) s += part[ww][rb * 3 + g][reg * 64 + ln];
+      gh[g] = s + bh[g];
+    }
+    const float r = sigmoidf_(gi[0] + gh[0]);
+    const float z = sigmoidf_(gi[1] + gh[1]);
+    const float n = tanhf_(gi[2] + r * gh[2]);
+    const float h = n + z * (hp - n);
+    hp = h;
+    a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
+    if (a.sr) {
+      const size_t so = ((size_t)t * Bp + b) * H + j;
+      a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = gh[2];
+    }
+    const u16 hb = f2bf(h);
+    stg[row][col] = hb;
+    stgT[col][row] = hb;
+    __syncthreads();
+    stamp(a.dbg, t, 3);
+    if (w == 0) {
+      // publish: the 32x16 bf16 tile, 16 B per lane, write-through; drain; one signal
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
+      const unsigned off = (unsigned)((((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) * 2);
+      st16_sc1(rH, off, v);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + blockIdx.x) * kFlagStride, (unsigned)(t + 1));
+      stamp(a.dbg, t, 4);
+    } else if (w == 1 && a.HT) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane >> 2][(lane & 3) * 8]);
+      *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
+    }
+  }
+}
+
+// ==================================================================== backward
+// NKW3: k-steps per wave of the dh GEMM (K = 3H split over 8 waves)
+// NTW : 16-col tiles per wave of the fused dW_hh accumulator (H / 128); 0 = not fused
+// NTP : 16-col tiles per wave of the fused dP accumulator (V / 128); 0 = not fused
+template <int NKW3, int NTW, int NTP>
+__global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float part[8][2][256];      // 16 KB
+  __shared__ __attribute__((aligned(16))) u16 srow[32][48];           // dGh tile, row-major (exchange)
+  __shared__ __attribute__((aligned(16))) u16 sgT[4][16][40];         // dGh^T gates r,z,n + dGi_n^T (padded rows)
+  __shared__ __attribute__((aligned(16))) float red[6][16][33];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = a.H, H3 = 3 * a.H, Bp = a.Bp, T = a.T;
+  const int j0 = blockIdx.x * 16, rbk = blockIdx.y, b0 = rbk * 32;
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const int k0 = w * NKW3 * 32;
+  const unsigned nunit = (unsigned)(H / 16);
+
+  bf16x8 bw[NKW3];    // this wave's K-slice of W_hh^T rows j0..j0+15 (dh = dGh · W_hh)
+#pragma unroll
+  for (int kk = 0; kk < NKW3; ++kk) bw[kk] = ld8(a.WhhT + (size_t)(j0 + lr) * H3 + k0 + kk * 32 + lk);
+
+  const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
+  const int row = rb * 16 + (ln >> 4) * 4 + reg, col = ln & 15;
+  const int b = b0 + row, j = j0 + col;
+  float carry = 0.f;
+  float dbh[3] = {0.f, 0.f, 0.f}, dbi = 0.f;   // dbi: only the n gate differs from dbh
+  f32x4 accW[3][NTW > 0 ? NTW : 1];
+  f32x4 accP[3][NTP > 0 ? NTP : 1];
+  zero_acc(accW);
+  zero_acc(accP);
+  const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)2 * Bp * H3 * 2));
+
+  for (int t = T - 1; t >= 0; --t) {
+    const int s = T - 1 - t;
+    const size_t o = ((size_t)t * Bp + b) * H + j;
+    const float dy = a.dy[o], sr = a.sr[o], sz = a.sz[o], sn = a.sn[o], sghn = a.sghn[o];
+    const float hprev = a.HSf[o];   // HS[t] = h_{t-1}
+    // operands of the fused weight-gradient MFMAs (independent of other workgroups)
+    bf16x8 hB[NTW > 0 ? NTW : 1];
+    if constexpr (NTW > 0) {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
+    }
+    int idv[8];
+    if constexpr (NTP > 0) {
+      const int4 i0 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk);
+      const int4 i1 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk + 4);
+      idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
+      idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
+    }
+    f32x4 acc[2];
+    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = acc[0];
+    if (s > 0) {
+      wait_flags(a.cnt + (size_t)rbk * nunit * kFlagStride, (int)nunit, (unsigned)s, a.err);
+      bf16x8 af[NKW3][2];
+      const unsigned base = (unsigned)((((size_t)((t + 1) & 1) * Bp + b0 + lr) * H3 + k0 + lk) * 2);
+#pragma unroll
+      for (int kk = 0; kk < NKW3; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, base + (unsigned)(r * 16 * H3 * 2 + kk * 64));
+#pragma unroll
+      for (int kk = 0; kk < NKW3; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[r] = mfma16(af[kk][r], bw[kk], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[w][r][i * 64 + lane] = acc[r][i];
+    __syncthreads();
+    float dh = dy + carry;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) dh += part[ww][rb][reg * 64 + ln];
+    const float dn = dh * (1.f - sz);
+    const float dz = dh * (hprev - sn);
+    const float dan = dn * (1.f - sn * sn);
+    const float dar = dan * sghn * sr * (1.f - sr);
+    const float daz = dz * sz * (1.f - sz);
+    const float dhn = dan * sr;
+    carry = sz * dh;
+    dbh[0] += dar; dbh[1] += daz; dbh[2] += dhn; dbi += dan;
+    const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dhn), bi = f2bf(dan);
+    srow[row][col] = br; srow[row][16 + col] = bz; srow[row][32 + col] = bn;
+    sgT[0][col][row] = br; sgT[1][col][row] = bz; sgT[2][col][row] = bn; sgT[3][col][row] = bi;
+    if (a.dgi) {
+      const size_t og = ((size_t)t * Bp + b) * H3 + j;
+      a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
+    }
+    __syncthreads();
+    if (w == 0) {
+      // publish dGh_t rows b0..b0+31, cols {g*H + j0 .. +15}: 3 x 16 B per lane, write-through
+      const int rr = lane >> 1, hf = lane & 1;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[rr][g * 16 + hf * 8]);
+        const unsigned off = (unsigned)((((size_t)(t & 1) * Bp + b0 + rr) * H3 + g * H + j0 + hf * 8) * 2);
+        st16_sc1(rX, off, v);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + blockIdx.x) * kFlagStride, (unsigned)(s + 1));
+    } else if (w <= 4 && a.dghT) {
+      // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate
+      const int g = w - 1;          // 0..3 : dGh r, z, n and dGi n
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&sgT[g][lane >> 2][(lane & 3) * 8]);
+      const size_t c0 = (size_t)t * Bp + b0 + (lane & 3) * 8;
+      const int gg = g < 3 ? g : 2;
+      const size_t rowsel = (size_t)(gg * H + j0 + (lane >> 2)) * a.ldG + c0;
+      if (g < 3) *reinterpret_cast<u32x4*>(a.dghT + rowsel) = v;
+      if (g != 2) *reinterpret_cast<u32x4*>(a.dgiT + rowsel) = v;
+    }
+    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS)
+    if constexpr (NTW > 0 || NTP > 0) {
+      bf16x8 ga[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) ga[g] = *reinterpret_cast<const bf16x8*>(&sgT[g][lr][lk]);
+      if constexpr (NTW > 0) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+          for (int nt = 0; nt < NTW; ++nt) accW[g][nt] = mfma16(ga[g], hB[nt], accW[g][nt]);
+      }
+      if constexpr (NTP > 0) {
+        ga[2] = *reinterpret_cast<const bf16x8*>(&sgT[3][lr][lk]);   // dGi: n gate without r
+#pragma unroll
+        for (int nt = 0; nt < NTP; ++nt) {
+          const int v = (w * NTP + nt) * 16 + lr;
+          bf16x8 oh;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) oh[e] = (__bf16)(idv[e] == v ? 1.0f : 0.0f);
+#pragma unroll
+          for (int g = 0; g < 3; ++g) accP[g][nt] = mfma16(ga[g], oh, accP[g][nt]);
+        }
+      }
+    }
+  }
+
+  // ---- partial weight gradients of this row block
+  if constexpr (NTW > 0) {
+    float* W = a.dWhh_part + (size_t)rbk * H3 * H;
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          W[(size_t)(g * H + j0 + (lane >> 4) * 4 + i) * H + (w * NTW + nt) * 16 + lr] = accW[g][nt][i];
+  }
+  if constexpr (NTP > 0) {
+    float* Pp = a.dP_part + (size_t)rbk * a.V * H3;
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int nt = 0; nt < NTP; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          Pp[(size_t)((w * NTP + nt) * 16 + lr) * H3 + g * H + j0 + (lane >> 4) * 4 + i] = accP[g][nt][i];
+  }
+  // ---- bias gradients: reduce the per-thread sums over the 32 rows of the block
+  red[0][col][row] = dbh[0]; red[1][col][row] = dbh[1]; red[2][col][row] = dbh[2];
+  red[3][col][row] = dbh[0]; red[4][col][row] = dbh[1]; red[5][col][row] = dbi;
+  __syncthreads();
+  if (tid < 96) {
+    const int k = tid >> 4, c = tid & 15;
+    float sum = 0.f;
+    for (int rr = 0; rr < 32; ++rr) sum += red[k][c][rr];
+    float* dst = (k < 3 ? a.dbhh_part : a.dbih_part);
+    if (dst) dst[(size_t)rbk * H3 + (k % 3) * H + j0 + c] = sum;
+  }
+}
+
+// ==================================================================== host side
+template <class K>
+static int resident_blocks(K kernel) {
+  int dev = 0, ncu = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 512, 0) != hipSuccess) return 0;
+  return ncu * per;
+}
+
+static bool fwd_kernel_for(int H, const void** k) {
+  switch (H) {
+    case 256: *k = (const void*)gru_fwd_seq_kernel<1>; return true;
+    case 512: *k = (const void*)gru_fwd_seq_kernel<2>; return true;
+    case 1024: *k = (const void*)gru_fwd_seq_kernel<4>; return true;
+    default: return false;
+  }
+}
+
+bool gru_fwd_seq_supported(int H, int Bp) {
+  const void* k;
+  if (!fwd_kernel_for(H, &k) || Bp % 32) return false;
+  int cap = 0;
+  switch (H) {
+    case 256: cap = resident_blocks(gru_fwd_seq_kernel<1>); break;
+    case 512: cap = resident_blocks(gru_fwd_seq_kernel<2>); break;
+    default: cap = resident_blocks(gru_fwd_seq_kernel<4>); break;
+  }
+  return (H / 16) * (Bp / 32) <= cap;
+}
+
+void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
+  dim3 grid(a.H / 16, a.Bp / 32), block(512);
+  switch (a.H) {
+    case 256: hipLaunchKernelGGL(gru_fwd_seq_kernel<1>, grid, block, 0, s, a); break;
+    case 512: hipLaunchKernelGGL(gru_fwd_seq_kernel<2>, grid, block, 0, s, a); break;
+    case 1024: hipLaunchKernelGGL(gru_fwd_seq_kernel<4>, grid, block, 0, s, a); break;
+    default: break;
+  }
+}
+
+// fused-variant table: (H, fuse dW_hh, fuse dP) -> kernel
+#define BWD_VARIANTS(X)               \
+  X(256, 3, 2, 2) X(256, 3, 2, 0) X(256, 3, 0, 0) \
+  X(512, 6, 4, 2) X(512, 6, 4, 0) X(512, 6, 0, 0) \
+  X(1024, 12, 0, 0)
+
+bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
+  if (Bp % 32) return false;
+  int cap = -1;
+#define X(HH, NK, NW, NP)                                                                      \
+  if (H == HH && (NW > 0) == fuse_w && (NP > 0) == fuse_p) cap = resident_blocks(gru_bwd_seq_kernel<NK, NW, NP>);
+  BWD_VARIANTS(X)
+#undef X
+  return cap >= (H / 16) * (Bp / 32);
+}
+
+void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
+  dim3 grid(a.H / 16, a.Bp / 32), block(512);
+  const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
+#define X(HH, NK, NW, NP)                                                        \
+  if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                          \
+    hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP>), grid, block, 0, s, a); \
+    return;                                                                      \
+  }
+  BWD_VARIANTS(X)
+#undef X
+}
+
+}  // namespace gk

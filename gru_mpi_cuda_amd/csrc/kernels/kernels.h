@@ -53,6 +53,50 @@ struct BwdStepArgs {
 };
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
 
+// ------------------------------------------------------------------ persistent sequence kernels
+// One launch per layer runs all T steps (gru_seq.hip).  Requires 512-thread co-residency of
+// (H/16) x (Bp/32) workgroups; callers check *_supported() and fall back to per-step kernels.
+struct SeqFwdArgs {
+  u16* HSb = nullptr;              // [T+1][Bp][H] bf16; HS[0] = h_init, step t writes HS[t+1]
+  float* HSf = nullptr;            // [T+1][Bp][H] fp32
+  u16* HT = nullptr; int ldT = 0;  // [H][ldT] bf16, h_t at column (t+1)*Bp + b (nullable)
+  float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
+  const u16* Whh = nullptr; const float* bhh = nullptr;
+  const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
+  const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
+  const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
+  unsigned* cnt = nullptr;         // [Bp/32] zeroed before launch
+  unsigned* err = nullptr;
+  unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
+  int T = 0, Bp = 0, H = 0;
+};
+// flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
+inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 16; }
+bool gru_fwd_seq_supported(int H, int Bp);
+void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
+
+struct SeqBwdArgs {
+  const float* dy = nullptr;       // [T][Bp][H]
+  const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
+  const float* HSf = nullptr;      // [T+1][Bp][H]
+  const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
+  const u16* WhhT = nullptr;       // [H][3H]
+  u16* xbuf = nullptr;             // [2][Bp][3H] dGh exchange buffer
+  u16* dghT = nullptr; u16* dgiT = nullptr; int ldG = 0;   // [3H][ldG] transposed copies (nullable)
+  u16* dgi = nullptr;              // [T][Bp][3H] row-major dGi (nullable)
+  float* dWhh_part = nullptr;      // [Bp/32][3H][H] fused dW_hh partials (nullable = not fused)
+  float* dbhh_part = nullptr;      // [Bp/32][3H]
+  float* dbih_part = nullptr;      // [Bp/32][3H]
+  const int* ids = nullptr;        // [T][Bp] (fused dP)
+  float* dP_part = nullptr; int V = 0;   // [Bp/32][V][3H] (nullable = not fused)
+  unsigned* cnt = nullptr;
+  unsigned* err = nullptr;
+  unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
+  int T = 0, Bp = 0, H = 0;
+};
+bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
+void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s);
+
 // ------------------------------------------------------------------ FC + softmax
 struct FcXentArgs {
   const u16* X = nullptr;          // [M][H] top-layer hidden states (bf16)

@@ -22,16 +22,34 @@ def rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("layers,chunks,B", [(1, 2, 64), (2, 4, 96), (1, 1, 40)])
-def test_trainer_grads_match_cpu(layers, chunks, B):
+SCHEDULES = {
+    # name: (GK_PERSIST env, overlap)
+    "persistent": ("1", False),
+    "perstep": ("0", False),
+    "overlap": ("1", True),
+}
+
+
+@pytest.mark.parametrize("sched", sorted(SCHEDULES))
+@pytest.mark.parametrize("layers,H,E,chunks,B", [(1, 128, 128, 2, 64), (2, 128, 128, 4, 96), (1, 128, 128, 1, 40),
+                                                 (1, 512, 512, 2, 64), (2, 256, 128, 2, 64), (1, 256, 256, 4, 256)])
+def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    cfg = GRUConfig(vocab=256, embed=128, hidden=128, layers=layers, batch=B, seq=8, time_chunks=chunks, seed=7)
+    env, overlap = SCHEDULES[sched]
+    monkeypatch.setenv("GK_PERSIST", env)
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=8, time_chunks=chunks, seed=7,
+                    overlap=overlap)
     params = init_params(cfg)
     if B == 40:    # padded batch with ignore labels
         x, y = make_padded_batch(synthetic_names(B, seed=3, max_len=10), cfg.seq)
     else:
         x, y = NameStream(B, cfg.seq, seed=3).next()
     tr = HipTrainer(cfg, params=params)
+    plan = tr.t.plan()
+    if sched == "persistent" and H >= 256:
+        assert "fwd=persistent" in plan and "bwd0=persistent" in plan, plan
+    if sched == "perstep":
+        assert "persistent" not in plan, plan
     tr.forward_backward(x, y)
     loss = tr.loss()
     g = tr.grad_dict()
@@ -40,7 +58,7 @@ def test_trainer_grads_match_cpu(layers, chunks, B):
     assert abs(loss - float(ref_loss)) < 1e-2 * float(ref_loss)
     for k in ref_g:
         e = rel(g[k], ref_g[k])
-        assert e < 0.04, f"{k}: rel err {e:.4f}"
+        assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
 
 
 def test_trainer_adam_step_and_learning():
