@@ -62,6 +62,13 @@ PYBIND11_MODULE(_C, m) {
           throw std::runtime_error("set_batch: x and y must both be [B, T]");
         t.set_batch(x.data(), y.data(), (int)x.shape(0), S(s));
       })
+      .def("set_batch_device", [](Trainer& t, uintptr_t x, uintptr_t y, int B, uintptr_t s) {
+        t.set_batch_device(Pp<const int>(x), Pp<const int>(y), B, S(s));
+      })
+      .def("set_comm", [](Trainer& t, RcclComm* c, std::vector<std::pair<long, long>> buckets) {
+        t.set_comm(c, buckets);
+      }, py::keep_alive<1, 2>())
+      .def("step", [](Trainer& t, uintptr_t s) { t.step(S(s)); })
       .def("forward_backward", [](Trainer& t, uintptr_t s) { t.forward_backward(S(s)); })
       .def("optimizer_step", [](Trainer& t, uintptr_t s) { t.optimizer_step(S(s)); })
       .def("read_loss", &Trainer::read_loss)
@@ -148,6 +155,24 @@ PYBIND11_MODULE(_C, m) {
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("bwd_seq", [](py::dict d, uintptr_t s) {
+    SeqBwdArgs a;
+    a.dy = GP(const float, d, "dy");
+    a.sr = GP(const float, d, "sr"); a.sz = GP(const float, d, "sz"); a.sn = GP(const float, d, "sn");
+    a.sghn = GP(const float, d, "sghn"); a.HSf = GP(const float, d, "HSf");
+    a.HT = GP(const u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0); a.WhhT = GP(const u16, d, "WhhT");
+    a.xbuf = GP(u16, d, "xbuf"); a.dghT = GP(u16, d, "dghT"); a.dgiT = GP(u16, d, "dgiT");
+    a.ldG = get<int>(d, "ldG", 0); a.dgi = GP(u16, d, "dgi");
+    a.dWhh_part = GP(float, d, "dWhh_part"); a.dbhh_part = GP(float, d, "dbhh_part");
+    a.dbih_part = GP(float, d, "dbih_part"); a.ids = GP(const int, d, "ids");
+    a.dP_part = GP(float, d, "dP_part"); a.V = get<int>(d, "V", 0);
+    a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
+    a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    if (!gru_bwd_seq_supported(a.H, a.Bp, a.dWhh_part != nullptr, a.dP_part != nullptr))
+      throw std::runtime_error("bwd_seq: shape not supported");
+    gru_bwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
   m.def("fc_xent", [](py::dict d, uintptr_t s) {

@@ -64,7 +64,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     any_bwd |= q.bwd;
   }
   splits_ = 8;
-  size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)2 * B * 3 * H * 2);
+  size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
   // split-K slab: large enough for every weight-gradient product it serves
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
@@ -115,19 +115,23 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   HIP_CHECK(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
   events_.resize(64 + 8 * C_ * L);
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  HIP_CHECK(hipHostMalloc(&h_stage_, (2 * tok + 4) * sizeof(int)));
-  HIP_CHECK(hipEventCreateWithFlags(&stage_done_, hipEventDisableTiming));
-  HIP_CHECK(hipEventRecord(stage_done_, s0_));
+  HIP_CHECK(hipHostMalloc(&h_stage_, 2 * (2 * tok + 16) * sizeof(int)));
+  std::memset(h_stage_, 0, 2 * (2 * tok + 16) * sizeof(int));
+  for (auto& e : stage_done_) {
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(e, s0_));
+  }
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
   overlap_ = d_.overlap != 0;
 }
 
 Trainer::~Trainer() {
-  g_fb_.reset();
+  for (auto& g : g_fb_) g.reset();
+  for (auto& g : g_step_) g.reset();
   g_opt_.reset();
   for (auto& e : events_) (void)hipEventDestroy(e);
-  if (stage_done_) (void)hipEventDestroy(stage_done_);
+  for (auto& e : stage_done_) if (e) (void)hipEventDestroy(e);
   if (h_stage_) (void)hipHostFree(h_stage_);
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
@@ -140,7 +144,8 @@ hipEvent_t Trainer::ev() {
 
 void Trainer::set_lr(float lr) {
   o_.lr = lr;
-  g_opt_.reset();   // lr is a kernel argument frozen into the captured graph
+  g_opt_.reset();   // lr is a kernel argument frozen into the captured graphs
+  for (auto& g : g_step_) g.reset();
 }
 
 void Trainer::refresh_weights(hipStream_t s) {
@@ -160,27 +165,38 @@ void Trainer::refresh_weights(hipStream_t s) {
 
 void Trainer::set_batch(const int* x, const int* y, int B, hipStream_t s) {
   if (B > Bp_ || B <= 0) throw std::runtime_error("set_batch: batch larger than the trainer was built for");
+  (void)s;
+  // Batch-major ids/labels are written into a pinned staging slot; the step graph captured
+  // against that slot reads it zero-copy in its first kernel (prep_batch: transpose + pad), so
+  // there is no SDMA copy and no per-element host transpose.  The slot is reused only after
+  // the graph that last read it has completed (stage_done_, recorded after each launch).
+  const int slot = (stage_slot_ ^= 1);
+  HIP_CHECK(hipEventSynchronize(stage_done_[slot]));
+  fill_slot(slot, x, y, B);
+}
+
+void Trainer::fill_slot(int slot, const int* x, const int* y, int B) {
   const int T = d_.T;
-  HIP_CHECK(hipEventSynchronize(stage_done_));       // previous upload finished with the staging buffer
-  int* ids = h_stage_;
-  int* lab = h_stage_ + (size_t)T * Bp_;
+  const size_t n = (size_t)Bp_ * T;
+  int* h = h_stage_ + (size_t)slot * slot_ints();
   long valid = 0;
-  for (int t = 0; t < T; ++t) {
-    for (int b = 0; b < B; ++b) {
-      ids[(size_t)t * Bp_ + b] = x[(size_t)b * T + t];
-      const int yy = y[(size_t)b * T + t];
-      lab[(size_t)t * Bp_ + b] = yy;
-      valid += yy >= 0;
-    }
-    for (int b = B; b < Bp_; ++b) { ids[(size_t)t * Bp_ + b] = 0; lab[(size_t)t * Bp_ + b] = -1; }
-  }
-  float inv = 1.0f / (float)std::max(1L, valid);
-  std::memcpy(h_stage_ + 2 * (size_t)T * Bp_, &inv, 4);
-  // ids_, labels_, inv_count_ are consecutive 256-B aligned arena regions: copy the pieces
-  HIP_CHECK(hipMemcpyAsync(ids_, ids, (size_t)T * Bp_ * 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(labels_, lab, (size_t)T * Bp_ * 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipMemcpyAsync(inv_count_, h_stage_ + 2 * (size_t)T * Bp_, 4, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipEventRecord(stage_done_, s));
+  for (size_t i = 0; i < (size_t)B * T; ++i) valid += y[i] >= 0;
+  const float inv = 1.0f / (float)std::max(1L, valid);
+  h[0] = B;
+  std::memcpy(h + 1, &inv, 4);
+  std::memcpy(h + 16, x, (size_t)B * T * 4);
+  std::memcpy(h + 16 + n, y, (size_t)B * T * 4);
+}
+
+void Trainer::set_batch_device(const int* x, const int* y, int B, hipStream_t s) {
+  // device-resident batch: bring it through host memory once (not a hot path)
+  if (B > Bp_ || B <= 0) throw std::runtime_error("set_batch_device: bad batch size");
+  const size_t cnt = (size_t)B * d_.T;
+  std::vector<int> hx(cnt), hy(cnt);
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipMemcpy(hx.data(), x, cnt * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(hy.data(), y, cnt * 4, hipMemcpyDeviceToHost));
+  set_batch(hx.data(), hy.data(), B, s);
 }
 
 void Trainer::fwd_step(int l, int t, hipStream_t s) {
@@ -234,6 +250,7 @@ void Trainer::record_fb(hipStream_t s0) {
     HIP_CHECK(hipEventRecord(e, from));
     HIP_CHECK(hipStreamWaitEvent(to, e, 0));
   };
+  prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s0);
   edge(s0, s1);   // fork
 
   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]  (exact: Emb[x]·W^T)
@@ -373,6 +390,8 @@ void Trainer::record_opt(hipStream_t s) {
 }
 
 void Trainer::forward_backward(hipStream_t s) {
+  const int slot = stage_slot_;
+  stage_src_ = h_stage_ + (size_t)slot * slot_ints();
   if (!use_graph_) {
     // eager: run on the internal streams, ordered after / before the caller's stream
     hipEvent_t a = events_.back();
@@ -381,14 +400,15 @@ void Trainer::forward_backward(hipStream_t s) {
     if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     HIP_CHECK(hipEventRecord(a, s0_));
     HIP_CHECK(hipStreamWaitEvent(s, a, 0));
-    return;
+  } else {
+    if (!g_fb_[slot].ready()) {
+      g_fb_[slot].begin(s0_);
+      if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+      g_fb_[slot].end(s0_);
+    }
+    g_fb_[slot].launch(s);
   }
-  if (!g_fb_.ready()) {
-    g_fb_.begin(s0_);
-    if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
-    g_fb_.end(s0_);
-  }
-  g_fb_.launch(s);
+  HIP_CHECK(hipEventRecord(stage_done_[slot], s));
 }
 
 void Trainer::optimizer_step(hipStream_t s) {
@@ -399,6 +419,49 @@ void Trainer::optimizer_step(hipStream_t s) {
     g_opt_.end(s0_);
   }
   g_opt_.launch(s);
+}
+
+void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets) {
+  comm_ = c;
+  buckets_ = buckets;
+  g_step_[0].reset();
+  g_step_[1].reset();
+}
+
+void Trainer::record_allreduce(hipStream_t s) {
+  // bucketed mean all-reduce of the flat fp32 gradient over xGMI (RCCL).  Buckets follow the
+  // gradient-readiness order of the flat layout (FC, top layer ... layer 0, embedding).
+  if (!comm_) return;
+  for (const auto& b : buckets_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
+}
+
+void Trainer::step(hipStream_t s) {
+  if (!use_graph_) {
+    forward_backward(s);
+    record_allreduce(s);
+    optimizer_step(s);
+    return;
+  }
+  const int slot = stage_slot_;
+  stage_src_ = h_stage_ + (size_t)slot * slot_ints();
+  Graph& g = g_step_[slot];
+  if (!g.ready()) {
+    g.begin(s0_);
+    try {
+      if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+      record_allreduce(s0_);
+      record_opt(s0_);
+    } catch (...) {
+      hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow
+      (void)hipStreamEndCapture(s0_, &broken);
+      if (broken) (void)hipGraphDestroy(broken);
+      (void)hipGetLastError();
+      throw;
+    }
+    g.end(s0_);
+  }
+  g.launch(s);
+  HIP_CHECK(hipEventRecord(stage_done_[slot], s));
 }
 
 float Trainer::read_loss() {

@@ -16,6 +16,7 @@
 #include <vector>
 #include "../runtime/runtime.h"
 #include "../kernels/kernels.h"
+#include "../comm/rccl_comm.h"
 
 namespace gk {
 
@@ -68,11 +69,27 @@ class Trainer {
   hipStream_t s0_ = nullptr, s1_ = nullptr;
   std::vector<hipEvent_t> events_;
   size_t ev_next_ = 0;
-  Graph g_fb_, g_opt_;
+  Graph g_fb_[2], g_opt_;          // one forward/backward graph per staging slot
   bool use_graph_ = true;
   bool overlap_ = true;
-  int* h_stage_ = nullptr;      // pinned [T*Bp ids][T*Bp labels][1 float]
-  hipEvent_t stage_done_ = nullptr;
+  // pinned host staging, 2 slots of [16 hdr][Bp*T x][Bp*T y] (batch-major); the step graph's
+  // first kernel reads its slot zero-copy.  Graph k is captured against slot k.
+  int* h_stage_ = nullptr;
+  hipEvent_t stage_done_[2] = {nullptr, nullptr};
+  int stage_slot_ = 0;
+  const int* stage_src_ = nullptr;   // slot the graph being recorded reads
+  size_t slot_ints() const { return 16 + 2 * (size_t)Bp_ * d_.T; }
+  void fill_slot(int slot, const int* x, const int* y, int B);
+  // single-graph step (prep + fwd/bwd + in-graph RCCL all-reduce + optimiser)
+  Graph g_step_[2];
+  RcclComm* comm_ = nullptr;
+  std::vector<std::pair<long, long>> buckets_;
+  void record_allreduce(hipStream_t s);
+ public:
+  void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
+  void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets);
+  void step(hipStream_t s);      // whole training step as one graph replay
+ private:
 
   struct Layer {
     float *HSf, *sr, *sz, *sn, *sghn, *dy, *Gi, *carry[2];

@@ -33,7 +33,11 @@ void Trainer::record_fb_seq(hipStream_t s) {
   const int H3 = 3 * H, nrb = B / 32;
   const long tok = (long)T * B;
   const long fw = seq_flag_words(H, B);
-  HIP_CHECK(hipMemsetAsync(cnt_, 0, (size_t)2 * L * fw * 4 + 64, s));   // re-initialise every call
+  // Flag blocks: forward(l) at cnt_ + l*fw, backward(l) at cnt_ + (L+l)*fw.  Each persistent
+  // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
+  // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
+  // is zeroed by a memset instead.  The arena starts zeroed for the first step.
+  prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
 
   {   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]
     GemmArgs g;
@@ -58,7 +62,9 @@ void Trainer::record_fb_seq(hipStream_t s) {
       a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
       if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
       a.cnt = cnt_ + (size_t)l * fw; a.err = err_;
+      if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
+      if (!seq_[l].bwd) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
       gru_fwd_seq(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
@@ -95,7 +101,9 @@ void Trainer::record_fb_seq(hipStream_t s) {
       a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
+      if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
+      if (!persist_fwd_) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
       gru_bwd_seq(a, s);
     } else {
       for (int t = T - 1; t >= 0; --t) bwd_step(l, t, s);

@@ -66,8 +66,37 @@ DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* 
   }
   __syncthreads();
 }
+// Wave-level variant: a wave's K-slice of the recurrent GEMM only reads the columns produced by
+// a few unit-tile workgroups, so each wave waits for exactly those (lane p polls producer
+// prod_p) and proceeds on its own -- no workgroup barrier, no coupling to the slowest of all
+// H/16 producers.  The acquire-at-wavefront fence only pins the following sc1 loads below
+// the poll (no instruction is emitted).
+DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch, unsigned* err) {
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+    if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSpinLimit) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 DEV void signal_flag(unsigned* flag, unsigned epoch) {
   __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Zero the flag block of the sequence kernel that runs NEXT on the stream (it cannot start
+// before this launch completes, so plain stores + the kernel boundary order it) -- replaces a
+// memset graph node per step.
+DEV void zero_next_flags(unsigned* p, long n) {
+  if (!p) return;
+  const long wg = (long)blockIdx.y * gridDim.x + blockIdx.x, nwg = (long)gridDim.x * gridDim.y;
+  for (long i = wg * blockDim.x + threadIdx.x; i < n; i += nwg * blockDim.x) p[i] = 0u;
 }
 
 // Diagnostic phase stamps (100 MHz wall clock) for the first and last workgroup, thread 0 only.
@@ -109,6 +138,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + j];
   float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
   const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+  zero_next_flags(a.zero_next, a.zero_words);
 
   for (int t = 0; t < T; ++t) {
     stamp(a.dbg, t, 0);
@@ -122,7 +152,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     f32x4 acc[2][3];
     zero_acc(acc);
     if (t > 0 || a.h0) {
-      if (t > 0) wait_flags(a.cnt + (size_t)rbk * nunit * kFlagStride, (int)nunit, (unsigned)t, a.err);
+      // wave w's K-slice [k0, k0 + 32*NKW) is produced by unit tiles k0/16 .. k0/16 + 2*NKW - 1
+      if (t > 0) wave_wait(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
+                           (unsigned)t, a.err);
       stamp(a.dbg, t, 1);
       bf16x8 af[NKW][2];
       const unsigned base = (unsigned)((((size_t)t * Bp + b0 + lr) * H + k0 + lk) * 2);
@@ -213,10 +245,12 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   f32x4 accP[3][NTP > 0 ? NTP : 1];
   zero_acc(accW);
   zero_acc(accP);
-  const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)2 * Bp * H3 * 2));
+  const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
+  zero_next_flags(a.zero_next, a.zero_words);
 
   for (int t = T - 1; t >= 0; --t) {
     const int s = T - 1 - t;
+    stamp(a.dbg, s, 0);
     const size_t o = ((size_t)t * Bp + b) * H + j;
     const float dy = a.dy[o], sr = a.sr[o], sz = a.sz[o], sn = a.sn[o], sghn = a.sghn[o];
     const float hprev = a.HSf[o];   // HS[t] = h_{t-1}
@@ -238,9 +272,12 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[1] = acc[0];
     if (s > 0) {
-      wait_flags(a.cnt + (size_t)rbk * nunit * kFlagStride, (int)nunit, (unsigned)s, a.err);
+      // wave w's columns [k0, k0 + 32*NKW3) of dGh (3 gates x H) come from unit tiles ((k0+16p) mod H)/16
+      wave_wait(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3, ((k0 + 16 * lane) % H) / 16,
+                (unsigned)s, a.err);
+      stamp(a.dbg, s, 1);
       bf16x8 af[NKW3][2];
-      const unsigned base = (unsigned)((((size_t)((t + 1) & 1) * Bp + b0 + lr) * H3 + k0 + lk) * 2);
+      const unsigned base = (unsigned)((((size_t)(t + 1) * Bp + b0 + lr) * H3 + k0 + lk) * 2);
 #pragma unroll
       for (int kk = 0; kk < NKW3; ++kk)
 #pragma unroll
@@ -255,6 +292,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) part[w][r][i * 64 + lane] = acc[r][i];
     __syncthreads();
+    stamp(a.dbg, s, 2);
     float dh = dy + carry;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) dh += part[ww][rb][reg * 64 + ln];
@@ -274,17 +312,19 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
     }
     __syncthreads();
+    stamp(a.dbg, s, 3);
     if (w == 0) {
       // publish dGh_t rows b0..b0+31, cols {g*H + j0 .. +15}: 3 x 16 B per lane, write-through
       const int rr = lane >> 1, hf = lane & 1;
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[rr][g * 16 + hf * 8]);
-        const unsigned off = (unsigned)((((size_t)(t & 1) * Bp + b0 + rr) * H3 + g * H + j0 + hf * 8) * 2);
+        const unsigned off = (unsigned)((((size_t)t * Bp + b0 + rr) * H3 + g * H + j0 + hf * 8) * 2);
         st16_sc1(rX, off, v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + blockIdx.x) * kFlagStride, (unsigned)(s + 1));
+      stamp(a.dbg, s, 4);
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate
       const int g = w - 1;          // 0..3 : dGh r, z, n and dGi n

@@ -65,7 +65,9 @@ struct SeqFwdArgs {
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
   const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
   const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
-  unsigned* cnt = nullptr;         // [Bp/32] zeroed before launch
+  unsigned* cnt = nullptr;         // [Bp/32][H/16][16] epoch flags, zero at launch
+  unsigned* zero_next = nullptr;   // flag block of the NEXT sequence kernel, zeroed here (nullable)
+  long zero_words = 0;
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int T = 0, Bp = 0, H = 0;
@@ -81,7 +83,7 @@ struct SeqBwdArgs {
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
   const u16* WhhT = nullptr;       // [H][3H]
-  u16* xbuf = nullptr;             // [2][Bp][3H] dGh exchange buffer
+  u16* xbuf = nullptr;             // [T][Bp][3H] dGh exchange buffer (one slot per step: no WAR reuse)
   u16* dghT = nullptr; u16* dgiT = nullptr; int ldG = 0;   // [3H][ldG] transposed copies (nullable)
   u16* dgi = nullptr;              // [T][Bp][3H] row-major dGi (nullable)
   float* dWhh_part = nullptr;      // [Bp/32][3H][H] fused dW_hh partials (nullable = not fused)
@@ -90,6 +92,8 @@ struct SeqBwdArgs {
   const int* ids = nullptr;        // [T][Bp] (fused dP)
   float* dP_part = nullptr; int V = 0;   // [Bp/32][V][3H] (nullable = not fused)
   unsigned* cnt = nullptr;
+  unsigned* zero_next = nullptr;   // as SeqFwdArgs
+  long zero_words = 0;
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int T = 0, Bp = 0, H = 0;
@@ -175,5 +179,10 @@ struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
   void add(const float* s, int R, int C, u16* d, u16* dT) { job[n++] = CastJob{s, d, dT, R, C}; } };
 void cast_multi(CastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
+
+// Batch preparation on device: in = [hdr 16 ints: B, float-bits of 1/#valid][x Bmax*T][y Bmax*T]
+// batch-major int32 (may be pinned host memory, read zero-copy); out ids/labels time-major [T][Bp]
+// (pad rows: id 0, label -1) and inv_count.
+void prep_batch(const int* in, int Bmax, int T, int Bp, int* ids, int* labels, float* inv_count, hipStream_t s);
 
 }  // namespace gk

@@ -240,6 +240,30 @@ void sum_partials(const float* partials, int n, float* out, hipStream_t s, int* 
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, s, partials, n, out, bump);
 }
 
+// Transpose [B][T] -> [T][Bp] with padding.  `in` may be pinned HOST memory: the kernel reads it
+// zero-copy over PCIe on the compute queue (no SDMA engine hand-off in front of the step graph).
+// Header: in[0] = B, in[1] = bits of 1/#valid labels (computed by the host).
+__global__ void prep_batch_kernel(const int* __restrict__ in, int Bmax, int T, int Bp, int* __restrict__ ids,
+                                  int* __restrict__ labels, float* __restrict__ inv_count) {
+  const int B = in[0];
+  const int* x = in + 16;
+  const int* y = x + (size_t)Bmax * T;
+  const int n = T * Bp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int b = i / T, t = i - b * T;          // read in batch-major order (coalesced)
+    int xi = 0, yi = -1;
+    if (b < B) { xi = x[i]; yi = y[i]; }
+    ids[(size_t)t * Bp + b] = xi;
+    labels[(size_t)t * Bp + b] = yi;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) inv_count[0] = __int_as_float(in[1]);
+}
+void prep_batch(const int* in, int Bmax, int T, int Bp, int* ids, int* labels, float* inv_count, hipStream_t s) {
+  const int n = T * Bp;
+  const int blocks = (n + 255) / 256 < 64 ? (n + 255) / 256 : 64;
+  hipLaunchKernelGGL(prep_batch_kernel, dim3(blocks), dim3(256), 0, s, in, Bmax, T, Bp, ids, labels, inv_count);
+}
+
 __global__ void fill_kernel(float* p, long n, float v) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
 }

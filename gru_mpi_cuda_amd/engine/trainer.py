@@ -59,7 +59,10 @@ class HipTrainer:
         self.t.set_use_graph(use_graph)
         if self.comm is not None:     # identical replicas: rank 0's weights everywhere
             self.comm.broadcast_f32(self.params.data_ptr(), self.layout.total, 0, self._stream())
+            # bucketed all-reduce recorded INTO the step graph (RCCL ops on a captured stream)
+            self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets])
         self.t.refresh_weights(self._stream())
+        self._one_graph = True
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
@@ -81,9 +84,25 @@ class HipTrainer:
         self.t.optimizer_step(self._stream())
 
     def step(self, x: np.ndarray, y: np.ndarray) -> None:
-        self.forward_backward(x, y)
+        """Whole step = one hipGraph replay: batch prep, forward, softmax-xent, BPTT, weight
+        gradients, bucketed RCCL all-reduce (if data-parallel) and Adam + bf16 weight refresh."""
+        s = self._stream()
+        self.t.set_batch(x, y, s)
+        if self._one_graph:
+            try:
+                self.t.step(s)
+                return
+            except RuntimeError as e:   # e.g. RCCL refusing stream capture: fall back, loudly
+                if self.comm is None:
+                    raise
+                import sys
+                print(f"[gru_mpi_cuda_amd] in-graph all-reduce unavailable ({e}); "
+                      "falling back to per-phase launches", file=sys.stderr)
+                self._one_graph = False
+                self.t.set_comm(None, [])
+        self.t.forward_backward(s)
         self.allreduce_grads()
-        self.optimizer_step()
+        self.t.optimizer_step(s)
 
     def loss(self) -> float:
         return self.t.read_loss()

@@ -11,6 +11,7 @@ step() {  # name, timeout, cmd...
   if [ $rc -gt 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
+python -m gru_mpi_cuda_amd.build_ext > gpurun_out/build.log 2>&1 || { echo "BUILD FAILED"; tail -20 gpurun_out/build.log; exit 3; }
 step kernels 500 python -m pytest tests/test_kernels_gpu.py -x -q
 step engine 500 python -m pytest tests/test_engine_gpu.py -x -q
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"

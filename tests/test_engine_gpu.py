@@ -109,3 +109,38 @@ def test_generator_matches_cpu():
     ref = cpu_ref.generate(pb, cfg, rf)
     same = (got == ref).all(1).mean()
     assert same >= 0.9, same
+
+
+def test_single_graph_step_with_rccl_world1():
+    """The whole step as one graph with a captured RCCL all-reduce (1-rank communicator):
+    must equal the no-comm step bit for bit (mean over one rank is the identity)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=3)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
+    comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1)
+    a = HipTrainer(cfg, params=init_params(cfg), comm=comm)
+    b = HipTrainer(cfg, params=init_params(cfg))
+    for _ in range(3):
+        a.step(x, y)
+        b.step(x, y)
+    assert a._one_graph, "in-graph RCCL all-reduce fell back"
+    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+
+
+def test_set_batch_device_matches_host():
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=48, seq=8, seed=3)
+    x, y = make_padded_batch(synthetic_names(48, seed=2, max_len=10), cfg.seq)
+    a = HipTrainer(cfg, params=init_params(cfg))
+    a.forward_backward(x, y)
+    la, ga = a.loss(), a.grad_dict()
+    s = torch.cuda.current_stream().cuda_stream
+    xd, yd = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
+    a.t.set_batch_device(xd.data_ptr(), yd.data_ptr(), 48, s)
+    a.t.forward_backward(s)
+    assert a.loss() == la
+    gb = a.grad_dict()
+    for k in ga:
+        torch.testing.assert_close(ga[k], gb[k], atol=0, rtol=0)
