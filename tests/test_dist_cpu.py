@@ -1,0 +1,116 @@
+"""Multi-process (gloo, CPU) tests of the distributed layer (SURVEY §4.2 'Distributed w/o GPUs').
+
+(a) namegen over P ranks == namegen on 1 rank, including N % P != 0 (the reference drops
+    those names, namegensf.cu:628-630; here the remainder is spread over the first ranks);
+(b) data-parallel training of P ranks x B/P == 1 rank x B, step for step.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from gru_mpi_cuda_amd.config import GRUConfig
+from gru_mpi_cuda_amd.models.params import init_params
+from gru_mpi_cuda_amd.utils import ckpt
+from gru_mpi_cuda_amd.utils.data import NameStream, random_floats
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+
+
+def _namegen_worker(rank, world, port, path, N, outdir):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine import generator as G
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(max_len=9)
+    rf = random_floats(N, 9, seed=7)
+    G.namegen_initialize(N, 0, path, None, "gen", ctx=ctx)
+    out = np.zeros(N * 10, dtype=np.uint8)
+    G.namegen(N, rf, out)
+    G.namegen_finalize()
+    if rank == 0:
+        np.save(os.path.join(outdir, f"names_{world}.npy"), out)
+    gdist.shutdown()
+
+
+@pytest.mark.parametrize("world,N", [(2, 37), (3, 20)])
+def test_namegen_independent_of_world_size(tmp_path, world, N):
+    cfg = GRUConfig(vocab=64, embed=8, hidden=16, layers=2, max_len=9, eos=3)
+    path = str(tmp_path / "m.bin")
+    ckpt.save(path, cfg, init_params(cfg, seed=11))
+    ctx = mp.get_context("spawn")
+    for w in (1, world):
+        port = _free_port()
+        procs = [ctx.Process(target=_namegen_worker, args=(r, w, port, path, N, str(tmp_path))) for r in range(w)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+    a = np.load(tmp_path / "names_1.npy")
+    b = np.load(tmp_path / f"names_{world}.npy")
+    np.testing.assert_array_equal(a, b)
+    assert (a.reshape(N, 10)[:, 0] != 0).any()
+
+
+def _train_worker(rank, world, port, outdir, steps):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=16, hidden=16, layers=2, batch=8, seq=6, bucket_mb=0.001, lr=1e-2)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1) if rank == 0 else init_params(cfg, seed=99))
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    per = cfg.batch // world
+    for _ in range(steps):
+        x, y = ds.next()
+        tr.step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    if rank == 0:
+        torch.save({k: v for k, v in tr.state_dict().items()}, os.path.join(outdir, f"p_{world}.pt"))
+    gdist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_training_equals_single_rank(tmp_path, world):
+    ctx = mp.get_context("spawn")
+    for w in (1, world):
+        port = _free_port()
+        procs = [ctx.Process(target=_train_worker, args=(r, w, port, str(tmp_path), 3)) for r in range(w)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(180)
+            assert p.exitcode == 0
+    a = torch.load(tmp_path / "p_1.pt", weights_only=True)
+    b = torch.load(tmp_path / f"p_{world}.pt", weights_only=True)
+    # fp32 sums in a different order; Adam (lr 1e-2) normalises tiny gradients, so compare at
+    # 1 % of one update step
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], atol=1e-4, rtol=1e-4)
+
+
+def test_shard_and_buckets():
+    from gru_mpi_cuda_amd.parallel.dist import shard, bucket_bounds
+    for n in (0, 1, 7, 37, 64):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert sum(c for _, c in parts) == n
+            assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+    b = bucket_bounds(1000, 300, [0, 100, 350, 900])
+    assert b[0][0] == 0 and b[-1][1] == 1000
+    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
