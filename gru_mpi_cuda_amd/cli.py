@@ -1,0 +1,205 @@
+"""Command-line entry point.
+
+    python -m gru_mpi_cuda_amd.cli train    --preset h512 --steps 200 --ckpt out/model.bin
+    python -m gru_mpi_cuda_amd.cli generate --ckpt out/model.bin -n 20 --seed 1
+    python -m gru_mpi_cuda_amd.cli info
+    python -m gru_mpi_cuda_amd.cli bench    [bench.py args]
+
+Multi-GPU: launch with ``python -m torch.distributed.run --nproc-per-node N ...`` (one process
+per GPU; RANK / WORLD_SIZE / LOCAL_RANK from the launcher).  The reference's own driver
+(main.cpp, missing from the repo) called namegen_initialize / namegen /
+namegen_finalize -- ``generate`` does exactly that; the native equivalent without Python is
+``gru_mpi_cuda_amd/bin/namegen``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _add_model_args(ap: argparse.ArgumentParser) -> None:
+    for name, typ in (("vocab", int), ("embed", int), ("hidden", int), ("layers", int), ("batch", int),
+                      ("seq", int), ("lr", float), ("max_len", int), ("sos", int), ("eos", int),
+                      ("clip_norm", float), ("seed", int), ("bucket_mb", float), ("time_chunks", int)):
+        ap.add_argument("--" + name.replace("_", "-"), dest=name, type=typ, default=None)
+    ap.add_argument("--optimizer", choices=["adam", "sgd"], default=None)
+
+
+def _cfg_from(args):
+    from .config import preset
+    cfg = preset(args.preset)
+    over = {k: v for k, v in vars(args).items()
+            if k in cfg.__dataclass_fields__ and v is not None}
+    return cfg.replace(**over)
+
+
+def save_checkpoint(tr, path: str, fmt: str = "gen") -> None:
+    """Weights (reference or generalised layout) + Adam state + step counter (rank 0 writes)."""
+    import torch
+    from .models.params import from_flat
+    from .utils import ckpt
+    if getattr(tr, "ctx", None) is not None and not tr.ctx.is_main:
+        return
+    cfg = tr.cfg
+    params = tr.state_dict()
+    if hasattr(tr, "t"):                    # HipTrainer
+        m, v, step = tr.m.cpu(), tr.v.cpu(), tr.t.get_step()
+    else:
+        from .models.params import to_flat
+        m, v, step = to_flat(cfg, tr.opt.m), to_flat(cfg, tr.opt.v), tr.opt.step_n
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    ckpt.save(path, cfg, params, fmt=fmt,
+              opt_state={"m": m, "v": v, "step": torch.tensor([step], dtype=torch.int64)})
+
+
+def load_checkpoint(tr, path: str) -> int:
+    """Restore weights (+ optimiser state when present) into a trainer; returns the step."""
+    import torch
+    from .models.params import from_flat, to_flat
+    from .utils import ckpt
+    _, params = ckpt.load(path, tr.cfg)
+    st = ckpt.load_opt_state(path)
+    if hasattr(tr, "t"):
+        tr.load_state(params)
+        if st is not None:
+            tr.m.copy_(st["m"].to(tr.m.device))
+            tr.v.copy_(st["v"].to(tr.v.device))
+            tr.t.set_step(int(st["step"][0]))
+    else:
+        for k in tr.params:
+            tr.params[k].copy_(params[k])
+        if st is not None:
+            for k, x in from_flat(tr.cfg, st["m"]).items():
+                tr.opt.m[k].copy_(x)
+            for k, x in from_flat(tr.cfg, st["v"]).items():
+                tr.opt.v[k].copy_(x)
+            tr.opt.step_n = int(st["step"][0])
+    return int(st["step"][0]) if st is not None else 0
+
+
+def cmd_train(args) -> int:
+    import torch
+    from .parallel import dist as gdist
+    from .parallel.rccl import make_comm
+    from .engine.trainer import make_trainer
+    from .utils.data import NameStream
+    from .utils.metrics import MetricsWriter, StepTimer, log
+    ctx = gdist.init(use_gpu=torch.cuda.is_available() and not args.cpu, verbose=True)
+    cfg = _cfg_from(args)
+    comm = make_comm(ctx) if ctx.device.type == "cuda" else None
+    tr = make_trainer(cfg, ctx, comm=comm)
+    start = load_checkpoint(tr, args.resume) if args.resume else 0
+    if hasattr(tr, "t"):
+        log(f"plan: {tr.t.plan()}, workspace {tr.t.workspace_bytes() / 2**20:.1f} MiB")
+    data = NameStream(cfg.batch // ctx.world, cfg.seq, cfg.sos, cfg.eos, seed=cfg.seed * 1000 + ctx.rank + start,
+                      max_len=cfg.max_len)
+    mw = MetricsWriter(args.metrics)
+    timer = StepTimer()
+    for it in range(start, start + args.steps):
+        tr.step(*data.next())
+        timer.tick()
+        if (it + 1) % args.log_every == 0 or it + 1 == start + args.steps:
+            loss = tr.loss()                # synchronises
+            r = timer.rate()
+            tok_s = r["steps_per_s"] * cfg.batch * cfg.seq
+            log(f"step {it + 1} loss {loss:.4f} {tok_s / 1e6:.2f} M char-tokens/s")
+            mw.write(step=it + 1, loss=loss, tokens_per_s=tok_s, world=ctx.world)
+        if args.ckpt and args.save_every and (it + 1) % args.save_every == 0:
+            save_checkpoint(tr, args.ckpt, args.fmt)
+    if args.ckpt:
+        save_checkpoint(tr, args.ckpt, args.fmt)
+        log(f"saved {args.ckpt} ({args.fmt})")
+    mw.close()
+    gdist.shutdown()
+    return 0
+
+
+def cmd_generate(args) -> int:
+    from .engine import generator as G
+    from .utils.data import random_floats
+    from .utils import ckpt
+    fmt = args.fmt
+    if fmt == "auto":
+        fmt = "gen" if os.path.exists(args.ckpt + ".json") else "ref"
+    cfg = _cfg_from(args) if fmt == "ref" else None
+    N = args.n
+    ml = args.max_len if args.max_len is not None else (
+        cfg.max_len if fmt == "ref" else ckpt.load(args.ckpt, None, "gen")[0].max_len)
+    rf = random_floats(N, ml, seed=args.seed)
+    t0 = time.perf_counter()
+    G.namegen_initialize(N, args.seed, args.ckpt, cfg, fmt)
+    out = np.zeros(N * (ml + 1), dtype=np.uint8)
+    t1 = time.perf_counter()
+    G.namegen(N, rf, out)
+    t2 = time.perf_counter()
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:
+        # raw bytes of an untrained model can be control chars: escape them for text output
+        names = ["".join(c if c.isprintable() else f"\\x{ord(c):02x}" for c in nm)
+                 for nm in G.decode_names(out, N, ml)]
+        if args.raw_out:
+            out.tofile(args.raw_out)        # the reference's N x (MAX_LEN+1) byte layout
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write("\n".join(names) + "\n")
+        else:
+            print("\n".join(names))
+        print(json.dumps({"names": N, "init_s": round(t1 - t0, 4), "generate_s": round(t2 - t1, 4),
+                          "names_per_s": round(N / max(t2 - t1, 1e-9), 1)}), file=sys.stderr)
+    G.namegen_finalize()
+    return 0
+
+
+def cmd_info(args) -> int:
+    import torch
+    info = {"torch": torch.__version__, "hip": torch.version.hip, "gpu": torch.cuda.is_available()}
+    if torch.cuda.is_available():
+        from .ops import load_ext
+        info["device"] = load_ext().device_info()
+    print(json.dumps(info, indent=1))
+    return 0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="gru_mpi_cuda_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("train", help="train on synthetic names (one process per GPU)")
+    t.add_argument("--preset", default="h512")
+    t.add_argument("--steps", type=int, default=100)
+    t.add_argument("--log-every", type=int, default=10)
+    t.add_argument("--ckpt", default=None)
+    t.add_argument("--fmt", choices=["gen", "ref"], default="gen")
+    t.add_argument("--save-every", type=int, default=0)
+    t.add_argument("--resume", default=None)
+    t.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
+    t.add_argument("--cpu", action="store_true", help="force the CPU reference path")
+    _add_model_args(t)
+    g = sub.add_parser("generate", help="namegen_initialize / namegen / namegen_finalize")
+    g.add_argument("--ckpt", required=True)
+    g.add_argument("--fmt", choices=["auto", "gen", "ref"], default="auto")
+    g.add_argument("-n", type=int, default=10)
+    g.add_argument("--out", default=None, help="names, one per line (non-printables escaped)")
+    g.add_argument("--raw-out", default=None, help="raw N x (MAX_LEN+1) output bytes")
+    g.add_argument("--preset", default="ref", help="dims for --fmt ref (headerless blob)")
+    _add_model_args(g)
+    g.set_defaults(seed=0)
+    sub.add_parser("info", help="device / build info")
+    b = sub.add_parser("bench", help="run bench.py", add_help=False)
+    args, rest = ap.parse_known_args(argv)
+    if args.cmd == "bench":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        sys.argv = ["bench.py"] + rest
+        return bench.main()
+    if rest:
+        ap.error(f"unrecognized arguments: {rest}")
+    return {"train": cmd_train, "generate": cmd_generate, "info": cmd_info}[args.cmd](args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

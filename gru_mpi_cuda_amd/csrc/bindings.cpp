@@ -73,6 +73,8 @@ PYBIND11_MODULE(_C, m) {
       .def("optimizer_step", [](Trainer& t, uintptr_t s) { t.optimizer_step(S(s)); })
       .def("read_loss", &Trainer::read_loss)
       .def("read_grad_norm", &Trainer::read_grad_norm)
+      .def("get_step", &Trainer::get_step)
+      .def("set_step", &Trainer::set_step)
       .def("set_lr", &Trainer::set_lr)
       .def("set_use_graph", &Trainer::set_use_graph)
       .def("padded_batch", &Trainer::padded_batch)

@@ -473,6 +473,18 @@ float Trainer::read_loss() {
   return v;
 }
 
+int Trainer::get_step() {
+  int v = 0;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(&v, step_, 4, hipMemcpyDeviceToHost));
+  return v;
+}
+
+void Trainer::set_step(int v) {
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(step_, &v, 4, hipMemcpyHostToDevice));
+}
+
 float Trainer::read_grad_norm() {
   float v[2] = {0.f, 0.f};
   HIP_CHECK(hipDeviceSynchronize());

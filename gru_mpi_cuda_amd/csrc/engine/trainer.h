@@ -41,6 +41,8 @@ class Trainer {
   void optimizer_step(hipStream_t s);                   // clip + Adam/SGD + refresh (graph)
   float read_loss();                                    // blocking
   float read_grad_norm();                               // blocking (valid when clip > 0)
+  int get_step();                                       // optimiser step counter (device)
+  void set_step(int v);                                 // for resume
   void set_lr(float lr);
   void set_use_graph(bool g) { use_graph_ = g; }
   int padded_batch() const { return Bp_; }

@@ -1,0 +1,42 @@
+"""CLI end-to-end on the CPU reference path: train -> checkpoint -> resume -> generate."""
+import json
+import os
+
+import numpy as np
+import torch
+
+from gru_mpi_cuda_amd import cli
+from gru_mpi_cuda_amd.utils import ckpt
+
+
+def test_train_resume_generate(tmp_path, capsys):
+    m = str(tmp_path / "model.bin")
+    met = str(tmp_path / "metrics.jsonl")
+    assert cli.main(["train", "--cpu", "--preset", "cpu_tiny", "--steps", "6", "--log-every", "3",
+                     "--ckpt", m, "--metrics", met, "--lr", "0.01"]) == 0
+    recs = [json.loads(l) for l in open(met)]
+    assert [r["step"] for r in recs] == [3, 6]
+    st = ckpt.load_opt_state(m)
+    assert int(st["step"][0]) == 6
+    cfg, p1 = ckpt.load(m)
+    assert cli.main(["train", "--cpu", "--preset", "cpu_tiny", "--steps", "2", "--log-every", "2",
+                     "--ckpt", m, "--resume", m, "--lr", "0.01"]) == 0
+    assert int(ckpt.load_opt_state(m)["step"][0]) == 8
+    _, p2 = ckpt.load(m)
+    assert not torch.equal(p1["fc.weight"], p2["fc.weight"])
+    out = str(tmp_path / "names.txt")
+    assert cli.main(["generate", "--ckpt", m, "-n", "5", "--seed", "2", "--out", out]) == 0
+    names = open(out).read().splitlines()
+    assert len(names) == 5
+
+
+def test_generate_reference_format(tmp_path):
+    from gru_mpi_cuda_amd.config import GRUConfig
+    from gru_mpi_cuda_amd.models.params import init_params
+    cfg = GRUConfig(vocab=256, embed=16, hidden=8, layers=2)
+    m = str(tmp_path / "ref.bin")
+    ckpt.save(m, cfg, init_params(cfg), fmt="ref")
+    out = str(tmp_path / "n.txt")
+    assert cli.main(["generate", "--ckpt", m, "--fmt", "ref", "--embed", "16", "--hidden", "8",
+                     "--max-len", "6", "-n", "4", "--out", out]) == 0
+    assert len(open(out).read().splitlines()) == 4
