@@ -109,6 +109,7 @@ PYBIND11_MODULE(_C, m) {
     a.bias = GP(const float, d, "bias"); a.rowsumA = GP(float, d, "rowsumA");
     a.M = get<int>(d, "M", 0); a.N = get<int>(d, "N", 0); a.K = get<int>(d, "K", 0);
     a.splits = get<int>(d, "splits", 1); a.accumulate = get<int>(d, "accumulate", 0);
+    a.algo = get<int>(d, "algo", 0);
     if (a.M % 64 || a.N % 64 || (a.K / a.splits) % 32 || a.K % a.splits)
       throw std::runtime_error("gemm_nt: M, N must be multiples of 64 and K/splits a multiple of 32");
     gemm_nt(a, S(s));

@@ -12,10 +12,15 @@
 // Tile 64x64 per 4-wave workgroup (2x2 waves of 32x32 = 2x2 MFMA 16x16x32 tiles), operands
 // straight to VGPRs with a two-batch software pipeline (mma_tile.h), XCD-aware bijective
 // block remap so tiles sharing an operand panel share an L2 (cdna_hip_programming.md T1).
+#include <stdexcept>
 #include "kernels.h"
 #include "mma_tile.h"
 
 namespace gk {
+
+[[noreturn]] static void throw_gemm_shape() {
+  throw std::runtime_error("gemm_nt: LDS kernel requested for an unsupported shape/alignment");
+}
 
 DEV int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
@@ -112,6 +117,12 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs a, int ntn, int n
 }
 
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
+  // the LDS-staged kernel measured faster on every engine shape it supports (scripts/bench_gemm.py)
+  if (a.algo == 2 || (a.algo == 0 && gemm_lds_ok(a))) {
+    if (!gemm_lds_ok(a)) throw_gemm_shape();
+    gemm_lds(a, s);
+    return;
+  }
   const int ntn = a.N / 64, ntm = a.M / 64;
   const int kper = a.K / a.splits;
   const int nks = kper / 32;

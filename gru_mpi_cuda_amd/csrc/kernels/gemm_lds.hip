@@ -1,0 +1,126 @@
+// LDS-staged bf16 MFMA GEMM for the large products (weight gradients over B*T tokens, hoisted
+// input projections, dH at large H):  C[M][N] (+)= A[M][K] · B[N][K]^T, fp32 accumulate.
+//
+// gfx950 structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop", 2-buffer form):
+//   * 128 x 128 x 64 tiles, 256 threads = 2 x 2 waves, each wave 64 x 64 = 4 x 4 MFMA 16x16x32;
+//   * global -> LDS with global_load_lds_dwordx4 (16 B per lane, no VGPR round trip); one
+//     wave-instruction writes 1 KiB = 8 rows x 128 B of the tile, so the LDS image is lane-linear
+//     and the bank swizzle goes on the per-lane SOURCE address (rule 21);
+//   * swizzle: logical 16-B chunk c of row r lives in slot c ^ ((r >> 1) & 7).  For the
+//     ds_read_b128 fragment reads (16 rows x one chunk per lane quarter) every 16-lane group then
+//     touches 16 distinct 16-B bank slots -> conflict-free (derivation in docs/DESIGN.md);
+//   * double-buffered: tile k+1's LDS-DMA is in flight while tile k's 32 MFMAs run, one
+//     vmcnt(0) + barrier per tile;
+//   * XCD-aware bijective block remap (T1) so neighbouring tiles share an L2;
+//   * split-K slabs for the K = B*T weight-gradient products.
+#include "kernels.h"
+#include "common.h"
+
+namespace gk {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+DEV int xcd_remap2(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <bool BIAS>
+__global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
+  const int id = xcd_remap2(blockIdx.x, gridDim.x);
+  const int tn = id % ntn, tm = (id / ntn) % ntm, sp = id / (ntn * ntm);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int row0 = tm * 128, col0 = tn * 128;
+  const int kbeg = sp * kper, nk = kper / 64;
+
+  // staging geometry: wave w, instruction q covers tile rows (4w+q)*8 .. +7
+  const int srow = lane >> 3, sslot = lane & 7;
+  const u16* srcA[4];
+  const u16* srcB[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = (4 * w + q) * 8 + srow;
+    const int c = sslot ^ ((r >> 1) & 7);
+    srcA[q] = a.A + (size_t)(row0 + r) * a.lda + kbeg + c * 8;
+    srcB[q] = a.B + (size_t)(col0 + r) * a.ldb + kbeg + c * 8;
+  }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int base = (4 * w + q) * 8 * 64;
+      __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void*)(&lds[buf][0][base]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void*)(&lds[buf][1][base]), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + lq;
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int ra = wm * 64 + t * 16 + lr;
+        const int rb = wn * 64 + t * 16 + lr;
+        af[t] = *reinterpret_cast<const bf16x8*>(&lds[cur][0][ra * 64 + ((c ^ ((ra >> 1) & 7)) * 8)]);
+        bfr[t] = *reinterpret_cast<const bf16x8*>(&lds[cur][1][rb * 64 + ((c ^ ((rb >> 1) & 7)) * 8)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  float* C = a.C + (size_t)sp * a.M * a.ldc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + wn * 64 + j * 16 + lr;
+    const float bb = BIAS ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + wm * 64 + i * 16 + lq * 4 + e;
+        float* dst = C + (size_t)row * a.ldc + col;
+        const float v = acc[i][j][e] + bb;
+        if (a.accumulate) *dst += v; else *dst = v;
+      }
+  }
+}
+
+bool gemm_lds_ok(const GemmArgs& a) {
+  if (a.onehot_ids || a.rowsumA) return false;
+  if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;
+  const int kper = a.K / a.splits;
+  if (kper % 64 || kper < 128) return false;
+  // 16-B aligned rows for the LDS-DMA loads
+  if ((a.lda % 8) || (a.ldb % 8)) return false;
+  if ((reinterpret_cast<uintptr_t>(a.A) | reinterpret_cast<uintptr_t>(a.B)) & 15) return false;
+  return true;
+}
+
+void gemm_lds(const GemmArgs& a, hipStream_t s) {
+  const int ntn = a.N / 128, ntm = a.M / 128, kper = a.K / a.splits;
+  dim3 grid(ntn * ntm * a.splits), block(256);
+  if (a.bias && a.splits == 1) hipLaunchKernelGGL(gemm_lds_kernel<true>, grid, block, 0, s, a, ntn, ntm, kper);
+  else hipLaunchKernelGGL(gemm_lds_kernel<false>, grid, block, 0, s, a, ntn, ntm, kper);
+}
+
+}  // namespace gk

@@ -140,8 +140,11 @@ struct GemmArgs {
   int M = 0, N = 0, K = 0;
   int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
   int accumulate = 0;              // C += result instead of C = result
+  int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
+bool gemm_lds_ok(const GemmArgs& a);
+void gemm_lds(const GemmArgs& a, hipStream_t s);
 
 // sum `splits` slabs [splits][n] -> dst[n] (optionally also as bf16 and/or accumulate)
 void reduce_slabs(const float* src, int splits, long n, float* dst, hipStream_t s);

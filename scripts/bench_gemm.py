@@ -1,0 +1,65 @@
+"""GEMM microbenchmark: register-direct 64x64 kernel vs LDS-staged 128x128 kernel vs torch
+(hipBLASLt) on the engine's shapes.  Random uniform [-1,1) bf16 operands (guide rule 25)."""
+import os, sys, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from gru_mpi_cuda_amd.ops import load_ext
+
+C = load_ext()
+dev = torch.device("cuda", 0)
+s = torch.cuda.current_stream().cuda_stream
+SHAPES = [  # (name, M, N, K, splits)
+    ("h512.dH", 8192, 512, 256, 1),
+    ("h512.P", 256, 1536, 512, 1),
+    ("h512.dEmb", 256, 512, 1536, 1),
+    ("h512.dW_ih0", 1536, 512, 256, 1),
+    ("h512.dW_fc", 256, 512, 8192, 8),
+    ("h512.dW_hh", 1536, 512, 8192, 8),
+    ("h1024.Gi", 8192, 3072, 1024, 1),
+    ("h1024.dWih", 3072, 1024, 8192, 8),
+    ("h2048.dW_hh", 6144, 2048, 65536, 8),
+    ("h2048.dH", 65536, 2048, 256, 1),
+    ("sq4096", 4096, 4096, 4096, 1),
+]
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(); fn(); e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3)
+    return float(np.median(ts))
+
+
+res = []
+for name, M, N, K, sp in SHAPES:
+    A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+    B = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
+    Cs = torch.empty(sp, M, N, device=dev)
+    flop = 2.0 * M * N * K
+    row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp}
+    ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 34 else None
+    for algo in (1, 2):
+        d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,
+                 splits=sp, algo=algo)
+        try:
+            us = timeit(lambda: C.gemm_nt(d, s))
+        except RuntimeError as e:
+            row[f"algo{algo}"] = str(e)[:60]
+            continue
+        row[f"algo{algo}_us"] = round(us, 1)
+        row[f"algo{algo}_tflops"] = round(flop / us / 1e6, 1)
+        if ref is not None:
+            err = float((Cs.sum(0) - ref).abs().max() / ref.abs().max())
+            row[f"algo{algo}_relerr"] = float(f"{err:.2e}")
+    us = timeit(lambda: A @ B.T)
+    row["torch_us"] = round(us, 1)
+    row["torch_tflops"] = round(flop / us / 1e6, 1)
+    res.append(row)
+    print(json.dumps(row), flush=True)
