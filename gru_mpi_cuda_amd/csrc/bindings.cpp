@@ -125,7 +125,7 @@ PYBIND11_MODULE(_C, m) {
     a.h_f = GP(float, d, "h_f"); a.h_bf = GP(u16, d, "h_bf"); a.hT = GP(u16, d, "hT");
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
     a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
-    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0); a.algo = get<int>(d, "algo", 0);
     if (a.Bp % 32 || a.H % 64) throw std::runtime_error("fwd_step: Bp % 32 and H % 64 required");
     gru_fwd_step(a, S(s));
     HIP_LAUNCH_CHECK();
@@ -139,7 +139,7 @@ PYBIND11_MODULE(_C, m) {
     a.carry_out = GP(float, d, "carry_out"); a.dgh = GP(u16, d, "dgh"); a.dghT = GP(u16, d, "dghT");
     a.dgiT = GP(u16, d, "dgiT"); a.dgi = GP(u16, d, "dgi");
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
-    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0); a.algo = get<int>(d, "algo", 0);
     if (a.Bp % 32 || a.H % 64) throw std::runtime_error("bwd_step: Bp % 32 and H % 64 required");
     gru_bwd_step(a, S(s));
     HIP_LAUNCH_CHECK();

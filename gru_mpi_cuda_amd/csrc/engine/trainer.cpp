@@ -53,6 +53,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const char* pe = std::getenv("GK_PERSIST");
   const bool allow = !(pe && pe[0] == '0');
   persist_fwd_ = allow && gru_fwd_seq_supported(H, B);
+  if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);
+  if (step_algo_ == 2 && !gru_step_lds_ok(H, B)) step_algo_ = 0;
   seq_.resize(L);
   bool any_bwd = false;
   for (int l = 0; l < L; ++l) {
@@ -214,7 +216,7 @@ void Trainer::fwd_step(int l, int t, hipStream_t s) {
   a.hT = y.HT; a.ldT = (d_.T + 1) * B; a.colT = (t + 1) * B;
   const size_t so = (size_t)t * B * H;
   a.sr = y.sr + so; a.sz = y.sz + so; a.sn = y.sn + so; a.sghn = y.sghn + so;
-  a.Bp = B; a.H = H;
+  a.Bp = B; a.H = H; a.algo = step_algo_;
   gru_fwd_step(a, s);
 }
 
@@ -234,7 +236,7 @@ void Trainer::bwd_step(int l, int t, hipStream_t s) {
   a.dgh = y.dgh[t & 1];
   a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = T * B; a.colT = t * B;
   a.dgi = y.dgi ? y.dgi + (size_t)t * B * 3 * H : nullptr;
-  a.Bp = B; a.H = H;
+  a.Bp = B; a.H = H; a.algo = step_algo_;
   gru_bwd_step(a, s);
 }
 

@@ -109,6 +109,7 @@ class Trainer {
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;
+  int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;
   int splits_ = 8;
   unsigned *cnt_ = nullptr, *err_ = nullptr;

@@ -165,6 +165,9 @@ std::string Trainer::plan() const {
     if (seq_[l].fuse_w) p += "+dWhh";
     if (seq_[l].fuse_p) p += "+dP";
   }
+  bool any_step = !persist_fwd_;
+  for (const SeqPlan& q : seq_) any_step |= !q.bwd;
+  if (any_step) p += std::string(" step=") + (gru_step_picks_lds(step_algo_, d_.H, Bp_) ? "lds" : "reg");
   p += overlap_ ? " overlap(chunks=" + std::to_string(C_) + ")" : " serial";
   return p;
 }

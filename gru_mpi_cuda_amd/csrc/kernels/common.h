@@ -40,11 +40,12 @@ DEV bf16x8 zero8() {
   return z;
 }
 
-DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence (div_scale/fmas/fixup)
+DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 DEV float tanhf_(float x) {
   // tanh via exp of a non-positive argument: no overflow, ~1 ulp-level agreement with tanhf
   float e = __expf(-2.0f * fabsf(x));
-  float t = (1.0f - e) / (1.0f + e);
+  float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
   return copysignf(t, x);
 }
 

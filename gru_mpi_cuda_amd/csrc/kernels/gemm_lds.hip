@@ -25,7 +25,14 @@ DEV int xcd_remap2(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <bool BIAS>
+DEV float sum8f(const bf16x8& v) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += (float)v[i];
+  return s;
+}
+
+template <bool BIAS, bool ROWSUM>
 __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, int ntm, int kper) {
   __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
   const int id = xcd_remap2(blockIdx.x, gridDim.x);
@@ -61,6 +68,10 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, i
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias gradients: row sums of A from the A fragments already in registers (one wave column
+  // of the first column tile does it; wave-uniform branch)
+  const bool do_rs = ROWSUM && tn == 0 && wn == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
 
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -83,6 +94,10 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, i
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (do_rs) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) rs[t] += sum8f(af[t]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -103,10 +118,19 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, i
         if (a.accumulate) *dst += v; else *dst = v;
       }
   }
+  if (do_rs) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float v = rs[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + wm * 64 + t * 16 + lane] = v;
+    }
+  }
 }
 
 bool gemm_lds_ok(const GemmArgs& a) {
-  if (a.onehot_ids || a.rowsumA) return false;
+  if (a.onehot_ids) return false;
   if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;
   const int kper = a.K / a.splits;
   if (kper % 64 || kper < 128) return false;
@@ -119,8 +143,14 @@ bool gemm_lds_ok(const GemmArgs& a) {
 void gemm_lds(const GemmArgs& a, hipStream_t s) {
   const int ntn = a.N / 128, ntm = a.M / 128, kper = a.K / a.splits;
   dim3 grid(ntn * ntm * a.splits), block(256);
-  if (a.bias && a.splits == 1) hipLaunchKernelGGL(gemm_lds_kernel<true>, grid, block, 0, s, a, ntn, ntm, kper);
-  else hipLaunchKernelGGL(gemm_lds_kernel<false>, grid, block, 0, s, a, ntn, ntm, kper);
+  const bool bias = a.bias && a.splits == 1;
+  if (a.rowsumA) {
+    if (bias) hipLaunchKernelGGL((gemm_lds_kernel<true, true>), grid, block, 0, s, a, ntn, ntm, kper);
+    else hipLaunchKernelGGL((gemm_lds_kernel<false, true>), grid, block, 0, s, a, ntn, ntm, kper);
+  } else {
+    if (bias) hipLaunchKernelGGL((gemm_lds_kernel<true, false>), grid, block, 0, s, a, ntn, ntm, kper);
+    else hipLaunchKernelGGL((gemm_lds_kernel<false, false>), grid, block, 0, s, a, ntn, ntm, kper);
+  }
 }
 
 }  // namespace gk

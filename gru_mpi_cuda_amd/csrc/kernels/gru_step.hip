@@ -11,6 +11,7 @@
 // loads), reduces the KS partial tiles through LDS, then runs the gate epilogue.
 // Backward (BPTT, no reference counterpart) is the mirror: dh_t = dGh_{t+1}·W_hh + carry
 // + dy_t as the MFMA product, and the gate-gradient math as its epilogue.
+#include <stdexcept>
 #include "kernels.h"
 #include "mma_tile.h"
 
@@ -221,7 +222,19 @@ static void pick_split(int nks_total, int& ks, int& kb) {
   ks = 1; kb = 1;
 }
 
+// auto choice: the big LDS tile once the per-step GEMM is large (H >= 1024); the register tile
+// below that, where its 32-row blocks give enough workgroups to fill 256 CUs
+bool gru_step_picks_lds(int algo, int H, int Bp) {
+  return algo == 2 || (algo == 0 && gru_step_lds_ok(H, Bp) && (H * 2 / 64) * (Bp / 128) >= 128);
+}
+static bool use_lds(int algo, int H, int Bp, bool fused, int ldT, int colT) {
+  const bool ok = !fused && gru_step_lds_ok(H, Bp) && ldT % 8 == 0 && colT % 8 == 0;
+  if (algo == 2 && !ok) throw std::runtime_error("gru step: LDS kernel requested for an unsupported shape");
+  return ok && gru_step_picks_lds(algo, H, Bp);
+}
+
 void gru_fwd_step(const FwdStepArgs& a, hipStream_t s) {
+  if (use_lds(a.algo, a.H, a.Bp, a.x_bf != nullptr, a.ldT, a.colT)) { gru_fwd_step_lds(a, s); return; }
   const int nks = a.H / 32;
   int ks, kb;
   pick_split(nks, ks, kb);
@@ -248,6 +261,7 @@ void gru_fwd_step(const FwdStepArgs& a, hipStream_t s) {
 }
 
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s) {
+  if (use_lds(a.algo, a.H, a.Bp, false, a.ldT, a.colT)) { gru_bwd_step_lds(a, s); return; }
   const int nks = 3 * a.H / 32;
   int ks, kb;
   pick_split(nks, ks, kb);

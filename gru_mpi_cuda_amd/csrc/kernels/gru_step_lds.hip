@@ -1,0 +1,304 @@
+// Large-H timestep kernels (H >= 1024 with a batch too big for the persistent kernels):
+// the per-step recurrent GEMM is a real GEMM here (B = 512, H = 2048: 12.9 GFLOP per step),
+// so it runs on the LDS-staged MFMA structure of gemm_lds.hip with the GRU math fused into the
+// epilogue.
+//
+//   forward : tile = 128 batch rows x 32 units x 3 gates.  The B tile's 96 rows are gathered
+//             from the three gate blocks of W_hh (row g*H + j0 + u), so wave (wm, wn) holds
+//             r/z/n pre-activations of the same (row, unit) in acc[i][0..2] -> gates, blend and
+//             all stores straight from registers.
+//   backward: tile = 64 rows x 64 units, K = 3H (dh = dGh_{t+1} · W_hh), then the gate-gradient
+//             epilogue; transposed copies (dGh^T, dGi^T for the weight-gradient GEMMs) go
+//             through the then-idle LDS.
+// Staging: global_load_lds_dwordx4 into a lane-linear LDS image, XOR swizzle on the source
+// address (conflict-free ds_read_b128), 2 buffers, one vmcnt(0) + barrier per 64-deep k-tile.
+#include "kernels.h"
+#include "common.h"
+
+namespace gk {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// Wait until k-tile kt has landed while `ahead` later k-tiles (PER LDS-DMA instructions each,
+// per wave) stay in flight.  vmcnt retires in issue order, so loads the compiler issues after
+// ours only make the wait more conservative.
+template <int N> DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+template <int PER, int A> DEV void wait_ahead(int ahead) {
+  if (ahead >= A) { vm_wait<A * PER>(); return; }
+  if constexpr (A > 0) wait_ahead<PER, A - 1>(ahead);
+}
+// Workgroup barrier WITHOUT the release fence __syncthreads() carries (that fence is an
+// s_waitcnt vmcnt(0), which would drain the whole prefetch ring): own LDS reads retired, then
+// s_barrier.  LDS-DMA completion is covered by the explicit vm_wait before it.
+DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+// NS-deep LDS ring: NS-1 k-tiles in flight.  One barrier per k-tile: it publishes tile kt and
+// proves every wave is done with the slot tile kt+NS-1 is about to overwrite.
+template <int NS, int PER, class Stage, class Compute>
+DEV void ring_loop(int nk, Stage&& stage, Compute&& compute) {
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_ahead<PER, NS - 2>(min(NS - 2, nk - 1 - kt));
+    lds_barrier();
+    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kt + NS - 1);
+    compute(kt % NS);
+  }
+  __syncthreads();
+}
+
+// ==================================================================== forward
+// LDS: [FNS slots] x (A 128x64 + B 96x64) bf16 = FNS x 28 KiB
+constexpr int FNS = 4, BNS = 6;
+__global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[FNS][(128 + 96) * 64];
+  const int H = a.H;
+  const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 128;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+
+  // ---- epilogue operands first (latency hides under the K loop)
+  float gi[4][4][3], bh[3], hp[4][4];
+  const int u = j0 + wn * 16 + lr;
+#pragma unroll
+  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
+  // source rows first (all 16 ids in one round trip), then the 48 gathers
+  const float* src[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int b = b0 + wm * 64 + i * 16 + lq * 4 + e;
+      src[i][e] = a.Gi + (size_t)b * 3 * H;
+      hp[i][e] = a.hprev_f[(size_t)b * H + u];
+    }
+  if (a.ids) {
+    const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int4 v = id4[i * 4];
+      src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
+      src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+
+  // ---- staging: A rows b0.., B rows (gate, unit) -> W_hh row g*H + j0 + unit
+  const u16* srcA[4];
+  const u16* srcB[3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = (4 * w + q) * 8 + srow;
+    srcA[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int r = (3 * w + q) * 8 + srow;       // 0..95
+    srcB[q] = a.Whh + (size_t)((r >> 5) * H + j0 + (r & 31)) * H + swz(r, sslot) * 8;
+  }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void_t*)(&lds[buf][(4 * w + q) * 8 * 64]), 16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(128 + (3 * w + q) * 8) * 64]), 16, 0, 0);
+  };
+
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ring_loop<FNS, 7>(H / 64, stage, [&](int cur) {
+    const u16* LA = lds[cur];
+    const u16* LB = lds[cur] + 128 * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + lq;
+      bf16x8 af[4], bfr[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+      }
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const int r = g * 32 + wn * 16 + lr;
+        bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
+    }
+  });
+
+  // ---- fused GRU epilogue from registers; bf16 h tile staged in LDS for the transposed copy
+  u16* st = lds[0];     // [128 rows][32 units]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rr = wm * 64 + i * 16 + lq * 4 + e;
+      const int b = b0 + rr;
+      const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
+      const float r = sigmoidf_(gi[i][e][0] + ghr);
+      const float z = sigmoidf_(gi[i][e][1] + ghz);
+      const float n = tanhf_(gi[i][e][2] + r * ghn);
+      const float h = n + z * (hp[i][e] - n);
+      const size_t o = (size_t)b * H + u;
+      a.h_f[o] = h;
+      const u16 hb = f2bf(h);
+      a.h_bf[o] = hb;
+      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+      st[rr * 32 + wn * 16 + lr] = hb;
+    }
+  if (a.hT) {
+    __syncthreads();
+    // 32 units x 128 rows: 512 x 16-B pieces, 2 per thread
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int q = threadIdx.x + p * 256;
+      const int unit = q >> 4, seg = q & 15;          // 16 segments of 8 rows
+      u16 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
+      *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
+          *reinterpret_cast<const uint4*>(v);
+    }
+  }
+}
+
+// ==================================================================== backward
+// tile 64 rows x 64 units; 4 waves 2 x 2 of 32 x 32 (2 x 2 MFMA tiles); K = 3H
+__global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[BNS][(64 + 64) * 64];
+  const int H = a.H, H3 = 3 * a.H;
+  const int j0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+
+  // epilogue operands: element (i, jt, e) -> row b0 + wm*32 + i*16 + lq*4 + e, unit j0 + wn*32 + jt*16 + lr
+  float dy[2][2][4], cin[2][2][4], sr_[2][2][4], sz_[2][2][4], sn_[2][2][4], sg_[2][2][4], hpv[2][2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t o = (size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * H + j0 + wn * 32 + jt * 16 + lr;
+        dy[i][jt][e] = a.dy[o];
+        cin[i][jt][e] = a.carry_in ? a.carry_in[o] : 0.f;
+        sr_[i][jt][e] = a.r[o]; sz_[i][jt][e] = a.z[o]; sn_[i][jt][e] = a.n[o];
+        sg_[i][jt][e] = a.ghn[o]; hpv[i][jt][e] = a.hprev[o];
+      }
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.dgh_next) {
+    const u16* srcA[2];
+    const u16* srcB[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (2 * w + q) * 8 + srow;
+      srcA[q] = a.dgh_next + (size_t)(b0 + r) * H3 + swz(r, sslot) * 8;
+      srcB[q] = a.WhhT + (size_t)(j0 + r) * H3 + swz(r, sslot) * 8;
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void_t*)(&lds[buf][(2 * w + q) * 8 * 64]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(64 + (2 * w + q) * 8) * 64]), 16, 0, 0);
+      }
+    };
+    ring_loop<BNS, 4>(H3 / 64, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 64 * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[2], bfr[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int ra = wm * 32 + t * 16 + lr, rb = wn * 32 + t * 16 + lr;
+          af[t] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
+          bfr[t] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    });
+  }
+
+  // ---- gate-gradient epilogue; transposed staging [4 kinds][64 units][64 rows] bf16 = 32 KiB
+  u16* st = lds[0];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = wm * 32 + i * 16 + lq * 4 + e, uu = wn * 32 + jt * 16 + lr;
+        const int b = b0 + rr, j = j0 + uu;
+        const float dh = dy[i][jt][e] + cin[i][jt][e] + acc[i][jt][e];
+        const float r = sr_[i][jt][e], z = sz_[i][jt][e], n = sn_[i][jt][e];
+        const float dn = dh * (1.f - z);
+        const float dz = dh * (hpv[i][jt][e] - n);
+        const float dan = dn * (1.f - n * n);
+        const float dar = dan * sg_[i][jt][e] * r * (1.f - r);
+        const float daz = dz * z * (1.f - z);
+        a.carry_out[(size_t)b * H + j] = z * dh;
+        const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
+        const size_t og = (size_t)b * H3 + j;
+        a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
+        if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
+        st[(0 * 64 + uu) * 64 + rr] = br;
+        st[(1 * 64 + uu) * 64 + rr] = bz;
+        st[(2 * 64 + uu) * 64 + rr] = bn;
+        st[(3 * 64 + uu) * 64 + rr] = bi;
+      }
+  __syncthreads();
+  // 4 kinds x 64 units x 64 rows = 2048 pieces of 8 rows (16 B), 8 per thread
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int q = threadIdx.x + p * 256;
+    const int kind = q >> 9, rem = q & 511, unit = rem >> 3, seg = rem & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 64 + unit) * 64 + seg * 8]);
+    const int g = kind < 3 ? kind : 2;
+    const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + seg * 8;
+    if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
+    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+  }
+}
+
+bool gru_step_lds_ok(int H, int Bp) { return H >= 1024 && H % 64 == 0 && Bp % 128 == 0; }
+
+void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(gru_fwd_step_lds_kernel, dim3(a.H / 32, a.Bp / 128), dim3(256), 0, s, a);
+}
+void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(gru_bwd_step_lds_kernel, dim3(a.H / 64, a.Bp / 64), dim3(256), 0, s, a);
+}
+
+}  // namespace gk

@@ -34,6 +34,7 @@ struct FwdStepArgs {
   int ldT = 0, colT = 0;
   float* sr = nullptr; float* sz = nullptr; float* sn = nullptr; float* sghn = nullptr;  // saves (nullable)
   int Bp = 0, H = 0;
+  int algo = 0;                    // 0 auto, 1 register-direct tile, 2 LDS-staged big tile (gru_step_lds.hip)
 };
 void gru_fwd_step(const FwdStepArgs& a, hipStream_t s);
 
@@ -50,8 +51,15 @@ struct BwdStepArgs {
   u16* dgiT = nullptr;             // [3H][ldT]
   u16* dgi = nullptr;              // [Bp][3H] row-major dGi (nullable; needed below layer 0 only)
   int ldT = 0, colT = 0, Bp = 0, H = 0;
+  int algo = 0;                    // as FwdStepArgs::algo
 };
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
+// LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
+bool gru_step_lds_ok(int H, int Bp);
+// which per-step kernel gru_fwd_step/gru_bwd_step pick for (algo, H, Bp) without fused input
+bool gru_step_picks_lds(int algo, int H, int Bp);
+void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s);
+void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ persistent sequence kernels
 // One launch per layer runs all T steps (gru_seq.hip).  Requires 512-thread co-residency of

@@ -61,6 +61,28 @@ def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
         assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
 
 
+@pytest.mark.parametrize("layers,B", [(1, 128), (2, 256)])
+def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B):
+    """Per-step schedule on the LDS-staged big-tile step kernels (the large-H path)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    monkeypatch.setenv("GK_PERSIST", "0")
+    monkeypatch.setenv("GK_STEP_ALGO", "2")
+    cfg = GRUConfig(vocab=256, embed=128, hidden=1024, layers=layers, batch=B, seq=6, time_chunks=2, seed=5)
+    params = init_params(cfg)
+    x, y = NameStream(B, cfg.seq, seed=4).next()
+    tr = HipTrainer(cfg, params=params)
+    plan = tr.t.plan()
+    assert "step=lds" in plan, plan
+    tr.forward_backward(x, y)
+    g = tr.grad_dict()
+    p64 = {k: v.double() for k, v in params.items()}
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
+    for k in ref_g:
+        e = rel(g[k], ref_g[k])
+        assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
+
+
 def test_trainer_adam_step_and_learning():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer, CpuTrainer
     cfg = GRUConfig(vocab=256, embed=128, hidden=128, layers=1, batch=64, seq=16, time_chunks=2, lr=3e-3, seed=1)

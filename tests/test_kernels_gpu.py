@@ -27,14 +27,18 @@ def rnd(*shape, scale=1.0, seed=0):
     return (torch.randn(*shape, generator=g) * scale).to(DEV)
 
 
-@pytest.mark.parametrize("M,N,K,splits", [(64, 64, 32, 1), (128, 192, 256, 1), (256, 512, 1024, 4), (192, 128, 512, 2)])
-def test_gemm_nt(ext, M, N, K, splits):
+@pytest.mark.parametrize("algo", [1, 2])
+@pytest.mark.parametrize("M,N,K,splits", [(64, 64, 32, 1), (128, 192, 256, 1), (256, 512, 1024, 4), (192, 128, 512, 2),
+                                          (384, 256, 768, 3), (128, 128, 128, 1)])
+def test_gemm_nt(ext, algo, M, N, K, splits):
+    if algo == 2 and (M % 128 or N % 128 or (K // splits) % 64 or K // splits < 128):
+        pytest.skip("shape not supported by the LDS kernel")
     A, B = bf(rnd(M, K, seed=1)), bf(rnd(N, K, seed=2) + 0.1 * torch.arange(K, device=DEV) / K)
     bias = rnd(N, seed=3) if splits == 1 else None
     C = torch.full((splits, M, N), float("nan"), device=DEV)
     rs = torch.full((splits, M), float("nan"), device=DEV)
     d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=M, N=N, K=K,
-             splits=splits, rowsumA=rs.data_ptr())
+             splits=splits, rowsumA=rs.data_ptr(), algo=algo)
     if bias is not None:
         d["bias"] = bias.data_ptr()
     ext.gemm_nt(d, S())
@@ -65,15 +69,19 @@ def _gates_ref(gi, gh, hp):
     return n + z * (hp - n), r, z, n, gh[:, 2 * H:]
 
 
+# algo 1 = register-direct 32x16 tile, 2 = LDS-staged 128-row big tile (gru_step_lds.hip)
 @pytest.mark.parametrize("mode", ["table", "gi", "fused"])
-@pytest.mark.parametrize("H", [128, 512])
-def test_fwd_step(ext, mode, H):
-    Bp, V, Kin = 64, 256, 256
+@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (512, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2)])
+def test_fwd_step(ext, mode, H, Bp, algo):
+    if algo == 2 and mode == "fused":
+        pytest.skip("LDS step kernel has no fused input projection")
+    V, Kin = 256, 256
     hp = rnd(Bp, H, scale=0.5, seed=1).clamp(-1, 1)
     hpb = bf(hp)
     Whh = bf(rnd(3 * H, H, scale=H ** -0.5, seed=2))
     bhh = rnd(3 * H, scale=0.1, seed=3)
-    d = dict(hprev_bf=hpb.data_ptr(), hprev_f=hp.data_ptr(), Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), Bp=Bp, H=H)
+    d = dict(hprev_bf=hpb.data_ptr(), hprev_f=hp.data_ptr(), Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), Bp=Bp, H=H,
+             algo=algo)
     keep = []
     if mode == "table":
         P = rnd(V, 3 * H, seed=4)
@@ -113,8 +121,9 @@ def test_fwd_step(ext, mode, H):
 
 
 @pytest.mark.parametrize("first", [False, True])
-def test_bwd_step(ext, first):
-    Bp, H, T = 64, 128, 4
+@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2)])
+def test_bwd_step(ext, first, H, Bp, algo):
+    T = 4
     t = 1
     dgn = bf(rnd(Bp, 3 * H, scale=0.1, seed=1))
     Whh = rnd(3 * H, H, scale=H ** -0.5, seed=2)
@@ -130,7 +139,7 @@ def test_bwd_step(ext, first):
     dgiT = torch.zeros(3 * H, T * Bp, device=DEV, dtype=torch.bfloat16)
     d = dict(WhhT=WhhT.data_ptr(), dy=dy.data_ptr(), r=r.data_ptr(), z=z.data_ptr(), n=n.data_ptr(),
              ghn=ghn.data_ptr(), hprev=hp.data_ptr(), carry_out=cout.data_ptr(), dgh=dgh.data_ptr(),
-             dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), dgi=dgi.data_ptr(), ldT=T * Bp, colT=t * Bp, Bp=Bp, H=H)
+             dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), dgi=dgi.data_ptr(), ldT=T * Bp, colT=t * Bp, Bp=Bp, H=H, algo=algo)
     if not first:
         d.update(dgh_next=dgn.data_ptr(), carry_in=carry.data_ptr())
     ext.bwd_step(d, S())
