@@ -42,6 +42,7 @@ class GRUConfig:
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
     overlap: bool = False       # True: chunked side-stream schedule; False: single stream built on
                                 # the persistent sequence kernels (faster on MI355X, profiles/)
+    watchdog_ms: int = 0        # >0: abort the RCCL communicator when a step is not done in time
 
     def __post_init__(self):
         if self.layers < 1:

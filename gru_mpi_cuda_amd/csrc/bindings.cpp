@@ -82,6 +82,9 @@ PYBIND11_MODULE(_C, m) {
       .def("plan", &Trainer::plan)
       .def("uses_persistent", &Trainer::uses_persistent)
       .def("read_error", &Trainer::read_error)
+      .def("enable_watchdog", &Trainer::enable_watchdog)
+      .def("watchdog_status", &Trainer::watchdog_status)
+      .def("watchdog_message", &Trainer::watchdog_message)
       .def("buffer", &Trainer::buffer);
 
   py::class_<Generator>(m, "Generator")
@@ -144,6 +147,7 @@ PYBIND11_MODULE(_C, m) {
     gru_bwd_step(a, S(s));
     HIP_LAUNCH_CHECK();
   });
+  m.def("spin_delay", [](int us, uintptr_t s) { spin_delay(us, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
@@ -234,6 +238,7 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("check_async_error", &RcclComm::check_async_error)
       .def("abort", &RcclComm::abort)
+      .def("aborted", &RcclComm::aborted)
       .def("rank", &RcclComm::rank)
       .def("world", &RcclComm::world);
 }

@@ -34,29 +34,35 @@ RcclComm::RcclComm(const std::string& uid, int rank, int world) : rank_(rank), w
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) (void)ncclCommDestroy(C(comm_));
+  if (void* c = comm_.exchange(nullptr)) (void)ncclCommDestroy(C(c));
+}
+
+void* RcclComm::live() const {
+  void* c = comm_.load();
+  if (!c) throw std::runtime_error("[rank " + std::to_string(rank_) + "] RCCL communicator was aborted");
+  return c;
 }
 
 void RcclComm::allreduce_avg_f32(float* p, long n, hipStream_t s) {
-  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclAvg, C(comm_), s));
+  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclAvg, C(live()), s));
 }
 void RcclComm::allreduce_sum_f32(float* p, long n, hipStream_t s) {
-  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclSum, C(comm_), s));
+  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclSum, C(live()), s));
 }
 void RcclComm::broadcast_f32(float* p, long n, int root, hipStream_t s) {
-  RCCL_CHECK(ncclBroadcast(p, p, (size_t)n, ncclFloat32, root, C(comm_), s));
+  RCCL_CHECK(ncclBroadcast(p, p, (size_t)n, ncclFloat32, root, C(live()), s));
 }
 void RcclComm::allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s) {
-  RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclUint8, C(comm_), s));
+  RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclUint8, C(live()), s));
 }
 void RcclComm::check_async_error() {
   ncclResult_t r = ncclSuccess;
-  RCCL_CHECK(ncclCommGetAsyncError(C(comm_), &r));
+  RCCL_CHECK(ncclCommGetAsyncError(C(live()), &r));
   if (r != ncclSuccess && r != ncclInProgress)
     throw std::runtime_error("[rank " + std::to_string(rank_) + "] RCCL async error: " + ncclGetErrorString(r));
 }
 void RcclComm::abort() {
-  if (comm_) { (void)ncclCommAbort(C(comm_)); comm_ = nullptr; }
+  if (void* c = comm_.exchange(nullptr)) (void)ncclCommAbort(C(c));
 }
 
 }  // namespace gk

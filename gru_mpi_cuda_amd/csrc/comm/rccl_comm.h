@@ -7,6 +7,7 @@
 // ncclCommInitRank.  Collectives issued on a stream that is being captured become graph
 // nodes, so gradient all-reduce can live inside the training step's hipGraph.
 #pragma once
+#include <atomic>
 #include <string>
 #include <hip/hip_runtime.h>
 
@@ -23,12 +24,14 @@ class RcclComm {
   void allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s);
   // watchdog hook: raises if the communicator reported an asynchronous error
   void check_async_error();
-  void abort();
+  void abort();                       // thread-safe (the watchdog calls it)
+  bool aborted() const { return comm_.load() == nullptr; }
   int rank() const { return rank_; }
   int world() const { return world_; }
 
  private:
-  void* comm_ = nullptr;   // ncclComm_t
+  std::atomic<void*> comm_{nullptr};   // ncclComm_t; null once aborted
+  void* live() const;
   int rank_ = 0, world_ = 1;
 };
 

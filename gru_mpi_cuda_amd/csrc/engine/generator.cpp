@@ -1,4 +1,5 @@
 #include "generator.h"
+#include "../runtime/trace.h"
 
 #include <algorithm>
 
@@ -90,6 +91,7 @@ void Generator::record_steps(int n, hipStream_t s) {
 }
 
 void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t s) {
+  GK_TRACE("gk.generate");
   const int ML = d_.max_len;
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);

@@ -1,4 +1,5 @@
 #include "trainer.h"
+#include "../runtime/trace.h"
 
 #include <cstring>
 #include <algorithm>
@@ -392,6 +393,7 @@ void Trainer::record_opt(hipStream_t s) {
 }
 
 void Trainer::forward_backward(hipStream_t s) {
+  GK_TRACE("gk.forward_backward");
   const int slot = stage_slot_;
   stage_src_ = h_stage_ + (size_t)slot * slot_ints();
   if (!use_graph_) {
@@ -414,6 +416,7 @@ void Trainer::forward_backward(hipStream_t s) {
 }
 
 void Trainer::optimizer_step(hipStream_t s) {
+  GK_TRACE("gk.optimizer_step");
   if (!use_graph_) { record_opt(s); return; }
   if (!g_opt_.ready()) {
     g_opt_.begin(s0_);
@@ -437,17 +440,25 @@ void Trainer::record_allreduce(hipStream_t s) {
   for (const auto& b : buckets_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
 }
 
+void Trainer::enable_watchdog(int timeout_ms) {
+  wd_.reset();
+  if (timeout_ms > 0) wd_ = std::make_unique<Watchdog>(comm_, timeout_ms);
+}
+
 void Trainer::step(hipStream_t s) {
+  GK_TRACE("gk.train_step");
   if (!use_graph_) {
     forward_backward(s);
     record_allreduce(s);
     optimizer_step(s);
+    if (wd_) { HIP_CHECK(hipEventRecord(stage_done_[stage_slot_], s)); wd_->watch(stage_done_[stage_slot_]); }
     return;
   }
   const int slot = stage_slot_;
   stage_src_ = h_stage_ + (size_t)slot * slot_ints();
   Graph& g = g_step_[slot];
   if (!g.ready()) {
+    GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
       if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
@@ -464,6 +475,7 @@ void Trainer::step(hipStream_t s) {
   }
   g.launch(s);
   HIP_CHECK(hipEventRecord(stage_done_[slot], s));
+  if (wd_) wd_->watch(stage_done_[slot]);
 }
 
 float Trainer::read_loss() {

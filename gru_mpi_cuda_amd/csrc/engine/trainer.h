@@ -17,6 +17,8 @@
 #include "../runtime/runtime.h"
 #include "../kernels/kernels.h"
 #include "../comm/rccl_comm.h"
+#include "../comm/watchdog.h"
+#include <memory>
 
 namespace gk {
 
@@ -91,7 +93,12 @@ class Trainer {
   void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
   void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets);
   void step(hipStream_t s);      // whole training step as one graph replay
+  // collective watchdog over the launched steps (needs set_comm first; 0 disables)
+  void enable_watchdog(int timeout_ms);
+  int watchdog_status() const { return wd_ ? wd_->status() : 0; }
+  std::string watchdog_message() { return wd_ ? wd_->message() : std::string(); }
  private:
+  std::unique_ptr<Watchdog> wd_;
 
   struct Layer {
     float *HSf, *sr, *sz, *sn, *sghn, *dy, *Gi, *carry[2];

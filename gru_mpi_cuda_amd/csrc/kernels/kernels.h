@@ -190,6 +190,8 @@ struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
   void add(const float* s, int R, int C, u16* d, u16* dT) { job[n++] = CastJob{s, d, dT, R, C}; } };
 void cast_multi(CastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
+// fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)
+void spin_delay(int us, hipStream_t s);
 
 // Batch preparation on device: in = [hdr 16 ints: B, float-bits of 1/#valid][x Bmax*T][y Bmax*T]
 // batch-major int32 (may be pinned host memory, read zero-copy); out ids/labels time-major [T][Bp]

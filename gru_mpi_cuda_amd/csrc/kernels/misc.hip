@@ -271,4 +271,14 @@ void fill_f32(float* p, long n, float v, hipStream_t s) {
   hipLaunchKernelGGL(fill_kernel, dim3(nblocks(n, 256, 1024)), dim3(256), 0, s, p, n, v);
 }
 
+__global__ void spin_kernel(unsigned long long ticks) {
+  // s_memrealtime is a constant 100 MHz counter; the loop always ends
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+void spin_delay(int us, hipStream_t s) {
+  const long capped = us < 0 ? 0 : (us > 5000000 ? 5000000 : us);
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, (unsigned long long)capped * 100ull);
+}
+
 }  // namespace gk

@@ -63,6 +63,13 @@ class HipTrainer:
             self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets])
         self.t.refresh_weights(self._stream())
         self._one_graph = True
+        if cfg.watchdog_ms > 0:       # host thread watching each launched step
+            self.t.enable_watchdog(int(cfg.watchdog_ms))
+
+    def check_watchdog(self) -> None:
+        """Raise if the collective watchdog fired (step timeout or RCCL async error)."""
+        if self.t.watchdog_status():
+            raise RuntimeError(f"watchdog: {self.t.watchdog_message()}")
 
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
@@ -88,6 +95,7 @@ class HipTrainer:
         gradients, bucketed RCCL all-reduce (if data-parallel) and Adam + bf16 weight refresh."""
         s = self._stream()
         self.t.set_batch(x, y, s)
+        self.check_watchdog()
         if self._one_graph:
             try:
                 self.t.step(s)

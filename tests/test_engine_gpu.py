@@ -166,3 +166,28 @@ def test_set_batch_device_matches_host():
     gb = a.grad_dict()
     for k in ga:
         torch.testing.assert_close(ga[k], gb[k], atol=0, rtol=0)
+
+
+def test_watchdog_detects_stalled_step():
+    """Fault injection: a 600 ms busy kernel in front of a step trips a 100 ms
+    watchdog; a healthy trainer with the same watchdog stays clean."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=128, hidden=128, layers=1, batch=64, seq=8, seed=3, watchdog_ms=100)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=1).next()
+    ok = HipTrainer(cfg)
+    for _ in range(3):
+        ok.step(x, y)
+    torch.cuda.synchronize()
+    assert ok.t.watchdog_status() == 0
+    bad = HipTrainer(cfg)
+    bad.step(x, y)
+    torch.cuda.synchronize()
+    bad.C.spin_delay(600_000, torch.cuda.current_stream().cuda_stream)
+    bad.step(x, y)
+    torch.cuda.synchronize()
+    import time
+    time.sleep(0.1)
+    assert bad.t.watchdog_status() == 1, bad.t.watchdog_message()
+    assert "not done after" in bad.t.watchdog_message()
+    with pytest.raises(RuntimeError, match="watchdog"):
+        bad.step(x, y)
