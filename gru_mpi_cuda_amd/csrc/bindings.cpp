@@ -189,7 +189,9 @@ PYBIND11_MODULE(_C, m) {
     a.dl = GP(u16, d, "dl"); a.dlT = GP(u16, d, "dlT"); a.loss_part = GP(float, d, "loss_part");
     a.M = get<int>(d, "M", 0); a.H = get<int>(d, "H", 0); a.V = get<int>(d, "V", 0);
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
-    if (a.M % 32 || a.V % 64 || a.V > 512 || a.H % 32) throw std::runtime_error("fc_xent: bad shape");
+    a.WT = GP(const u16, d, "WT"); a.dy = GP(float, d, "dy");
+    if (a.M % 32 || a.V % 64 || a.V > 512 || a.H % 32 || a.ldT % 8 || a.colT % 8)
+      throw std::runtime_error("fc_xent: bad shape");
     fc_xent(a, S(s));
     HIP_LAUNCH_CHECK();
   });

@@ -72,6 +72,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
   size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
+  size_t o_sfc2 = R((size_t)splits_ * V * H * 4), o_rfc2 = R((size_t)splits_ * V * 4);
+  size_t o_se = R((size_t)splits_ * V * E * 4);
   std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0);
   for (int l = 0; l < L; ++l) {
     if (seq_[l].fuse_w) o_pw[l] = R((size_t)nrb * 3 * H * H * 4);
@@ -82,6 +84,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
   slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
+  slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
   for (int l = 0; l < L; ++l) {
     seq_[l].dWhh_part = seq_[l].fuse_w ? arena_.get<float>(o_pw[l]) : nullptr;
     seq_[l].dbhh_part = seq_[l].bwd ? arena_.get<float>(o_pbh[l]) : nullptr;
@@ -387,8 +390,26 @@ void Trainer::record_opt(hipStream_t s) {
   a.p = params_; a.g = grads_; a.m = m_; a.v = v_; a.n = nflat_; a.step = step_;
   a.gscale = o_.clip > 0.f ? gscale_ : nullptr;
   a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
-  adam_step(a, s);
-  refresh_weights(s);
+  const int V = d_.V, E = d_.E, H = d_.H;
+  if (V % 64 == 0 && E % 64 == 0 && H % 64 == 0) {
+    // one launch: update every tensor and write its bf16 (+ transposed) MFMA copies from the
+    // freshly updated registers (no second pass over the fp32 master weights)
+    OptCastJobs j;
+    j.add(off_.at("embedding"), V, E, Emb, EmbT);
+    for (int l = 0; l < d_.L; ++l) {
+      const std::string k = std::to_string(l);
+      j.add(off_.at("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
+      j.add(off_.at("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
+      j.add(off_.at("bias_ih_l" + k), 0, 3 * H, nullptr, nullptr);
+      j.add(off_.at("bias_hh_l" + k), 0, 3 * H, nullptr, nullptr);
+    }
+    j.add(off_.at("fc.weight"), V, H, Wfc, WfcT);
+    j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
+    adam_cast_multi(a, j, s);
+  } else {
+    adam_step(a, s);
+    refresh_weights(s);
+  }
   HIP_LAUNCH_CHECK();
 }
 

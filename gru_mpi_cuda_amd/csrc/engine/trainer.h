@@ -122,6 +122,8 @@ class Trainer {
   unsigned *cnt_ = nullptr, *err_ = nullptr;
   u16* xbuf_ = nullptr;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
+  // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
+  float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }
   std::string plan() const;

@@ -72,19 +72,35 @@ void Trainer::record_fb_seq(hipStream_t s) {
   }
   // ------------------------------------------------------------------ FC + loss + dH
   Layer& top = Ls_[L - 1];
+  SlabJobs tail;   // reductions deferred to the last multi-tensor reduce (layer 0's)
   {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
     f.labels = labels_; f.inv_count = inv_count_;
     f.dl = dl_; f.dlT = dlT_; f.ldT = (int)tok; f.colT = 0;
     f.loss_part = loss_part_; f.M = (int)tok; f.H = H; f.V = V;
-    fc_xent(f, s);
-    GemmArgs g;   // dy_top = dlogits · W_fc
-    g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
-    g.M = (int)tok; g.N = H; g.K = V;
-    gemm_nt(g, s);
-    // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T
-    wgrad_gemm(dlT_, (int)tok, top.HT + B, (T + 1) * B, V, H, (int)tok, G("fc.weight"), G("fc.bias"), s);
+    if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
+      // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
+      f.dl = nullptr; f.WT = WfcT; f.dy = top.dy;
+      fc_xent(f, s);
+    } else {
+      fc_xent(f, s);
+      GemmArgs g;   // dy_top = dlogits · W_fc
+      g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
+      g.M = (int)tok; g.N = H; g.K = V;
+      gemm_nt(g, s);
+    }
+    // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T: split-K into dedicated slabs whose
+    // reduce joins the multi-tensor reduce after the backward sweep (one launch fewer)
+    int sp = splits_;
+    while (sp > 1 && (tok % sp || (tok / sp) % 128)) sp >>= 1;
+    GemmArgs w;
+    w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;
+    w.C = slab_fc2_; w.ldc = H; w.rowsumA = rs_fc2_;
+    w.M = V; w.N = H; w.K = (int)tok; w.splits = sp;
+    gemm_nt(w, s);
+    tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
+    tail.add(rs_fc2_, sp, V, G("fc.bias"));
   }
   // ------------------------------------------------------------------ backward (BPTT)
   for (int l = L - 1; l >= 0; --l) {
@@ -112,8 +128,14 @@ void Trainer::record_fb_seq(hipStream_t s) {
     SlabJobs j;
     if (q.fuse_w) j.add(q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
     if (q.bwd) j.add(q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
-    if (l == 0 && q.fuse_p) j.add(dP_part_, nrb, (long)V * H3, dP_);
+    // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail
+    if (l == 0 && q.fuse_p) j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     if (l == 0 && q.bwd) j.add(q.dbih_part, nrb, H3, G("bias_ih_l0"));
+    if (l == 0) {   // + dW_fc / db_fc slabs, the loss partials, and the optimiser step counter
+      for (int k2 = 0; k2 < tail.n; ++k2) j.job[j.n++] = tail.job[k2];
+      j.add(loss_part_, (int)(tok / 32), 1, loss_);
+      j.bump = step_;
+    }
     if (j.n) reduce_slabs_multi(j, s);
     if (!q.fuse_w)
       wgrad_gemm(y.dghT, (int)tok, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
@@ -142,19 +164,30 @@ void Trainer::record_fb_seq(hipStream_t s) {
   }
   // ------------------------------------------------------------------ embedding-side gradients
   {
-    CastJobs j;
-    j.add(dP_, V, H3, dP_bf_, dPT_bf_);
-    cast_multi(j, s);
+    if (!seq_[0].fuse_p) {
+      CastJobs j;
+      j.add(dP_, V, H3, dP_bf_, dPT_bf_);
+      cast_multi(j, s);
+    }
     GemmArgs g;   // dW_ih0 = dP^T · Emb
     g.A = dPT_bf_; g.lda = V; g.B = EmbT; g.ldb = V; g.C = G("weight_ih_l0"); g.ldc = E;
     g.M = H3; g.N = E; g.K = V;
-    gemm_nt(g, s);
-    GemmArgs e;   // dEmb = dP · W_ih0
-    e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = G("embedding"); e.ldc = E;
-    e.M = V; e.N = E; e.K = H3;
-    gemm_nt(e, s);
+    GemmArgs e;   // dEmb = dP · W_ih0, split-K (K = 3H on only V x E outputs) into slab_e_
+    int se = splits_;
+    while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
+    e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = slab_e_; e.ldc = E;
+    e.M = V; e.N = E; e.K = H3; e.splits = se;
+    const GemmArgs both[2] = {g, e};
+    if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
+      gemm_lds_group(both, 2, s);   // one launch for both small products
+    } else {
+      gemm_nt(g, s);
+      gemm_nt(e, s);
+    }
+    SlabJobs r;
+    r.add(slab_e_, se, (long)V * E, G("embedding"));
+    reduce_slabs_multi(r, s);
   }
-  sum_partials(loss_part_, (int)(tok / 32), loss_, s, step_);
   HIP_LAUNCH_CHECK();
 }
 

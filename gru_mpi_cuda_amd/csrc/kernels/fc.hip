@@ -8,6 +8,7 @@
 // A workgroup owns 32 full rows (all V columns) so the row reductions stay on chip:
 // each of the V/64 waves holds a 32x64 slab in 8 MFMA accumulators, rows are reduced
 // across the 16 column lanes with DPP-able xor shuffles and across waves through LDS.
+#include <stdexcept>
 #include "kernels.h"
 #include "mma_tile.h"
 
@@ -72,12 +73,48 @@ DEV void row_stats(const f32x4 (&acc)[2][4], float* red /*[2][NW][32]*/, int NW,
     }
 }
 
+// dH tile: rows m0..m0+31 x CT*16 columns from n0, K = V, A = dl from LDS (row-major, padded
+// stride ldr), B = W_fc^T rows from global (all V/32 k-steps of B issued up front).
+template <int CT>
+DEV void fc_dh_tile(const u16* dlr, int ldr, const u16* WT, int V, int H, float* dy, int m0, int n0,
+                    int lane) {
+  const int lr = lane & 15, lq = lane >> 4;
+  f32x4 acc[2][CT];
+  zero_acc(acc);
+  const u16* B = WT + (size_t)(n0 + lr) * V + 8 * lq;
+  for (int k0 = 0; k0 < V; k0 += 128) {       // 4 k-steps of B in flight per round
+    bf16x8 bf[4][CT];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) bf[kk][c] = ld8(B + (size_t)c * 16 * V + k0 + kk * 32);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        af[r] = *reinterpret_cast<const bf16x8*>(dlr + (r * 16 + lr) * ldr + k0 + kk * 32 + 8 * lq);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[r][c] = mfma16(af[r], bf[kk][c], acc[r][c]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = acc[r][c][i];
+}
+
 template <int KB>
 __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
   const int m0 = blockIdx.x * FROWS;
-  const int V = a.V;
+  const int V = a.V, ldr = V + 8;
   f32x4 acc[2][4];
   fc_logits<KB>(acc, a.X, a.W, a.b, a.H, m0, lane, w);
 
@@ -85,6 +122,7 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   float* lab = smem + 2 * NW * 32;                 // [32] label logit
   float* lrow = lab + 32;                          // [32] per-row loss
   u16* st = reinterpret_cast<u16*>(lrow + 32);     // [V][32] bf16 dl^T staging
+  u16* dlr = st + (size_t)V * FROWS;               // [32][V+8] bf16 dl row-major (dH A operand)
   float mx[2][4], se[2][4];
   row_stats(acc, red, NW, lane, w, mx, se);
   const float inv = a.inv_count[0];
@@ -96,7 +134,7 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
       const int row = r * 16 + (lane >> 4) * 4 + i;
       const int y = a.labels[m0 + row];
       const float scale = (y >= 0) ? inv : 0.f;
-      const float rs = 1.f / se[r][i];
+      const float rs = __builtin_amdgcn_rcpf(se[r][i]);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int col = w * 64 + c * 16 + lr;
@@ -105,8 +143,9 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
         const float p = __expf(x - mx[r][i]) * rs;
         const float d = (p - (col == y ? 1.f : 0.f)) * scale;
         const u16 db = f2bf(d);
-        a.dl[(size_t)(m0 + row) * V + col] = db;
+        if (a.dl) a.dl[(size_t)(m0 + row) * V + col] = db;
         st[col * FROWS + row] = db;
+        dlr[row * ldr + col] = db;
       }
     }
   __syncthreads();
@@ -114,16 +153,23 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   if (threadIdx.x < FROWS) {
     const int row = threadIdx.x;
     const int y = a.labels[m0 + row];
-    // recompute this row's max / sum from wave-level partials
     float m = red[row];
     for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
     float s = 0.f;
     for (int ww = 0; ww < NW; ++ww) s += red[NW * 32 + ww * 32 + row];
     lrow[row] = (y >= 0) ? (logf(s) + m - lab[row]) * inv : 0.f;
   }
-  for (int q = threadIdx.x; q < V * FROWS; q += blockDim.x) {
-    const int col = q >> 5, row = q & 31;
-    a.dlT[(size_t)col * a.ldT + a.colT + m0 + row] = st[col * FROWS + row];
+  // dl^T: each column's 32 rows are 64 contiguous bytes -> four 16-B stores
+  for (int q = threadIdx.x; q < V * 4; q += blockDim.x) {
+    const int col = q >> 2, seg = q & 3;
+    *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) =
+        *reinterpret_cast<const uint4*>(st + col * FROWS + seg * 8);
+  }
+  if (a.dy) {   // fused dH = dl · W_fc; each wave owns H/NW columns
+    const int per = a.H / NW, n0 = w * per;
+    int c = 0;
+    for (; c + 64 <= per; c += 64) fc_dh_tile<4>(dlr, ldr, a.WT, V, a.H, a.dy, m0, n0 + c, lane);
+    for (; c < per; c += 16) fc_dh_tile<1>(dlr, ldr, a.WT, V, a.H, a.dy, m0, n0 + c, lane);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -198,10 +244,13 @@ __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
 
 void fc_xent(const FcXentArgs& a, hipStream_t s) {
   const int NW = a.V / 64;
-  const size_t shm = (2 * NW * 32 + 64) * 4 + (size_t)a.V * FROWS * 2;
+  if (a.dy && (a.H % (16 * NW) || a.V % 128 || !a.WT))
+    throw std::runtime_error("fc_xent: fused dH needs H % (V/4) == 0, V % 128 == 0 and W_fc^T");
+  const size_t shm = (2 * NW * 32 + 64) * 4 + (size_t)a.V * FROWS * 2 + (size_t)FROWS * (a.V + 8) * 2;
   const int nks = a.H / 32;
   dim3 grid(a.M / FROWS), block(64 * NW);
-  if (nks % 2 == 0) hipLaunchKernelGGL(fc_xent_kernel<2>, grid, block, shm, s, a);
+  if (nks % 8 == 0) hipLaunchKernelGGL(fc_xent_kernel<4>, grid, block, shm, s, a);
+  else if (nks % 2 == 0) hipLaunchKernelGGL(fc_xent_kernel<2>, grid, block, shm, s, a);
   else hipLaunchKernelGGL(fc_xent_kernel<1>, grid, block, shm, s, a);
 }
 

@@ -13,6 +13,8 @@
 //     vmcnt(0) + barrier per tile;
 //   * XCD-aware bijective block remap (T1) so neighbouring tiles share an L2;
 //   * split-K slabs for the K = B*T weight-gradient products.
+#include <stdexcept>
+#include <string>
 #include "kernels.h"
 #include "common.h"
 
@@ -33,9 +35,7 @@ DEV float sum8f(const bf16x8& v) {
 }
 
 template <bool BIAS, bool ROWSUM>
-__global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, int ntm, int kper) {
-  __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
-  const int id = xcd_remap2(blockIdx.x, gridDim.x);
+DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u16 (&lds)[2][2][128 * 64]) {
   const int tn = id % ntn, tm = (id / ntn) % ntm, sp = id / (ntn * ntm);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -129,6 +129,25 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, i
   }
 }
 
+template <bool BIAS, bool ROWSUM>
+__global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
+  gemm_lds_body<BIAS, ROWSUM>(a, xcd_remap2(blockIdx.x, gridDim.x), ntn, ntm, kper, lds);
+}
+
+// grouped launch: block range [start[k], start[k+1]) serves job k (after the XCD remap, so each
+// job's neighbouring tiles still share an L2)
+struct GemmGroup { GemmArgs job[4]; int start[5]; int ntn[4], ntm[4], kper[4]; int n; };
+
+template <bool BIAS, bool ROWSUM>
+__global__ void __launch_bounds__(256, 2) gemm_lds_group_kernel(GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
+  const int id = xcd_remap2(blockIdx.x, gridDim.x);
+  int k = 0;
+  while (k + 1 < g.n && id >= g.start[k + 1]) ++k;
+  gemm_lds_body<BIAS, ROWSUM>(g.job[k], id - g.start[k], g.ntn[k], g.ntm[k], g.kper[k], lds);
+}
+
 bool gemm_lds_ok(const GemmArgs& a) {
   if (a.onehot_ids) return false;
   if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;
@@ -138,6 +157,32 @@ bool gemm_lds_ok(const GemmArgs& a) {
   if ((a.lda % 8) || (a.ldb % 8)) return false;
   if ((reinterpret_cast<uintptr_t>(a.A) | reinterpret_cast<uintptr_t>(a.B)) & 15) return false;
   return true;
+}
+
+void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s) {
+  if (n < 1 || n > 4) throw std::runtime_error("gemm_lds_group: 1..4 jobs");
+  GemmGroup g;
+  g.n = n;
+  int tot = 0;
+  const bool bias = jobs[0].bias && jobs[0].splits == 1, rs = jobs[0].rowsumA != nullptr;
+  for (int k = 0; k < n; ++k) {
+    const GemmArgs& a = jobs[k];
+    if (!gemm_lds_ok(a) || (a.bias && a.splits == 1) != bias || (a.rowsumA != nullptr) != rs)
+      throw std::runtime_error("gemm_lds_group: job " + std::to_string(k) + " incompatible");
+    g.job[k] = a;
+    g.ntn[k] = a.N / 128; g.ntm[k] = a.M / 128; g.kper[k] = a.K / a.splits;
+    g.start[k] = tot;
+    tot += g.ntn[k] * g.ntm[k] * a.splits;
+  }
+  g.start[n] = tot;
+  dim3 grid(tot), block(256);
+  if (rs) {
+    if (bias) hipLaunchKernelGGL((gemm_lds_group_kernel<true, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((gemm_lds_group_kernel<false, true>), grid, block, 0, s, g);
+  } else {
+    if (bias) hipLaunchKernelGGL((gemm_lds_group_kernel<true, false>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((gemm_lds_group_kernel<false, false>), grid, block, 0, s, g);
+  }
 }
 
 void gemm_lds(const GemmArgs& a, hipStream_t s) {

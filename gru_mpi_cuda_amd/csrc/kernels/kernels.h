@@ -119,6 +119,9 @@ struct FcXentArgs {
   u16* dl = nullptr;               // [M][V] bf16 dL/dlogits
   u16* dlT = nullptr;              // [V][ldT] at column colT + row
   float* loss_part = nullptr;      // [M/32] per-block partial (already scaled)
+  // fused dH = dlogits · W_fc (nullable): dy [M][H] fp32 from WT = W_fc^T [H][V] bf16
+  const u16* WT = nullptr;
+  float* dy = nullptr;
   int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
 };
 void fc_xent(const FcXentArgs& a, hipStream_t s);
@@ -152,6 +155,9 @@ struct GemmArgs {
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
+// several independent LDS-GEMM problems in ONE launch (fills the chip with small products);
+// all jobs gemm_lds_ok, with the same bias / row-sum flags; n <= 4
+void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s);
 void gemm_lds(const GemmArgs& a, hipStream_t s);
 
 // sum `splits` slabs [splits][n] -> dst[n] (optionally also as bf16 and/or accumulate)
@@ -181,14 +187,28 @@ void clip_scale_finalize(const float* partials, int nparts, float clip, float* s
 void sum_partials(const float* partials, int n, float* out, hipStream_t s, int* bump = nullptr);
 
 // multi-tensor launches (one kernel for the whole list)
-struct SlabJob { const float* src; float* dst; long n; int splits; };
-struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0;
-  void add(const float* s, int splits, long n_, float* d) { job[n++] = SlabJob{s, d, n_, splits}; } };
+// job: dst = sum of `splits` consecutive slabs of n floats.  Cast jobs (bf and/or bfT set) see the
+// slab as [R][C] (R, C multiples of 64) and also write bf16 [R][C] / bf16 [C][R] (dst nullable).
+// `bump` (nullable): the launch also increments the device step counter once.
+struct SlabJob { const float* src; float* dst; long n; int splits; u16* bf; u16* bfT; int R, C; };
+struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0; int* bump = nullptr;
+  void add(const float* s, int splits, long n_, float* d) {
+    job[n++] = SlabJob{s, d, n_, splits, nullptr, nullptr, 0, 0}; }
+  void add_cast(const float* s, int splits, int R, int C, float* d, u16* bf, u16* bfT) {
+    job[n++] = SlabJob{s, d, (long)R * C, splits, bf, bfT, R, C}; } };
 void reduce_slabs_multi(SlabJobs& j, hipStream_t s);
 struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; };
 struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
   void add(const float* s, int R, int C, u16* d, u16* dT) { job[n++] = CastJob{s, d, dT, R, C}; } };
 void cast_multi(CastJobs& j, hipStream_t s);
+// Fused optimiser + weight refresh, one launch over every parameter tensor: Adam/SGD on the fp32
+// master slice [off, off+R*C) of the flat buffers, then (matrix jobs) its bf16 copy and/or bf16
+// transpose.  Matrix jobs need R % 64 == 0 and C % 64 == 0; R == 0 marks a flat (bias) job of C
+// elements, C % 4 == 0.
+struct OptCastJob { long off; int R, C; u16* dst; u16* dstT; };
+struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
+  void add(long off, int R, int C, u16* d, u16* dT) { job[n++] = OptCastJob{off, R, C, d, dT}; } };
+void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)
 void spin_delay(int us, hipStream_t s);

@@ -2,6 +2,7 @@
 // weights, column sums, fused Adam/SGD, gradient-norm clipping and deterministic scalar
 // reductions.  All vectorised 16 B per lane (cdna_hip_programming.md Guideline 13) and free
 // of float atomics, so a training step is bitwise reproducible run to run.
+#include <stdexcept>
 #include "kernels.h"
 #include "common.h"
 
@@ -88,10 +89,43 @@ void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
 // One launch for many independent jobs (the tail of a training step is otherwise a chain of
 // tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
 // prefix sum over their block counts.
-__global__ void reduce_multi_kernel(SlabJobs j) {
+__global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
+  __shared__ u16 tile[64][72];
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
+  if (j.bump && b == 0 && threadIdx.x == 0) *j.bump += 1;
   const SlabJob& J = j.job[k];
+  if (J.bf || J.bfT) {   // 64x64 tile: slab sum -> fp32 / bf16 / bf16 transposed
+    const int tiles_c = J.C / 64, t = b - j.blk_start[k];
+    const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const size_t o = (size_t)(r0 + ty + 16 * q) * J.C + c0 + 4 * tx;
+      float4 acc = *reinterpret_cast<const float4*>(J.src + o);
+      for (int sl = 1; sl < J.splits; ++sl) {
+        const float4 v = *reinterpret_cast<const float4*>(J.src + (size_t)sl * J.n + o);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      if (J.dst) *reinterpret_cast<float4*>(J.dst + o) = acc;
+      uint2 w;
+      w.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
+      w.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
+      if (J.bf) *reinterpret_cast<uint2*>(J.bf + o) = w;
+      *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w;
+    }
+    if (!J.bfT) return;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int piece = threadIdx.x + 256 * q, col = piece >> 3, seg = piece & 7;
+      u16 v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
+      *reinterpret_cast<uint4*>(J.bfT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+    }
+    return;
+  }
   const long n4 = J.n / 4;
   const long nb = j.blk_start[k + 1] - j.blk_start[k];
   for (long i = (b - j.blk_start[k]) * (long)blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
@@ -102,18 +136,35 @@ __global__ void reduce_multi_kernel(SlabJobs j) {
     }
     reinterpret_cast<float4*>(J.dst)[i] = acc;
   }
-  if (b == j.blk_start[k])
-    for (long i = n4 * 4 + threadIdx.x; i < J.n; i += blockDim.x) {
-      float acc = 0.f;
-      for (int s = 0; s < J.splits; ++s) acc += J.src[(size_t)s * J.n + i];
-      J.dst[i] = acc;
+  if (b == j.blk_start[k]) {
+    if (J.n < 4) {   // tiny job (e.g. the loss: many one-float partials): one wave, fixed order
+      if (threadIdx.x < 64)
+        for (long i = 0; i < J.n; ++i) {
+          float acc = 0.f;
+          for (int s = threadIdx.x; s < J.splits; s += 64) acc += J.src[(size_t)s * J.n + i];
+          acc = wave_sum(acc);
+          if (threadIdx.x == 0) J.dst[i] = acc;
+        }
+    } else {
+      for (long i = n4 * 4 + threadIdx.x; i < J.n; i += blockDim.x) {
+        float acc = 0.f;
+        for (int s = 0; s < J.splits; ++s) acc += J.src[(size_t)s * J.n + i];
+        J.dst[i] = acc;
+      }
     }
+  }
 }
 void reduce_slabs_multi(SlabJobs& j, hipStream_t s) {
   int tot = 0;
   for (int k = 0; k < j.n; ++k) {
+    const SlabJob& J = j.job[k];
     j.blk_start[k] = tot;
-    long b = (j.job[k].n / 4 + 255) / 256;
+    if (J.bf || J.bfT) {
+      if (J.R % 64 || J.C % 64) throw std::runtime_error("reduce_slabs_multi: cast job needs R, C % 64 == 0");
+      tot += (J.R / 64) * (J.C / 64);
+      continue;
+    }
+    long b = (J.n / 4 + 255) / 256;
     tot += (int)(b < 1 ? 1 : (b > 512 ? 512 : b));
   }
   j.blk_start[j.n] = tot;
@@ -187,6 +238,98 @@ __global__ void adam_kernel(OptimArgs a) {
 }
 void adam_step(const OptimArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks(a.n / 4, 256, 2048)), dim3(256), 0, s, a);
+}
+
+// Adam/SGD update of 4 consecutive elements (same math as adam_kernel)
+struct AdamCoef { float sc, ib1, ib2; };
+DEV AdamCoef adam_coef(const OptimArgs& a) {
+  const int t = *a.step;
+  return AdamCoef{a.gscale ? *a.gscale : 1.f, 1.f / (1.f - powf(a.b1, (float)t)), 1.f / (1.f - powf(a.b2, (float)t))};
+}
+DEV float4 adam4(const OptimArgs& a, const AdamCoef& k, long i /*float4 index*/) {
+  float4 p = reinterpret_cast<float4*>(a.p)[i];
+  const float4 g4 = reinterpret_cast<const float4*>(a.g)[i];
+  float pv[4] = {p.x, p.y, p.z, p.w};
+  const float gv[4] = {g4.x * k.sc, g4.y * k.sc, g4.z * k.sc, g4.w * k.sc};
+  if (a.sgd) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+  } else {
+    const float4 m = reinterpret_cast<float4*>(a.m)[i];
+    const float4 v = reinterpret_cast<float4*>(a.v)[i];
+    float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      mv[e] = a.b1 * mv[e] + (1.f - a.b1) * gv[e];
+      vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
+      float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
+      if (a.wd != 0.f) u += a.wd * pv[e];
+      pv[e] -= a.lr * u;
+    }
+    reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+  }
+  p = make_float4(pv[0], pv[1], pv[2], pv[3]);
+  reinterpret_cast<float4*>(a.p)[i] = p;
+  return p;
+}
+
+// Matrix job: one 64x64 tile per block; thread (ty = tid/16, tx = tid%16) updates rows ty+16q,
+// columns 4tx..4tx+3 with float4 traffic, writes the row-major bf16 copy as 8-B stores, and the
+// transpose leaves through an LDS tile as 16-B stores (8 consecutive rows of one column).
+__global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs j) {
+  __shared__ u16 tile[64][72];    // [row][col] bf16, padded
+  int b = blockIdx.x, k = 0;
+  while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
+  const OptCastJob& J = j.job[k];
+  const int t = b - j.blk_start[k];
+  const AdamCoef co = adam_coef(a);
+  if (J.R == 0) {   // flat job: 1024 elements per block
+    const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
+    if ((long)t * 1024 + threadIdx.x * 4 < J.C) adam4(a, co, i4);
+    return;
+  }
+  const int tiles_c = J.C / 64;
+  const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + ty + 16 * q, c = c0 + 4 * tx;
+    const float4 p = adam4(a, co, (J.off + (long)r * J.C + c) >> 2);
+    const u16 h0 = f2bf(p.x), h1 = f2bf(p.y), h2 = f2bf(p.z), h3 = f2bf(p.w);
+    if (J.dst) {
+      uint2 w;
+      w.x = (unsigned)h0 | ((unsigned)h1 << 16);
+      w.y = (unsigned)h2 | ((unsigned)h3 << 16);
+      *reinterpret_cast<uint2*>(J.dst + (size_t)r * J.C + c) = w;
+    }
+    if (!J.dstT) continue;
+    uint2 w2;
+    w2.x = (unsigned)h0 | ((unsigned)h1 << 16);
+    w2.y = (unsigned)h2 | ((unsigned)h3 << 16);
+    *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w2;
+  }
+  if (!J.dstT) return;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int piece = threadIdx.x + 256 * q;          // 64 columns x 8 row segments
+    const int col = piece >> 3, seg = piece & 7;
+    u16 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
+    *reinterpret_cast<uint4*>(J.dstT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+  }
+}
+void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
+  int tot = 0;
+  for (int k = 0; k < j.n; ++k) {
+    const OptCastJob& J = j.job[k];
+    j.blk_start[k] = tot;
+    tot += J.R == 0 ? (J.C + 1023) / 1024 : (J.R / 64) * (J.C / 64);
+  }
+  j.blk_start[j.n] = tot;
+  hipLaunchKernelGGL(adam_cast_kernel, dim3(tot), dim3(256), 0, s, a, j);
 }
 
 __global__ void bump_kernel(int* step) { *step += 1; }

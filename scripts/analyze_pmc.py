@@ -1,0 +1,47 @@
+"""Summarise rocprofv3 --pmc counter CSVs (scripts/gpu_pmc.sh) per kernel: sums each counter over
+the dispatches of the LAST timed step window (all dispatches / number of bench steps incl. warmup
+is not used -- totals are per whole run) and derives MFMA utilisation, LDS conflict rate, bytes."""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.split("(")[0]
+    return name[:60]
+
+
+def main(root: str) -> None:
+    tot = defaultdict(lambda: defaultdict(float))
+    nd = defaultdict(set)
+    for f in glob.glob(os.path.join(root, "g*", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k = short(r.get("Kernel_Name", "?"))
+                tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                nd[k].add((f, r.get("Dispatch_Id")))
+    rows = []
+    for k, c in tot.items():
+        mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0)
+        busy = c.get("SQ_BUSY_CU_CYCLES", 0.0)
+        lds = c.get("SQ_LDS_IDX_ACTIVE", 0.0)
+        bc = c.get("SQ_LDS_BANK_CONFLICT", 0.0)
+        rows.append((gui, k, dict(
+            mfma_util_pct=100.0 * mf / (gui * 1024) if gui else None,   # 256 CUs x 4 SIMDs
+            mfma_bf16_gflop=c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512 / 1e9,
+            lds_conflict_pct=100.0 * bc / lds if lds else None,
+            fetch_MB=c.get("FETCH_SIZE", 0.0) / 1024, write_MB=c.get("WRITE_SIZE", 0.0) / 1024,
+            cu_busy_cycles=busy)))
+    rows.sort(reverse=True)
+    print(f"{'kernel':60s} {'MFMA%':>7s} {'bf16GF':>9s} {'LDSconf%':>9s} {'fetchMB':>9s} {'writeMB':>9s}")
+    for gui, k, d in rows:
+        f = lambda v, fmt: (fmt % v) if v is not None else "-"  # noqa: E731
+        print(f"{k:60s} {f(d['mfma_util_pct'], '%7.1f')} {d['mfma_bf16_gflop']:9.2f} "
+              f"{f(d['lds_conflict_pct'], '%9.2f')} {d['fetch_MB']:9.1f} {d['write_MB']:9.1f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

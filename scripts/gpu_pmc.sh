@@ -1,0 +1,17 @@
+#!/bin/bash
+# usage: gpu_pmc.sh TAG [bench args...] -> gpurun_out/pmc_TAG/{g1,g2,g3}/ + pmc_TAG/summary.txt
+# Hardware counters per kernel (MFMA busy, LDS bank conflicts, HBM bytes), one counter group per
+# rocprofv3 run, --pmc combined with --kernel-trace only (never with sys/runtime traces).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=$1; shift
+out=gpurun_out/pmc_$tag; mkdir -p $out
+groups=("SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16"
+        "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES"
+        "FETCH_SIZE WRITE_SIZE")
+i=0
+for g in "${groups[@]}"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $g --output-format csv -d $out/g$i -o run -- python3 bench.py --steps 3 --warmup 2 "$@" > $out/g$i.log 2>&1
+  rc=$?; echo "pmc group $i rc=$rc"; [ $rc -gt 1 ] && exit $rc
+done
+python3 scripts/analyze_pmc.py $out | tee $out/summary.txt

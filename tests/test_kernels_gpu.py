@@ -161,8 +161,10 @@ def test_bwd_step(ext, first, H, Bp, algo):
     torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
 
 
-def test_fc_xent(ext):
-    M, H, V = 128, 256, 256
+@pytest.mark.parametrize("fused_dh", [False, True])
+@pytest.mark.parametrize("H", [256, 320])
+def test_fc_xent(ext, fused_dh, H):
+    M, V = 128, 256
     X = bf(rnd(M, H, seed=1))
     W = bf(rnd(V, H, scale=H ** -0.5, seed=2))
     b = rnd(V, scale=0.5, seed=3)
@@ -172,8 +174,13 @@ def test_fc_xent(ext):
     dl = torch.empty(M, V, device=DEV, dtype=torch.bfloat16)
     dlT = torch.zeros(V, 2 * M, device=DEV, dtype=torch.bfloat16)
     lp = torch.empty(M // 32, device=DEV)
-    ext.fc_xent(dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), labels=y.data_ptr(), inv_count=inv.data_ptr(),
-                     dl=dl.data_ptr(), dlT=dlT.data_ptr(), loss_part=lp.data_ptr(), M=M, H=H, V=V, ldT=2 * M, colT=M), S())
+    d = dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), labels=y.data_ptr(), inv_count=inv.data_ptr(),
+             dl=dl.data_ptr(), dlT=dlT.data_ptr(), loss_part=lp.data_ptr(), M=M, H=H, V=V, ldT=2 * M, colT=M)
+    WT = W.T.contiguous()
+    dy = torch.full((M, H), float("nan"), device=DEV)
+    if fused_dh:
+        d.update(WT=WT.data_ptr(), dy=dy.data_ptr())
+    ext.fc_xent(d, S())
     torch.cuda.synchronize()
     logits = X.float() @ W.float().T + b
     valid = y >= 0
@@ -184,6 +191,8 @@ def test_fc_xent(ext):
     torch.testing.assert_close(lp.sum(), loss, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(dl.float(), ref, atol=1e-4, rtol=1e-2)
     torch.testing.assert_close(dlT[:, M:].T, dl, atol=0, rtol=0)
+    if fused_dh:   # dH = dlogits(bf16) · W_fc, fp32 accumulate
+        torch.testing.assert_close(dy, dl.float() @ W.float(), atol=1e-5, rtol=1e-3)
 
 
 def test_fc_sample(ext):
