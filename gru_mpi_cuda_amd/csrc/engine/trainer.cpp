@@ -450,14 +450,38 @@ void Trainer::optimizer_step(hipStream_t s) {
 void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets) {
   comm_ = c;
   buckets_ = buckets;
+  // buckets minus the embedding and W_ih0 segments (their gradients are recomputed from the
+  // all-reduced dP after the collective)
+  const long e0 = off_.at("embedding"), e1 = e0 + (long)d_.V * d_.E;
+  const long w0 = off_.at("weight_ih_l0"), w1 = w0 + 3L * d_.H * d_.E;
+  buckets_dp_.clear();
+  for (const auto& b : buckets) {
+    std::vector<std::pair<long, long>> pieces{{b.first, b.first + b.second}};
+    for (const auto& ex : {std::make_pair(e0, e1), std::make_pair(w0, w1)}) {
+      std::vector<std::pair<long, long>> next;
+      for (const auto& p : pieces) {
+        if (ex.second <= p.first || ex.first >= p.second) { next.push_back(p); continue; }
+        if (p.first < ex.first) next.push_back({p.first, ex.first});
+        if (ex.second < p.second) next.push_back({ex.second, p.second});
+      }
+      pieces.swap(next);
+    }
+    for (const auto& p : pieces)
+      if (p.second > p.first) buckets_dp_.push_back({p.first, p.second - p.first});
+  }
   g_step_[0].reset();
   g_step_[1].reset();
 }
 
-void Trainer::record_allreduce(hipStream_t s) {
+void Trainer::record_allreduce(hipStream_t s, bool dp_trick) {
   // bucketed mean all-reduce of the flat fp32 gradient over xGMI (RCCL).  Buckets follow the
   // gradient-readiness order of the flat layout (FC, top layer ... layer 0, embedding).
   if (!comm_) return;
+  if (dp_trick) {
+    for (const auto& b : buckets_dp_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
+    comm_->allreduce_avg_f32(dP_, (long)d_.V * 3 * d_.H, s);
+    return;
+  }
   for (const auto& b : buckets_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
 }
 
@@ -482,8 +506,16 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
-      if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
-      record_allreduce(s0_);
+      if (dp_trick()) {
+        // all-reduce [fc, recurrent, bias grads, dP] (5.25 MB instead of 7.35 MB at H=512), then
+        // derive dEmb / dW_ih0 from the averaged dP locally
+        record_fb_seq(s0_, /*defer_tail=*/true);
+        record_allreduce(s0_, true);
+        record_emb_tail(s0_, true);
+      } else {
+        if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+        record_allreduce(s0_);
+      }
       record_opt(s0_);
     } catch (...) {
       hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow

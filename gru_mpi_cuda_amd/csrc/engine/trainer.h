@@ -88,7 +88,11 @@ class Trainer {
   Graph g_step_[2];
   RcclComm* comm_ = nullptr;
   std::vector<std::pair<long, long>> buckets_;
-  void record_allreduce(hipStream_t s);
+  // data-parallel: all-reduce dP = dL/d(Emb·W_ih0^T) [V][3H] instead of dEmb + dW_ih0 (both are
+  // linear in dP with replicated Emb / W_ih0): buckets_dp_ = buckets_ minus those two segments
+  std::vector<std::pair<long, long>> buckets_dp_;
+  bool dp_trick() const { return comm_ != nullptr && !overlap_; }
+  void record_allreduce(hipStream_t s, bool dp_trick = false);
  public:
   void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
   void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets);
@@ -112,7 +116,8 @@ class Trainer {
     bool bwd = false, fuse_w = false, fuse_p = false;
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
   };
-  void record_fb_seq(hipStream_t s0);
+  void record_fb_seq(hipStream_t s0, bool defer_tail = false);
+  void record_emb_tail(hipStream_t s, bool from_fp32);
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;

@@ -28,7 +28,7 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
   reduce_slabs_multi(j, s);
 }
 
-void Trainer::record_fb_seq(hipStream_t s) {
+void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
   const int H3 = 3 * H, nrb = B / 32;
   const long tok = (long)T * B;
@@ -128,8 +128,12 @@ void Trainer::record_fb_seq(hipStream_t s) {
     SlabJobs j;
     if (q.fuse_w) j.add(q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
     if (q.bwd) j.add(q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
-    // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail
-    if (l == 0 && q.fuse_p) j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
+    // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail -- or, when the
+    // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
+    if (l == 0 && q.fuse_p) {
+      if (defer_tail) j.add(dP_part_, nrb, (long)V * H3, dP_);
+      else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
+    }
     if (l == 0 && q.bwd) j.add(q.dbih_part, nrb, H3, G("bias_ih_l0"));
     if (l == 0) {   // + dW_fc / db_fc slabs, the loss partials, and the optimiser step counter
       for (int k2 = 0; k2 < tail.n; ++k2) j.job[j.n++] = tail.job[k2];
@@ -163,31 +167,36 @@ void Trainer::record_fb_seq(hipStream_t s) {
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients
-  {
-    if (!seq_[0].fuse_p) {
-      CastJobs j;
-      j.add(dP_, V, H3, dP_bf_, dPT_bf_);
-      cast_multi(j, s);
-    }
-    GemmArgs g;   // dW_ih0 = dP^T · Emb
-    g.A = dPT_bf_; g.lda = V; g.B = EmbT; g.ldb = V; g.C = G("weight_ih_l0"); g.ldc = E;
-    g.M = H3; g.N = E; g.K = V;
-    GemmArgs e;   // dEmb = dP · W_ih0, split-K (K = 3H on only V x E outputs) into slab_e_
-    int se = splits_;
-    while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
-    e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = slab_e_; e.ldc = E;
-    e.M = V; e.N = E; e.K = H3; e.splits = se;
-    const GemmArgs both[2] = {g, e};
-    if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
-      gemm_lds_group(both, 2, s);   // one launch for both small products
-    } else {
-      gemm_nt(g, s);
-      gemm_nt(e, s);
-    }
-    SlabJobs r;
-    r.add(slab_e_, se, (long)V * E, G("embedding"));
-    reduce_slabs_multi(r, s);
+  if (!defer_tail) record_emb_tail(s, !seq_[0].fuse_p);
+  HIP_LAUNCH_CHECK();
+}
+
+// dEmb = dP · W_ih0 and dW_ih0 = dP^T · Emb from the layer-0 table gradient dP
+void Trainer::record_emb_tail(hipStream_t s, bool from_fp32) {
+  const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
+  if (from_fp32) {
+    CastJobs j;
+    j.add(dP_, V, H3, dP_bf_, dPT_bf_);
+    cast_multi(j, s);
   }
+  GemmArgs g;   // dW_ih0 = dP^T · Emb
+  g.A = dPT_bf_; g.lda = V; g.B = EmbT; g.ldb = V; g.C = G("weight_ih_l0"); g.ldc = E;
+  g.M = H3; g.N = E; g.K = V;
+  GemmArgs e;   // dEmb = dP · W_ih0, split-K (K = 3H on only V x E outputs) into slab_e_
+  int se = splits_;
+  while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
+  e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = slab_e_; e.ldc = E;
+  e.M = V; e.N = E; e.K = H3; e.splits = se;
+  const GemmArgs both[2] = {g, e};
+  if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
+    gemm_lds_group(both, 2, s);   // one launch for both small products
+  } else {
+    gemm_nt(g, s);
+    gemm_nt(e, s);
+  }
+  SlabJobs r;
+  r.add(slab_e_, se, (long)V * E, G("embedding"));
+  reduce_slabs_multi(r, s);
   HIP_LAUNCH_CHECK();
 }
 

@@ -121,8 +121,9 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   float* red = smem;                               // [2][NW][32]
   float* lab = smem + 2 * NW * 32;                 // [32] label logit
   float* lrow = lab + 32;                          // [32] per-row loss
-  u16* st = reinterpret_cast<u16*>(lrow + 32);     // [V][32] bf16 dl^T staging
-  u16* dlr = st + (size_t)V * FROWS;               // [32][V+8] bf16 dl row-major (dH A operand)
+  u16* st = reinterpret_cast<u16*>(lrow + 32);     // [V][40] bf16 dl^T staging (80-B column stride:
+                                                   // the 16 column lanes of a write hit distinct banks)
+  u16* dlr = st + (size_t)V * 40;                  // [32][V+8] bf16 dl row-major (dH A operand)
   float mx[2][4], se[2][4];
   row_stats(acc, red, NW, lane, w, mx, se);
   const float inv = a.inv_count[0];
@@ -144,7 +145,7 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
         const float d = (p - (col == y ? 1.f : 0.f)) * scale;
         const u16 db = f2bf(d);
         if (a.dl) a.dl[(size_t)(m0 + row) * V + col] = db;
-        st[col * FROWS + row] = db;
+        st[col * 40 + row] = db;
         dlr[row * ldr + col] = db;
       }
     }
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   for (int q = threadIdx.x; q < V * 4; q += blockDim.x) {
     const int col = q >> 2, seg = q & 3;
     *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) =
-        *reinterpret_cast<const uint4*>(st + col * FROWS + seg * 8);
+        *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
   }
   if (a.dy) {   // fused dH = dl · W_fc; each wave owns H/NW columns
     const int per = a.H / NW, n0 = w * per;
@@ -246,7 +247,7 @@ void fc_xent(const FcXentArgs& a, hipStream_t s) {
   const int NW = a.V / 64;
   if (a.dy && (a.H % (16 * NW) || a.V % 128 || !a.WT))
     throw std::runtime_error("fc_xent: fused dH needs H % (V/4) == 0, V % 128 == 0 and W_fc^T");
-  const size_t shm = (2 * NW * 32 + 64) * 4 + (size_t)a.V * FROWS * 2 + (size_t)FROWS * (a.V + 8) * 2;
+  const size_t shm = (2 * NW * 32 + 64) * 4 + (size_t)a.V * 40 * 2 + (size_t)FROWS * (a.V + 8) * 2;
   const int nks = a.H / 32;
   dim3 grid(a.M / FROWS), block(64 * NW);
   if (nks % 8 == 0) hipLaunchKernelGGL(fc_xent_kernel<4>, grid, block, shm, s, a);

@@ -90,7 +90,7 @@ void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
 // tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
 // prefix sum over their block counts.
 __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
-  __shared__ u16 tile[64][72];
+  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   if (j.bump && b == 0 && threadIdx.x == 0) *j.bump += 1;
@@ -278,7 +278,7 @@ DEV float4 adam4(const OptimArgs& a, const AdamCoef& k, long i /*float4 index*/)
 // columns 4tx..4tx+3 with float4 traffic, writes the row-major bf16 copy as 8-B stores, and the
 // transpose leaves through an LDS tile as 16-B stores (8 consecutive rows of one column).
 __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs j) {
-  __shared__ u16 tile[64][72];    // [row][col] bf16, padded
+  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)    // [row][col] bf16, padded
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   const OptCastJob& J = j.job[k];

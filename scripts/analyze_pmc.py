@@ -1,6 +1,6 @@
-"""Summarise rocprofv3 --pmc counter CSVs (scripts/gpu_pmc.sh) per kernel: sums each counter over
-the dispatches of the LAST timed step window (all dispatches / number of bench steps incl. warmup
-is not used -- totals are per whole run) and derives MFMA utilisation, LDS conflict rate, bytes."""
+"""Summarise rocprofv3 --pmc counter CSVs (scripts/gpu_pmc.sh) per kernel, summed over all of its
+dispatches in the run: MFMA utilisation (busy cycles / SIMD cycles), bf16 MFMA GFLOP
+(MOPS x 512), LDS bank-conflict rate (conflict cycles / LDS active cycles)."""
 import csv
 import glob
 import os
@@ -30,7 +30,8 @@ def main(root: str) -> None:
         lds = c.get("SQ_LDS_IDX_ACTIVE", 0.0)
         bc = c.get("SQ_LDS_BANK_CONFLICT", 0.0)
         rows.append((gui, k, dict(
-            mfma_util_pct=100.0 * mf / (gui * 1024) if gui else None,   # 256 CUs x 4 SIMDs
+            # MFMA_BUSY is summed over the 1024 SIMDs; GRBM_GUI_ACTIVE over the 8 XCDs
+            mfma_util_pct=100.0 * mf / (1024 * gui / 8) if gui else None,
             mfma_bf16_gflop=c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512 / 1e9,
             lds_conflict_pct=100.0 * bc / lds if lds else None,
             fetch_MB=c.get("FETCH_SIZE", 0.0) / 1024, write_MB=c.get("WRITE_SIZE", 0.0) / 1024,

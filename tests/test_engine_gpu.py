@@ -133,13 +133,16 @@ def test_generator_matches_cpu():
     assert same >= 0.9, same
 
 
-def test_single_graph_step_with_rccl_world1():
+@pytest.mark.parametrize("layers,E,H,bucket_mb", [(1, 256, 256, 8.0), (2, 128, 256, 0.25), (1, 512, 512, 1.0)])
+def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb):
     """The whole step as one graph with a captured RCCL all-reduce (1-rank communicator):
-    must equal the no-comm step bit for bit (mean over one rank is the identity)."""
+    must equal the no-comm step bit for bit (mean over one rank is the identity).  With a
+    communicator the step all-reduces dP instead of dEmb / dW_ih0 and derives those two after
+    the collective; small buckets exercise the bucket split around the excluded segments."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
-    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=3)
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=64, seq=8, seed=3, bucket_mb=bucket_mb)
     x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
     comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1)
     a = HipTrainer(cfg, params=init_params(cfg), comm=comm)
