@@ -153,6 +153,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
     SeqFwdArgs a;
     a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+    a.xch = GP(u16, d, "xch");
+    if (!a.xch) throw std::runtime_error("fwd_seq: exchange buffer xch [T][Bp][H] bf16 required");
     a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
     a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
     a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");

@@ -72,7 +72,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
   size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
-  size_t o_sfc2 = R((size_t)splits_ * V * H * 4), o_rfc2 = R((size_t)splits_ * V * 4);
+  size_t o_sfc2 = R((size_t)kFcSplitsMax * V * H * 4), o_rfc2 = R((size_t)kFcSplitsMax * V * 4);
   size_t o_se = R((size_t)splits_ * V * E * 4);
   std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0);
   for (int l = 0; l < L; ++l) {

@@ -9,6 +9,7 @@
 // Every layer falls back to the per-timestep kernels when its shape cannot be made
 // co-resident (gru_*_seq_supported), so any config still runs -- just slower.
 #include "trainer.h"
+#include <algorithm>
 
 namespace gk {
 
@@ -58,6 +59,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
     if (persist_fwd_) {
       SeqFwdArgs a;
       a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B;
+      a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
       a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
       a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
       if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
@@ -92,8 +94,11 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
     }
     // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T: split-K into dedicated slabs whose
     // reduce joins the multi-tensor reduce after the backward sweep (one launch fewer)
-    int sp = splits_;
-    while (sp > 1 && (tok % sp || (tok / sp) % 128)) sp >>= 1;
+    // few output tiles (V x H): split K until ~256 workgroups fill the chip
+    const int tiles = std::max(1, (V / 128) * (H / 128));
+    int sp = 1;
+    while (sp * 2 <= kFcSplitsMax && tiles * sp < 256 && tok % (sp * 2) == 0 && (tok / (sp * 2)) % 128 == 0)
+      sp *= 2;
     GemmArgs w;
     w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;
     w.C = slab_fc2_; w.ldc = H; w.rowsumA = rs_fc2_;

@@ -86,6 +86,39 @@ DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch,
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Streaming variant: lane p polls producer p; k-step kk reads the columns of producers 2kk and
+// 2kk+1, and its payload loads (loadk(kk): sc1 loads into registers) are issued as soon as BOTH
+// have published -- the early producers' data is in flight while the wave still waits for the
+// late ones.  The MFMAs run afterwards in fixed k order, so results stay deterministic.  Every
+// load follows, in this wave, a poll that saw its producers' flags (R1 hand-off, no acquire).
+template <int NK, class LoadK>
+DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned epoch, unsigned* err,
+                        LoadK&& loadk) {
+  constexpr unsigned all = (1u << NK) - 1u;
+  unsigned loaded = 0, spins = 0;
+  for (;;) {
+    bool ok = true;
+    if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+    const unsigned long long m = __ballot(ok);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk)
+      if (!((loaded >> kk) & 1u) && ((m >> (2 * kk)) & 3ull) == 3ull) {
+        loadk(kk);
+        loaded |= 1u << kk;
+      }
+    if (loaded == all) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSpinLimit) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk)
+        if (!((loaded >> kk) & 1u)) loadk(kk);   // garbage, flagged: keep the grid draining
+      break;
+    }
+  }
+}
 DEV void signal_flag(unsigned* flag, unsigned epoch) {
   __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -95,7 +128,7 @@ DEV void signal_flag(unsigned* flag, unsigned epoch) {
 // memset graph node per step.
 DEV void zero_next_flags(unsigned* p, long n) {
   if (!p) return;
-  const long wg = (long)blockIdx.y * gridDim.x + blockIdx.x, nwg = (long)gridDim.x * gridDim.y;
+  const long wg = blockIdx.x, nwg = gridDim.x;
   for (long i = wg * blockDim.x + threadIdx.x; i < n; i += nwg * blockDim.x) p[i] = 0u;
 }
 
@@ -103,12 +136,18 @@ DEV void zero_next_flags(unsigned* p, long n) {
 // Only written when the caller passes a dbg buffer; nothing reads them inside the kernel.
 DEV void stamp(unsigned long long* dbg, int t, int k) {
   if (!dbg || threadIdx.x != 0) return;
-  const bool first = blockIdx.x == 0 && blockIdx.y == 0;
-  const bool last = blockIdx.x == gridDim.x - 1 && blockIdx.y == gridDim.y - 1;
+  const bool first = blockIdx.x == 0;
+  const bool last = blockIdx.x == gridDim.x - 1;
   if (!first && !last) return;
   const unsigned long long v = __builtin_amdgcn_s_memrealtime();
   dbg[((last ? 1 : 0) * 4096 + t) * 8 + k] = v;
 }
+
+// Workgroup -> (unit tile, row block): 1-D grid, unit tile as the fast index.  (Putting all unit
+// tiles of a row block on one XCD -- row block fast, so blocks b and b+8 of a row block share an
+// L2 -- measured no faster standalone and ~25 us slower inside the step: profiles/.)
+DEV int seq_unit_tile(int nrb) { return (int)(blockIdx.x % (gridDim.x / nrb)); }
+DEV int seq_row_block(int nrb) { return (int)(blockIdx.x / (gridDim.x / nrb)); }
 
 // ==================================================================== forward
 template <int NKW>
@@ -118,7 +157,8 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   __shared__ __attribute__((aligned(16))) u16 stgT[16][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = a.H, Bp = a.Bp, T = a.T;
-  const int j0 = blockIdx.x * 16, rbk = blockIdx.y, b0 = rbk * 32;
+  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
+  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
   const int k0 = w * NKW * 32;
   const unsigned nunit = (unsigned)(H / 16);
@@ -138,6 +178,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + j];
   float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
   const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+  const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
   zero_next_flags(a.zero_next, a.zero_words);
 
   for (int t = 0; t < T; ++t) {
@@ -153,15 +194,26 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     zero_acc(acc);
     if (t > 0 || a.h0) {
       // wave w's K-slice [k0, k0 + 32*NKW) is produced by unit tiles k0/16 .. k0/16 + 2*NKW - 1
-      if (t > 0) wave_wait(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
-                           (unsigned)t, a.err);
-      stamp(a.dbg, t, 1);
       bf16x8 af[NKW][2];
-      const unsigned base = (unsigned)((((size_t)t * Bp + b0 + lr) * H + k0 + lk) * 2);
+      if (t > 0) {
+        // h_t from the producers' exchange tiles (written at step t-1); unit u = k0 + 32kk + lk
+        // lives in tile u/16 at column u%16
+        const size_t slot = ((size_t)(t - 1) * nrb + rbk) * nunit;
+        wave_wait_load<NKW>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
+                            (unsigned)t, a.err, [&](int kk) {
+          const int u = k0 + kk * 32 + lk;
+          const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
 #pragma unroll
-      for (int kk = 0; kk < NKW; ++kk)
+          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 16 * 2));
+        });
+      } else {   // h_init, row-major HS[0] (written before the launch)
+        const unsigned base = (unsigned)((((size_t)b0 + lr) * H + k0 + lk) * 2);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rH, base + (unsigned)(r * 16 * H * 2 + kk * 64));
+        for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rH, base + (unsigned)(r * 16 * H * 2 + kk * 64));
+      }
+      stamp(a.dbg, t, 1);
 #pragma unroll
       for (int kk = 0; kk < NKW; ++kk)
 #pragma unroll
@@ -190,27 +242,29 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     const float n = tanhf_(gi[2] + r * gh[2]);
     const float h = n + z * (hp - n);
     hp = h;
-    a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
-    if (a.sr) {
-      const size_t so = ((size_t)t * Bp + b) * H + j;
-      a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = gh[2];
-    }
     const u16 hb = f2bf(h);
     stg[row][col] = hb;
     stgT[col][row] = hb;
     __syncthreads();
     stamp(a.dbg, t, 3);
     if (w == 0) {
-      // publish: the 32x16 bf16 tile, 16 B per lane, write-through; drain; one signal
+      // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
+      // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
-      const unsigned off = (unsigned)((((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) * 2);
-      st16_sc1(rH, off, v);
+      st16_sc1(rX, (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2, v);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + blockIdx.x) * kFlagStride, (unsigned)(t + 1));
+      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride, (unsigned)(t + 1));
       stamp(a.dbg, t, 4);
+      *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
     } else if (w == 1 && a.HT) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane >> 2][(lane & 3) * 8]);
       *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
+    }
+    // saves for the backward pass AFTER the publish, so they are not part of wave 0's drain
+    a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
+    if (a.sr) {
+      const size_t so = ((size_t)t * Bp + b) * H + j;
+      a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = gh[2];
     }
   }
 }
@@ -227,7 +281,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float red[6][16][33];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = a.H, H3 = 3 * a.H, Bp = a.Bp, T = a.T;
-  const int j0 = blockIdx.x * 16, rbk = blockIdx.y, b0 = rbk * 32;
+  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
+  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
   const int k0 = w * NKW3 * 32;
   const unsigned nunit = (unsigned)(H / 16);
@@ -273,15 +328,18 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     acc[1] = acc[0];
     if (s > 0) {
       // wave w's columns [k0, k0 + 32*NKW3) of dGh (3 gates x H) come from unit tiles ((k0+16p) mod H)/16
-      wave_wait(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3, ((k0 + 16 * lane) % H) / 16,
-                (unsigned)s, a.err);
-      stamp(a.dbg, s, 1);
       bf16x8 af[NKW3][2];
-      const unsigned base = (unsigned)((((size_t)(t + 1) * Bp + b0 + lr) * H3 + k0 + lk) * 2);
+      // dGh_{t+1} column c = k0 + 32kk + lk (gate c/H, unit c%H) lives in producer tile (c%H)/16 of
+      // slot t+1 at column (c/H)*16 + c%16
+      const size_t slot = ((size_t)(t + 1) * nrb + rbk) * nunit;
+      wave_wait_load<NKW3>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3,
+                           ((k0 + 16 * lane) % H) / 16, (unsigned)s, a.err, [&](int kk) {
+        const int c = k0 + kk * 32 + lk, u = c % H;
+        const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 48 + (c / H) * 16 + (u & 15)) * 2;
 #pragma unroll
-      for (int kk = 0; kk < NKW3; ++kk)
-#pragma unroll
-        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, base + (unsigned)(r * 16 * H3 * 2 + kk * 64));
+        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 48 * 2));
+      });
+      stamp(a.dbg, s, 1);
 #pragma unroll
       for (int kk = 0; kk < NKW3; ++kk)
 #pragma unroll
@@ -307,23 +365,20 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dhn), bi = f2bf(dan);
     srow[row][col] = br; srow[row][16 + col] = bz; srow[row][32 + col] = bn;
     sgT[0][col][row] = br; sgT[1][col][row] = bz; sgT[2][col][row] = bn; sgT[3][col][row] = bi;
-    if (a.dgi) {
-      const size_t og = ((size_t)t * Bp + b) * H3 + j;
-      a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
-    }
     __syncthreads();
     stamp(a.dbg, s, 3);
     if (w == 0) {
-      // publish dGh_t rows b0..b0+31, cols {g*H + j0 .. +15}: 3 x 16 B per lane, write-through
-      const int rr = lane >> 1, hf = lane & 1;
+      // publish the dGh_t tile [32 rows][3 gates x 16] (3 KB, whole lines of its own) to slot t:
+      // 3 x 16 B per lane, write-through
+      const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (32 * 48);
 #pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[rr][g * 16 + hf * 8]);
-        const unsigned off = (unsigned)((((size_t)t * Bp + b0 + rr) * H3 + g * H + j0 + hf * 8) * 2);
-        st16_sc1(rX, off, v);
+      for (int i = 0; i < 3; ++i) {
+        const int q = lane + 64 * i, rr = q / 6, sg = q % 6;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[rr][sg * 8]);
+        st16_sc1(rX, (unsigned)((tile + rr * 48 + sg * 8) * 2), v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + blockIdx.x) * kFlagStride, (unsigned)(s + 1));
+      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride, (unsigned)(s + 1));
       stamp(a.dbg, s, 4);
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate
@@ -334,6 +389,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       const size_t rowsel = (size_t)(gg * H + j0 + (lane >> 2)) * a.ldG + c0;
       if (g < 3) *reinterpret_cast<u32x4*>(a.dghT + rowsel) = v;
       if (g != 2) *reinterpret_cast<u32x4*>(a.dgiT + rowsel) = v;
+    }
+    if (a.dgi) {   // row-major dGi for the layer below, after the publish (not in wave 0's drain)
+      const size_t og = ((size_t)t * Bp + b) * H3 + j;
+      a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
     }
     // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS)
     if constexpr (NTW > 0 || NTP > 0) {
@@ -427,7 +486,7 @@ bool gru_fwd_seq_supported(int H, int Bp) {
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
-  dim3 grid(a.H / 16, a.Bp / 32), block(512);
+  dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   switch (a.H) {
     case 256: hipLaunchKernelGGL(gru_fwd_seq_kernel<1>, grid, block, 0, s, a); break;
     case 512: hipLaunchKernelGGL(gru_fwd_seq_kernel<2>, grid, block, 0, s, a); break;
@@ -453,7 +512,7 @@ bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
 }
 
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
-  dim3 grid(a.H / 16, a.Bp / 32), block(512);
+  dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
 #define X(HH, NK, NW, NP)                                                        \
   if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                          \

@@ -66,6 +66,9 @@ void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s);
 // (H/16) x (Bp/32) workgroups; callers check *_supported() and fall back to per-step kernels.
 struct SeqFwdArgs {
   u16* HSb = nullptr;              // [T+1][Bp][H] bf16; HS[0] = h_init, step t writes HS[t+1]
+  // exchange copy of h_{t+1}, tiled per producer: [T][Bp/32][H/16][32 rows][16] bf16 -- every
+  // 128-B line belongs to ONE producer, so a consumer never loads a line part of which is unpublished
+  u16* xch = nullptr;
   float* HSf = nullptr;            // [T+1][Bp][H] fp32
   u16* HT = nullptr; int ldT = 0;  // [H][ldT] bf16, h_t at column (t+1)*Bp + b (nullable)
   float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
@@ -91,7 +94,8 @@ struct SeqBwdArgs {
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
   const u16* WhhT = nullptr;       // [H][3H]
-  u16* xbuf = nullptr;             // [T][Bp][3H] dGh exchange buffer (one slot per step: no WAR reuse)
+  u16* xbuf = nullptr;             // dGh exchange, one slot per step (no WAR reuse), tiled per producer:
+                                   // [T][Bp/32][H/16][32 rows][48 = 3 gates x 16] bf16
   u16* dghT = nullptr; u16* dgiT = nullptr; int ldG = 0;   // [3H][ldG] transposed copies (nullable)
   u16* dgi = nullptr;              // [T][Bp][3H] row-major dGi (nullable)
   float* dWhh_part = nullptr;      // [Bp/32][3H][H] fused dW_hh partials (nullable = not fused)

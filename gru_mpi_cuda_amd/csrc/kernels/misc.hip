@@ -89,6 +89,23 @@ void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
 // One launch for many independent jobs (the tail of a training step is otherwise a chain of
 // tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
 // prefix sum over their block counts.
+// acc = sum over `splits` slabs (stride n floats) of the float4 at src + o, slab order 0,1,2,...
+// (deterministic), with the loads of 8 slabs in flight at once instead of one dependent
+// round trip per slab
+DEV float4 sum_slabs4(const float* __restrict__ src, long n, int splits, size_t o) {
+  float4 acc = *reinterpret_cast<const float4*>(src + o);
+  for (int s0 = 1; s0 < splits; s0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (s0 + k < splits) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(s0 + k) * n + o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (s0 + k < splits) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+  }
+  return acc;
+}
+
 __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
   __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)
   int b = blockIdx.x, k = 0;
@@ -102,11 +119,7 @@ __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const size_t o = (size_t)(r0 + ty + 16 * q) * J.C + c0 + 4 * tx;
-      float4 acc = *reinterpret_cast<const float4*>(J.src + o);
-      for (int sl = 1; sl < J.splits; ++sl) {
-        const float4 v = *reinterpret_cast<const float4*>(J.src + (size_t)sl * J.n + o);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
+      const float4 acc = sum_slabs4(J.src, J.n, J.splits, o);
       if (J.dst) *reinterpret_cast<float4*>(J.dst + o) = acc;
       uint2 w;
       w.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
@@ -128,14 +141,8 @@ __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
   }
   const long n4 = J.n / 4;
   const long nb = j.blk_start[k + 1] - j.blk_start[k];
-  for (long i = (b - j.blk_start[k]) * (long)blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x) {
-    float4 acc = reinterpret_cast<const float4*>(J.src)[i];
-    for (int s = 1; s < J.splits; ++s) {
-      const float4 v = reinterpret_cast<const float4*>(J.src + (size_t)s * J.n)[i];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
-    reinterpret_cast<float4*>(J.dst)[i] = acc;
-  }
+  for (long i = (b - j.blk_start[k]) * (long)blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x)
+    reinterpret_cast<float4*>(J.dst)[i] = sum_slabs4(J.src, J.n, J.splits, (size_t)i * 4);
   if (b == j.blk_start[k]) {
     if (J.n < 4) {   // tiny job (e.g. the loss: many one-float partials): one wave, fixed order
       if (threadIdx.x < 64)
@@ -274,6 +281,43 @@ DEV float4 adam4(const OptimArgs& a, const AdamCoef& k, long i /*float4 index*/)
   return p;
 }
 
+// adam4 on 4 float4s at element offsets off + q*stride (q = 0..3): every load issued before any
+// update, so one memory round trip instead of four
+DEV void adam4x4(const OptimArgs& a, const AdamCoef& k, long off, long stride, float4 (&out)[4]) {
+  float4 p[4], g[4], m[4], v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long i = (off + q * stride) >> 2;
+    p[q] = reinterpret_cast<const float4*>(a.p)[i];
+    g[q] = reinterpret_cast<const float4*>(a.g)[i];
+    if (!a.sgd) { m[q] = reinterpret_cast<const float4*>(a.m)[i]; v[q] = reinterpret_cast<const float4*>(a.v)[i]; }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long i = (off + q * stride) >> 2;
+    float pv[4] = {p[q].x, p[q].y, p[q].z, p[q].w};
+    const float gv[4] = {g[q].x * k.sc, g[q].y * k.sc, g[q].z * k.sc, g[q].w * k.sc};
+    if (a.sgd) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+    } else {
+      float mv[4] = {m[q].x, m[q].y, m[q].z, m[q].w}, vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        mv[e] = a.b1 * mv[e] + (1.f - a.b1) * gv[e];
+        vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
+        float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
+        if (a.wd != 0.f) u += a.wd * pv[e];
+        pv[e] -= a.lr * u;
+      }
+      reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    out[q] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+    reinterpret_cast<float4*>(a.p)[i] = out[q];
+  }
+}
+
 // Matrix job: one 64x64 tile per block; thread (ty = tid/16, tx = tid%16) updates rows ty+16q,
 // columns 4tx..4tx+3 with float4 traffic, writes the row-major bf16 copy as 8-B stores, and the
 // transpose leaves through an LDS tile as 16-B stores (8 consecutive rows of one column).
@@ -292,10 +336,12 @@ __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs
   const int tiles_c = J.C / 64;
   const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float4 upd[4];
+  adam4x4(a, co, J.off + (long)(r0 + ty) * J.C + c0 + 4 * tx, 16L * J.C, upd);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = r0 + ty + 16 * q, c = c0 + 4 * tx;
-    const float4 p = adam4(a, co, (J.off + (long)r * J.C + c) >> 2);
+    const float4 p = upd[q];
     const u16 h0 = f2bf(p.x), h1 = f2bf(p.y), h2 = f2bf(p.z), h3 = f2bf(p.w);
     if (J.dst) {
       uint2 w;
