@@ -65,9 +65,10 @@ PYBIND11_MODULE(_C, m) {
       .def("set_batch_device", [](Trainer& t, uintptr_t x, uintptr_t y, int B, uintptr_t s) {
         t.set_batch_device(Pp<const int>(x), Pp<const int>(y), B, S(s));
       })
-      .def("set_comm", [](Trainer& t, RcclComm* c, std::vector<std::pair<long, long>> buckets) {
-        t.set_comm(c, buckets);
-      }, py::keep_alive<1, 2>())
+      .def("set_comm", [](Trainer& t, RcclComm* c, std::vector<std::pair<long, long>> buckets, long min_bucket) {
+        t.set_comm(c, buckets, min_bucket);
+      }, py::arg("comm"), py::arg("buckets"), py::arg("min_bucket_floats") = 2L << 20, py::keep_alive<1, 2>())
+      .def("allreduce_log", &Trainer::allreduce_log)
       .def("step", [](Trainer& t, uintptr_t s) { t.step(S(s)); })
       .def("forward_backward", [](Trainer& t, uintptr_t s) { t.forward_backward(S(s)); })
       .def("optimizer_step", [](Trainer& t, uintptr_t s) { t.optimizer_step(S(s)); })

@@ -119,6 +119,11 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
 
   HIP_CHECK(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+  {   // gradient collectives: highest-priority stream so their kernels dispatch ahead of compute
+    int lo = 0, hi = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_CHECK(hipStreamCreateWithPriority(&sc_, hipStreamNonBlocking, hi));
+  }
   events_.resize(64 + 8 * C_ * L);
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(&h_stage_, 2 * (2 * tok + 16) * sizeof(int)));
@@ -141,6 +146,7 @@ Trainer::~Trainer() {
   if (h_stage_) (void)hipHostFree(h_stage_);
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
+  if (sc_) (void)hipStreamDestroy(sc_);
 }
 
 hipEvent_t Trainer::ev() {
@@ -447,41 +453,60 @@ void Trainer::optimizer_step(hipStream_t s) {
   g_opt_.launch(s);
 }
 
-void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets) {
+void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets, long min_bucket_floats) {
   comm_ = c;
   buckets_ = buckets;
-  // buckets minus the embedding and W_ih0 segments (their gradients are recomputed from the
-  // all-reduced dP after the collective)
-  const long e0 = off_.at("embedding"), e1 = e0 + (long)d_.V * d_.E;
-  const long w0 = off_.at("weight_ih_l0"), w1 = w0 + 3L * d_.H * d_.E;
-  buckets_dp_.clear();
-  for (const auto& b : buckets) {
-    std::vector<std::pair<long, long>> pieces{{b.first, b.first + b.second}};
-    for (const auto& ex : {std::make_pair(e0, e1), std::make_pair(w0, w1)}) {
-      std::vector<std::pair<long, long>> next;
-      for (const auto& p : pieces) {
-        if (ex.second <= p.first || ex.first >= p.second) { next.push_back(p); continue; }
-        if (p.first < ex.first) next.push_back({p.first, ex.first});
-        if (ex.second < p.second) next.push_back({ex.second, p.second});
-      }
-      pieces.swap(next);
+  min_bucket_ = std::max(1L, min_bucket_floats);
+  // the overlapped path relies on the readiness order of the flat layout (models/params.py)
+  const int L = d_.L;
+  long prev = off_.at("fc.weight");
+  bool ok = prev == 0 && off_.at("fc.bias") > prev;
+  prev = off_.at("fc.bias");
+  for (int l = L - 1; l >= 0; --l) {
+    const std::string k = std::to_string(l);
+    for (const char* n : {"weight_hh_l", "bias_hh_l", "bias_ih_l", "weight_ih_l"}) {
+      const long o = off_.at(n + k);
+      ok = ok && o > prev;
+      prev = o;
     }
-    for (const auto& p : pieces)
-      if (p.second > p.first) buckets_dp_.push_back({p.first, p.second - p.first});
   }
+  ok = ok && off_.at("embedding") > prev;
+  if (!ok) throw std::runtime_error("set_comm: flat gradient layout is not in readiness order");
+  // dP [V][3H] goes into the W_ih0 gradient slot when it fits (one contiguous collective)
+  dP_inplace_ = (long)d_.V * 3 * d_.H <= 3L * d_.H * d_.E;
   g_step_[0].reset();
   g_step_[1].reset();
 }
 
-void Trainer::record_allreduce(hipStream_t s, bool dp_trick) {
-  // bucketed mean all-reduce of the flat fp32 gradient over xGMI (RCCL).  Buckets follow the
-  // gradient-readiness order of the flat layout (FC, top layer ... layer 0, embedding).
+long Trainer::group_end(int l) const {
+  if (l >= d_.L) return off_.at("weight_hh_l" + std::to_string(d_.L - 1));   // FC group
+  if (l > 0) return off_.at("weight_hh_l" + std::to_string(l - 1));
+  return off_.at("weight_ih_l0") + (dP_inplace_ ? (long)d_.V * 3 * d_.H : 0L);
+}
+
+void Trainer::ar_flush(hipStream_t s, bool force) {
+  const long n = ar_ready_ - ar_launched_;
+  if (n <= 0 || (!force && n < min_bucket_)) return;
+  hipEvent_t e = ev();
+  HIP_CHECK(hipEventRecord(e, s));          // fork: everything recorded on s so far
+  HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
+  comm_->allreduce_avg_f32(grads_ + ar_launched_, n, sc_);
+  ar_log_.push_back({ar_launched_, n});
+  ar_launched_ = ar_ready_;
+  ar_busy_ = true;
+}
+
+void Trainer::ar_join(hipStream_t s) {
+  if (!ar_busy_) return;
+  hipEvent_t e = ev();
+  HIP_CHECK(hipEventRecord(e, sc_));
+  HIP_CHECK(hipStreamWaitEvent(s, e, 0));
+  ar_busy_ = false;
+}
+
+void Trainer::record_allreduce(hipStream_t s) {
+  // plain bucketed mean all-reduce of the whole flat fp32 gradient after the backward
   if (!comm_) return;
-  if (dp_trick) {
-    for (const auto& b : buckets_dp_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
-    comm_->allreduce_avg_f32(dP_, (long)d_.V * 3 * d_.H, s);
-    return;
-  }
   for (const auto& b : buckets_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
 }
 
@@ -506,12 +531,10 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
-      if (dp_trick()) {
-        // all-reduce [fc, recurrent, bias grads, dP] (5.25 MB instead of 7.35 MB at H=512), then
-        // derive dEmb / dW_ih0 from the averaged dP locally
-        record_fb_seq(s0_, /*defer_tail=*/true);
-        record_allreduce(s0_, true);
-        record_emb_tail(s0_, true);
+      if (dp_overlap()) {
+        // readiness-ordered collectives on the comm stream, overlapped with the rest of the
+        // backward; joined before the optimiser (the embedding-side tail runs after the join)
+        record_fb_seq(s0_, /*dp=*/true);
       } else {
         if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
         record_allreduce(s0_);

@@ -87,15 +87,34 @@ class Trainer {
   // single-graph step (prep + fwd/bwd + in-graph RCCL all-reduce + optimiser)
   Graph g_step_[2];
   RcclComm* comm_ = nullptr;
-  std::vector<std::pair<long, long>> buckets_;
-  // data-parallel: all-reduce dP = dL/d(Emb·W_ih0^T) [V][3H] instead of dEmb + dW_ih0 (both are
-  // linear in dP with replicated Emb / W_ih0): buckets_dp_ = buckets_ minus those two segments
-  std::vector<std::pair<long, long>> buckets_dp_;
-  bool dp_trick() const { return comm_ != nullptr && !overlap_; }
-  void record_allreduce(hipStream_t s, bool dp_trick = false);
+  std::vector<std::pair<long, long>> buckets_;   // plain buckets (eager / chunked-overlap paths)
+  void record_allreduce(hipStream_t s);
+  // ---- readiness-ordered, overlapped all-reduce (persistent single-graph path)
+  // The flat gradient is laid out in readiness order (FC, layer L-1 ... layer 0: W_hh, b_hh, b_ih,
+  // W_ih).  Layer 0's group ends inside the W_ih0 segment: instead of dEmb + dW_ih0 the engine
+  // all-reduces dP = dL/d(Emb·W_ih0^T) [V][3H] written there (both are linear in dP with
+  // replicated Emb / W_ih0; 5.25 vs 7.35 MB at H=512) and derives them after the collective.
+  // While recording, the ready prefix [0, ar_ready_) grows as groups finish; ar_flush() hands
+  // [ar_launched_, ar_ready_) to RCCL on the comm stream sc_ once it reaches min_bucket_ floats
+  // (or at the end).  Collectives never run concurrently with a persistent sequence kernel
+  // (its workgroups must all be co-resident, and an RCCL kernel holding CUs while waiting on a
+  // peer could starve it): flushes happen right after a persistent kernel, and the step stream
+  // joins the comm stream before launching the next one.
+  bool dp_overlap() const { return comm_ != nullptr && !overlap_; }
+  long group_end(int l) const;       // end of layer l's readiness group (l == L: the FC group)
+  void ar_flush(hipStream_t s, bool force);
+  void ar_join(hipStream_t s);
+  float* dP_target() { return dP_inplace_ ? G("weight_ih_l0") : dP_; }
+  hipStream_t sc_ = nullptr;
+  long min_bucket_ = 0, ar_ready_ = 0, ar_launched_ = 0;
+  bool ar_busy_ = false, dP_inplace_ = false;
+  std::vector<std::pair<long, long>> ar_log_;   // (offset, floats) of every recorded collective
  public:
   void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
-  void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets);
+  // buckets: plain bucket list; min_bucket_floats: smallest collective of the overlapped path
+  void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets, long min_bucket_floats);
+  // collectives recorded into the last captured step graph (tests / plan printing)
+  const std::vector<std::pair<long, long>>& allreduce_log() const { return ar_log_; }
   void step(hipStream_t s);      // whole training step as one graph replay
   // collective watchdog over the launched steps (needs set_comm first; 0 disables)
   void enable_watchdog(int timeout_ms);
@@ -116,8 +135,9 @@ class Trainer {
     bool bwd = false, fuse_w = false, fuse_p = false;
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
   };
-  void record_fb_seq(hipStream_t s0, bool defer_tail = false);
-  void record_emb_tail(hipStream_t s, bool from_fp32);
+  // dp: data-parallel recording (overlapped readiness-ordered all-reduce, dP in place, tail after)
+  void record_fb_seq(hipStream_t s0, bool dp = false);
+  void record_emb_tail(hipStream_t s, const float* dP_fp32);   // dP_fp32 null: bf16 copies already made
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;

@@ -29,11 +29,13 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
   reduce_slabs_multi(j, s);
 }
 
-void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
+void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
   const int H3 = 3 * H, nrb = B / 32;
   const long tok = (long)T * B;
   const long fw = seq_flag_words(H, B);
+  ev_next_ = 0;
+  if (dp) { ar_ready_ = ar_launched_ = 0; ar_busy_ = false; ar_log_.clear(); }
   // Flag blocks: forward(l) at cnt_ + l*fw, backward(l) at cnt_ + (L+l)*fw.  Each persistent
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
@@ -129,6 +131,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
     } else {
       for (int t = T - 1; t >= 0; --t) bwd_step(l, t, s);
     }
+    // data-parallel: groups that became ready before this kernel go out now (they cannot overlap it)
+    if (dp && q.bwd) ar_flush(s, false);
     // weight gradients not accumulated inside the sequence kernel
     SlabJobs j;
     if (q.fuse_w) j.add(q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
@@ -136,12 +140,15 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
     // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail -- or, when the
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
-      if (defer_tail) j.add(dP_part_, nrb, (long)V * H3, dP_);
+      if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
       else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     }
     if (l == 0 && q.bwd) j.add(q.dbih_part, nrb, H3, G("bias_ih_l0"));
-    if (l == 0) {   // + dW_fc / db_fc slabs, the loss partials, and the optimiser step counter
+    // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
+    // all-reduced with it), else with layer 0's reduce
+    if (dp ? l == L - 1 : l == 0)
       for (int k2 = 0; k2 < tail.n; ++k2) j.job[j.n++] = tail.job[k2];
+    if (l == 0) {   // + the loss partials and the optimiser step counter
       j.add(loss_part_, (int)(tok / 32), 1, loss_);
       j.bump = step_;
     }
@@ -157,14 +164,33 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
         p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)tok;
         p.C = slab_w_; p.ldc = H3; p.M = V; p.N = H3; p.K = (int)tok; p.splits = sp;
         gemm_nt(p, s);
-        reduce_slabs(slab_w_, sp, (long)V * H3, dP_, s);
-        if (!q.bwd) colsum(dP_, V, H3, G("bias_ih_l0"), s);
+        float* dPd = dp ? dP_target() : dP_;
+        reduce_slabs(slab_w_, sp, (long)V * H3, dPd, s);
+        if (!q.bwd) colsum(dPd, V, H3, G("bias_ih_l0"), s);
+      }
+      if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
+        ar_ready_ = group_end(0);
+        ar_flush(s, true);
+        if (!dP_inplace_) {
+          hipEvent_t e = ev();
+          HIP_CHECK(hipEventRecord(e, s));
+          HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
+          comm_->allreduce_avg_f32(dP_, (long)V * H3, sc_);
+          ar_log_.push_back({-1, (long)V * H3});
+          ar_busy_ = true;
+        }
+        ar_join(s);
       }
     } else {
       const int K = in_dim(l);
       // dW_ih = dGi^T · h_below, db_ih = row sums of dGi^T
       wgrad_gemm(y.dgiT, (int)tok, Ls_[l - 1].HT + B, (T + 1) * B, H3, K, (int)tok, G("weight_ih_l" + k),
                  G("bias_ih_l" + k), s);
+      if (dp) {
+        ar_ready_ = group_end(l);   // FC (if l is the top layer) + this layer's four gradients
+        if (!seq_[l - 1].bwd) ar_flush(s, false);   // next backward is per-step: overlap it now
+        else ar_join(s);   // (no-op unless an earlier flush is still open) before the persistent kernel
+      }
       GemmArgs dx;  // dy of the layer below = dGi · W_ih
       dx.A = y.dgi; dx.lda = H3; dx.B = y.WihT; dx.ldb = H3;
       dx.C = Ls_[l - 1].dy; dx.ldc = H; dx.M = (int)tok; dx.N = H; dx.K = H3;
@@ -172,16 +198,19 @@ void Trainer::record_fb_seq(hipStream_t s, bool defer_tail) {
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients
-  if (!defer_tail) record_emb_tail(s, !seq_[0].fuse_p);
+  if (dp) record_emb_tail(s, dP_target());          // from the averaged dP
+  else record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
   HIP_LAUNCH_CHECK();
 }
 
-// dEmb = dP · W_ih0 and dW_ih0 = dP^T · Emb from the layer-0 table gradient dP
-void Trainer::record_emb_tail(hipStream_t s, bool from_fp32) {
+// dEmb = dP · W_ih0 and dW_ih0 = dP^T · Emb from the layer-0 table gradient dP.  dP_fp32 may
+// alias the W_ih0 gradient slot (data-parallel): it is fully read by the cast before the GEMM
+// below overwrites that slot (same stream).
+void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
-  if (from_fp32) {
+  if (dP_fp32) {
     CastJobs j;
-    j.add(dP_, V, H3, dP_bf_, dPT_bf_);
+    j.add(dP_fp32, V, H3, dP_bf_, dPT_bf_);
     cast_multi(j, s);
   }
   GemmArgs g;   // dW_ih0 = dP^T · Emb

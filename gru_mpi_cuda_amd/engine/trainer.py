@@ -59,8 +59,10 @@ class HipTrainer:
         self.t.set_use_graph(use_graph)
         if self.comm is not None:     # identical replicas: rank 0's weights everywhere
             self.comm.broadcast_f32(self.params.data_ptr(), self.layout.total, 0, self._stream())
-            # bucketed all-reduce recorded INTO the step graph (RCCL ops on a captured stream)
-            self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets])
+            # all-reduce recorded INTO the step graph: readiness-ordered buckets of at least
+            # bucket_mb on a comm stream, overlapped with the rest of the backward
+            self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets],
+                            max(1024, int(cfg.bucket_mb * (1 << 20) / 4)))
         self.t.refresh_weights(self._stream())
         self._one_graph = True
         if cfg.watchdog_ms > 0:       # host thread watching each launched step
@@ -107,7 +109,7 @@ class HipTrainer:
                 print(f"[gru_mpi_cuda_amd] in-graph all-reduce unavailable ({e}); "
                       "falling back to per-phase launches", file=sys.stderr)
                 self._one_graph = False
-                self.t.set_comm(None, [])
+                self.t.set_comm(None, [], 1)
         self.t.forward_backward(s)
         self.allreduce_grads()
         self.t.optimizer_step(s)

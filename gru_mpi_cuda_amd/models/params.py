@@ -12,7 +12,7 @@ Two orderings exist:
   (namegensf.cu:375-407).
 * **flat order** (``flat_layout``): the engine's single contiguous fp32 buffer,
   ordered by gradient *readiness* during backprop-through-time (FC first, then
-  layers top-down, embedding last) so that gradient all-reduce buckets are
+  layers top-down as W_hh, b_hh, b_ih, W_ih, embedding last) so that gradient all-reduce buckets are
   contiguous slices that become ready in order.  Each segment starts at a
   multiple of 64 floats (256 B) so kernels can use 16-byte vector accesses.
 """
@@ -55,7 +55,9 @@ def ckpt_order(cfg: GRUConfig) -> List[str]:
 def flat_order(cfg: GRUConfig) -> List[str]:
     names = ["fc.weight", "fc.bias"]
     for l in reversed(range(cfg.layers)):
-        names += [f"weight_hh_l{l}", f"bias_hh_l{l}", f"weight_ih_l{l}", f"bias_ih_l{l}"]
+        # biases before W_ih: layer 0's data-parallel bucket ends inside the W_ih0 segment (the
+        # engine all-reduces the V x 3H table gradient dP there and derives dW_ih0 / dEmb after)
+        names += [f"weight_hh_l{l}", f"bias_hh_l{l}", f"bias_ih_l{l}", f"weight_ih_l{l}"]
     names.append("embedding")
     return names
 

@@ -12,7 +12,7 @@ step() {  # name, timeout, cmd...
   return 0
 }
 python -m gru_mpi_cuda_amd.build_ext > gpurun_out/build.log 2>&1 || { echo "BUILD FAILED"; tail -20 gpurun_out/build.log; exit 3; }
-step kernels 500 python -m pytest tests/test_kernels_gpu.py -x -q
-step engine 500 python -m pytest tests/test_engine_gpu.py -x -q
+step kernels 500 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread
+step engine 500 python -u -m pytest tests/test_engine_gpu.py tests/test_capi_gpu.py -x -q --timeout 120 --timeout-method thread
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 python bench.py --steps 20 --warmup 5

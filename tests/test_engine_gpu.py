@@ -133,12 +133,15 @@ def test_generator_matches_cpu():
     assert same >= 0.9, same
 
 
-@pytest.mark.parametrize("layers,E,H,bucket_mb", [(1, 256, 256, 8.0), (2, 128, 256, 0.25), (1, 512, 512, 1.0)])
-def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb):
-    """The whole step as one graph with a captured RCCL all-reduce (1-rank communicator):
-    must equal the no-comm step bit for bit (mean over one rank is the identity).  With a
-    communicator the step all-reduces dP instead of dEmb / dW_ih0 and derives those two after
-    the collective; small buckets exercise the bucket split around the excluded segments."""
+@pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll", [(1, 256, 256, 8.0, 1), (2, 128, 256, 0.25, 3),
+                                                         (1, 512, 512, 1.0, 1), (2, 512, 256, 0.25, 2),
+                                                         (2, 512, 256, 64.0, 1)])
+def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
+    """The whole step as one graph with captured RCCL all-reduces (1-rank communicator) on the
+    comm stream: must equal the no-comm step bit for bit (mean over one rank is the identity).
+    With a communicator the step all-reduces dP instead of dEmb / dW_ih0 (in the W_ih0 slot when
+    V <= E, else as its own collective) and derives those two after the join; small buckets
+    make the top layer's group go out while layer 0 is still in its backward."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
@@ -151,6 +154,8 @@ def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb):
         a.step(x, y)
         b.step(x, y)
     assert a._one_graph, "in-graph RCCL all-reduce fell back"
+    log = a.t.allreduce_log()
+    assert len(log) == n_coll, log
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
 
 
