@@ -287,9 +287,18 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   const int k0 = w * NKW3 * 32;
   const unsigned nunit = (unsigned)(H / 16);
 
-  bf16x8 bw[NKW3];    // this wave's K-slice of W_hh^T rows j0..j0+15 (dh = dGh · W_hh)
+  // this wave's K-slice of W_hh^T rows j0..j0+15 (dh = dGh · W_hh), resident all sequence: in
+  // VGPRs, or -- for the variants with fused weight gradients, whose accumulators take the
+  // register file -- lane-linear in LDS (each lane re-reads only its own 16-B slots: conflict-free,
+  // and program order suffices, no barrier)
+  constexpr bool kBwLds = NTW > 0;
+  __shared__ __attribute__((aligned(16))) bf16x8 bwL[kBwLds ? NKW3 : 1][kBwLds ? 512 : 1];
+  bf16x8 bw[kBwLds ? 1 : NKW3];
 #pragma unroll
-  for (int kk = 0; kk < NKW3; ++kk) bw[kk] = ld8(a.WhhT + (size_t)(j0 + lr) * H3 + k0 + kk * 32 + lk);
+  for (int kk = 0; kk < NKW3; ++kk) {
+    const bf16x8 v = ld8(a.WhhT + (size_t)(j0 + lr) * H3 + k0 + kk * 32 + lk);
+    if constexpr (kBwLds) bwL[kk][tid] = v; else bw[kk] = v;
+  }
 
   const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
   const int row = rb * 16 + (ln >> 4) * 4 + reg, col = ln & 15;
@@ -302,27 +311,19 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   zero_acc(accP);
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   zero_next_flags(a.zero_next, a.zero_words);
+  // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
+  // next poll they would delay it (vmcnt retires in order), and they have a whole step to land
+  float sv[6];
+  auto load_saves = [&](int t) {
+    const size_t o = ((size_t)t * Bp + b) * H + j;
+    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
+  };
+  load_saves(T - 1);
 
   for (int t = T - 1; t >= 0; --t) {
     const int s = T - 1 - t;
     stamp(a.dbg, s, 0);
-    const size_t o = ((size_t)t * Bp + b) * H + j;
-    const float dy = a.dy[o], sr = a.sr[o], sz = a.sz[o], sn = a.sn[o], sghn = a.sghn[o];
-    const float hprev = a.HSf[o];   // HS[t] = h_{t-1}
-    // operands of the fused weight-gradient MFMAs (independent of other workgroups)
-    bf16x8 hB[NTW > 0 ? NTW : 1];
-    if constexpr (NTW > 0) {
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt)
-        hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
-    }
-    int idv[8];
-    if constexpr (NTP > 0) {
-      const int4 i0 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk);
-      const int4 i1 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk + 4);
-      idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
-      idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
-    }
     f32x4 acc[2];
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[1] = acc[0];
@@ -341,9 +342,29 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       });
       stamp(a.dbg, s, 1);
 #pragma unroll
-      for (int kk = 0; kk < NKW3; ++kk)
+      for (int kk = 0; kk < NKW3; ++kk) {
+        bf16x8 bk;
+        if constexpr (kBwLds) bk = bwL[kk][tid]; else bk = bw[kk];
 #pragma unroll
-        for (int r = 0; r < 2; ++r) acc[r] = mfma16(af[kk][r], bw[kk], acc[r]);
+        for (int r = 0; r < 2; ++r) acc[r] = mfma16(af[kk][r], bk, acc[r]);
+      }
+    }
+    const float dy = sv[0], sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4], hprev = sv[5];
+    if (t > 0) load_saves(t - 1);
+    // operands of the fused weight-gradient MFMAs (independent of other workgroups): issued after
+    // the hand-off so the poll above does not wait behind them; first used after the publish
+    bf16x8 hB[NTW > 0 ? NTW : 1];
+    if constexpr (NTW > 0) {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt)
+        hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
+    }
+    int idv[8];
+    if constexpr (NTP > 0) {
+      const int4 i0 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk);
+      const int4 i1 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk + 4);
+      idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
+      idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)

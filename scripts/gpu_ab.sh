@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU-box iteration run: engine tests, persistent-kernel phase probes, headline bench
+# (each step under its own time limit; stops at the first crash-type exit).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+run() {  # name, timeout, cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name"; timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 "gpurun_out/$name.log"
+  if [ $rc -gt 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+run engine 300 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread
+run probe_fwd 120 python scripts/probe_seq.py
+run probe_bwd 120 python scripts/probe_seq_bwd.py
+run bench 200 python bench.py --steps 50 --warmup 10
+run bench2 200 python bench.py --steps 50 --warmup 10
