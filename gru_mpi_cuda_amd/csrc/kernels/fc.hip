@@ -8,6 +8,7 @@
 // A workgroup owns 32 full rows (all V columns) so the row reductions stay on chip:
 // each of the V/64 waves holds a 32x64 slab in 8 MFMA accumulators, rows are reduced
 // across the 16 column lanes with DPP-able xor shuffles and across waves through LDS.
+#include <cstdlib>
 #include <stdexcept>
 #include "kernels.h"
 #include "mma_tile.h"
@@ -180,6 +181,212 @@ __global__ void __launch_bounds__(512) fc_xent_kernel(FcXentArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fc_xent for V = 256 with fused dH (the training path at every H % 512 == 0): 8 waves per 32-row
+// block, so each SIMD has two waves to overlap latency with, and every weight fragment a wave
+// needs is in flight at once instead of a few k-steps at a time:
+//   * X [32][H] staged once in LDS (rows padded by 16 B: the 16 rows of a fragment read land in
+//     distinct 16-B slots), read as MFMA A operand by all waves;
+//   * wave w owns logits columns [32w, 32w+32): its W_fc slab (H/16 fragments) streams in chunks
+//     of 8 k-steps, two chunks in flight;
+//   * softmax row statistics across the 8 waves through LDS (two barriers);
+//   * dlogits (bf16) to LDS as the A operand of dH and as the dl^T staging tile;
+//   * wave w owns dH columns [w H/8, (w+1) H/8): its W_fc^T fragments (64 columns x K = 256 per
+//     pass) are loaded before the softmax, while the row statistics are being reduced.
+// profiles/: 34.5 us -> see r1 notes for the measured time of this variant.
+namespace {
+constexpr int kX2Pad = 8;   // bf16 of padding per staged X row
+}
+
+template <int NKC>
+DEV void fc2_load_w(bf16x8 (&b)[NKC][2], const u16* W, int H, int v0, int ks, int lane) {
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+#pragma unroll
+  for (int kk = 0; kk < NKC; ++kk)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) b[kk][c] = ld8(W + (size_t)(v0 + c * 16 + lr) * H + (ks + kk) * 32 + lk);
+}
+template <int NKC>
+DEV void fc2_mma(f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], const u16* xs, int ldx, int ks, int lane) {
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+#pragma unroll
+  for (int kk = 0; kk < NKC; ++kk) {
+    bf16x8 af[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(xs + (r * 16 + lr) * ldx + (ks + kk) * 32 + lk);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) acc[r][c] = mfma16(af[r], b[kk][c], acc[r][c]);
+  }
+}
+// W_fc^T fragments of one 64-column dH pass: [8 k-steps of V=256][4 column tiles]
+DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WT, int n0, int lane) {
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WT + (size_t)(n0 + c * 16 + lr) * 256 + kk * 32 + lk);
+}
+
+__global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int nst = 0;
+  auto STAMP = [&]() {
+    if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) a.dbg[nst] = __builtin_amdgcn_s_memrealtime();
+    ++nst;
+  };
+  STAMP();
+  constexpr int V = 256, NW = 8, NKC = 8, LDR = V + 8;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int H = a.H, ldx = H + kX2Pad, m0 = blockIdx.x * FROWS;
+  u16* xs = reinterpret_cast<u16*>(smem);                         // [32][H + 8]
+  float* red = reinterpret_cast<float*>(xs + FROWS * ldx);         // [2][8][32]
+  float* lab = red + 2 * NW * 32;                                  // [32]
+  float* lrow = lab + 32;                                          // [32]
+  u16* st = reinterpret_cast<u16*>(lrow + 32);                     // [V][40]   dl^T staging
+  u16* dlr = st + V * 40;                                          // [32][V+8] dl row-major
+
+  // ---- stage X, and put the first two chunks of this wave's W_fc slab in flight
+  const int v0 = w * 32, nks = H / 32;
+  bf16x8 b0[NKC][2], b1[NKC][2];
+  fc2_load_w<NKC>(b0, a.W, H, v0, 0, lane);
+  if (nks > NKC) fc2_load_w<NKC>(b1, a.W, H, v0, NKC, lane);
+  for (int q = tid; q < FROWS * H / 8 && !(a.skip & 16); q += 512) {
+    const int row = q / (H / 8), c8 = q % (H / 8);
+    *reinterpret_cast<uint4*>(xs + row * ldx + c8 * 8) =
+        *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
+  }
+  int* ys = reinterpret_cast<int*>(dlr + FROWS * LDR);           // [32] labels of the block
+  if (tid < FROWS) ys[tid] = a.labels[m0 + tid];
+  __syncthreads();
+  STAMP();
+
+  // ---- logits: 32 rows x this wave's 32 columns, K = H in chunks of 8 k-steps (2 in flight)
+  f32x4 acc[2][2];
+  zero_acc(acc);
+  for (int ks = 0; ks < nks && !(a.skip & 4); ks += 2 * NKC) {
+    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane);
+    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.W, H, v0, ks + 2 * NKC, lane);
+    if (ks + NKC < nks) {
+      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane);
+      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.W, H, v0, ks + 3 * NKC, lane);
+    }
+  }
+  // the first dH pass's W_fc^T fragments go out now, under the softmax reductions (not earlier:
+  // the scheduler barrier keeps them from overlapping the W_fc slab's registers)
+  __builtin_amdgcn_sched_barrier(0);
+  STAMP();
+  const int per = H / NW;                 // dH columns of this wave (a multiple of 64)
+  bf16x8 bt[8][4];
+  fc2_load_wt(bt, a.WT, w * per, lane);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float bb = a.b[v0 + c * 16 + lr];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[r][c][i] += bb;
+  }
+
+  // ---- softmax statistics over the 8 waves' columns
+  float mx[2][4], se[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float m = max16(fmaxf(acc[r][0][i], acc[r][1][i]));
+      if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i;
+      float m = red[row];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+      mx[r][i] = m;
+      const float e = sum16(__expf(acc[r][0][i] - m) + __expf(acc[r][1][i] - m));
+      if (lr == 0) red[NW * 32 + w * 32 + row] = e;
+    }
+  __syncthreads();
+  const float inv = a.inv_count[0];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i;
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
+      se[r][i] = sum;
+      const int y = ys[row];
+      const float scale = (y >= 0) ? inv : 0.f;
+      const float rs = __builtin_amdgcn_rcpf(sum);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int col = v0 + c * 16 + lr;
+        const float x = acc[r][c][i];
+        if (col == y) lab[row] = x;
+        const float d = (__expf(x - mx[r][i]) * rs - (col == y ? 1.f : 0.f)) * scale;
+        const u16 db = f2bf(d);
+        st[col * 40 + row] = db;
+        dlr[row * LDR + col] = db;
+      }
+    }
+  __syncthreads();
+  STAMP();
+  // per-row nll (one thread per row; the statistics are still in LDS)
+  if (tid < FROWS) {
+    const int row = tid, y = ys[row];
+    float m = red[row], sum = 0.f;
+    for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+    for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
+    lrow[row] = (y >= 0) ? (logf(sum) + m - lab[row]) * inv : 0.f;
+  }
+  // dl^T: each column's 32 rows are 64 contiguous bytes -> four 16-B stores
+  for (int q = tid; q < V * 4 && !(a.skip & 2); q += 512) {
+    const int col = q >> 2, seg = q & 3;
+    *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) =
+        *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
+  }
+  STAMP();
+  // ---- dH = dl · W_fc: 32 rows x this wave's columns, 64 per pass, K = V = 256
+  for (int n0 = w * per; n0 < (w + 1) * per && !(a.skip & 8); n0 += 64) {
+    if (n0 != w * per) fc2_load_wt(bt, a.WT, n0, lane);
+    f32x4 dacc[2][4];
+    zero_acc(dacc);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(dlr + (r * 16 + lr) * LDR + kk * 32 + 8 * lq);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dacc[r][c] = mfma16(af[r], bt[kk][c], dacc[r][c]);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (!(a.skip & 1)) a.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = dacc[r][c][i];
+  }
+  STAMP();
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int i = 0; i < FROWS; ++i) t += lrow[i];
+    a.loss_part[blockIdx.x] = t;
+  }
+  STAMP();
+}
+
 template <int KB>
 __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -243,7 +450,25 @@ __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
   }
 }
 
-void fc_xent(const FcXentArgs& a, hipStream_t s) {
+static bool fc_xent_v256_ok(const FcXentArgs& a) {
+  return a.V == 256 && a.dy && a.WT && !a.dl && a.H % 512 == 0 && a.M % FROWS == 0 &&
+         !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');
+}
+
+void fc_xent(const FcXentArgs& a0, hipStream_t s) {
+  FcXentArgs a = a0;
+  if (std::getenv("GK_FC_SKIP")) a.skip = std::atoi(std::getenv("GK_FC_SKIP"));
+  if (fc_xent_v256_ok(a)) {
+    const size_t shm = (size_t)FROWS * (a.H + kX2Pad) * 2 + (2 * 8 * 32 + 64) * 4 + 256 * 40 * 2 +
+                       (size_t)FROWS * (256 + 8) * 2 + FROWS * 4;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(fc_xent_v256_kernel, dim3(a.M / FROWS), dim3(512), shm, s, a);
+    return;
+  }
   const int NW = a.V / 64;
   if (a.dy && (a.H % (16 * NW) || a.V % 128 || !a.WT))
     throw std::runtime_error("fc_xent: fused dH needs H % (V/4) == 0, V % 128 == 0 and W_fc^T");

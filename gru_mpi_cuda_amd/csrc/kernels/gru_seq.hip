@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 template <int NKW3, int NTW, int NTP>
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][2][256];      // 16 KB
-  __shared__ __attribute__((aligned(16))) u16 srow[32][48];           // dGh tile, row-major (exchange)
+  __shared__ __attribute__((aligned(16))) u16 srow[3][32][16];        // dGh tile, gate-major (exchange)
   __shared__ __attribute__((aligned(16))) u16 sgT[4][16][40];         // dGh^T gates r,z,n + dGi_n^T (padded rows)
   __shared__ __attribute__((aligned(16))) float red[6][16][33];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -336,9 +336,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       wave_wait_load<NKW3>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3,
                            ((k0 + 16 * lane) % H) / 16, (unsigned)s, a.err, [&](int kk) {
         const int c = k0 + kk * 32 + lk, u = c % H;
-        const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 48 + (c / H) * 16 + (u & 15)) * 2;
+        const unsigned tb = (unsigned)(((slot + u / 16) * 3 + c / H) * 512 + lr * 16 + (u & 15)) * 2;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 48 * 2));
+        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 16 * 2));
       });
       stamp(a.dbg, s, 1);
 #pragma unroll
@@ -384,19 +384,19 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     carry = sz * dh;
     dbh[0] += dar; dbh[1] += daz; dbh[2] += dhn; dbi += dan;
     const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dhn), bi = f2bf(dan);
-    srow[row][col] = br; srow[row][16 + col] = bz; srow[row][32 + col] = bn;
+    srow[0][row][col] = br; srow[1][row][col] = bz; srow[2][row][col] = bn;
     sgT[0][col][row] = br; sgT[1][col][row] = bz; sgT[2][col][row] = bn; sgT[3][col][row] = bi;
     __syncthreads();
     stamp(a.dbg, s, 3);
     if (w == 0) {
-      // publish the dGh_t tile [32 rows][3 gates x 16] (3 KB, whole lines of its own) to slot t:
-      // 3 x 16 B per lane, write-through
-      const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (32 * 48);
+      // publish the dGh_t tile as 3 gate blocks of [32 rows][16 units] (1 KB each, whole lines of its
+      // own): a consumer's 16-row fragment of one gate is then 512 contiguous bytes per producer
+      // (8 full lines per load instruction instead of 16-row x 96-B strided pieces)
+      const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (3 * 32 * 16);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int q = lane + 64 * i, rr = q / 6, sg = q % 6;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[rr][sg * 8]);
-        st16_sc1(rX, (unsigned)((tile + rr * 48 + sg * 8) * 2), v);
+      for (int g = 0; g < 3; ++g) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[g][lane >> 1][(lane & 1) * 8]);
+        st16_sc1(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride, (unsigned)(s + 1));

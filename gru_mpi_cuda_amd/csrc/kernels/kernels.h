@@ -95,7 +95,7 @@ struct SeqBwdArgs {
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
   const u16* WhhT = nullptr;       // [H][3H]
   u16* xbuf = nullptr;             // dGh exchange, one slot per step (no WAR reuse), tiled per producer:
-                                   // [T][Bp/32][H/16][32 rows][48 = 3 gates x 16] bf16
+                                   // [T][Bp/32][H/16][3 gates][32 rows][16 units] bf16
   u16* dghT = nullptr; u16* dgiT = nullptr; int ldG = 0;   // [3H][ldG] transposed copies (nullable)
   u16* dgi = nullptr;              // [T][Bp][3H] row-major dGi (nullable)
   float* dWhh_part = nullptr;      // [Bp/32][3H][H] fused dW_hh partials (nullable = not fused)
@@ -127,6 +127,8 @@ struct FcXentArgs {
   const u16* WT = nullptr;
   float* dy = nullptr;
   int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
+  int skip = 0;   // EXPERIMENT
+  unsigned long long* dbg = nullptr;   // diagnostic phase stamps of workgroup 0 (nullable)
 };
 void fc_xent(const FcXentArgs& a, hipStream_t s);
 
