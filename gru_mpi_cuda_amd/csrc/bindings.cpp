@@ -194,6 +194,7 @@ PYBIND11_MODULE(_C, m) {
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
     a.WT = GP(const u16, d, "WT"); a.dy = GP(float, d, "dy");
     a.dbg = GP(unsigned long long, d, "dbg");
+    a.Wf = GP(const u16, d, "Wf"); a.WTf = GP(const u16, d, "WTf");
     if (a.M % 32 || a.V % 64 || a.V > 512 || a.H % 32 || a.ldT % 8 || a.colT % 8)
       throw std::runtime_error("fc_xent: bad shape");
     fc_xent(a, S(s));

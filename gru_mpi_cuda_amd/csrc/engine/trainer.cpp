@@ -29,6 +29,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_sP = R((size_t)C_ * V * 3 * H * 4), o_dP = R((size_t)V * 3 * H * 4);
   size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
   size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
+  size_t o_WfcF = R((size_t)V * H * 2), o_WfcTF = R((size_t)V * H * 2);
   size_t o_dl = R(tok * V * 2), o_dlT = R(tok * V * 2), o_dPb = R((size_t)V * 3 * H * 2), o_dPTb = R((size_t)V * 3 * H * 2);
   struct LO { size_t HSf, sr, sz, sn, sghn, dy, Gi, c0, c1, HSb, HT, g0, g1, dghT, dgiT, dgi, Whh, WhhT, Wih, WihT, shh, rhh, sih, rih; };
   std::vector<LO> los(L);
@@ -98,6 +99,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   dP_ = arena_.get<float>(o_dP); norm_parts_ = arena_.get<float>(o_np); gscale_ = arena_.get<float>(o_gs);
   step_ = arena_.get<int>(o_step);
   Emb = arena_.get<u16>(o_Emb); EmbT = arena_.get<u16>(o_EmbT); Wfc = arena_.get<u16>(o_Wfc); WfcT = arena_.get<u16>(o_WfcT);
+  WfcF = arena_.get<u16>(o_WfcF); WfcTF = arena_.get<u16>(o_WfcTF);
   dl_ = arena_.get<u16>(o_dl); dlT_ = arena_.get<u16>(o_dlT); dP_bf_ = arena_.get<u16>(o_dPb); dPT_bf_ = arena_.get<u16>(o_dPTb);
   Ls_.resize(L);
   for (int l = 0; l < L; ++l) {
@@ -170,7 +172,7 @@ void Trainer::refresh_weights(hipStream_t s) {
     j.add(P("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
     j.add(P("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
   }
-  j.add(P("fc.weight"), V, H, Wfc, WfcT);
+  j.add(P("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
   cast_multi(j, s);
   HIP_LAUNCH_CHECK();
 }
@@ -409,7 +411,7 @@ void Trainer::record_opt(hipStream_t s) {
       j.add(off_.at("bias_ih_l" + k), 0, 3 * H, nullptr, nullptr);
       j.add(off_.at("bias_hh_l" + k), 0, 3 * H, nullptr, nullptr);
     }
-    j.add(off_.at("fc.weight"), V, H, Wfc, WfcT);
+    j.add(off_.at("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
     j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
     adam_cast_multi(a, j, s);
   } else {

@@ -85,7 +85,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     f.loss_part = loss_part_; f.M = (int)tok; f.H = H; f.V = V;
     if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
-      f.dl = nullptr; f.WT = WfcT; f.dy = top.dy;
+      f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
       fc_xent(f, s);
     } else {
       fc_xent(f, s);

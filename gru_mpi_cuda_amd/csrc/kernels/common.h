@@ -49,26 +49,38 @@ DEV float tanhf_(float x) {
   return copysignf(t, x);
 }
 
-DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+// Cross-lane reductions.  Within a 16-lane row they use DPP (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror: four VALU ops, every lane ends with the same value); __shfl_xor
+// lowers to ds_bpermute, an LDS round trip with an lgkmcnt(0) wait per step, which serialised
+// the FC softmax (profiles/: 3 us of bpermute chains per 32-row block).  Only the steps across
+// rows (16, 32) still use shuffles.
+template <int CTRL>
+DEV float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+DEV float max16(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));    // quad_perm [1,0,3,2]
+  v = fmaxf(v, dppf<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = fmaxf(v, dppf<0x141>(v));   // row_half_mirror
+  v = fmaxf(v, dppf<0x140>(v));   // row_mirror
   return v;
+}
+DEV float sum16(float v) {   // commutative pairings: identical in every lane of the row
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  return v;
+}
+DEV float wave_max(float v) {
+  v = max16(v);
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
 }
 DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-// reduce across the 16 lanes that share (l>>4) -- i.e. across the 16 columns of a C tile
-DEV float max16(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-DEV float sum16(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = sum16(v);
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
 }
 
 }  // namespace gk

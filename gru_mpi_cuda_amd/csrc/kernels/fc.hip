@@ -198,13 +198,13 @@ namespace {
 constexpr int kX2Pad = 8;   // bf16 of padding per staged X row
 }
 
+// fragments from the FT layout (kernels.h ft_offset): one whole 1-KB block per load instruction
 template <int NKC>
-DEV void fc2_load_w(bf16x8 (&b)[NKC][2], const u16* W, int H, int v0, int ks, int lane) {
-  const int lr = lane & 15, lk = 8 * (lane >> 4);
+DEV void fc2_load_w(bf16x8 (&b)[NKC][2], const u16* Wf, int H, int v0, int ks, int lane) {
 #pragma unroll
   for (int kk = 0; kk < NKC; ++kk)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) b[kk][c] = ld8(W + (size_t)(v0 + c * 16 + lr) * H + (ks + kk) * 32 + lk);
+    for (int c = 0; c < 2; ++c) b[kk][c] = ld8(Wf + ((size_t)((v0 / 16 + c) * (H / 32) + ks + kk) * 64 + lane) * 8);
 }
 template <int NKC>
 DEV void fc2_mma(f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], const u16* xs, int ldx, int ks, int lane) {
@@ -221,14 +221,14 @@ DEV void fc2_mma(f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], const u16* xs, i
   }
 }
 // W_fc^T fragments of one 64-column dH pass: [8 k-steps of V=256][4 column tiles]
-DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WT, int n0, int lane) {
-  const int lr = lane & 15, lk = 8 * (lane >> 4);
+DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WTf, int n0, int lane) {
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WT + (size_t)(n0 + c * 16 + lr) * 256 + kk * 32 + lk);
+    for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WTf + ((size_t)((n0 / 16 + c) * 8 + kk) * 64 + lane) * 8);
 }
 
+template <int HH>
 __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int nst = 0;
@@ -240,7 +240,8 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   constexpr int V = 256, NW = 8, NKC = 8, LDR = V + 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
-  const int H = a.H, ldx = H + kX2Pad, m0 = blockIdx.x * FROWS;
+  constexpr int H = HH;
+  const int ldx = H + kX2Pad, m0 = blockIdx.x * FROWS;
   u16* xs = reinterpret_cast<u16*>(smem);                         // [32][H + 8]
   float* red = reinterpret_cast<float*>(xs + FROWS * ldx);         // [2][8][32]
   float* lab = red + 2 * NW * 32;                                  // [32]
@@ -248,30 +249,45 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   u16* st = reinterpret_cast<u16*>(lrow + 32);                     // [V][40]   dl^T staging
   u16* dlr = st + V * 40;                                          // [32][V+8] dl row-major
 
-  // ---- stage X, and put the first two chunks of this wave's W_fc slab in flight
+  // ---- scalars first (a global load issued behind the weight stream would wait for all of it:
+  // vmcnt retires in order), then stage X, and put the first two chunks of this wave's W_fc
+  // slab in flight
   const int v0 = w * 32, nks = H / 32;
+  const float inv = a.inv_count[0];
+  float bias[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) bias[c] = a.b[v0 + c * 16 + lr];
   bf16x8 b0[NKC][2], b1[NKC][2];
-  fc2_load_w<NKC>(b0, a.W, H, v0, 0, lane);
-  if (nks > NKC) fc2_load_w<NKC>(b1, a.W, H, v0, NKC, lane);
-  for (int q = tid; q < FROWS * H / 8 && !(a.skip & 16); q += 512) {
-    const int row = q / (H / 8), c8 = q % (H / 8);
-    *reinterpret_cast<uint4*>(xs + row * ldx + c8 * 8) =
-        *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
+  // X: H/128 16-B pieces per thread, loaded ahead of the weight stream
+  constexpr int nxp = FROWS * H / 8 / 512;
+  uint4 xv[nxp];
+#pragma unroll
+  for (int e = 0; e < nxp; ++e) {
+    const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+    xv[e] = *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
+  }
+  const int ylab = tid < FROWS ? a.labels[m0 + tid] : 0;
+  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane);
+  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane);
+#pragma unroll
+  for (int e = 0; e < nxp; ++e) {
+    const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+    *reinterpret_cast<uint4*>(xs + row * ldx + c8 * 8) = xv[e];
   }
   int* ys = reinterpret_cast<int*>(dlr + FROWS * LDR);           // [32] labels of the block
-  if (tid < FROWS) ys[tid] = a.labels[m0 + tid];
+  if (tid < FROWS) ys[tid] = ylab;
   __syncthreads();
   STAMP();
 
   // ---- logits: 32 rows x this wave's 32 columns, K = H in chunks of 8 k-steps (2 in flight)
   f32x4 acc[2][2];
   zero_acc(acc);
-  for (int ks = 0; ks < nks && !(a.skip & 4); ks += 2 * NKC) {
+  for (int ks = 0; ks < nks; ks += 2 * NKC) {
     fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane);
-    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.W, H, v0, ks + 2 * NKC, lane);
+    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane);
     if (ks + NKC < nks) {
       fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane);
-      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.W, H, v0, ks + 3 * NKC, lane);
+      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane);
     }
   }
   // the first dH pass's W_fc^T fragments go out now, under the softmax reductions (not earlier:
@@ -280,15 +296,13 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   STAMP();
   const int per = H / NW;                 // dH columns of this wave (a multiple of 64)
   bf16x8 bt[8][4];
-  fc2_load_wt(bt, a.WT, w * per, lane);
+  fc2_load_wt(bt, a.WTf, w * per, lane);
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float bb = a.b[v0 + c * 16 + lr];
+  for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[r][c][i] += bb;
-  }
+      for (int i = 0; i < 4; ++i) acc[r][c][i] += bias[c];
 
   // ---- softmax statistics over the 8 waves' columns
   float mx[2][4], se[2][4];
@@ -313,7 +327,6 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       if (lr == 0) red[NW * 32 + w * 32 + row] = e;
     }
   __syncthreads();
-  const float inv = a.inv_count[0];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -348,15 +361,15 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
     lrow[row] = (y >= 0) ? (logf(sum) + m - lab[row]) * inv : 0.f;
   }
   // dl^T: each column's 32 rows are 64 contiguous bytes -> four 16-B stores
-  for (int q = tid; q < V * 4 && !(a.skip & 2); q += 512) {
+  for (int q = tid; q < V * 4; q += 512) {
     const int col = q >> 2, seg = q & 3;
     *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) =
         *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
   }
   STAMP();
   // ---- dH = dl · W_fc: 32 rows x this wave's columns, 64 per pass, K = V = 256
-  for (int n0 = w * per; n0 < (w + 1) * per && !(a.skip & 8); n0 += 64) {
-    if (n0 != w * per) fc2_load_wt(bt, a.WT, n0, lane);
+  for (int n0 = w * per; n0 < (w + 1) * per; n0 += 64) {
+    if (n0 != w * per) fc2_load_wt(bt, a.WTf, n0, lane);
     f32x4 dacc[2][4];
     zero_acc(dacc);
 #pragma unroll
@@ -375,7 +388,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (!(a.skip & 1)) a.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = dacc[r][c][i];
+          a.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = dacc[r][c][i];
   }
   STAMP();
   __syncthreads();
@@ -451,22 +464,22 @@ __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
 }
 
 static bool fc_xent_v256_ok(const FcXentArgs& a) {
-  return a.V == 256 && a.dy && a.WT && !a.dl && a.H % 512 == 0 && a.M % FROWS == 0 &&
+  return a.V == 256 && a.dy && a.Wf && a.WTf && !a.dl && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
          !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');
 }
 
-void fc_xent(const FcXentArgs& a0, hipStream_t s) {
-  FcXentArgs a = a0;
-  if (std::getenv("GK_FC_SKIP")) a.skip = std::atoi(std::getenv("GK_FC_SKIP"));
+void fc_xent(const FcXentArgs& a, hipStream_t s) {
   if (fc_xent_v256_ok(a)) {
     const size_t shm = (size_t)FROWS * (a.H + kX2Pad) * 2 + (2 * 8 * 32 + 64) * 4 + 256 * 40 * 2 +
                        (size_t)FROWS * (256 + 8) * 2 + FROWS * 4;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    hipLaunchKernelGGL(fc_xent_v256_kernel, dim3(a.M / FROWS), dim3(512), shm, s, a);
+    if (a.H == 512) hipLaunchKernelGGL(fc_xent_v256_kernel<512>, dim3(a.M / FROWS), dim3(512), shm, s, a);
+    else hipLaunchKernelGGL(fc_xent_v256_kernel<1024>, dim3(a.M / FROWS), dim3(512), shm, s, a);
     return;
   }
   const int NW = a.V / 64;

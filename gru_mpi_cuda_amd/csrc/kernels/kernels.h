@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 typedef unsigned short u16;
+#define DEV_HOST_INLINE __host__ __device__ __forceinline__
 
 namespace gk {
 
@@ -127,7 +128,9 @@ struct FcXentArgs {
   const u16* WT = nullptr;
   float* dy = nullptr;
   int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
-  int skip = 0;   // EXPERIMENT
+  // FT-layout copies of W [V][H] and W^T [H][V] (ft_offset): required by the 8-wave V = 256 kernel
+  const u16* Wf = nullptr;
+  const u16* WTf = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic phase stamps of workgroup 0 (nullable)
 };
 void fc_xent(const FcXentArgs& a, hipStream_t s);
@@ -203,17 +206,28 @@ struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0; int* bump = nul
   void add_cast(const float* s, int splits, int R, int C, float* d, u16* bf, u16* bfT) {
     job[n++] = SlabJob{s, d, (long)R * C, splits, bf, bfT, R, C}; } };
 void reduce_slabs_multi(SlabJobs& j, hipStream_t s);
-struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; };
+// "FT" (fragment-tiled) bf16 layout of a K-contiguous [R][K] matrix: element (r, k) at
+//   ((r/16 * K/32 + k/32) * 64 + (r%16) + 16*((k%32)/8)) * 8 + k%8
+// i.e. every 16x32 MFMA operand fragment is 1 KB contiguous in lane order, so a fragment load is
+// 8 whole 128-B lines instead of 16 rows x 64-B pieces (per-CU load throughput is bound by line
+// requests: profiles/r1_fc_xent_notes).  ft_offset() gives the element index.
+DEV_HOST_INLINE long ft_offset(int r, int k, int K) {
+  return ((long)((r >> 4) * (K >> 5) + (k >> 5)) * 64 + (r & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+}
+struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; u16* dstF = nullptr; u16* dstTF = nullptr; };
 struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
-  void add(const float* s, int R, int C, u16* d, u16* dT) { job[n++] = CastJob{s, d, dT, R, C}; } };
+  void add(const float* s, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
+    job[n++] = CastJob{s, d, dT, R, C, dF, dTF}; } };
 void cast_multi(CastJobs& j, hipStream_t s);
 // Fused optimiser + weight refresh, one launch over every parameter tensor: Adam/SGD on the fp32
 // master slice [off, off+R*C) of the flat buffers, then (matrix jobs) its bf16 copy and/or bf16
 // transpose.  Matrix jobs need R % 64 == 0 and C % 64 == 0; R == 0 marks a flat (bias) job of C
 // elements, C % 4 == 0.
-struct OptCastJob { long off; int R, C; u16* dst; u16* dstT; };
+// dstF / dstTF (nullable): FT-layout copies of the matrix / its transpose (see ft_offset)
+struct OptCastJob { long off; int R, C; u16* dst; u16* dstT; u16* dstF = nullptr; u16* dstTF = nullptr; };
 struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
-  void add(long off, int R, int C, u16* d, u16* dT) { job[n++] = OptCastJob{off, R, C, d, dT}; } };
+  void add(long off, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
+    job[n++] = OptCastJob{off, R, C, d, dT, dF, dTF}; } };
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)

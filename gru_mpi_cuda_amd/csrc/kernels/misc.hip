@@ -194,16 +194,36 @@ __global__ void cast_multi_kernel(CastJobs j) {
     tile[y][tx] = v;
     if (J.dst && r < J.R && c < J.C) J.dst[(size_t)r * J.C + c] = f2bf(v);
   }
-  if (!J.dstT) return;
+  if (!J.dstT && !J.dstF && !J.dstTF) return;
   __syncthreads();
-  for (int y = ty; y < 64; y += 4) {
-    const int c = c0 + y, r = r0 + tx;
-    if (c < J.C && r < J.R) J.dstT[(size_t)c * J.R + r] = f2bf(tile[tx][y]);
+  if (J.dstT)
+    for (int y = ty; y < 64; y += 4) {
+      const int c = c0 + y, r = r0 + tx;
+      if (c < J.C && r < J.R) J.dstT[(size_t)c * J.R + r] = f2bf(tile[tx][y]);
+    }
+  if (J.R % 64 || J.C % 64) return;   // FT copies: whole 64 x 64 tiles only (checked on the host)
+  // 512 16-B pieces per tile: (4 row tiles x 2 k-steps) fragments of 64 lanes
+  for (int q = threadIdx.x; q < 512; q += 256) {
+    const int fl = q & 63, fr = (q >> 6) & 3, fk = q >> 8;   // lane, 16-row tile, 32-k step
+    const int rr = fr * 16 + (fl & 15), kk = fk * 32 + 8 * (fl >> 4);
+    u16 v[8];
+    if (J.dstF) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(tile[rr][kk + e]);
+      *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = *reinterpret_cast<const uint4*>(v);
+    }
+    if (J.dstTF) {   // transpose: rows are columns of the tile, k runs down its rows
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(tile[kk + e][rr]);
+      *reinterpret_cast<uint4*>(J.dstTF + ft_offset(c0 + rr, r0 + kk, J.R)) = *reinterpret_cast<const uint4*>(v);
+    }
   }
 }
 void cast_multi(CastJobs& j, hipStream_t s) {
   int tot = 0;
   for (int k = 0; k < j.n; ++k) {
+    if ((j.job[k].dstF || j.job[k].dstTF) && (j.job[k].R % 64 || j.job[k].C % 64))
+      throw std::runtime_error("cast_multi: FT copies need R, C % 64 == 0");
     j.blk_start[k] = tot;
     tot += ((j.job[k].R + 63) / 64) * ((j.job[k].C + 63) / 64);
   }
@@ -349,22 +369,42 @@ __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs
       w.y = (unsigned)h2 | ((unsigned)h3 << 16);
       *reinterpret_cast<uint2*>(J.dst + (size_t)r * J.C + c) = w;
     }
-    if (!J.dstT) continue;
+    if (!J.dstT && !J.dstF && !J.dstTF) continue;
     uint2 w2;
     w2.x = (unsigned)h0 | ((unsigned)h1 << 16);
     w2.y = (unsigned)h2 | ((unsigned)h3 << 16);
     *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w2;
   }
-  if (!J.dstT) return;
+  if (!J.dstT && !J.dstF && !J.dstTF) return;
   __syncthreads();
+  if (J.dstT) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int piece = threadIdx.x + 256 * q;          // 64 columns x 8 row segments
+      const int col = piece >> 3, seg = piece & 7;
+      u16 v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
+      *reinterpret_cast<uint4*>(J.dstT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+    }
+  }
+  // FT copies (fragment-tiled, kernels.h ft_offset): 512 16-B pieces per 64 x 64 tile
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int piece = threadIdx.x + 256 * q;          // 64 columns x 8 row segments
-    const int col = piece >> 3, seg = piece & 7;
+    const int pc = threadIdx.x + 256 * q;
+    const int fl = pc & 63, fr = (pc >> 6) & 3, fk = pc >> 8;   // lane, 16-row tile, 32-k step
+    const int rr = fr * 16 + (fl & 15), kk = fk * 32 + 8 * (fl >> 4);
     u16 v[8];
+    if (J.dstF) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
-    *reinterpret_cast<uint4*>(J.dstT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+      for (int e = 0; e < 8; ++e) v[e] = tile[rr][kk + e];
+      *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = *reinterpret_cast<const uint4*>(v);
+    }
+    if (J.dstTF) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[kk + e][rr];
+      *reinterpret_cast<uint4*>(J.dstTF + ft_offset(c0 + rr, r0 + kk, J.R)) = *reinterpret_cast<const uint4*>(v);
+    }
   }
 }
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {

@@ -34,3 +34,12 @@ def load_ext(build_if_missing: bool = True):
         raise ImportError(f"failed to load native extension {ext_path()}: {e}. "
                           "Rebuild with `python -m gru_mpi_cuda_amd.build_ext --force`") from e
     return _EXT
+
+
+def ft_layout(t):
+    """FT (fragment-tiled) copy of a K-contiguous [R][K] tensor (kernels.h ``ft_offset``):
+    every 16x32 MFMA operand fragment becomes 1 KB contiguous in lane order."""
+    R, K = t.shape
+    assert R % 16 == 0 and K % 32 == 0
+    # [R/16][16 rows][K/32][4 k-groups][8] -> [R/16][K/32][4 k-groups][16 rows][8]
+    return t.reshape(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)

@@ -13,6 +13,8 @@ s = torch.cuda.current_stream().cuda_stream
 X = (torch.randn(M, H, device=dev)).bfloat16()
 W = (torch.randn(V, H, device=dev) / H ** 0.5).bfloat16()
 WT = W.T.contiguous()
+from gru_mpi_cuda_amd.ops import ft_layout
+Wf, WTf = ft_layout(W), ft_layout(WT)
 b = torch.randn(V, device=dev) * 0.1
 y = torch.randint(0, V, (M,), device=dev, dtype=torch.int32)
 inv = torch.tensor([1.0 / M], device=dev)
@@ -21,7 +23,7 @@ lp = torch.empty(M // 32, device=dev)
 dy = torch.empty(M, H, device=dev)
 d = dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), labels=y.data_ptr(), inv_count=inv.data_ptr(),
          dlT=dlT.data_ptr(), loss_part=lp.data_ptr(), M=M, H=H, V=V, ldT=M, colT=0,
-         WT=WT.data_ptr(), dy=dy.data_ptr())
+         WT=WT.data_ptr(), dy=dy.data_ptr(), Wf=Wf.data_ptr(), WTf=WTf.data_ptr())
 # 20 launches captured in one graph: host launch overhead out of the measurement
 C.fc_xent(d, s)
 torch.cuda.synchronize()

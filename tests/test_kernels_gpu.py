@@ -178,8 +178,11 @@ def test_fc_xent(ext, fused_dh, H):
              dl=dl.data_ptr(), dlT=dlT.data_ptr(), loss_part=lp.data_ptr(), M=M, H=H, V=V, ldT=2 * M, colT=M)
     WT = W.T.contiguous()
     dy = torch.full((M, H), float("nan"), device=DEV)
-    if fused_dh:   # the training path: no row-major dl (H % 512 == 0 takes the 8-wave V=256 kernel)
-        d.update(WT=WT.data_ptr(), dy=dy.data_ptr())
+    if fused_dh:   # the training path: no row-major dl; with the FT copies and H % 512 == 0 it
+        # takes the 8-wave V = 256 kernel
+        from gru_mpi_cuda_amd.ops import ft_layout
+        Wf, WTf = ft_layout(W), ft_layout(WT)
+        d.update(WT=WT.data_ptr(), dy=dy.data_ptr(), Wf=Wf.data_ptr(), WTf=WTf.data_ptr())
         del d["dl"]
     ext.fc_xent(d, S())
     torch.cuda.synchronize()
