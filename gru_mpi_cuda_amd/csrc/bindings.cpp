@@ -154,6 +154,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
     SeqFwdArgs a;
     a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+    a.HF = GP(u16, d, "HF");
     a.xch = GP(u16, d, "xch");
     if (!a.xch) throw std::runtime_error("fwd_seq: exchange buffer xch [T][Bp][H] bf16 required");
     a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
@@ -173,6 +174,7 @@ PYBIND11_MODULE(_C, m) {
     a.sr = GP(const float, d, "sr"); a.sz = GP(const float, d, "sz"); a.sn = GP(const float, d, "sn");
     a.sghn = GP(const float, d, "sghn"); a.HSf = GP(const float, d, "HSf");
     a.HT = GP(const u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0); a.WhhT = GP(const u16, d, "WhhT");
+    a.HF = GP(const u16, d, "HF");
     a.xbuf = GP(u16, d, "xbuf"); a.dghT = GP(u16, d, "dghT"); a.dgiT = GP(u16, d, "dgiT");
     a.ldG = get<int>(d, "ldG", 0); a.dgi = GP(u16, d, "dgi");
     a.dWhh_part = GP(float, d, "dWhh_part"); a.dbhh_part = GP(float, d, "dbhh_part");

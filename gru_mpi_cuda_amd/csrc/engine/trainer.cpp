@@ -75,9 +75,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
   size_t o_sfc2 = R((size_t)kFcSplitsMax * V * H * 4), o_rfc2 = R((size_t)kFcSplitsMax * V * 4);
   size_t o_se = R((size_t)splits_ * V * E * 4);
-  std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0);
+  std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0), o_hf(L, 0);
   for (int l = 0; l < L; ++l) {
     if (seq_[l].fuse_w) o_pw[l] = R((size_t)nrb * 3 * H * H * 4);
+    if (seq_[l].fuse_w && persist_fwd_) o_hf[l] = R((tok + B) * H * 2);
     if (seq_[l].bwd) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
   }
   size_t o_pP = seq_[0].fuse_p ? R((size_t)nrb * V * 3 * H * 4) : 0;
@@ -88,6 +89,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
   for (int l = 0; l < L; ++l) {
     seq_[l].dWhh_part = seq_[l].fuse_w ? arena_.get<float>(o_pw[l]) : nullptr;
+    seq_[l].HF = o_hf[l] ? arena_.get<u16>(o_hf[l]) : nullptr;   // zero-filled: HF[0] = h_init
     seq_[l].dbhh_part = seq_[l].bwd ? arena_.get<float>(o_pbh[l]) : nullptr;
     seq_[l].dbih_part = seq_[l].bwd ? arena_.get<float>(o_pbi[l]) : nullptr;
   }

@@ -134,6 +134,7 @@ class Trainer {
   struct SeqPlan {
     bool bwd = false, fuse_w = false, fuse_p = false;
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
+    u16* HF = nullptr;   // fragment-tiled h for the fused dW_hh (SeqFwdArgs::HF)
   };
   // dp: data-parallel recording (overlapped readiness-ordered all-reduce, dP in place, tail after)
   void record_fb_seq(hipStream_t s0, bool dp = false);

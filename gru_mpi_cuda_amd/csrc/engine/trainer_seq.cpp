@@ -60,7 +60,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     if (persist_fwd_) {
       SeqFwdArgs a;
-      a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B;
+      a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = seq_[l].HF;
       a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
       a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
       a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
@@ -117,7 +117,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (q.bwd) {
       SeqBwdArgs a;
       a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
-      a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.WhhT = y.WhhT; a.xbuf = xbuf_;
+      a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
       a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;
       a.dgi = y.dgi;

@@ -259,6 +259,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     } else if (w == 1 && a.HT) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane >> 2][(lane & 3) * 8]);
       *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
+    } else if (w == 2 && a.HF) {   // the backward's dW_hh operand: one whole 1-KB block
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane & 15][8 * (lane >> 4)]);
+      *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
     }
     // saves for the backward pass AFTER the publish, so they are not part of wave 0's drain
     a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
@@ -355,9 +358,15 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     // the hand-off so the poll above does not wait behind them; first used after the publish
     bf16x8 hB[NTW > 0 ? NTW : 1];
     if constexpr (NTW > 0) {
+      if (a.HF) {   // whole 1-KB fragment blocks (8 lines each) instead of 16 rows x 64 B
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt)
-        hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
+        for (int nt = 0; nt < NTW; ++nt)
+          hB[nt] = ld8(a.HF + (((size_t)t * nunit + w * NTW + nt) * nrb + rbk) * 512 + lane * 8);
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+          hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
+      }
     }
     int idv[8];
     if constexpr (NTP > 0) {

@@ -72,6 +72,11 @@ struct SeqFwdArgs {
   u16* xch = nullptr;
   float* HSf = nullptr;            // [T+1][Bp][H] fp32
   u16* HT = nullptr; int ldT = 0;  // [H][ldT] bf16, h_t at column (t+1)*Bp + b (nullable)
+  // fragment-tiled copy of h for the backward's fused dW_hh (nullable): block (t, unit tile u,
+  // row block rb) at ((t * H/16 + u) * Bp/32 + rb) * 512 holds HS[t] units 16u + (l & 15), rows
+  // 32rb + 8(l >> 4) .. +8 in lane l's 16 bytes; step t writes block t+1, HF[0] = h_init is the
+  // caller's
+  u16* HF = nullptr;
   float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
   const u16* Whh = nullptr; const float* bhh = nullptr;
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
@@ -94,6 +99,7 @@ struct SeqBwdArgs {
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
+  const u16* HF = nullptr;         // SeqFwdArgs::HF of the same layer: preferred over HT when set
   const u16* WhhT = nullptr;       // [H][3H]
   u16* xbuf = nullptr;             // dGh exchange, one slot per step (no WAR reuse), tiled per producer:
                                    // [T][Bp/32][H/16][3 gates][32 rows][16 units] bf16

@@ -16,6 +16,7 @@ dy, sr, sz, sn, sghn = f(T, Bp, H), torch.rand(T, Bp, H, device=dev), torch.rand
     torch.tanh(f(T, Bp, H)), f(T, Bp, H)
 HSf = f(T + 1, Bp, H)
 HT = f(H, (T + 1) * Bp).bfloat16()
+HF = f((T + 1) * Bp * H).bfloat16()     # fragment-tiled h (SeqBwdArgs::HF); values irrelevant here
 WhhT = (torch.randn(H, H3, device=dev) / H ** 0.5).bfloat16()
 xbuf = torch.zeros(T, Bp, H3, device=dev, dtype=torch.bfloat16)
 dghT = torch.zeros(H3, T * Bp, device=dev, dtype=torch.bfloat16)
@@ -33,6 +34,8 @@ d = dict(dy=dy.data_ptr(), sr=sr.data_ptr(), sz=sz.data_ptr(), sn=sn.data_ptr(),
          T=T, Bp=Bp, H=H, V=V)
 if fuse_w:
     d["dWhh_part"] = dWp.data_ptr()
+    if int(os.environ.get("HF", 1)):
+        d["HF"] = HF.data_ptr()
 if fuse_p:
     d.update(ids=ids.data_ptr(), dP_part=dPp.data_ptr())
 if not (fuse_w and fuse_p):
