@@ -170,16 +170,30 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       }
       if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
         ar_ready_ = group_end(0);
-        ar_flush(s, true);
-        if (!dP_inplace_) {
-          hipEvent_t e = ev();
-          HIP_CHECK(hipEventRecord(e, s));
-          HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
-          comm_->allreduce_avg_f32(dP_, (long)V * H3, sc_);
-          ar_log_.push_back({-1, (long)V * H3});
-          ar_busy_ = true;
+        if (!ar_busy_) {
+          // nothing left to overlap with: the last collectives go on the step stream itself (a
+          // fork + join around them only adds graph edges -- measured: a forked branch in the
+          // step graph slowed the kernels beside it)
+          if (ar_ready_ > ar_launched_) {
+            comm_->allreduce_avg_f32(grads_ + ar_launched_, ar_ready_ - ar_launched_, s);
+            ar_log_.push_back({ar_launched_, ar_ready_ - ar_launched_});
+            ar_launched_ = ar_ready_;
+          }
+          if (!dP_inplace_) {
+            comm_->allreduce_avg_f32(dP_, (long)V * H3, s);
+            ar_log_.push_back({-1, (long)V * H3});
+          }
+        } else {
+          ar_flush(s, true);
+          if (!dP_inplace_) {
+            hipEvent_t e = ev();
+            HIP_CHECK(hipEventRecord(e, s));
+            HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
+            comm_->allreduce_avg_f32(dP_, (long)V * H3, sc_);
+            ar_log_.push_back({-1, (long)V * H3});
+          }
+          ar_join(s);
         }
-        ar_join(s);
       }
     } else {
       const int K = in_dim(l);
