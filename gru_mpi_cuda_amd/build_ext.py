@@ -81,6 +81,31 @@ def _link(objs, out, shared=True, libs=()):
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
+HOST_TOOL = ["capi/ckpt_check.cpp", "capi/ckpt_reader.cpp"]
+
+
+def build_host_tools(force: bool = False) -> list:
+    """Host-only tools (g++, no device code): bin/ckpt_check and bin/ckpt_check_asan, the latter
+    with AddressSanitizer + UBSan (sanitizers on host code; GPU sanitizers are not
+    available on the target pool)."""
+    gxx = shutil.which("g++") or "g++"
+    srcs = [os.path.join(CSRC, s) for s in HOST_TOOL]
+    newest = max(os.path.getmtime(p) for p in srcs + list(_headers()))
+    outs = []
+    for name, extra in (("ckpt_check", ["-O2"]),
+                        ("ckpt_check_asan", ["-O1", "-g", "-fsanitize=address,undefined",
+                                             "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"])):
+        out = os.path.join(HERE, "bin", name)
+        outs.append(out)
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+            continue
+        cmd = [gxx, "-std=c++17", *extra, f"-I{CSRC}", *srcs, "-o", out]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"host tool build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return outs
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
@@ -100,6 +125,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
             _link(drv, os.path.join(HERE, "bin", "namegen"), shared=False,
                   libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl", "-lrocprofiler-sdk-roctx",
                         f"-Wl,-rpath,{os.path.join(HERE, 'bin')}", "-Wl,-rpath,$ORIGIN"])
+    build_host_tools(force)
     if verbose:
         print(f"[build_ext] {ext_path()} ({len(srcs)} sources, arch {ARCH})")
     return ext_path()

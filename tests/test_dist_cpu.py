@@ -47,7 +47,7 @@ def _namegen_worker(rank, world, port, path, N, outdir):
     gdist.shutdown()
 
 
-@pytest.mark.parametrize("world,N", [(2, 37), (3, 20)])
+@pytest.mark.parametrize("world,N", [(2, 37), (3, 20), (8, 29)])
 def test_namegen_independent_of_world_size(tmp_path, world, N):
     cfg = GRUConfig(vocab=64, embed=8, hidden=16, layers=2, max_len=9, eos=3)
     path = str(tmp_path / "m.bin")
