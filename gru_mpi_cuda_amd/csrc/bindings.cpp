@@ -149,6 +149,8 @@ PYBIND11_MODULE(_C, m) {
     HIP_LAUNCH_CHECK();
   });
   m.def("spin_delay", [](int us, uintptr_t s) { spin_delay(us, S(s)); HIP_LAUNCH_CHECK(); });
+  m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
+    xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
@@ -162,7 +164,7 @@ PYBIND11_MODULE(_C, m) {
     a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
     a.h0 = GP(const float, d, "h0");
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
-    a.dbg = GP(unsigned long long, d, "dbg");
+    a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
@@ -181,6 +183,7 @@ PYBIND11_MODULE(_C, m) {
     a.dbih_part = GP(float, d, "dbih_part"); a.ids = GP(const int, d, "ids");
     a.dP_part = GP(float, d, "dP_part"); a.V = get<int>(d, "V", 0);
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
+    a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (!gru_bwd_seq_supported(a.H, a.Bp, a.dWhh_part != nullptr, a.dP_part != nullptr))
       throw std::runtime_error("bwd_seq: shape not supported");

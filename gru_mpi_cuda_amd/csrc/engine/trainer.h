@@ -146,6 +146,7 @@ class Trainer {
   std::vector<SeqPlan> seq_;
   int splits_ = 8;
   unsigned *cnt_ = nullptr, *err_ = nullptr;
+  int xcd_local_ = 1;          // persistent kernels may use the L2-local hand-off (GK_XCD_LOCAL=0: never)
   u16* xbuf_ = nullptr;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce

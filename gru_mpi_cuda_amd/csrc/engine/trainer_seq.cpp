@@ -65,7 +65,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
       a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
       if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
-      a.cnt = cnt_ + (size_t)l * fw; a.err = err_;
+      a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
       if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
       if (!seq_[l].bwd) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
@@ -123,7 +123,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dgi = y.dgi;
       a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
-      a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
+      a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));

@@ -143,11 +143,54 @@ DEV void stamp(unsigned long long* dbg, int t, int k) {
   dbg[((last ? 1 : 0) * 4096 + t) * 8 + k] = v;
 }
 
-// Workgroup -> (unit tile, row block): 1-D grid, unit tile as the fast index.  (Putting all unit
-// tiles of a row block on one XCD -- row block fast, so blocks b and b+8 of a row block share an
-// L2 -- measured no faster standalone and ~25 us slower inside the step: profiles/.)
-DEV int seq_unit_tile(int nrb) { return (int)(blockIdx.x % (gridDim.x / nrb)); }
-DEV int seq_row_block(int nrb) { return (int)(blockIdx.x / (gridDim.x / nrb)); }
+// Workgroup -> (unit tile, row block).  With Bp/32 a multiple of 8 the row block is the fast index
+// (block b -> row block b % nrb), so under the dispatcher's observed round-robin placement all unit
+// tiles of a row block share one XCD and its L2 (MI355X_MICROARCH.md § placement; a speed choice:
+// row_block_local() below checks the placement at run time and picks the protocol from it).
+DEV bool seq_rb_fast(int nrb) { return nrb % 8 == 0; }
+DEV int seq_unit_tile(int nrb) {
+  return seq_rb_fast(nrb) ? (int)(blockIdx.x / nrb) : (int)(blockIdx.x % (gridDim.x / nrb));
+}
+DEV int seq_row_block(int nrb) {
+  return seq_rb_fast(nrb) ? (int)(blockIdx.x % nrb) : (int)(blockIdx.x / (gridDim.x / nrb));
+}
+
+// Exchange protocol per row block, decided once per launch from where its workgroups actually
+// run: each workgroup publishes its XCC id (HW_REG_XCC_ID + 1, agent-scope sc1 store) in word 1
+// of its own flag line and reads every producer's word of its row block.  All on one XCD ->
+// L2-local hand-off: payload and flag are PLAIN stores (they stay in the shared L2; the producer's
+// vmcnt(0) covers them), consumers keep their L1-bypassing sc1 loads, served by that L2.  Any
+// producer elsewhere -> the placement-independent write-through (sc1) protocol.  Every member of
+// the row block evaluates the same words, so all agree.  The flag block is zeroed before the launch.
+DEV bool row_block_local(unsigned* flags /* the row block's producer lines */, int ut, int nunit,
+                         unsigned* err) {
+  __shared__ int s_local;
+  unsigned id;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+  if (threadIdx.x == 0)
+    __hip_atomic_store(flags + ut * kFlagStride + 1, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned v = id + 1u, spins = 0;
+    for (;;) {
+      if (lane < nunit) v = __hip_atomic_load(flags + lane * kFlagStride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all(v != 0u)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    const bool loc = __all(v == id + 1u);
+    if (lane == 0) s_local = loc ? 1 : 0;
+  }
+  __syncthreads();
+  return s_local != 0;
+}
+DEV void st16_plain(rsrc_t r, unsigned off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0); }
+DEV void signal_flag_local(unsigned* flag, unsigned epoch) {
+  __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);   // plain store: stays in L2
+}
 
 // ==================================================================== forward
 template <int NKW>
@@ -180,6 +223,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
   const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
   zero_next_flags(a.zero_next, a.zero_words);
+  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
 
   for (int t = 0; t < T; ++t) {
     stamp(a.dbg, t, 0);
@@ -251,9 +295,17 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
       // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
-      st16_sc1(rX, (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2, v);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride, (unsigned)(t + 1));
+      const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
+      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      if (loc) {
+        st16_plain(rX, xo, v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_flag_local(fl, (unsigned)(t + 1));
+      } else {
+        st16_sc1(rX, xo, v);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_flag(fl, (unsigned)(t + 1));
+      }
       stamp(a.dbg, t, 4);
       *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
     } else if (w == 1 && a.HT) {
@@ -314,6 +366,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   zero_acc(accP);
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   zero_next_flags(a.zero_next, a.zero_words);
+  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
   // next poll they would delay it (vmcnt retires in order), and they have a whole step to land
   float sv[6];
@@ -405,10 +458,15 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[g][lane >> 1][(lane & 1) * 8]);
-        st16_sc1(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
+        if (loc) st16_plain(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
+        else st16_sc1(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) signal_flag(a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride, (unsigned)(s + 1));
+      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      if (lane == 0) {
+        if (loc) signal_flag_local(fl, (unsigned)(s + 1));
+        else signal_flag(fl, (unsigned)(s + 1));
+      }
       stamp(a.dbg, s, 4);
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate

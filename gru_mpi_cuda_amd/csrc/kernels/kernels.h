@@ -87,6 +87,7 @@ struct SeqFwdArgs {
   long zero_words = 0;
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
+  int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -115,6 +116,7 @@ struct SeqBwdArgs {
   long zero_words = 0;
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
+  int allow_local = 1;             // as SeqFwdArgs::allow_local
   int T = 0, Bp = 0, H = 0;
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
@@ -236,6 +238,8 @@ struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
     job[n++] = OptCastJob{off, R, C, d, dT, dF, dTF}; } };
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 void fill_f32(float* p, long n, float v, hipStream_t s);
+// placement census: out[b] = HW_REG_XCC_ID of the CU that ran block b
+void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)
 void spin_delay(int us, hipStream_t s);
 

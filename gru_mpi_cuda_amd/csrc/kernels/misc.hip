@@ -510,4 +510,14 @@ void spin_delay(int us, hipStream_t s) {
   hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, (unsigned long long)capped * 100ull);
 }
 
+// Placement census (diagnostic): out[b] = XCC id of the CU that ran block b (HW_REG_XCC_ID).
+__global__ void xcc_census_kernel(unsigned* out) {
+  unsigned id;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(id));
+  if (threadIdx.x == 0) out[blockIdx.x] = id;
+}
+void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s) {
+  hipLaunchKernelGGL(xcc_census_kernel, dim3(nblocks), dim3(threads), 0, s, out);
+}
+
 }  // namespace gk

@@ -24,7 +24,7 @@ ids = torch.randint(0, V, (T, Bp), device=dev, dtype=torch.int32)
 cnt = torch.zeros(Bp // 32 * H // 16 * 16 + 64, device=dev, dtype=torch.int32)
 err = torch.zeros(16, device=dev, dtype=torch.int32)
 dbg = torch.zeros(2 * 4096 * 8, device=dev, dtype=torch.int64)
-d = dict(HSb=HSb.data_ptr(), xch=xch.data_ptr(), HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp,
+d = dict(allow_local=int(os.environ.get("LOCAL", 1)), HSb=HSb.data_ptr(), xch=xch.data_ptr(), HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp,
          sr=sv[0].data_ptr(), sz=sv[1].data_ptr(), sn=sv[2].data_ptr(), sghn=sv[3].data_ptr(),
          Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), P=P.data_ptr(), ids=ids.data_ptr(),
          cnt=cnt.data_ptr(), err=err.data_ptr(), T=T, Bp=Bp, H=H)

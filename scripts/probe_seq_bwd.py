@@ -28,7 +28,7 @@ dPp = torch.zeros(nrb, V, H3, device=dev)
 cnt = torch.zeros(nrb * H // 16 * 16 + 64, device=dev, dtype=torch.int32)
 err = torch.zeros(16, device=dev, dtype=torch.int32)
 dbg = torch.zeros(2 * 4096 * 8, device=dev, dtype=torch.int64)
-d = dict(dy=dy.data_ptr(), sr=sr.data_ptr(), sz=sz.data_ptr(), sn=sn.data_ptr(), sghn=sghn.data_ptr(),
+d = dict(allow_local=int(os.environ.get("LOCAL", 1)), dy=dy.data_ptr(), sr=sr.data_ptr(), sz=sz.data_ptr(), sn=sn.data_ptr(), sghn=sghn.data_ptr(),
          HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp, WhhT=WhhT.data_ptr(), xbuf=xbuf.data_ptr(),
          dbhh_part=dbh.data_ptr(), dbih_part=dbi.data_ptr(), cnt=cnt.data_ptr(), err=err.data_ptr(),
          T=T, Bp=Bp, H=H, V=V)

@@ -23,8 +23,9 @@ def rel(a, b):
 
 
 SCHEDULES = {
-    # name: (GK_PERSIST env, overlap)
+    # name: (GK_PERSIST env, overlap[, GK_XCD_LOCAL env])
     "persistent": ("1", False),
+    "persistent_sc1": ("1", False, "0"),   # the placement-independent write-through hand-off only
     "perstep": ("0", False),
     "overlap": ("1", True),
 }
@@ -32,11 +33,15 @@ SCHEDULES = {
 
 @pytest.mark.parametrize("sched", sorted(SCHEDULES))
 @pytest.mark.parametrize("layers,H,E,chunks,B", [(1, 128, 128, 2, 64), (2, 128, 128, 4, 96), (1, 128, 128, 1, 40),
-                                                 (1, 512, 512, 2, 64), (2, 256, 128, 2, 64), (1, 256, 256, 4, 256)])
+                                                 (1, 512, 512, 2, 64), (2, 256, 128, 2, 64), (1, 256, 256, 4, 256),
+                                                 (1, 512, 512, 4, 256), (2, 256, 256, 2, 512)])
 def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
+    """Row blocks (Bp/32) a multiple of 8 take the L2-local hand-off where the placement allows
+    (gru_seq.hip row_block_local); persistent_sc1 forces the write-through protocol."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    env, overlap = SCHEDULES[sched]
+    env, overlap, *xl = SCHEDULES[sched]
     monkeypatch.setenv("GK_PERSIST", env)
+    monkeypatch.setenv("GK_XCD_LOCAL", xl[0] if xl else "1")
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=8, time_chunks=chunks, seed=7,
                     overlap=overlap)
     params = init_params(cfg)
