@@ -133,8 +133,14 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(&h_stage_, 2 * (2 * tok + 16) * sizeof(int)));
   std::memset(h_stage_, 0, 2 * (2 * tok + 16) * sizeof(int));
+  // The staging events only tell the host that the graph which read a pinned slot has finished;
+  // the host never reads device results through them, so they skip the system-scope release
+  // (an end-of-step L2 writeback to host-coherent memory between consecutive step graphs).
+  const char* sf = std::getenv("GK_STAGE_SYSTEM_FENCE");
+  const unsigned stage_flags = hipEventDisableTiming |
+                               ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
   for (auto& e : stage_done_) {
-    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
     HIP_CHECK(hipEventRecord(e, s0_));
   }
   const char* ng = std::getenv("GK_NO_GRAPH");
