@@ -40,13 +40,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
-  prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
-
-  {   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]
+  {   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched
+      // together with the batch preparation (independent work, one graph node)
     GemmArgs g;
     g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
     g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
-    gemm_nt(g, s);
+    gemm_with_prep(g, PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_}, s);
   }
   // ------------------------------------------------------------------ forward
   for (int l = 0; l < L; ++l) {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include "kernels.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -81,6 +82,23 @@ DEV float wave_sum(float v) {
   v = sum16(v);
   v += __shfl_xor(v, 16, 64);
   return v + __shfl_xor(v, 32, 64);
+}
+
+
+// Batch preparation body (see prep_batch in kernels.h): block `blk` of `nblk` 256-thread blocks.
+DEV void prep_batch_body(const PrepJob& j, int blk, int nblk) {
+  const int B = j.in[0];
+  const int* x = j.in + 16;
+  const int* y = x + (size_t)j.Bmax * j.T;
+  const int n = j.T * j.Bp;
+  for (int i = blk * 256 + (int)threadIdx.x; i < n; i += nblk * 256) {
+    const int b = i / j.T, t = i - b * j.T;       // read in batch-major order (coalesced)
+    int xi = 0, yi = -1;
+    if (b < B) { xi = x[i]; yi = y[i]; }
+    j.ids[(size_t)t * j.Bp + b] = xi;
+    j.labels[(size_t)t * j.Bp + b] = yi;
+  }
+  if (blk == 0 && threadIdx.x == 0) j.inv_count[0] = __int_as_float(j.in[1]);
 }
 
 }  // namespace gk

@@ -148,6 +148,33 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_group_kernel(GemmGroup g) {
   gemm_lds_body<BIAS, ROWSUM>(g.job[k], id - g.start[k], g.ntn[k], g.ntm[k], g.kper[k], lds);
 }
 
+template <bool BIAS>
+__global__ void __launch_bounds__(256, 2) gemm_lds_prep_kernel(GemmArgs a, int ntn, int ntm, int kper, PrepJob pj,
+                                                                int nprep) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
+  const int ng = ntn * ntm * a.splits;
+  if ((int)blockIdx.x >= ng) {   // trailing blocks: batch transpose (block-uniform branch)
+    prep_batch_body(pj, (int)blockIdx.x - ng, nprep);
+    return;
+  }
+  gemm_lds_body<BIAS, false>(a, xcd_remap2(blockIdx.x, ng), ntn, ntm, kper, lds);
+}
+
+void gemm_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
+  if (!gemm_lds_ok(a) || a.rowsumA || a.accumulate) {
+    prep_batch(p.in, p.Bmax, p.T, p.Bp, p.ids, p.labels, p.inv_count, s);
+    gemm_nt(a, s);
+    return;
+  }
+  const int ntn = a.N / 128, ntm = a.M / 128, kper = a.K / a.splits;
+  const int nprep = prep_batch_blocks(p.T, p.Bp);
+  dim3 grid(ntn * ntm * a.splits + nprep), block(256);
+  if (a.bias && a.splits == 1)
+    hipLaunchKernelGGL((gemm_lds_prep_kernel<true>), grid, block, 0, s, a, ntn, ntm, kper, p, nprep);
+  else
+    hipLaunchKernelGGL((gemm_lds_prep_kernel<false>), grid, block, 0, s, a, ntn, ntm, kper, p, nprep);
+}
+
 bool gemm_lds_ok(const GemmArgs& a) {
   if (a.onehot_ids) return false;
   if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;

@@ -247,5 +247,16 @@ void spin_delay(int us, hipStream_t s);
 // batch-major int32 (may be pinned host memory, read zero-copy); out ids/labels time-major [T][Bp]
 // (pad rows: id 0, label -1) and inv_count.
 void prep_batch(const int* in, int Bmax, int T, int Bp, int* ids, int* labels, float* inv_count, hipStream_t s);
+struct PrepJob { const int* in; int Bmax, T, Bp; int* ids; int* labels; float* inv_count; };
+inline int prep_batch_blocks(int T, int Bp) {
+  const int n = (T * Bp + 255) / 256;
+  return n < 64 ? n : 64;
+}
+// The layer-0 P-table GEMM (P = Emb·W_ih0^T + b_ih0, only V/128 x 3H/128 tiles) and the batch
+// preparation in ONE launch: the transpose's latency-bound zero-copy reads of the pinned slot run
+// on blocks beside the GEMM tiles instead of as a kernel of their own (a forked graph branch for
+// it measured +95 us per step: profiles/r1_sched_fork_fence_ab.jsonl).  Falls back to two launches
+// when the GEMM shape is not LDS-kernel compatible.
+void gemm_with_prep(const GemmArgs& g, const PrepJob& p, hipStream_t s);
 
 }  // namespace gk

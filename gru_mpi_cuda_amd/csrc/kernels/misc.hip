@@ -474,22 +474,10 @@ void sum_partials(const float* partials, int n, float* out, hipStream_t s, int* 
 // Header: in[0] = B, in[1] = bits of 1/#valid labels (computed by the host).
 __global__ void prep_batch_kernel(const int* __restrict__ in, int Bmax, int T, int Bp, int* __restrict__ ids,
                                   int* __restrict__ labels, float* __restrict__ inv_count) {
-  const int B = in[0];
-  const int* x = in + 16;
-  const int* y = x + (size_t)Bmax * T;
-  const int n = T * Bp;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int b = i / T, t = i - b * T;          // read in batch-major order (coalesced)
-    int xi = 0, yi = -1;
-    if (b < B) { xi = x[i]; yi = y[i]; }
-    ids[(size_t)t * Bp + b] = xi;
-    labels[(size_t)t * Bp + b] = yi;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) inv_count[0] = __int_as_float(in[1]);
+  prep_batch_body(PrepJob{in, Bmax, T, Bp, ids, labels, inv_count}, blockIdx.x, gridDim.x);
 }
 void prep_batch(const int* in, int Bmax, int T, int Bp, int* ids, int* labels, float* inv_count, hipStream_t s) {
-  const int n = T * Bp;
-  const int blocks = (n + 255) / 256 < 64 ? (n + 255) / 256 : 64;
+  const int blocks = prep_batch_blocks(T, Bp);
   hipLaunchKernelGGL(prep_batch_kernel, dim3(blocks), dim3(256), 0, s, in, Bmax, T, Bp, ids, labels, inv_count);
 }
 
