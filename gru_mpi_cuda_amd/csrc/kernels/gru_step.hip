@@ -227,14 +227,15 @@ static void pick_split(int nks_total, int& ks, int& kb) {
 bool gru_step_picks_lds(int algo, int H, int Bp) {
   return algo == 2 || (algo == 0 && gru_step_lds_ok(H, Bp) && (H * 2 / 64) * (Bp / 128) >= 128);
 }
-static bool use_lds(int algo, int H, int Bp, bool fused, int ldT, int colT) {
-  const bool ok = !fused && gru_step_lds_ok(H, Bp) && ldT % 8 == 0 && colT % 8 == 0;
+static bool use_lds(int algo, int H, int Bp, bool fused, int Kin, int ldT, int colT) {
+  // fused input projection: a first K phase of Kin (whole 64-deep k-tiles)
+  const bool ok = (!fused || (Kin % 64 == 0 && Kin >= 64)) && gru_step_lds_ok(H, Bp) && ldT % 8 == 0 && colT % 8 == 0;
   if (algo == 2 && !ok) throw std::runtime_error("gru step: LDS kernel requested for an unsupported shape");
   return ok && gru_step_picks_lds(algo, H, Bp);
 }
 
 void gru_fwd_step(const FwdStepArgs& a, hipStream_t s) {
-  if (use_lds(a.algo, a.H, a.Bp, a.x_bf != nullptr, a.ldT, a.colT)) { gru_fwd_step_lds(a, s); return; }
+  if (use_lds(a.algo, a.H, a.Bp, a.x_bf != nullptr, a.Kin, a.ldT, a.colT)) { gru_fwd_step_lds(a, s); return; }
   const int nks = a.H / 32;
   int ks, kb;
   pick_split(nks, ks, kb);
@@ -261,7 +262,7 @@ void gru_fwd_step(const FwdStepArgs& a, hipStream_t s) {
 }
 
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s) {
-  if (use_lds(a.algo, a.H, a.Bp, false, a.ldT, a.colT)) { gru_bwd_step_lds(a, s); return; }
+  if (use_lds(a.algo, a.H, a.Bp, false, 0, a.ldT, a.colT)) { gru_bwd_step_lds(a, s); return; }
   const int nks = 3 * a.H / 32;
   int ks, kb;
   pick_split(nks, ks, kb);

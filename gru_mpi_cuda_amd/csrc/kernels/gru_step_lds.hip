@@ -12,6 +12,7 @@
 //             through the then-idle LDS.
 // Staging: global_load_lds_dwordx4 into a lane-linear LDS image, XOR swizzle on the source
 // address (conflict-free ds_read_b128), 2 buffers, one vmcnt(0) + barrier per 64-deep k-tile.
+#include <type_traits>
 #include "kernels.h"
 #include "common.h"
 
@@ -55,7 +56,13 @@ DEV void ring_loop(int nk, Stage&& stage, Compute&& compute) {
 
 // ==================================================================== forward
 // LDS: [FNS slots] x (A 128x64 + B 96x64) bf16 = FNS x 28 KiB
+// FUSED: the layer's input projection runs in the same tile as a first K phase (A = x rows,
+// B = W_ih gate rows, K = Kin) ahead of the recurrent phase (A = h_{t-1}, B = W_hh, K = H): the
+// r/z pre-activations of both phases share accumulators, the n gate keeps its input part apart
+// (n = tanh(gi_n + r * gh_n)).  Used for layers >= 1 of batched generation, where Gi cannot be
+// hoisted out of the time loop (the input is the layer below at the same step).
 constexpr int FNS = 4, BNS = 6;
+template <bool FUSED>
 __global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[FNS][(128 + 96) * 64];
   const int H = a.H;
@@ -66,86 +73,104 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a)
   const int srow = lane >> 3, sslot = lane & 7;
 
   // ---- epilogue operands first (latency hides under the K loop)
-  float gi[4][4][3], bh[3], hp[4][4];
+  constexpr int NGI = FUSED ? 1 : 4;
+  float gi[NGI][4][3], bh[3], bi[3], hp[4][4];
   const int u = j0 + wn * 16 + lr;
 #pragma unroll
-  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
-  // source rows first (all 16 ids in one round trip), then the 48 gathers
-  const float* src[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int b = b0 + wm * 64 + i * 16 + lq * 4 + e;
-      src[i][e] = a.Gi + (size_t)b * 3 * H;
-      hp[i][e] = a.hprev_f[(size_t)b * H + u];
-    }
-  if (a.ids) {
-    const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int4 v = id4[i * 4];
-      src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
-      src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
-    }
+  for (int g = 0; g < 3; ++g) {
+    bh[g] = a.bhh[g * H + u];
+    bi[g] = FUSED ? a.bih[g * H + u] : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+    for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * H + u];
+  if constexpr (!FUSED) {
+    // source rows first (all 16 ids in one round trip), then the 48 gathers
+    const float* src[4][4];
 #pragma unroll
-      for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
-
-  // ---- staging: A rows b0.., B rows (gate, unit) -> W_hh row g*H + j0 + unit
-  const u16* srcA[4];
-  const u16* srcB[3];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = (4 * w + q) * 8 + srow;
-    srcA[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
-  }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int r = (3 * w + q) * 8 + srow;       // 0..95
-    srcB[q] = a.Whh + (size_t)((r >> 5) * H + j0 + (r & 31)) * H + swz(r, sslot) * 8;
-  }
-  auto stage = [&](int buf, int kt) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void_t*)(&lds[buf][(4 * w + q) * 8 * 64]), 16, 0, 0);
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(128 + (3 * w + q) * 8) * 64]), 16, 0, 0);
-  };
-
-  f32x4 acc[4][3];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-  ring_loop<FNS, 7>(H / 64, stage, [&](int cur) {
-    const u16* LA = lds[cur];
-    const u16* LB = lds[cur] + 128 * 64;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + lq;
-      bf16x8 af[4], bfr[3];
+      for (int e = 0; e < 4; ++e) src[i][e] = a.Gi + (size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * 3 * H;
+    if (a.ids) {
+      const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + i * 16 + lr;
-        af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+        const int4 v = id4[i * 4];
+        src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
+        src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
       }
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const int r = g * 32 + wn * 16 + lr;
-        bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
     }
-  });
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+  }
+
+  f32x4 acc[4][3];
+  f32x4 accN[FUSED ? 4 : 1];   // input part of the n gate (FUSED)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (FUSED) accN[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // one K phase: A rows b0.. of Am [.][K], B rows (gate, unit) -> Bm row g*H + j0 + unit; the n
+  // gate accumulates into acc[.][2] or (input phase) accN
+  auto phase = [&](const u16* Am, const u16* Bm, int K, auto input_tag) {
+    constexpr bool input = decltype(input_tag)::value;
+    const u16* srcA[4];
+    const u16* srcB[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (4 * w + q) * 8 + srow;
+      srcA[q] = Am + (size_t)(b0 + r) * K + swz(r, sslot) * 8;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int r = (3 * w + q) * 8 + srow;       // 0..95
+      srcB[q] = Bm + (size_t)((r >> 5) * H + j0 + (r & 31)) * K + swz(r, sslot) * 8;
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void_t*)(&lds[buf][(4 * w + q) * 8 * 64]), 16, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(128 + (3 * w + q) * 8) * 64]), 16, 0, 0);
+    };
+    ring_loop<FNS, 7>(K / 64, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 128 * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[4], bfr[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm * 64 + i * 16 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+        }
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const int r = g * 32 + wn * 16 + lr;
+          bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i][0] = mfma16(af[i], bfr[0], acc[i][0]);
+          acc[i][1] = mfma16(af[i], bfr[1], acc[i][1]);
+          if constexpr (FUSED && input) accN[FUSED ? i : 0] = mfma16(af[i], bfr[2], accN[FUSED ? i : 0]);
+          else acc[i][2] = mfma16(af[i], bfr[2], acc[i][2]);
+        }
+      }
+    });
+  };
+  if constexpr (FUSED) phase(a.x_bf, a.Wih, a.Kin, std::true_type{});
+  phase(a.hprev_bf, a.Whh, H, std::false_type{});
 
   // ---- fused GRU epilogue from registers; bf16 h tile staged in LDS for the transposed copy
   u16* st = lds[0];     // [128 rows][32 units]
@@ -156,9 +181,12 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a)
       const int rr = wm * 64 + i * 16 + lq * 4 + e;
       const int b = b0 + rr;
       const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
-      const float r = sigmoidf_(gi[i][e][0] + ghr);
-      const float z = sigmoidf_(gi[i][e][1] + ghz);
-      const float n = tanhf_(gi[i][e][2] + r * ghn);
+      float gir, giz, gin;
+      if constexpr (FUSED) { gir = bi[0]; giz = bi[1]; gin = accN[FUSED ? i : 0][e] + bi[2]; }
+      else { gir = gi[FUSED ? 0 : i][e][0]; giz = gi[FUSED ? 0 : i][e][1]; gin = gi[FUSED ? 0 : i][e][2]; }
+      const float r = sigmoidf_(gir + ghr);
+      const float z = sigmoidf_(giz + ghz);
+      const float n = tanhf_(gin + r * ghn);
       const float h = n + z * (hp[i][e] - n);
       const size_t o = (size_t)b * H + u;
       a.h_f[o] = h;
@@ -295,7 +323,9 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a)
 bool gru_step_lds_ok(int H, int Bp) { return H >= 1024 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(gru_fwd_step_lds_kernel, dim3(a.H / 32, a.Bp / 128), dim3(256), 0, s, a);
+  const dim3 grid(a.H / 32, a.Bp / 128), block(256);
+  if (a.x_bf) hipLaunchKernelGGL(gru_fwd_step_lds_kernel<true>, grid, block, 0, s, a);
+  else hipLaunchKernelGGL(gru_fwd_step_lds_kernel<false>, grid, block, 0, s, a);
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(gru_bwd_step_lds_kernel, dim3(a.H / 64, a.Bp / 64), dim3(256), 0, s, a);
