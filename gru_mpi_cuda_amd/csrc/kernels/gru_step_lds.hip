@@ -12,6 +12,7 @@
 //             through the then-idle LDS.
 // Staging: global_load_lds_dwordx4 into a lane-linear LDS image, XOR swizzle on the source
 // address (conflict-free ds_read_b128), 2 buffers, one vmcnt(0) + barrier per 64-deep k-tile.
+#include <cstdlib>
 #include <type_traits>
 #include "kernels.h"
 #include "common.h"
@@ -62,9 +63,12 @@ DEV void ring_loop(int nk, Stage&& stage, Compute&& compute) {
 // (n = tanh(gi_n + r * gh_n)).  Used for layers >= 1 of batched generation, where Gi cannot be
 // hoisted out of the time loop (the input is the layer below at the same step).
 constexpr int FNS = 4, BNS = 6;
-template <bool FUSED>
-__global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[FNS][(128 + 96) * 64];
+// NS: LDS ring depth.  4 (112 KiB, one workgroup per CU) when the grid is about one wave of
+// workgroups (training at H = 2048: 256 tiles); 2 (56 KiB, two per CU) for big-batch generation,
+// where several rounds of tiles per CU need the second workgroup to hide latency.
+template <bool FUSED, int NS>
+__global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
   const int H = a.H;
   const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 128;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -142,7 +146,7 @@ __global__ void __launch_bounds__(256, 1) gru_fwd_step_lds_kernel(FwdStepArgs a)
       for (int q = 0; q < 3; ++q)
         __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(128 + (3 * w + q) * 8) * 64]), 16, 0, 0);
     };
-    ring_loop<FNS, 7>(K / 64, stage, [&](int cur) {
+    ring_loop<NS, 7>(K / 64, stage, [&](int cur) {
       const u16* LA = lds[cur];
       const u16* LB = lds[cur] + 128 * 64;
 #pragma unroll
@@ -324,8 +328,15 @@ bool gru_step_lds_ok(int H, int Bp) { return H >= 1024 && H % 64 == 0 && Bp % 12
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);
-  if (a.x_bf) hipLaunchKernelGGL(gru_fwd_step_lds_kernel<true>, grid, block, 0, s, a);
-  else hipLaunchKernelGGL(gru_fwd_step_lds_kernel<false>, grid, block, 0, s, a);
+  int ns = grid.x * grid.y >= 512 ? 2 : 4;
+  if (const char* e = std::getenv("GK_STEP_LDS_NS")) ns = std::atoi(e) == 2 ? 2 : 4;
+  if (ns == 2) {
+    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 2>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 2>), grid, block, 0, s, a);
+  } else {
+    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, FNS>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, FNS>), grid, block, 0, s, a);
+  }
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(gru_bwd_step_lds_kernel, dim3(a.H / 64, a.Bp / 64), dim3(256), 0, s, a);
