@@ -208,6 +208,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fc_sample", [](py::dict d, uintptr_t s) {
     FcSampleArgs a;
     a.X = GP(const u16, d, "X"); a.W = GP(const u16, d, "W"); a.b = GP(const float, d, "b");
+    a.Wf = GP(const u16, d, "Wf");
     a.rf = GP(const float, d, "rf"); a.ids = GP(int, d, "ids"); a.out = GP(unsigned char, d, "out");
     a.alive = GP(int, d, "alive"); a.probs = GP(float, d, "probs");
     a.N = get<int>(d, "N", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0); a.V = get<int>(d, "V", 0);

@@ -20,13 +20,15 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
     oWih.push_back(arena_.reserve((size_t)3 * H * (l == 0 ? E : H) * 2));
   }
   size_t oEmb = arena_.reserve((size_t)V * E * 2), oWfc = arena_.reserve((size_t)V * H * 2);
+  size_t oWfcF = arena_.reserve((size_t)V * H * 2);   // fragment-tiled copy for the 8-wave sampler
   size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
   arena_.commit();
   for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
   for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
-  Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); Ptab_ = arena_.get<float>(oP);
+  Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); WfcF_ = arena_.get<u16>(oWfcF);
+  Ptab_ = arena_.get<float>(oP);
   rf_ = arena_.get<float>(orf); ids_ = arena_.get<int>(oids); alive_ = arena_.get<int>(oal);
   out_ = arena_.get<unsigned char>(oout);
   HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
@@ -48,7 +50,7 @@ void Generator::refresh_weights(hipStream_t s) {
     j.add(P("weight_hh_l" + k), 3 * H, H, Whh_[l], nullptr);
     j.add(P("weight_ih_l" + k), 3 * H, l == 0 ? E : H, Wih_[l], nullptr);
   }
-  j.add(P("fc.weight"), V, H, Wfc_, nullptr);
+  j.add(P("fc.weight"), V, H, Wfc_, nullptr, (V % 64 || H % 64) ? nullptr : WfcF_);
   cast_multi(j, s);
   GemmArgs g;   // layer-0 input projection table P = Emb · W_ih0^T + b_ih0  ([V][3H])
   g.A = Emb_; g.lda = E; g.B = Wih_[0]; g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
@@ -82,7 +84,7 @@ void Generator::record_steps(int n, hipStream_t s) {
       gru_fwd_step(a, s);
     }
     FcSampleArgs f;
-    f.X = hb_[2 * (L - 1) + nxt]; f.W = Wfc_; f.b = P("fc.bias"); f.rf = rf_;
+    f.X = hb_[2 * (L - 1) + nxt]; f.W = Wfc_; f.Wf = WfcF_; f.b = P("fc.bias"); f.rf = rf_;
     f.ids = ids_; f.out = out_; f.alive = alive_; f.probs = (st == ML - 1) ? probe_ : nullptr;
     f.N = n; f.Bp = Bp; f.H = H; f.V = V; f.step = st; f.max_len = ML; f.eos = d_.eos;
     fc_sample(f, s);

@@ -49,7 +49,7 @@ class Generator {
   std::vector<float*> hf_;             // [L*2][Bmax][H]
   std::vector<u16*> hb_;
   std::vector<u16*> Whh_, Wih_;
-  u16 *Emb_, *Wfc_;
+  u16 *Emb_, *Wfc_, *WfcF_;
   float *Ptab_, *rf_;
   int *ids_, *alive_;
   unsigned char* out_;

@@ -463,6 +463,132 @@ __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
   }
 }
 
+// Generation at V = 256: the 8-wave logits structure of fc_xent_v256 (X tile staged in LDS, each
+// wave streaming a 32-column W_fc slab from the fragment-tiled copy, whole lines per load), then
+// softmax into an LDS probability tile and the same inverse-CDF scan as fc_sample_kernel.
+template <int HH>
+__global__ void __launch_bounds__(512, 1) fc_sample_v256_kernel(FcSampleArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int V = 256, NW = 8, NKC = 8, H = HH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int ldx = H + kX2Pad, m0 = blockIdx.x * FROWS;
+  u16* xs = reinterpret_cast<u16*>(smem);                         // [32][H + 8]
+  float* red = reinterpret_cast<float*>(xs + FROWS * ldx);         // [2][8][32]
+  float* prob = red + 2 * NW * 32;                                 // [32][V]
+  const int v0 = w * 32, nks = H / 32;
+  float bias[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) bias[c] = a.b[v0 + c * 16 + lr];
+  bf16x8 b0[NKC][2], b1[NKC][2];
+  constexpr int nxp = FROWS * H / 8 / 512;
+  uint4 xv[nxp];
+#pragma unroll
+  for (int e = 0; e < nxp; ++e) {
+    const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+    xv[e] = *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
+  }
+  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane);
+  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane);
+#pragma unroll
+  for (int e = 0; e < nxp; ++e) {
+    const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+    *reinterpret_cast<uint4*>(xs + row * ldx + c8 * 8) = xv[e];
+  }
+  __syncthreads();
+  f32x4 acc[2][2];
+  zero_acc(acc);
+  for (int ks = 0; ks < nks; ks += 2 * NKC) {
+    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane);
+    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane);
+    if (ks + NKC < nks) {
+      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane);
+      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[r][c][i] += bias[c];
+  // softmax over the 8 waves' columns: row max, then row sum of exp
+  float mx[2][4];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float m = max16(fmaxf(acc[r][0][i], acc[r][1][i]));
+      if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i;
+      float m = red[row];
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+      mx[r][i] = m;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) acc[r][c][i] = __expf(acc[r][c][i] - m);
+      const float e = sum16(acc[r][0][i] + acc[r][1][i]);
+      if (lr == 0) red[NW * 32 + w * 32 + row] = e;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i;
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
+      const float rs = 1.f / sum;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int col = v0 + c * 16 + lr;
+        const float p = acc[r][c][i] * rs;
+        prob[row * V + col] = p;
+        if (a.probs) a.probs[(size_t)(m0 + row) * V + col] = p;
+      }
+    }
+  __syncthreads();
+  // inverse CDF (namegensf.cu:326-331): one wave per row, 4 consecutive probabilities per lane
+  for (int row = w; row < FROWS; row += NW) {
+    const int b = m0 + row;
+    if (b >= a.N) continue;                              // padding rows (wave-uniform)
+    const float rnd = a.rf[(size_t)b * a.max_len + a.step];
+    const float4 pv = *reinterpret_cast<const float4*>(prob + row * V + lane * 4);
+    const float loc = ((pv.x + pv.y) + pv.z) + pv.w;     // index order, as the reference's loop
+    float inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    float psum = inc - loc;
+    int hit = V;
+    const float pe[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      psum += pe[e];
+      if (hit == V && psum > rnd) hit = lane * 4 + e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hit = min(hit, __shfl_xor(hit, o, 64));
+    if (lane == 0) {
+      const int sel = (hit >= V) ? V - 1 : hit;
+      if (a.alive[b]) {
+        a.out[(size_t)b * (a.max_len + 1) + a.step] = (unsigned char)sel;
+        if (sel == a.eos) a.alive[b] = 0;
+      }
+      a.ids[b] = sel;
+    }
+  }
+}
+
 static bool fc_xent_v256_ok(const FcXentArgs& a) {
   return a.V == 256 && a.dy && a.Wf && a.WTf && !a.dl && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
          !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');
@@ -494,6 +620,18 @@ void fc_xent(const FcXentArgs& a, hipStream_t s) {
 }
 
 void fc_sample(const FcSampleArgs& a, hipStream_t s) {
+  if (a.Wf && a.V == 256 && (a.H == 512 || a.H == 1024) && a.Bp % FROWS == 0) {
+    const size_t shm = (size_t)FROWS * (a.H + kX2Pad) * 2 + (2 * 8 * 32) * 4 + (size_t)FROWS * 256 * 4;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)fc_sample_v256_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)fc_sample_v256_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    if (a.H == 512) hipLaunchKernelGGL(fc_sample_v256_kernel<512>, dim3(a.Bp / FROWS), dim3(512), shm, s, a);
+    else hipLaunchKernelGGL(fc_sample_v256_kernel<1024>, dim3(a.Bp / FROWS), dim3(512), shm, s, a);
+    return;
+  }
   const int NW = a.V / 64;
   const size_t shm = (2 * NW * 32) * 4 + (size_t)a.V * FROWS * 4;
   const int nks = a.H / 32;

@@ -146,6 +146,7 @@ void fc_xent(const FcXentArgs& a, hipStream_t s);
 struct FcSampleArgs {              // generation: logits -> softmax -> inverse-CDF sample
   const u16* X = nullptr;          // [Bp][H]
   const u16* W = nullptr;          // [V][H]
+  const u16* Wf = nullptr;         // FT copy of W (nullable; V = 256, H in {512, 1024}: 8-wave kernel)
   const float* b = nullptr;        // [V]
   const float* rf = nullptr;       // [N][max_len] uniforms (global name index)
   int* ids = nullptr;              // [Bp] in: unused / out: sampled char (next input)

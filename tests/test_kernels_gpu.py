@@ -199,9 +199,11 @@ def test_fc_xent(ext, fused_dh, H):
         torch.testing.assert_close(dy, dl.float() @ W.float(), atol=1e-5, rtol=1e-3)
 
 
-def test_fc_sample(ext):
+@pytest.mark.parametrize("H", [128, 512, 1024])   # 512/1024: 8-wave kernel on the FT copy of W_fc
+def test_fc_sample(ext, H):
     from gru_mpi_cuda_amd.models.cpu_ref import sample_inverse_cdf
-    N, Bp, H, V, ML = 50, 64, 128, 256, 6
+    from gru_mpi_cuda_amd.ops import ft_layout
+    N, Bp, V, ML = 50, 64, 256, 6
     X = bf(rnd(Bp, H, seed=1))
     W = bf(rnd(V, H, scale=3 * H ** -0.5, seed=2))
     b = rnd(V, seed=3)
@@ -212,9 +214,13 @@ def test_fc_sample(ext):
     out = torch.zeros(N, ML + 1, device=DEV, dtype=torch.uint8)
     probs = torch.zeros(Bp, V, device=DEV)
     step = 2
-    ext.fc_sample(dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), rf=rf.data_ptr(), ids=ids.data_ptr(),
-                       out=out.data_ptr(), alive=alive.data_ptr(), probs=probs.data_ptr(), N=N, Bp=Bp, H=H, V=V,
-                       step=step, max_len=ML, eos=0), S())
+    d = dict(X=X.data_ptr(), W=W.data_ptr(), b=b.data_ptr(), rf=rf.data_ptr(), ids=ids.data_ptr(),
+             out=out.data_ptr(), alive=alive.data_ptr(), probs=probs.data_ptr(), N=N, Bp=Bp, H=H, V=V,
+             step=step, max_len=ML, eos=0)
+    if H >= 512:
+        Wf = ft_layout(W)
+        d["Wf"] = Wf.data_ptr()
+    ext.fc_sample(d, S())
     torch.cuda.synchronize()
     ref_p = torch.softmax(X.float() @ W.float().T + b, -1)
     torch.testing.assert_close(probs, ref_p, atol=1e-5, rtol=1e-4)
