@@ -28,6 +28,8 @@ def _add_model_args(ap: argparse.ArgumentParser) -> None:
                       ("clip_norm", float), ("seed", int), ("bucket_mb", float), ("time_chunks", int)):
         ap.add_argument("--" + name.replace("_", "-"), dest=name, type=typ, default=None)
     ap.add_argument("--optimizer", choices=["adam", "sgd"], default=None)
+    ap.add_argument("--carry-hidden", dest="carry_hidden", action="store_const", const=True, default=None,
+                    help="truncated BPTT: carry each step's final hidden state into the next step")
 
 
 def _cfg_from(args):

@@ -37,6 +37,8 @@ class GRUConfig:
     clip_norm: float = 0.0      # 0 = off; global-norm gradient clipping otherwise
     dtype: str = "bf16"         # compute dtype of the HIP engine (fp32 master weights)
     seed: int = 1234
+    carry_hidden: bool = False  # truncated BPTT over a continuous stream: each step starts from the
+                                # previous step's final (detached) hidden state
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step

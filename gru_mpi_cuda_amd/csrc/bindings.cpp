@@ -78,6 +78,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_step", &Trainer::set_step)
       .def("set_lr", &Trainer::set_lr)
       .def("set_use_graph", &Trainer::set_use_graph)
+      .def("set_carry", &Trainer::set_carry)
+      .def("carry", &Trainer::carry)
+      .def("reset_hidden", [](Trainer& t, uintptr_t s) { t.reset_hidden(S(s)); })
       .def("padded_batch", &Trainer::padded_batch)
       .def("workspace_bytes", &Trainer::workspace_bytes)
       .def("plan", &Trainer::plan)

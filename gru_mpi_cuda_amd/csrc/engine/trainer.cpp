@@ -165,6 +165,44 @@ hipEvent_t Trainer::ev() {
   return events_[ev_next_++];
 }
 
+void Trainer::set_carry(bool on) {
+  if (on == carry_) return;
+  carry_ = on;
+  for (auto& g : g_fb_) g.reset();   // the copies and the kernels' h0 argument are captured
+  for (auto& g : g_step_) g.reset();
+}
+
+// Every copy of h kept per step: fp32 and bf16 row-major [T+1][Bp][H], the transposed bf16
+// [H][(T+1)Bp] (columns t*Bp..) and, for fused backward layers, the fragment-tiled HF (slot t
+// contiguous, Bp*H elements).  HS[0] is h_init for the forward and h_{-1} for the backward.
+void Trainer::record_carry(hipStream_t s) {
+  const int H = d_.H, T = d_.T, B = Bp_;
+  const size_t n = (size_t)B * H, ldT = (size_t)(T + 1) * B;
+  for (int l = 0; l < d_.L; ++l) {
+    Layer& y = Ls_[l];
+    HIP_CHECK(hipMemcpyAsync(y.HSf, y.HSf + (size_t)T * n, n * 4, hipMemcpyDeviceToDevice, s));
+    HIP_CHECK(hipMemcpyAsync(y.HSb, y.HSb + (size_t)T * n, n * 2, hipMemcpyDeviceToDevice, s));
+    HIP_CHECK(hipMemcpy2DAsync(y.HT, ldT * 2, y.HT + (size_t)T * B, ldT * 2, (size_t)B * 2, H,
+                               hipMemcpyDeviceToDevice, s));
+    if (seq_[l].HF)
+      HIP_CHECK(hipMemcpyAsync(seq_[l].HF, seq_[l].HF + (size_t)T * n, n * 2, hipMemcpyDeviceToDevice, s));
+  }
+}
+
+void Trainer::reset_hidden(hipStream_t s) {
+  const int H = d_.H, T = d_.T, B = Bp_;
+  const size_t n = (size_t)B * H, ldT = (size_t)(T + 1) * B;
+  for (int l = 0; l < d_.L; ++l) {
+    Layer& y = Ls_[l];
+    for (int t : {0, T}) {
+      HIP_CHECK(hipMemsetAsync(y.HSf + (size_t)t * n, 0, n * 4, s));
+      HIP_CHECK(hipMemsetAsync(y.HSb + (size_t)t * n, 0, n * 2, s));
+      HIP_CHECK(hipMemset2DAsync(y.HT + (size_t)t * B, ldT * 2, 0, (size_t)B * 2, H, s));
+      if (seq_[l].HF) HIP_CHECK(hipMemsetAsync(seq_[l].HF + (size_t)t * n, 0, n * 2, s));
+    }
+  }
+}
+
 void Trainer::set_lr(float lr) {
   o_.lr = lr;
   g_opt_.reset();   // lr is a kernel argument frozen into the captured graphs
@@ -274,6 +312,7 @@ void Trainer::record_fb(hipStream_t s0) {
     HIP_CHECK(hipStreamWaitEvent(to, e, 0));
   };
   prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s0);
+  if (carry_) record_carry(s0);
   edge(s0, s1);   // fork
 
   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)]  (exact: Emb[x]·W^T)

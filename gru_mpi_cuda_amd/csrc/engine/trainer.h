@@ -47,6 +47,12 @@ class Trainer {
   void set_step(int v);                                 // for resume
   void set_lr(float lr);
   void set_use_graph(bool g) { use_graph_ = g; }
+  // Truncated BPTT over a continuous stream: with carry on, each step starts from
+  // the previous step's final hidden state (HS[T] -> HS[0] copies at the head of the step graph;
+  // no gradient flows into it).  reset_hidden zeroes the carried state.
+  void set_carry(bool on);
+  bool carry() const { return carry_; }
+  void reset_hidden(hipStream_t s);
   int padded_batch() const { return Bp_; }
   long workspace_bytes() const { return (long)arena_.bytes(); }
   // test/debug access to internal buffers by name
@@ -54,6 +60,8 @@ class Trainer {
 
  private:
   void record_fb(hipStream_t s0);
+  void record_carry(hipStream_t s);     // HS[T] -> HS[0] of every layer and copy (carry_ only)
+  bool carry_ = false;
   void record_opt(hipStream_t s0);
   void fwd_step(int l, int t, hipStream_t s);
   void bwd_step(int l, int t, hipStream_t s);

@@ -47,6 +47,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
     gemm_with_prep(g, PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_}, s);
   }
+  if (carry_) record_carry(s);
   // ------------------------------------------------------------------ forward
   for (int l = 0; l < L; ++l) {
     Layer& y = Ls_[l];
@@ -67,6 +68,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
       if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
+      if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
       if (!seq_[l].bwd) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
       gru_fwd_seq(a, s);
     } else {

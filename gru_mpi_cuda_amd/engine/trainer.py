@@ -57,6 +57,7 @@ class HipTrainer:
         self.t = self.C.Trainer(dims, opt, self.params.data_ptr(), self.grads.data_ptr(),
                                 self.m.data_ptr(), self.v.data_ptr(), self.layout.total, offsets)
         self.t.set_use_graph(use_graph)
+        self.t.set_carry(bool(cfg.carry_hidden))
         if self.comm is not None:     # identical replicas: rank 0's weights everywhere
             self.comm.broadcast_f32(self.params.data_ptr(), self.layout.total, 0, self._stream())
             # all-reduce recorded INTO the step graph: readiness-ordered buckets of at least
@@ -117,6 +118,10 @@ class HipTrainer:
     def loss(self) -> float:
         return self.t.read_loss()
 
+    def reset_state(self) -> None:
+        """Zero the carried hidden state (truncated BPTT, ``cfg.carry_hidden``)."""
+        self.t.reset_hidden(self._stream())
+
     def state_dict(self) -> Dict[str, torch.Tensor]:
         torch.cuda.synchronize(self.dev)
         return {k: v.cpu() for k, v in from_flat(self.cfg, self.params).items()}
@@ -150,10 +155,18 @@ class CpuTrainer:
         self.opt = cpu_ref.Adam(cfg, self.params)
         self.buckets = _bucket_list(cfg, self.layout.total)
         self._loss = float("nan")
+        self._state = None            # carried hidden state (cfg.carry_hidden)
+
+    def reset_state(self) -> None:
+        self._state = None
 
     def forward_backward(self, x: np.ndarray, y: np.ndarray) -> None:
+        out = [] if self.cfg.carry_hidden else None
         loss, grads = cpu_ref.manual_backward(self.params, self.cfg, torch.from_numpy(np.asarray(x)),
-                                              torch.from_numpy(np.asarray(y)))
+                                              torch.from_numpy(np.asarray(y)), h0=self._state,
+                                              state_out=out)
+        if out is not None:
+            self._state = out
         for k, g in grads.items():
             self.gviews[k].copy_(g)
         self._loss = float(loss)

@@ -75,10 +75,16 @@ def xent(logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return (nll * valid).sum() / valid.sum().clamp_min(1)
 
 
-def manual_backward(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Tensor
+def manual_backward(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Tensor,
+                    h0: Optional[List[torch.Tensor]] = None, state_out: Optional[list] = None
                     ) -> Tuple[torch.Tensor, Params]:
-    """Explicit BPTT. Returns (loss, grads) with grads keyed like params."""
-    logits, caches = forward(params, cfg, x, keep_cache=True)
+    """Explicit BPTT. Returns (loss, grads) with grads keyed like params.
+
+    h0: optional per-layer initial states (truncated BPTT: treated as constants, no gradient
+    flows into them).  state_out: if a list, receives the per-layer final states h_{T-1}."""
+    logits, caches = forward(params, cfg, x, h0=h0, keep_cache=True)
+    if state_out is not None:
+        state_out[:] = [c["out"][:, -1].detach().clone() for c in caches]
     B, T, V = logits.shape
     H = cfg.hidden
     valid = (y >= 0)
@@ -121,9 +127,11 @@ def manual_backward(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Te
     return loss, g
 
 
-def autograd_grads(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Tensor):
+def autograd_grads(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Tensor,
+                   h0: Optional[List[torch.Tensor]] = None):
     ps = {k: v.detach().clone().requires_grad_(True) for k, v in params.items()}
-    loss = xent(forward(ps, cfg, x), y)
+    h0 = None if h0 is None else [h.detach() for h in h0]
+    loss = xent(forward(ps, cfg, x, h0=h0), y)
     loss.backward()
     return loss.detach(), {k: v.grad for k, v in ps.items()}
 

@@ -149,3 +149,37 @@ def test_data_streams():
     np.testing.assert_array_equal(x[:, 1:], y[:, :-1])     # next-char targets
     xp, yp = make_padded_batch(synthetic_names(5, seed=1), 16)
     assert (yp == -1).any() and (xp[:, 0] == 0).all()
+
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_truncated_bptt_carried_state(layers):
+    """carry_hidden: h0 is a constant of the step -- manual BPTT with h0 equals
+    autograd with a detached h0, and CpuTrainer carries each step's final state into the next."""
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    cfg = GRUConfig(vocab=256, embed=24, hidden=16, layers=layers, batch=6, seq=5, seed=3, carry_hidden=True)
+    p = {k: v.double() for k, v in init_params(cfg).items()}
+    ds = NameStream(cfg.batch, cfg.seq, seed=9)
+    x, y = (torch.from_numpy(a) for a in ds.next())
+    h0 = [torch.randn(cfg.batch, cfg.hidden, dtype=torch.float64) * 0.5 for _ in range(layers)]
+    out = []
+    loss, g = cpu_ref.manual_backward(p, cfg, x, y, h0=h0, state_out=out)
+    loss_a, g_a = cpu_ref.autograd_grads(p, cfg, x, y, h0=h0)
+    assert abs(float(loss) - float(loss_a)) < 1e-10
+    for k in g:
+        torch.testing.assert_close(g[k], g_a[k], atol=1e-10, rtol=1e-8)
+    logits, caches = cpu_ref.forward(p, cfg, x, h0=h0, keep_cache=True)
+    for l in range(layers):
+        torch.testing.assert_close(out[l], caches[l]["out"][:, -1])
+    # the trainer: step 2 starts from step 1's final state; reset_state goes back to zeros
+    ct = CpuTrainer(cfg.replace(lr=0.0), params={k: v.float() for k, v in p.items()})
+    b1, b2 = ds.next(), ds.next()
+    ct.forward_backward(*b1)
+    s1 = [h.clone() for h in ct._state]
+    ct.forward_backward(*b2)
+    pf = {k: v.float() for k, v in p.items()}
+    ref_loss, _ = cpu_ref.manual_backward(pf, cfg, torch.from_numpy(b2[0]), torch.from_numpy(b2[1]), h0=s1)
+    assert abs(ct.loss() - float(ref_loss)) < 1e-5
+    ct.reset_state()
+    ct.forward_backward(*b2)
+    ref0, _ = cpu_ref.manual_backward(pf, cfg, torch.from_numpy(b2[0]), torch.from_numpy(b2[1]))
+    assert abs(ct.loss() - float(ref0)) < 1e-5

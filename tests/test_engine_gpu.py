@@ -204,3 +204,38 @@ def test_watchdog_detects_stalled_step():
     assert "not done after" in bad.t.watchdog_message()
     with pytest.raises(RuntimeError, match="watchdog"):
         bad.step(x, y)
+
+
+@pytest.mark.parametrize("sched", ["persistent", "perstep", "overlap"])
+@pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 128, 64)])
+def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
+    """Truncated BPTT (cfg.carry_hidden): the step graph copies HS[T] -> HS[0] of every h copy
+    (fp32, bf16, transposed, fragment-tiled), so step k+1 starts from step k's final state; the
+    grads match manual BPTT with that h0 (fp64), and reset_state() returns to zeros."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    env, overlap, *_ = SCHEDULES[sched]
+    monkeypatch.setenv("GK_PERSIST", env)
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, time_chunks=2, seed=8,
+                    overlap=overlap, carry_hidden=True)
+    params = init_params(cfg)
+    ds = NameStream(B, cfg.seq, seed=6)
+    tr = HipTrainer(cfg, params=params)
+    p64 = {k: v.double() for k, v in params.items()}
+    state = None
+    for it in range(3):
+        x, y = ds.next()
+        tr.forward_backward(x, y)   # no optimiser step: the weights stay those of the oracle
+        g = tr.grad_dict()
+        out = []
+        ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y),
+                                                  h0=state, state_out=out)
+        state = out
+        assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss), it
+        for k in ref_g:
+            e = rel(g[k], ref_g[k])
+            assert e < 0.05, f"step {it} {k}: rel err {e:.4f} ({tr.t.plan()})"
+    tr.reset_state()
+    x, y = ds.next()
+    tr.forward_backward(x, y)
+    ref_loss, _ = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
