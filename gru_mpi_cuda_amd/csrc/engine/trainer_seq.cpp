@@ -15,13 +15,21 @@ namespace gk {
 
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
-  // split-K into slab_w_ / rs_w_, then reduce straight into the gradient segment(s)
-  int sp = splits_;
-  while (sp > 1 && (K % sp || (K / sp) % 128)) sp >>= 1;
+  // split K only as deep as it takes to give the chip ~256 workgroups: every extra split costs a
+  // full M x N fp32 slab written and read again (8 slabs of dW_hh at H=1024 = 100 MB).  With no
+  // split the GEMM writes the gradient (and the bias row sums) directly.
+  const int tiles = std::max(1, (M / 128) * (N / 128));
+  int sp = 1;
+  while (sp * 2 <= splits_ && tiles * sp < 256 && K % (sp * 2) == 0 && (K / (sp * 2)) % 128 == 0) sp *= 2;
   GemmArgs w;
   w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb;
-  w.C = slab_w_; w.ldc = N; w.rowsumA = rowsum_dst ? rs_w_ : nullptr;
   w.M = M; w.N = N; w.K = K; w.splits = sp;
+  if (sp == 1 && gemm_lds_ok(w)) {
+    w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
+    gemm_nt(w, s);
+    return;
+  }
+  w.C = slab_w_; w.ldc = N; w.rowsumA = rowsum_dst ? rs_w_ : nullptr;
   gemm_nt(w, s);
   SlabJobs j;
   j.add(slab_w_, sp, (long)M * N, dst);

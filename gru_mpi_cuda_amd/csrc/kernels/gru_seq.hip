@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   // VGPRs, or -- for the variants with fused weight gradients, whose accumulators take the
   // register file -- lane-linear in LDS (each lane re-reads only its own 16-B slots: conflict-free,
   // and program order suffices, no barrier)
-  constexpr bool kBwLds = NTW > 0;
+  constexpr bool kBwLds = NTW > 0 || NTP > 0;
   __shared__ __attribute__((aligned(16))) bf16x8 bwL[kBwLds ? NKW3 : 1][kBwLds ? 512 : 1];
   bf16x8 bw[kBwLds ? 1 : NKW3];
 #pragma unroll
@@ -587,7 +587,7 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
 #define BWD_VARIANTS(X)               \
   X(256, 3, 2, 2) X(256, 3, 2, 0) X(256, 3, 0, 0) \
   X(512, 6, 4, 2) X(512, 6, 4, 0) X(512, 6, 0, 0) \
-  X(1024, 12, 0, 0)
+  X(1024, 12, 0, 2) X(1024, 12, 0, 0)
 
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
   if (Bp % 32) return false;

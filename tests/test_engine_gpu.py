@@ -34,7 +34,8 @@ SCHEDULES = {
 @pytest.mark.parametrize("sched", sorted(SCHEDULES))
 @pytest.mark.parametrize("layers,H,E,chunks,B", [(1, 128, 128, 2, 64), (2, 128, 128, 4, 96), (1, 128, 128, 1, 40),
                                                  (1, 512, 512, 2, 64), (2, 256, 128, 2, 64), (1, 256, 256, 4, 256),
-                                                 (1, 512, 512, 4, 256), (2, 256, 256, 2, 512)])
+                                                 (1, 512, 512, 4, 256), (2, 256, 256, 2, 512),
+                                                 (2, 1024, 1024, 2, 128)])
 def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
     """Row blocks (Bp/32) a multiple of 8 take the L2-local hand-off where the placement allows
     (gru_seq.hip row_block_local); persistent_sc1 forces the write-through protocol."""
