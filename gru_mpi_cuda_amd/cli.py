@@ -109,8 +109,22 @@ def cmd_train(args) -> int:
             loss = tr.loss()                # synchronises
             r = timer.rate()
             tok_s = r["steps_per_s"] * cfg.batch * cfg.seq
+            rec = dict(step=it + 1, loss=loss, tokens_per_s=tok_s, world=ctx.world,
+                       ms_per_step=1e3 / r["steps_per_s"] if r["steps_per_s"] else None)
+            if ctx.device.type == "cuda":
+                free, total = torch.cuda.mem_get_info(ctx.device)
+                rec["hbm_used_gb"] = (total - free) / 2 ** 30
+                if hasattr(tr, "t"):
+                    rec["workspace_mb"] = tr.t.workspace_bytes() / 2 ** 20
+                if hasattr(tr, "comm_stats"):
+                    cs = tr.comm_stats()
+                    rec.update(cs)
+                    if cs and rec["ms_per_step"]:
+                        # upper bound of the step share the collectives take if none of it overlaps
+                        rec["allreduce_step_fraction_max"] = cs["allreduce_ms_standalone"] / rec["ms_per_step"]
+                timer.rate()                # the probe above is not training time
             log(f"step {it + 1} loss {loss:.4f} {tok_s / 1e6:.2f} M char-tokens/s")
-            mw.write(step=it + 1, loss=loss, tokens_per_s=tok_s, world=ctx.world)
+            mw.write(**rec)
         if args.ckpt and args.save_every and (it + 1) % args.save_every == 0:
             save_checkpoint(tr, args.ckpt, args.fmt)
     if args.ckpt:

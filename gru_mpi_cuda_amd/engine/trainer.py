@@ -122,6 +122,26 @@ class HipTrainer:
         """Zero the carried hidden state (truncated BPTT, ``cfg.carry_hidden``)."""
         self.t.reset_hidden(self._stream())
 
+    def comm_stats(self) -> Dict[str, float]:
+        """Gradient-collective observability: bytes all-reduced per step inside the
+        step graph, and the time of the same collectives run on their own (a probe: it re-reduces
+        the gradient buffer after the step, whose Adam update has already consumed it)."""
+        if self.comm is None:
+            return {}
+        log = self.t.allreduce_log() or [(a, b - a) for a, b in self.buckets]
+        nbytes = 4 * sum(n for _, n in log)
+        s = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        base = self.grads.data_ptr()
+        for off, n in log:
+            if off >= 0:
+                self.comm.allreduce_avg_f32(base + 4 * off, n, s.cuda_stream)
+        e1.record(s)
+        e1.synchronize()
+        return {"allreduce_mb_per_step": nbytes / 2 ** 20, "allreduce_collectives": len(log),
+                "allreduce_ms_standalone": e0.elapsed_time(e1)}
+
     def state_dict(self) -> Dict[str, torch.Tensor]:
         torch.cuda.synchronize(self.dev)
         return {k: v.cpu() for k, v in from_flat(self.cfg, self.params).items()}
