@@ -89,7 +89,7 @@ def cmd_train(args) -> int:
     from .parallel import dist as gdist
     from .parallel.rccl import make_comm
     from .engine.trainer import make_trainer
-    from .utils.data import NameStream
+    from .utils.data import make_stream
     from .utils.metrics import MetricsWriter, StepTimer, log
     ctx = gdist.init(use_gpu=torch.cuda.is_available() and not args.cpu, verbose=True)
     cfg = _cfg_from(args)
@@ -98,8 +98,8 @@ def cmd_train(args) -> int:
     start = load_checkpoint(tr, args.resume) if args.resume else 0
     if hasattr(tr, "t"):
         log(f"plan: {tr.t.plan()}, workspace {tr.t.workspace_bytes() / 2**20:.1f} MiB")
-    data = NameStream(cfg.batch // ctx.world, cfg.seq, cfg.sos, cfg.eos, seed=cfg.seed * 1000 + ctx.rank + start,
-                      max_len=cfg.max_len)
+    data = make_stream(cfg.batch // ctx.world, cfg.seq, cfg.sos, cfg.eos, seed=cfg.seed * 1000 + ctx.rank + start,
+                       max_len=cfg.max_len, path=args.data)
     mw = MetricsWriter(args.metrics)
     timer = StepTimer()
     for it in range(start, start + args.steps):
@@ -194,6 +194,8 @@ def main(argv=None) -> int:
     t.add_argument("--resume", default=None)
     t.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
     t.add_argument("--cpu", action="store_true", help="force the CPU reference path")
+    t.add_argument("--data", default=None,
+                   help="names file, one per line (default: synthetic names); read by the native loader")
     _add_model_args(t)
     g = sub.add_parser("generate", help="namegen_initialize / namegen / namegen_finalize")
     g.add_argument("--ckpt", required=True)

@@ -9,6 +9,7 @@
 #include "engine/trainer.h"
 #include "engine/generator.h"
 #include "comm/rccl_comm.h"
+#include "data/name_loader.h"
 
 namespace py = pybind11;
 using namespace gk;
@@ -27,6 +28,29 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "gru_mpi_cuda_amd native engine (HIP/CDNA4 kernels, hipGraph executor, RCCL comm)";
 
   m.def("set_rank", [](int r) { global_rank() = r; });
+
+  py::class_<NameLoader>(m, "NameLoader")
+      .def(py::init([](py::dict d) {
+        LoaderCfg c;
+        c.B = get<int>(d, "B", 256); c.T = get<int>(d, "T", 32);
+        c.sos = get<int>(d, "sos", 0); c.eos = get<int>(d, "eos", 0); c.max_len = get<int>(d, "max_len", 10);
+        c.seed = get<uint64_t>(d, "seed", 0); c.prefetch = get<int>(d, "prefetch", 4);
+        c.path = get<std::string>(d, "path", "");
+        return new NameLoader(c);
+      }))
+      .def("next", [](NameLoader& L, int B, int T) {
+        py::array_t<int32_t> x({B, T}), y({B, T});
+        int32_t* px = x.mutable_data();
+        int32_t* py_ = y.mutable_data();
+        {
+          py::gil_scoped_release nogil;   // the producer thread may still be filling the batch
+          L.next(px, py_);
+        }
+        return py::make_tuple(x, y);
+      })
+      .def("batches", &NameLoader::batches)
+      .def("epoch", &NameLoader::epoch)
+      .def("names_in_file", &NameLoader::names_in_file);
   m.def("device_info", []() {
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
