@@ -34,6 +34,7 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
+  if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);   // 0 auto, 1 reg, 2 LDS
 }
 
 Generator::~Generator() {
@@ -80,7 +81,7 @@ void Generator::record_steps(int n, hipStream_t s) {
       if (l == 0) { a.P = Ptab_; a.ids = ids_; }
       else { a.x_bf = hb_[2 * (l - 1) + nxt]; a.Wih = Wih_[l]; a.bih = P("bias_ih_l" + k); a.Kin = H; }
       a.h_f = hf_[2 * l + nxt]; a.h_bf = hb_[2 * l + nxt];
-      a.Bp = Bp; a.H = H;
+      a.Bp = Bp; a.H = H; a.algo = step_algo_;
       gru_fwd_step(a, s);
     }
     FcSampleArgs f;

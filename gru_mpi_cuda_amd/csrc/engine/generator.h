@@ -50,6 +50,7 @@ class Generator {
   std::vector<u16*> hb_;
   std::vector<u16*> Whh_, Wih_;
   u16 *Emb_, *Wfc_, *WfcF_;
+  int step_algo_ = 0;
   float *Ptab_, *rf_;
   int *ids_, *alive_;
   unsigned char* out_;

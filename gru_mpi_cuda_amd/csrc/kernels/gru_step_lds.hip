@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a)
   }
 }
 
-bool gru_step_lds_ok(int H, int Bp) { return H >= 1024 && H % 64 == 0 && Bp % 128 == 0; }
+bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);

@@ -71,7 +71,8 @@ def _gates_ref(gi, gh, hp):
 
 # algo 1 = register-direct 32x16 tile, 2 = LDS-staged 128-row big tile (gru_step_lds.hip)
 @pytest.mark.parametrize("mode", ["table", "gi", "fused"])
-@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (512, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2)])
+@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (512, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2),
+                                      (512, 256, 2), (256, 128, 2)])
 def test_fwd_step(ext, mode, H, Bp, algo):
     V, Kin = 256, 256   # fused mode, algo 2: input phase of 4 k-tiles ahead of the recurrent phase
     hp = rnd(Bp, H, scale=0.5, seed=1).clamp(-1, 1)
@@ -119,7 +120,7 @@ def test_fwd_step(ext, mode, H, Bp, algo):
 
 
 @pytest.mark.parametrize("first", [False, True])
-@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2)])
+@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2), (512, 128, 2)])
 def test_bwd_step(ext, first, H, Bp, algo):
     T = 4
     t = 1
