@@ -34,7 +34,13 @@ def main(root: str) -> None:
             mfma_util_pct=100.0 * mf / (1024 * gui / 8) if gui else None,
             mfma_bf16_gflop=c.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512 / 1e9,
             lds_conflict_pct=100.0 * bc / lds if lds else None,
-            fetch_MB=c.get("FETCH_SIZE", 0.0) / 1024, write_MB=c.get("WRITE_SIZE", 0.0) / 1024,
+            # FETCH_SIZE / WRITE_SIZE expressions of `rocprofv3 --list-avail` (bytes)
+            fetch_MB=(c.get("TCC_BUBBLE_sum", 0.0) * 128
+                      + (c.get("TCC_EA0_RDREQ_sum", 0.0) - c.get("TCC_BUBBLE_sum", 0.0)
+                         - c.get("TCC_EA0_RDREQ_32B_sum", 0.0)) * 64
+                      + c.get("TCC_EA0_RDREQ_32B_sum", 0.0) * 32) / 2 ** 20,
+            write_MB=((c.get("TCC_EA0_WRREQ_sum", 0.0) - c.get("TCC_EA0_WRREQ_64B_sum", 0.0)) * 32
+                      + c.get("TCC_EA0_WRREQ_64B_sum", 0.0) * 64) / 2 ** 20,
             cu_busy_cycles=busy)))
     rows.sort(reverse=True)
     print(f"{'kernel':60s} {'MFMA%':>7s} {'bf16GF':>9s} {'LDSconf%':>9s} {'fetchMB':>9s} {'writeMB':>9s}")

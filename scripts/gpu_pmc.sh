@@ -6,8 +6,11 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 tag=$1; shift
 out=gpurun_out/pmc_$tag; mkdir -p $out
 groups=("SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16"
-        "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES")
-# (derived FETCH_SIZE / WRITE_SIZE need many replay passes and exceeded 300 s on the bench)
+        "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES"
+        "TCC_BUBBLE_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"
+        "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum")
+# HBM bytes from the raw TCC counters (the derived FETCH_SIZE / WRITE_SIZE expressions of
+# `rocprofv3 --list-avail`, evaluated in analyze_pmc.py: one group fits the 4-TCC-counter limit)
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))
