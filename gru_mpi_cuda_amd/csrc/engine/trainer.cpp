@@ -165,6 +165,11 @@ hipEvent_t Trainer::ev() {
   return events_[ev_next_++];
 }
 
+static bool env_on(const char* name, bool dflt) {
+  const char* v = std::getenv(name);
+  return v && v[0] ? v[0] != '0' : dflt;
+}
+
 void Trainer::set_carry(bool on) {
   if (on == carry_) return;
   carry_ = on;
@@ -461,11 +466,29 @@ void Trainer::record_opt(hipStream_t s) {
     }
     j.add(off_.at("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
     j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
+    // deferred slab reductions: summed inside the Adam launch where a job covers exactly the
+    // gradient segment; anything else is reduced first
+    SlabJobs rest;
+    for (int d = 0; d < deferred_.n; ++d) {
+      const SlabJob& D = deferred_.job[d];
+      bool used = false;
+      for (int k = 0; k < j.n && !used; ++k) {
+        OptCastJob& J = j.job[k];
+        const long n = J.R ? (long)J.R * J.C : (long)J.C;
+        if (!J.gsl && D.dst == grads_ + J.off && D.n == n && !D.bf && !D.bfT) {
+          J.gsl = D.src; J.nsl = D.splits; used = true;
+        }
+      }
+      if (!used) rest.job[rest.n++] = D;
+    }
+    if (rest.n) reduce_slabs_multi(rest, s);
     adam_cast_multi(a, j, s);
   } else {
+    if (deferred_.n) reduce_slabs_multi(deferred_, s);
     adam_step(a, s);
     refresh_weights(s);
   }
+  deferred_.n = 0;
   HIP_LAUNCH_CHECK();
 }
 
@@ -586,11 +609,16 @@ void Trainer::step(hipStream_t s) {
         // backward; joined before the optimiser (the embedding-side tail runs after the join)
         record_fb_seq(s0_, /*dp=*/true);
       } else {
+        deferred_.n = 0;
+        defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
         if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+        defer_slabs_ = false;
         record_allreduce(s0_);
       }
       record_opt(s0_);
     } catch (...) {
+      defer_slabs_ = false;
+      deferred_.n = 0;
       hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow
       (void)hipStreamEndCapture(s0_, &broken);
       if (broken) (void)hipGraphDestroy(broken);

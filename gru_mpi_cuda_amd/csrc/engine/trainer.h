@@ -60,6 +60,12 @@ class Trainer {
 
  private:
   void record_fb(hipStream_t s0);
+  // Slab reductions whose only consumer is the optimiser (single GPU, no clipping, one-graph step):
+  // handed to the fused Adam/cast launch, which sums the partials itself (one launch and one pass
+  // over the gradients fewer).  slab_job() routes a job to `j` or, when deferring, to deferred_.
+  bool defer_slabs_ = false;
+  SlabJobs deferred_;
+  void slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst);
   void record_carry(hipStream_t s);     // HS[T] -> HS[0] of every layer and copy (carry_ only)
   bool carry_ = false;
   void record_opt(hipStream_t s0);

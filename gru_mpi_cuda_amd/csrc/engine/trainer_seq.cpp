@@ -37,6 +37,18 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
   reduce_slabs_multi(j, s);
 }
 
+void Trainer::slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst) {
+  // deep split-K slabs (the dW_fc GEMM's 32) stay with the reduce kernel: summed inside the Adam
+  // launch they serialise 32 loads per element on its few tile blocks
+  static const int max_splits = [] {
+    const char* e = std::getenv("GK_DEFER_MAX_SPLITS");
+    return e ? std::atoi(e) : 8;
+  }();
+  SlabJobs& t = (defer_slabs_ && splits <= max_splits) ? deferred_ : j;
+  if (t.n >= 24) throw std::runtime_error("slab job list full");
+  t.add(src, splits, n, dst);
+}
+
 void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
   const int H3 = 3 * H, nrb = B / 32;
@@ -144,19 +156,20 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (dp && q.bwd) ar_flush(s, false);
     // weight gradients not accumulated inside the sequence kernel
     SlabJobs j;
-    if (q.fuse_w) j.add(q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
-    if (q.bwd) j.add(q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
+    if (q.fuse_w) slab_job(j, q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
+    if (q.bwd) slab_job(j, q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
     // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail -- or, when the
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
       if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
       else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     }
-    if (l == 0 && q.bwd) j.add(q.dbih_part, nrb, H3, G("bias_ih_l0"));
+    if (l == 0 && q.bwd) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
     // all-reduced with it), else with layer 0's reduce
     if (dp ? l == L - 1 : l == 0)
-      for (int k2 = 0; k2 < tail.n; ++k2) j.job[j.n++] = tail.job[k2];
+      for (int k2 = 0; k2 < tail.n; ++k2)
+        slab_job(j, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
     if (l == 0) {   // + the loss partials and the optimiser step counter
       j.add(loss_part_, (int)(tok / 32), 1, loss_);
       j.bump = step_;
@@ -252,8 +265,8 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
     gemm_nt(e, s);
   }
   SlabJobs r;
-  r.add(slab_e_, se, (long)V * E, G("embedding"));
-  reduce_slabs_multi(r, s);
+  slab_job(r, slab_e_, se, (long)V * E, G("embedding"));
+  if (r.n) reduce_slabs_multi(r, s);
   HIP_LAUNCH_CHECK();
 }
 

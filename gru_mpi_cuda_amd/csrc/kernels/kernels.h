@@ -233,7 +233,11 @@ void cast_multi(CastJobs& j, hipStream_t s);
 // transpose.  Matrix jobs need R % 64 == 0 and C % 64 == 0; R == 0 marks a flat (bias) job of C
 // elements, C % 4 == 0.
 // dstF / dstTF (nullable): FT-layout copies of the matrix / its transpose (see ft_offset)
-struct OptCastJob { long off; int R, C; u16* dst; u16* dstT; u16* dstF = nullptr; u16* dstTF = nullptr; };
+// gsl (nullable): the job's gradient is the fixed-order sum of nsl slabs gsl[s * R*C + i] (split-K /
+// per-row-block partials), summed here instead of by a separate reduce launch; the sum is also
+// written to the gradient buffer (it stays observable).
+struct OptCastJob { long off; int R, C; u16* dst; u16* dstT; u16* dstF = nullptr; u16* dstTF = nullptr;
+                    const float* gsl = nullptr; int nsl = 0; };
 struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
   void add(long off, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
     job[n++] = OptCastJob{off, R, C, d, dT, dF, dTF}; } };

@@ -273,9 +273,18 @@ DEV AdamCoef adam_coef(const OptimArgs& a) {
   const int t = *a.step;
   return AdamCoef{a.gscale ? *a.gscale : 1.f, 1.f / (1.f - powf(a.b1, (float)t)), 1.f / (1.f - powf(a.b2, (float)t))};
 }
-DEV float4 adam4(const OptimArgs& a, const AdamCoef& k, long i /*float4 index*/) {
+// gradient float4 i (flat index) of job J: from the gradient buffer, or summed from J's slabs
+// (same order as sum_slabs4 in reduce_multi) and written back to the gradient buffer
+DEV float4 job_grad4(const OptimArgs& a, const OptCastJob& J, long i) {
+  if (!J.gsl) return reinterpret_cast<const float4*>(a.g)[i];
+  const long n = J.R ? (long)J.R * J.C : (long)J.C;
+  const float4 g = sum_slabs4(J.gsl, n, J.nsl, (size_t)(i * 4 - J.off));
+  reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
+  return g;
+}
+DEV float4 adam4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, long i /*float4 index*/) {
   float4 p = reinterpret_cast<float4*>(a.p)[i];
-  const float4 g4 = reinterpret_cast<const float4*>(a.g)[i];
+  const float4 g4 = job_grad4(a, J, i);
   float pv[4] = {p.x, p.y, p.z, p.w};
   const float gv[4] = {g4.x * k.sc, g4.y * k.sc, g4.z * k.sc, g4.w * k.sc};
   if (a.sgd) {
@@ -303,13 +312,14 @@ DEV float4 adam4(const OptimArgs& a, const AdamCoef& k, long i /*float4 index*/)
 
 // adam4 on 4 float4s at element offsets off + q*stride (q = 0..3): every load issued before any
 // update, so one memory round trip instead of four
-DEV void adam4x4(const OptimArgs& a, const AdamCoef& k, long off, long stride, float4 (&out)[4]) {
+DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, long off, long stride,
+                 float4 (&out)[4]) {
   float4 p[4], g[4], m[4], v[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const long i = (off + q * stride) >> 2;
     p[q] = reinterpret_cast<const float4*>(a.p)[i];
-    g[q] = reinterpret_cast<const float4*>(a.g)[i];
+    g[q] = job_grad4(a, J, i);
     if (!a.sgd) { m[q] = reinterpret_cast<const float4*>(a.m)[i]; v[q] = reinterpret_cast<const float4*>(a.v)[i]; }
   }
 #pragma unroll
@@ -350,14 +360,14 @@ __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs
   const AdamCoef co = adam_coef(a);
   if (J.R == 0) {   // flat job: 1024 elements per block
     const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
-    if ((long)t * 1024 + threadIdx.x * 4 < J.C) adam4(a, co, i4);
+    if ((long)t * 1024 + threadIdx.x * 4 < J.C) adam4(a, J, co, i4);
     return;
   }
   const int tiles_c = J.C / 64;
   const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   float4 upd[4];
-  adam4x4(a, co, J.off + (long)(r0 + ty) * J.C + c0 + 4 * tx, 16L * J.C, upd);
+  adam4x4(a, J, co, J.off + (long)(r0 + ty) * J.C + c0 + 4 * tx, 16L * J.C, upd);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = r0 + ty + 16 * q, c = c0 + 4 * tx;

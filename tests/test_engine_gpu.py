@@ -240,3 +240,24 @@ def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
     tr.forward_backward(x, y)
     ref_loss, _ = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
     assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
+
+
+@pytest.mark.parametrize("layers,H,B,opt", [(1, 512, 256, "adam"), (2, 256, 64, "adam"), (1, 256, 64, "sgd")])
+def test_one_graph_step_equals_phased_step(layers, H, B, opt):
+    """The one-graph step hands optimiser-only slab reductions (dW_hh / bias / dW_fc / dEmb
+    partials) to the fused Adam launch; the phased path (forward_backward, then optimizer_step)
+    reduces them first.  Same partials, same summation order: bitwise-equal weights and grads."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=12, optimizer=opt)
+    params = init_params(cfg)
+    ds = NameStream(B, cfg.seq, seed=2)
+    batches = [ds.next() for _ in range(3)]
+    a = HipTrainer(cfg, params=params)
+    b = HipTrainer(cfg, params=params)
+    for x, y in batches:
+        a.step(x, y)
+        b.forward_backward(x, y)
+        b.optimizer_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.grads, b.grads)
+    assert torch.equal(a.params, b.params)
