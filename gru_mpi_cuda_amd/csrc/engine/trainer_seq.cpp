@@ -19,8 +19,13 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
   // full M x N fp32 slab written and read again (8 slabs of dW_hh at H=1024 = 100 MB).  With no
   // split the GEMM writes the gradient (and the bias row sums) directly.
   const int tiles = std::max(1, (M / 128) * (N / 128));
+  auto can_split = [&](int s2) { return s2 <= splits_ && K % s2 == 0 && (K / s2) % 128 == 0; };
   int sp = 1;
-  while (sp * 2 <= splits_ && tiles * sp < 256 && K % (sp * 2) == 0 && (K / (sp * 2)) % 128 == 0) sp *= 2;
+  while (can_split(sp * 2) && tiles * sp < 256) sp *= 2;
+  // a ragged last round of workgroups (two resident per CU: 512 slots) idles part of the chip for a
+  // whole K-slice; one more split evens it out (H = 2048: 768 tiles -> 1536 = 3 full rounds)
+  const int slots = 512, wg = tiles * sp;
+  if (wg > slots && wg % slots && (double)wg / slots / ((wg + slots - 1) / slots) < 0.85 && can_split(sp * 2)) sp *= 2;
   GemmArgs w;
   w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb;
   w.M = M; w.N = N; w.K = K; w.splits = sp;

@@ -34,7 +34,10 @@ DEV float sum8f(const bf16x8& v) {
   return s;
 }
 
-template <bool BIAS, bool ROWSUM>
+// OH: one-hot A (dP = onehot(ids)^T · B, the embedding-table gradient): A[m][k] = (ids[k] == m) is
+// synthesised into the same swizzled LDS image the LDS-DMA would have written, from char ids
+// prefetched one k-tile ahead -- no A operand in memory at all.
+template <bool BIAS, bool ROWSUM, bool OH = false>
 DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u16 (&lds)[2][2][128 * 64]) {
   const int tn = id % ntn, tm = (id / ntn) % ntm, sp = id / (ntn * ntm);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -51,10 +54,41 @@ DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u1
   for (int q = 0; q < 4; ++q) {
     const int r = (4 * w + q) * 8 + srow;
     const int c = sslot ^ ((r >> 1) & 7);
-    srcA[q] = a.A + (size_t)(row0 + r) * a.lda + kbeg + c * 8;
+    srcA[q] = OH ? nullptr : a.A + (size_t)(row0 + r) * a.lda + kbeg + c * 8;
     srcB[q] = a.B + (size_t)(col0 + r) * a.ldb + kbeg + c * 8;
   }
+  // one-hot: row r = (4w+q)*8 + srow keeps logical chunk c = sslot ^ (4(q&1) + (srow>>1)) in this
+  // lane's slot, so a lane needs the 8 ids of two chunks per k-tile
+  int4 idn[2][2];
+  auto load_ids = [&](int kt) {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int c = sslot ^ (4 * v + (srow >> 1));
+      const int4* p = reinterpret_cast<const int4*>(a.onehot_ids + kbeg + kt * 64 + c * 8);
+      idn[v][0] = p[0];
+      idn[v][1] = p[1];
+    }
+  };
+  if constexpr (OH) load_ids(0);
   auto stage = [&](int buf, int kt) {
+    if constexpr (OH) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (4 * w + q) * 8 + srow, m = row0 + r;
+        const int4 i0 = idn[q & 1][0], i1 = idn[q & 1][1];
+        const int iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+        unsigned wv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          wv[e] = (iv[2 * e] == m ? 0x3F80u : 0u) | ((iv[2 * e + 1] == m ? 0x3F80u : 0u) << 16);
+        *reinterpret_cast<uint4*>(&lds[buf][0][r * 64 + sslot * 8]) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+      }
+      if (kt + 1 < nk) load_ids(kt + 1);   // lands by the vmcnt(0) that ends this k-tile
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void*)(&lds[buf][1][(4 * w + q) * 8 * 64]), 16, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int base = (4 * w + q) * 8 * 64;
@@ -129,10 +163,10 @@ DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u1
   }
 }
 
-template <bool BIAS, bool ROWSUM>
+template <bool BIAS, bool ROWSUM, bool OH = false>
 __global__ void __launch_bounds__(256, 2) gemm_lds_kernel(GemmArgs a, int ntn, int ntm, int kper) {
   __shared__ __attribute__((aligned(16))) u16 lds[2][2][128 * 64];
-  gemm_lds_body<BIAS, ROWSUM>(a, xcd_remap2(blockIdx.x, gridDim.x), ntn, ntm, kper, lds);
+  gemm_lds_body<BIAS, ROWSUM, OH>(a, xcd_remap2(blockIdx.x, gridDim.x), ntn, ntm, kper, lds);
 }
 
 // grouped launch: block range [start[k], start[k+1]) serves job k (after the XCD remap, so each
@@ -176,10 +210,13 @@ void gemm_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
 }
 
 bool gemm_lds_ok(const GemmArgs& a) {
-  if (a.onehot_ids) return false;
   if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;
   const int kper = a.K / a.splits;
   if (kper % 64 || kper < 128) return false;
+  if (a.onehot_ids) {   // synthesised A: 16-B aligned id chunks, no bias / row sums
+    return !a.rowsumA && !a.bias && !(a.ldb % 8) && !(reinterpret_cast<uintptr_t>(a.B) & 15) &&
+           !(reinterpret_cast<uintptr_t>(a.onehot_ids) & 15);
+  }
   // 16-B aligned rows for the LDS-DMA loads
   if ((a.lda % 8) || (a.ldb % 8)) return false;
   if ((reinterpret_cast<uintptr_t>(a.A) | reinterpret_cast<uintptr_t>(a.B)) & 15) return false;
@@ -215,6 +252,10 @@ void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s) {
 void gemm_lds(const GemmArgs& a, hipStream_t s) {
   const int ntn = a.N / 128, ntm = a.M / 128, kper = a.K / a.splits;
   dim3 grid(ntn * ntm * a.splits), block(256);
+  if (a.onehot_ids) {
+    hipLaunchKernelGGL((gemm_lds_kernel<false, false, true>), grid, block, 0, s, a, ntn, ntm, kper);
+    return;
+  }
   const bool bias = a.bias && a.splits == 1;
   if (a.rowsumA) {
     if (bias) hipLaunchKernelGGL((gemm_lds_kernel<true, true>), grid, block, 0, s, a, ntn, ntm, kper);

@@ -49,16 +49,20 @@ def test_gemm_nt(ext, algo, M, N, K, splits):
     torch.testing.assert_close(rs.sum(0), A.float().sum(1), atol=1e-2, rtol=1e-3)
 
 
-def test_gemm_onehot(ext):
-    V, N, K = 256, 192, 512
+@pytest.mark.parametrize("N,K,splits,algo", [(192, 512, 1, 1), (384, 1024, 1, 2), (256, 2048, 4, 2)])
+def test_gemm_onehot(ext, N, K, splits, algo):
+    """algo 2: the one-hot A tile is synthesised into the swizzled LDS image of the LDS GEMM."""
+    V = 256
     ids = torch.randint(0, V, (K,), device=DEV, dtype=torch.int32)
+    ids[:64] = 7                                                   # a heavy bucket
     B = bf(rnd(N, K, seed=5))
-    C = torch.zeros(V, N, device=DEV)
-    ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=V, N=N, K=K), S())
+    C = torch.zeros(splits, V, N, device=DEV)
+    ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=V, N=N, K=K,
+                     splits=splits, algo=algo), S())
     torch.cuda.synchronize()
     oh = torch.nn.functional.one_hot(ids.long(), V).float()      # [K][V]
     ref = oh.T @ B.float().T
-    torch.testing.assert_close(C, ref, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(C.sum(0), ref, atol=1e-3, rtol=1e-3)
 
 
 def _gates_ref(gi, gh, hp):
