@@ -31,6 +31,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
   size_t o_WfcF = R((size_t)V * H * 2), o_WfcTF = R((size_t)V * H * 2);
   size_t o_dl = R(tok * V * 2), o_dlT = R(tok * V * 2), o_dPb = R((size_t)V * 3 * H * 2), o_dPTb = R((size_t)V * 3 * H * 2);
+  // fp32 logits of the GEMM + row-softmax FC path (shapes the fused 8-wave kernel does not cover)
+  fc_split_ = !fc_xent_fused_ok(V, H, (int)tok) && tok % 128 == 0 && V % 128 == 0 && V <= 512 && H % 64 == 0 &&
+              H >= 128;
+  size_t o_lg = fc_split_ ? R(tok * V * 4) : 0;
   struct LO { size_t HSf, sr, sz, sn, sghn, dy, Gi, c0, c1, HSb, HT, g0, g1, dghT, dgiT, dgi, Whh, WhhT, Wih, WihT, shh, rhh, sih, rih; };
   std::vector<LO> los(L);
   for (int l = 0; l < L; ++l) {
@@ -103,6 +107,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   step_ = arena_.get<int>(o_step);
   Emb = arena_.get<u16>(o_Emb); EmbT = arena_.get<u16>(o_EmbT); Wfc = arena_.get<u16>(o_Wfc); WfcT = arena_.get<u16>(o_WfcT);
   WfcF = arena_.get<u16>(o_WfcF); WfcTF = arena_.get<u16>(o_WfcTF);
+  logits_ = fc_split_ ? arena_.get<float>(o_lg) : nullptr;
   dl_ = arena_.get<u16>(o_dl); dlT_ = arena_.get<u16>(o_dlT); dP_bf_ = arena_.get<u16>(o_dPb); dPT_bf_ = arena_.get<u16>(o_dPTb);
   Ls_.resize(L);
   for (int l = 0; l < L; ++l) {

@@ -176,6 +176,8 @@ class Trainer {
   float *norm_parts_, *gscale_;
   int* step_;
   u16 *Emb, *EmbT, *Wfc, *WfcT, *dl_, *dlT_, *dP_bf_, *dPT_bf_;
+  bool fc_split_ = false;        // FC as LDS GEMM (logits) + softmax_xent + LDS GEMM (dH)
+  float* logits_ = nullptr;
   u16 *WfcF, *WfcTF;   // fragment-tiled (kernels.h ft_offset) copies of W_fc and W_fc^T for fc_xent
 };
 

@@ -109,7 +109,19 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     f.labels = labels_; f.inv_count = inv_count_;
     f.dl = dl_; f.dlT = dlT_; f.ldT = (int)tok; f.colT = 0;
     f.loss_part = loss_part_; f.M = (int)tok; f.H = H; f.V = V;
-    if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
+    if (fc_split_) {
+      // large H: logits and dH as LDS GEMMs around a row-wise softmax-xent (the fused FC kernel
+      // stages a 32 x H tile of X per workgroup; at H = 2048 that leaves it at ~0.2 PF)
+      GemmArgs lg;   // logits = X · W_fc^T + b_fc
+      lg.A = f.X; lg.lda = H; lg.B = Wfc; lg.ldb = H; lg.C = logits_; lg.ldc = V; lg.bias = f.b;
+      lg.M = (int)tok; lg.N = V; lg.K = H;
+      gemm_nt(lg, s);
+      softmax_xent(logits_, f, s);
+      GemmArgs g;   // dy_top = dlogits · W_fc
+      g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
+      g.M = (int)tok; g.N = H; g.K = V;
+      gemm_nt(g, s);
+    } else if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
       f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
       fc_xent(f, s);

@@ -589,6 +589,67 @@ __global__ void __launch_bounds__(512, 1) fc_sample_v256_kernel(FcSampleArgs a) 
   }
 }
 
+// Row-wise softmax cross-entropy on precomputed logits: one 256-thread block per 32 rows, one wave
+// per row at a time (V/64 consecutive logits per lane), fp32 statistics, deterministic loss
+// partial (fixed-order sum of the block's rows).
+__global__ void __launch_bounds__(256) softmax_xent_kernel(const float* __restrict__ logits, FcXentArgs a) {
+  __shared__ u16 st[512][34];        // dl^T staging [V][32 rows] (+2 pad)
+  __shared__ float nll[32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, V = a.V, per = V / 64;
+  const int m0 = blockIdx.x * 32;
+  const float inv = a.inv_count[0];
+  for (int rr = w; rr < 32; rr += 4) {
+    const int row = m0 + rr, y = a.labels[row];
+    const float* L = logits + (size_t)row * V + lane * per;
+    float x[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < per) { x[e] = L[e]; mx = fmaxf(mx, x[e]); }
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < per) se += __expf(x[e] - mx);
+    se = wave_sum(se);
+    const float rs = 1.f / se, scale = (y >= 0) ? inv : 0.f;
+    float ly = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < per) {
+        const int col = lane * per + e;
+        if (col == y) ly = x[e];
+        const u16 d = f2bf((__expf(x[e] - mx) * rs - (col == y ? 1.f : 0.f)) * scale);
+        if (a.dl) a.dl[(size_t)row * V + col] = d;
+        st[col][rr] = d;
+      }
+    ly = wave_sum(ly);   // only the label's lane contributes
+    if (lane == 0) nll[rr] = (y >= 0) ? (logf(se) + mx - ly) * inv : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float acc = 0.f;
+    for (int r = 0; r < 32; ++r) acc += nll[r];
+    a.loss_part[blockIdx.x] = acc;
+  }
+  // dl^T: each vocab column's 32 rows are 64 contiguous bytes -> four 16-B stores
+  for (int q = threadIdx.x; q < V * 4; q += 256) {
+    const int col = q >> 2, seg = q & 3;
+    u16 v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = st[col][seg * 8 + e];
+    *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+  }
+}
+
+void softmax_xent(const float* logits, const FcXentArgs& a, hipStream_t s) {
+  if (a.V % 64 || a.V > 512 || a.M % 32 || (a.ldT % 8) || (a.colT % 8))
+    throw std::runtime_error("softmax_xent: needs V % 64 == 0, V <= 512, M % 32 == 0, 16-B aligned dl^T columns");
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3(a.M / 32), dim3(256), 0, s, logits, a);
+}
+
+bool fc_xent_fused_ok(int V, int H, int M) { return V == 256 && (H == 512 || H == 1024) && M % FROWS == 0; }
+
 static bool fc_xent_v256_ok(const FcXentArgs& a) {
   return a.V == 256 && a.dy && a.Wf && a.WTf && !a.dl && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
          !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');

@@ -142,6 +142,12 @@ struct FcXentArgs {
   unsigned long long* dbg = nullptr;   // diagnostic phase stamps of workgroup 0 (nullable)
 };
 void fc_xent(const FcXentArgs& a, hipStream_t s);
+// Softmax-xent over precomputed fp32 logits [M][V] (V % 64 == 0, V <= 512, M % 32 == 0): the large-H
+// path, where the logits and dH are LDS GEMMs and only this row-wise part stays fused.  Writes dl
+// (row-major, nullable), dlT (transposed) and the per-32-row loss partials like fc_xent.
+void softmax_xent(const float* logits, const FcXentArgs& a, hipStream_t s);
+// the 8-wave fused kernel covers this shape (else the trainer takes the GEMM + softmax_xent path)
+bool fc_xent_fused_ok(int V, int H, int M);
 
 struct FcSampleArgs {              // generation: logits -> softmax -> inverse-CDF sample
   const u16* X = nullptr;          // [Bp][H]
