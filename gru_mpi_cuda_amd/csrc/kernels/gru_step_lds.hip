@@ -324,6 +324,136 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a)
   }
 }
 
+// 8-wave variant: the same 64 x 64 tile, but two wave groups split every 64-deep k-tile by its two
+// 32-deep k-steps (group g does k-step g), so each wave issues half the LDS-DMA pieces and half the
+// MFMAs of the 4-wave kernel and two waves share each SIMD (one's DMA issue and LDS latency hide
+// under the other's MFMAs).  Group 1's partial dh tile is added to group 0's through LDS before the
+// epilogue.
+__global__ void __launch_bounds__(512, 1) gru_bwd_step_lds8_kernel(BwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[BNS][(64 + 64) * 64];
+  const int H = a.H, H3 = 3 * a.H;
+  const int j0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = w >> 2, wl = w & 3;
+  const int wm = wl >> 1, wn = wl & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+
+  // epilogue operands (group 0), loaded ahead of the K loop so their latency hides under it:
+  // element (i, jt, e) -> row b0 + wm*32 + i*16 + lq*4 + e, unit j0 + wn*32 + jt*16 + lr
+  float dy[2][2][4], cin[2][2][4], sr_[2][2][4], sz_[2][2][4], sn_[2][2][4], sg_[2][2][4], hpv[2][2][4];
+  if (grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const size_t o = (size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * H + j0 + wn * 32 + jt * 16 + lr;
+          dy[i][jt][e] = a.dy[o];
+          cin[i][jt][e] = a.carry_in ? a.carry_in[o] : 0.f;
+          sr_[i][jt][e] = a.r[o]; sz_[i][jt][e] = a.z[o]; sn_[i][jt][e] = a.n[o];
+          sg_[i][jt][e] = a.ghn[o]; hpv[i][jt][e] = a.hprev[o];
+        }
+  }
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.dgh_next) {
+    // 16 DMA pieces (8 rows x 128 B) per k-tile: piece p = 2w + q covers image rows 8p..8p+7,
+    // the A rows (dGh_{t+1}) for p < 8, the B rows (W_hh^T) after
+    const u16* src[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (2 * w + q) * 8 + srow, rr = r & 63;
+      const u16* base = r < 64 ? a.dgh_next + (size_t)(b0 + rr) * H3 : a.WhhT + (size_t)(j0 + rr) * H3;
+      src[q] = base + swz(rr, sslot) * 8;
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(2 * w + q) * 8 * 64]), 16, 0, 0);
+    };
+    ring_loop<BNS, 2>(H3 / 64, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 64 * 64;
+      const int c = grp * 4 + lq;   // this group's 32-deep k-step
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ra = wm * 32 + t * 16 + lr, rb = wn * 32 + t * 16 + lr;
+        af[t] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
+        bfr[t] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    });
+    // group 1 -> LDS -> group 0 (ring_loop ended with a barrier: the ring is free)
+    f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);   // [4 waves][4 tiles][64 lanes]
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) red[(wl * 4 + i * 2 + j) * 64 + lane] = acc[i][j];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] += red[(wl * 4 + i * 2 + j) * 64 + lane];
+    }
+    __syncthreads();
+  }
+
+  // ---- gate-gradient epilogue (group 0); transposed staging [4 kinds][64 units][64 rows] bf16
+  u16* st = lds[0];
+  if (grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = wm * 32 + i * 16 + lq * 4 + e, uu = wn * 32 + jt * 16 + lr;
+          const int b = b0 + rr, j = j0 + uu;
+          const size_t o = (size_t)b * H + j;
+          const float dh = dy[i][jt][e] + cin[i][jt][e] + acc[i][jt][e];
+          const float r = sr_[i][jt][e], z = sz_[i][jt][e], n = sn_[i][jt][e];
+          const float dn = dh * (1.f - z);
+          const float dz = dh * (hpv[i][jt][e] - n);
+          const float dan = dn * (1.f - n * n);
+          const float dar = dan * sg_[i][jt][e] * r * (1.f - r);
+          const float daz = dz * z * (1.f - z);
+          a.carry_out[o] = z * dh;
+          const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
+          const size_t og = (size_t)b * H3 + j;
+          a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
+          if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
+          st[(0 * 64 + uu) * 64 + rr] = br;
+          st[(1 * 64 + uu) * 64 + rr] = bz;
+          st[(2 * 64 + uu) * 64 + rr] = bn;
+          st[(3 * 64 + uu) * 64 + rr] = bi;
+        }
+  }
+  __syncthreads();
+  // 4 kinds x 64 units x 64 rows = 2048 pieces of 8 rows (16 B), 4 per thread
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int q = threadIdx.x + p * 512;
+    const int kind = q >> 9, rem = q & 511, unit = rem >> 3, seg = rem & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 64 + unit) * 64 + seg * 8]);
+    const int g = kind < 3 ? kind : 2;
+    const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + seg * 8;
+    if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
+    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+  }
+}
+
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
@@ -339,6 +469,14 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   }
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
+  static const bool eight = [] {
+    const char* e = std::getenv("GK_BWD_LDS8");
+    return !(e && e[0] == '0');
+  }();
+  if (eight) {
+    hipLaunchKernelGGL(gru_bwd_step_lds8_kernel, dim3(a.H / 64, a.Bp / 64), dim3(512), 0, s, a);
+    return;
+  }
   hipLaunchKernelGGL(gru_bwd_step_lds_kernel, dim3(a.H / 64, a.Bp / 64), dim3(256), 0, s, a);
 }
 
