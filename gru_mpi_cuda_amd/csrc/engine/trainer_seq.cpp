@@ -143,6 +143,17 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;
     w.C = slab_fc2_; w.ldc = H; w.rowsumA = rs_fc2_;
     w.M = V; w.N = H; w.K = (int)tok; w.splits = sp;
+    // one-shot small GEMM over 512-deep K-slices when that fits the slab budget: one memory
+    // latency per workgroup and half the slabs of the 32-way 128 x 128 split
+    static const int kslice = [] {
+      const char* e = std::getenv("GK_FC_SMALL_K");
+      return e ? std::atoi(e) : 0;   // 0: 128x128 split-K (measured equal, profiles/r1_small_gemm_ab.jsonl)
+    }();
+    if (kslice > 0 && tok % kslice == 0 && tok / kslice <= kFcSplitsMax) {
+      GemmArgs ws = w;
+      ws.splits = (int)(tok / kslice); ws.algo = 3;
+      if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
+    }
     gemm_nt(w, s);
     tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
     tail.add(rs_fc2_, sp, V, G("fc.bias"));
@@ -274,6 +285,21 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
   e.A = dP_bf_; e.lda = H3; e.B = Ls_[0].WihT; e.ldb = H3; e.C = slab_e_; e.ldc = E;
   e.M = V; e.N = E; e.K = H3; e.splits = se;
+  // one-shot small GEMMs when dEmb's K-slice can match dW_ih0's (K = V): one grouped launch
+  if (H3 % V == 0 && H3 / V <= splits_) {
+    GemmArgs es = e;
+    es.splits = H3 / V;
+    const int nkb = gemm_small_kblocks(g);
+    if (nkb && nkb == gemm_small_kblocks(es)) {
+      const GemmArgs pair[2] = {g, es};
+      gemm_small_group(pair, 2, s);
+      SlabJobs r;
+      slab_job(r, slab_e_, es.splits, (long)V * E, G("embedding"));
+      if (r.n) reduce_slabs_multi(r, s);
+      HIP_LAUNCH_CHECK();
+      return;
+    }
+  }
   const GemmArgs both[2] = {g, e};
   if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
     gemm_lds_group(both, 2, s);   // one launch for both small products

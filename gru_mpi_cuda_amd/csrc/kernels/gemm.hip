@@ -117,6 +117,17 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs a, int ntn, int n
 }
 
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
+  if (a.algo == 3) {
+    if (!gemm_small_kblocks(a)) throw_gemm_shape();
+    gemm_small(a, s);
+    return;
+  }
+  // latency-bound regime (fewer than one 128 x 128 workgroup per CU): the one-shot small kernel
+  if (a.algo == 0 && gemm_small_kblocks(a) &&
+      (a.M % 128 || a.N % 128 || (a.M / 128) * (a.N / 128) * a.splits < 256)) {
+    gemm_small(a, s);
+    return;
+  }
   // the LDS-staged kernel measured faster on every engine shape it supports (scripts/bench_gemm.py)
   if (a.algo == 2 || (a.algo == 0 && gemm_lds_ok(a))) {
     if (!gemm_lds_ok(a)) throw_gemm_shape();

@@ -195,6 +195,10 @@ __global__ void __launch_bounds__(256, 2) gemm_lds_prep_kernel(GemmArgs a, int n
 }
 
 void gemm_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
+  if (gemm_small_kblocks(a) && !a.rowsumA && (a.M % 128 || a.N % 128 || (a.M / 128) * (a.N / 128) * a.splits < 256)) {
+    gemm_small_with_prep(a, p, s);
+    return;
+  }
   if (!gemm_lds_ok(a) || a.rowsumA || a.accumulate) {
     prep_batch(p.in, p.Bmax, p.T, p.Bp, p.ids, p.labels, p.inv_count, s);
     gemm_nt(a, s);

@@ -175,7 +175,8 @@ struct GemmArgs {
   int M = 0, N = 0, K = 0;
   int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
   int accumulate = 0;              // C += result instead of C = result
-  int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128
+  int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
+                                   // 3 one-shot 64x64 (gemm_small)
 };
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
@@ -183,6 +184,11 @@ bool gemm_lds_ok(const GemmArgs& a);
 // all jobs gemm_lds_ok, with the same bias / row-sum flags; n <= 4
 void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s);
 void gemm_lds(const GemmArgs& a, hipStream_t s);
+// one-shot 64 x 64 small GEMM (gemm_small.hip): the whole K-slice (128, 192, 256 or 512 deep) staged
+// at once; for the latency-bound small products.  kblocks = 64-deep blocks per K-slice, 0 = unsupported
+int gemm_small_kblocks(const GemmArgs& a);
+void gemm_small(const GemmArgs& a, hipStream_t s);
+void gemm_small_group(const GemmArgs* jobs, int n, hipStream_t s);   // same kblocks / flags, n <= 4
 
 // sum `splits` slabs [splits][n] -> dst[n] (optionally also as bf16 and/or accumulate)
 void reduce_slabs(const float* src, int splits, long n, float* dst, hipStream_t s);
@@ -269,5 +275,6 @@ inline int prep_batch_blocks(int T, int Bp) {
 // it measured +95 us per step: profiles/r1_sched_fork_fence_ab.jsonl).  Falls back to two launches
 // when the GEMM shape is not LDS-kernel compatible.
 void gemm_with_prep(const GemmArgs& g, const PrepJob& p, hipStream_t s);
+void gemm_small_with_prep(const GemmArgs& g, const PrepJob& p, hipStream_t s);
 
 }  // namespace gk
