@@ -23,6 +23,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
+
 // Wait until k-tile kt has landed while `ahead` later k-tiles (PER LDS-DMA instructions each,
 // per wave) stay in flight.  vmcnt retires in issue order, so loads the compiler issues after
 // ours only make the wait more conservative.
@@ -209,6 +210,151 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
       u16 v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
+      *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
+          *reinterpret_cast<const uint4*>(v);
+    }
+  }
+}
+
+// ==================================================================== forward, big batch
+// Tile 256 rows x 64 units x 3 gates for big-batch steps (batched generation: 4096+ names): 8 waves
+// of 64 rows x 32 units, each holding the r/z/n pre-activations of its items in acc[4][2][3]
+// (+ the input part of n in accN when FUSED).  Per 64-deep k-tile a wave issues 7 LDS-DMA pieces
+// for 48 MFMAs -- twice the MFMA work per DMA piece of the 128 x 96 tile, whose issue cost bounds
+// it.  2-deep ring of 56 KiB slots; epilogue operands are gathered after the K loop (the
+// accumulators take the register file).
+template <bool FUSED>
+__global__ void __launch_bounds__(512, 1) gru_fwd_step_big_kernel(FwdStepArgs a) {
+  constexpr int NS = 2, RA = 256, RB = 192, NP = (RA + RB) / 8 / 8;   // pieces per wave per k-tile
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][(RA + RB) * 64];
+  const int H = a.H;
+  const int j0 = blockIdx.x * 64, b0 = blockIdx.y * RA;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+
+  f32x4 acc[4][2][3];
+  f32x4 accN[FUSED ? 4 : 1][FUSED ? 2 : 1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) acc[i][jt][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (FUSED) accN[i][jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  auto phase = [&](const u16* Am, const u16* Bm, int K, auto input_tag) {
+    constexpr bool input = decltype(input_tag)::value;
+    // piece p = w*NP + q covers image rows 8p..8p+7: A rows (batch) below RA, then B rows
+    // (gate g = rb / 64, unit rb % 64 -> W row g*H + j0 + unit)
+    const u16* src[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int r = (w * NP + q) * 8 + srow;
+      if (r < RA) {
+        src[q] = Am + (size_t)(b0 + r) * K + swz(r, sslot) * 8;
+      } else {
+        const int rb = r - RA;
+        src[q] = Bm + (size_t)((rb >> 6) * H + j0 + (rb & 63)) * K + swz(rb, sslot) * 8;
+      }
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(w * NP + q) * 8 * 64]), 16, 0, 0);
+    };
+    ring_loop<NS, NP>(K / 64, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + RA * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[4], bfr[2][3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = wm * 64 + i * 16 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+        }
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            const int r = g * 64 + wn * 32 + jt * 16 + lr;
+            bfr[jt][g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+          }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt) {
+            acc[i][jt][0] = mfma16(af[i], bfr[jt][0], acc[i][jt][0]);
+            acc[i][jt][1] = mfma16(af[i], bfr[jt][1], acc[i][jt][1]);
+            if constexpr (FUSED && input) accN[FUSED ? i : 0][FUSED ? jt : 0] = mfma16(af[i], bfr[jt][2], accN[FUSED ? i : 0][FUSED ? jt : 0]);
+            else acc[i][jt][2] = mfma16(af[i], bfr[jt][2], acc[i][jt][2]);
+          }
+      }
+    });
+  };
+  if constexpr (FUSED) phase(a.x_bf, a.Wih, a.Kin, std::true_type{});
+  phase(a.hprev_bf, a.Whh, H, std::false_type{});
+
+  // ---- epilogue: per unit tile, gather this lane's operands, then the GRU math; bf16 h tile
+  // staged in LDS [256 rows][64 units] for the transposed copy
+  u16* st = lds[0];
+  const int* idp = a.ids ? a.ids + b0 + wm * 64 + lq * 4 : nullptr;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int uu = wn * 32 + jt * 16 + lr, u = j0 + uu;
+    float bh[3], bi[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      bh[g] = a.bhh[g * H + u];
+      bi[g] = FUSED ? a.bih[g * H + u] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float gi[4][3], hp[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int b = b0 + wm * 64 + i * 16 + lq * 4 + e;
+        hp[e] = a.hprev_f[(size_t)b * H + u];
+        if constexpr (!FUSED) {
+          const float* src = idp ? a.P + (size_t)idp[i * 16 + e] * 3 * H : a.Gi + (size_t)b * 3 * H;
+#pragma unroll
+          for (int g = 0; g < 3; ++g) gi[e][g] = src[g * H + u];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = wm * 64 + i * 16 + lq * 4 + e, b = b0 + rr;
+        const float ghr = acc[i][jt][0][e] + bh[0], ghz = acc[i][jt][1][e] + bh[1], ghn = acc[i][jt][2][e] + bh[2];
+        float gir, giz, gin;
+        if constexpr (FUSED) { gir = bi[0]; giz = bi[1]; gin = accN[FUSED ? i : 0][FUSED ? jt : 0][e] + bi[2]; }
+        else { gir = gi[e][0]; giz = gi[e][1]; gin = gi[e][2]; }
+        const float r = sigmoidf_(gir + ghr);
+        const float z = sigmoidf_(giz + ghz);
+        const float n = tanhf_(gin + r * ghn);
+        const float h = n + z * (hp[e] - n);
+        const size_t o = (size_t)b * H + u;
+        a.h_f[o] = h;
+        const u16 hb = f2bf(h);
+        a.h_bf[o] = hb;
+        if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+        st[rr * 64 + uu] = hb;
+      }
+    }
+  }
+  if (a.hT) {
+    __syncthreads();
+    // 64 units x 256 rows: 2048 x 16-B pieces, 4 per thread
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int q = threadIdx.x + p * 512;
+      const int unit = q >> 5, seg = q & 31;          // 32 segments of 8 rows
+      u16 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 64 + unit];
       *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
           *reinterpret_cast<const uint4*>(v);
     }
@@ -457,6 +603,18 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_lds8_kernel(BwdStepArgs a
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
+  static const bool big_ok = [] {
+    const char* e = std::getenv("GK_STEP_BIG");
+    return !(e && e[0] == '0');
+  }();
+  // big tile: only with the fused input phase on a full round of tiles (without it, the P-table
+  // gather moves behind the K loop and it measured slower: profiles/r1_generate_step_kernel_ab.json)
+  if (big_ok && a.x_bf && a.Kin % 64 == 0 && a.Bp % 256 == 0 && a.H % 64 == 0 && (a.H / 64) * (a.Bp / 256) >= 256) {
+    const dim3 grid(a.H / 64, a.Bp / 256), block(512);
+    if (a.x_bf) hipLaunchKernelGGL(gru_fwd_step_big_kernel<true>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(gru_fwd_step_big_kernel<false>, grid, block, 0, s, a);
+    return;
+  }
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
   if (const char* e = std::getenv("GK_STEP_LDS_NS")) ns = std::atoi(e) == 2 ? 2 : 4;

@@ -79,8 +79,9 @@ def _gates_ref(gi, gh, hp):
 # algo 1 = register-direct 32x16 tile, 2 = LDS-staged 128-row big tile (gru_step_lds.hip)
 @pytest.mark.parametrize("mode", ["table", "gi", "fused"])
 @pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (512, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2),
-                                      (512, 256, 2), (256, 128, 2)])
+                                      (512, 256, 2), (256, 128, 2), (1024, 2048, 2), (1024, 4096, 2)])
 def test_fwd_step(ext, mode, H, Bp, algo):
+    """algo 2, fused, (H/64)*(Bp/256) >= 256 (H=1024, Bp=4096): the 256 x 64 x 3 big-batch tile."""
     V, Kin = 256, 256   # fused mode, algo 2: input phase of 4 k-tiles ahead of the recurrent phase
     hp = rnd(Bp, H, scale=0.5, seed=1).clamp(-1, 1)
     hpb = bf(hp)
