@@ -1,0 +1,108 @@
+"""Multi-GPU tier (SURVEY §4.2 'Distributed on GPU'): the same checks as tests/test_dist_cpu.py, on
+the HIP engine with the native RCCL communicator, one process per GPU over xGMI.
+
+    (a) data-parallel training: P ranks x B/P sequences == 1 GPU x B, step for step (bf16 engine,
+        in-graph RCCL all-reduce of the readiness-ordered gradient groups);
+    (b) the bench's data-parallel step runs and reports one JSON line.
+
+Needs >= 2 visible GPUs; skipped otherwise (the 1-GPU test boxes run tests/test_engine_gpu.py's
+1-rank-communicator test of the same graph structure instead).  Launched through
+torch.distributed.run with 127.0.0.1 rendezvous, each worker a separate process (no GPU state
+in the pytest process)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _gpus() -> int:
+    try:
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+needs2 = pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+WORKER = r'''
+import os, sys, torch
+sys.path.insert(0, os.environ["GK_ROOT"])
+from gru_mpi_cuda_amd.config import GRUConfig
+from gru_mpi_cuda_amd.models.params import init_params
+from gru_mpi_cuda_amd.parallel import dist as gdist
+from gru_mpi_cuda_amd.parallel.rccl import make_comm
+from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+from gru_mpi_cuda_amd.utils.data import NameStream
+ctx = gdist.init(use_gpu=True)
+cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=128, seq=8, seed=5, lr=1e-2)
+stream = NameStream(cfg.batch, cfg.seq, seed=21)
+batches = [stream.next() for _ in range(3)]
+per = cfg.batch // ctx.world
+tr = HipTrainer(cfg, ctx, params=init_params(cfg), comm=make_comm(ctx))
+for x, y in batches:   # every rank takes its contiguous slice of the same global batch
+    tr.step(x[ctx.rank * per:(ctx.rank + 1) * per], y[ctx.rank * per:(ctx.rank + 1) * per])
+torch.cuda.synchronize()
+if ctx.rank == 0:
+    torch.save({k: v for k, v in tr.state_dict().items()}, os.environ["GK_OUT"])
+gdist.shutdown()
+'''
+
+
+def _run(n, script_path, out, timeout=240):
+    env = dict(os.environ, GK_ROOT=ROOT, GK_OUT=out, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if n == 1:
+        cmd = [sys.executable, script_path]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), script_path]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p
+
+
+@needs2
+def test_dp_training_on_gpus_equals_one_gpu(tmp_path):
+    n = 2 if _gpus() < 4 else 4
+    a, b = str(tmp_path / "p1.pt"), str(tmp_path / f"p{n}.pt")
+    worker = tmp_path / "worker.py"
+    worker.write_text(WORKER)
+    _run(1, str(worker), a)
+    _run(n, str(worker), b)
+    pa = torch.load(a, weights_only=True)
+    pb = torch.load(b, weights_only=True)
+    # bf16 MFMA operands and a different summation split: compare the Adam updates loosely
+    for k in pa:
+        d = (pa[k] - pb[k]).abs().max().item()
+        assert d < 2e-3, f"{k}: max |diff| {d}"
+
+
+@needs2
+def test_bench_dp_step_reports():
+    n = 2
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+                        "--gpus", str(n), "--steps", "10", "--warmup", "3"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == n and r["config"]["global_batch"] == 256 * n and r["value"] > 0
+    assert r["config"]["collectives"] >= 1
