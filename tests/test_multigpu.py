@@ -51,7 +51,7 @@ from gru_mpi_cuda_amd.parallel.rccl import make_comm
 from gru_mpi_cuda_amd.engine.trainer import HipTrainer
 from gru_mpi_cuda_amd.utils.data import NameStream
 ctx = gdist.init(use_gpu=True)
-cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=128, seq=8, seed=5, lr=1e-2)
+cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=128, seq=8, seed=5, lr=0.5, optimizer="sgd")
 stream = NameStream(cfg.batch, cfg.seq, seed=21)
 batches = [stream.next() for _ in range(3)]
 per = cfg.batch // ctx.world
@@ -87,10 +87,11 @@ def test_dp_training_on_gpus_equals_one_gpu(tmp_path):
     _run(n, str(worker), b)
     pa = torch.load(a, weights_only=True)
     pb = torch.load(b, weights_only=True)
-    # bf16 MFMA operands and a different summation split: compare the Adam updates loosely
+    # SGD (an update proportional to the gradient, unlike Adam's sign-like steps on near-zero
+    # gradients); the mean over ranks differs from the 1-GPU sum only in fp32 summation order
     for k in pa:
         d = (pa[k] - pb[k]).abs().max().item()
-        assert d < 2e-3, f"{k}: max |diff| {d}"
+        assert d < 1e-4, f"{k}: max |diff| {d}"
 
 
 @needs2
