@@ -193,17 +193,26 @@ DEV void signal_flag_local(unsigned* flag, unsigned epoch) {
 }
 
 // ==================================================================== forward
-template <int NKW>
+// RS = 1: every wave covers both 16-row tiles of the row block over a K/8 slice (NKW = H/256
+//         k-steps); the 8 partial sums of each output meet in LDS.
+// RS = 2: waves 0-3 own row tile 0, waves 4-7 row tile 1, each over a K/4 slice (NKW = H/128):
+//         the same MFMAs and exchange loads per wave, half the LDS partial traffic (4 partials of
+//         3 gates per output instead of 8, read by the epilogue thread of the same row tile).
+template <int NKW, int RS>
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][6][256];
-  __shared__ __attribute__((aligned(16))) u16 stg[32][16];
-  __shared__ __attribute__((aligned(16))) u16 stgT[16][32];
+  // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
+  // u16 writes -- rows 4 apart within a wave -- land in distinct banks (unpadded: 2-way / 4-way)
+  __shared__ __attribute__((aligned(16))) u16 stg[32][24];
+  __shared__ __attribute__((aligned(16))) u16 stgT[16][40];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = a.H, Bp = a.Bp, T = a.T;
   const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
   const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
-  const int k0 = w * NKW * 32;
+  constexpr int NR = RS == 2 ? 1 : 2;           // row tiles per wave
+  const int rt = RS == 2 ? (w >> 2) : 0;        // first row tile of this wave
+  const int k0 = (RS == 2 ? (w & 3) : w) * NKW * 32;
   const unsigned nunit = (unsigned)(H / 16);
 
   bf16x8 bw[NKW][3];   // this wave's K-slice of W_h{r,z,n} for the 16 units, resident all sequence
@@ -234,11 +243,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
     }
-    f32x4 acc[2][3];
+    f32x4 acc[NR][3];
     zero_acc(acc);
     if (t > 0 || a.h0) {
       // wave w's K-slice [k0, k0 + 32*NKW) is produced by unit tiles k0/16 .. k0/16 + 2*NKW - 1
-      bf16x8 af[NKW][2];
+      bf16x8 af[NKW][NR];
       if (t > 0) {
         // h_t from the producers' exchange tiles (written at step t-1); unit u = k0 + 32kk + lk
         // lives in tile u/16 at column u%16
@@ -248,25 +257,25 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
           const int u = k0 + kk * 32 + lk;
           const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
 #pragma unroll
-          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 16 * 2));
+          for (int r = 0; r < NR; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)((rt + r) * 16 * 16 * 2));
         });
       } else {   // h_init, row-major HS[0] (written before the launch)
-        const unsigned base = (unsigned)((((size_t)b0 + lr) * H + k0 + lk) * 2);
+        const unsigned base = (unsigned)((((size_t)b0 + rt * 16 + lr) * H + k0 + lk) * 2);
 #pragma unroll
         for (int kk = 0; kk < NKW; ++kk)
 #pragma unroll
-          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rH, base + (unsigned)(r * 16 * H * 2 + kk * 64));
+          for (int r = 0; r < NR; ++r) af[kk][r] = ld8_sc1(rH, base + (unsigned)(r * 16 * H * 2 + kk * 64));
       }
       stamp(a.dbg, t, 1);
 #pragma unroll
       for (int kk = 0; kk < NKW; ++kk)
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
           for (int g = 0; g < 3; ++g) acc[r][g] = mfma16(af[kk][r], bw[kk][g], acc[r][g]);
     }
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int g = 0; g < 3; ++g)
 #pragma unroll
@@ -277,8 +286,13 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       float s = 0.f;
+      if constexpr (RS == 2) {
 #pragma unroll
-      for (int ww = 0; ww < 8; ++ww) s += part[ww][rb * 3 + g][reg * 64 + ln];
+        for (int ww = 0; ww < 4; ++ww) s += part[rb * 4 + ww][g][reg * 64 + ln];
+      } else {
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) s += part[ww][rb * 3 + g][reg * 64 + ln];
+      }
       gh[g] = s + bh[g];
     }
     const float r = sigmoidf_(gi[0] + gh[0]);
@@ -331,7 +345,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 template <int NKW3, int NTW, int NTP>
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][2][256];      // 16 KB
-  __shared__ __attribute__((aligned(16))) u16 srow[3][32][16];        // dGh tile, gate-major (exchange)
+  __shared__ __attribute__((aligned(16))) u16 srow[3][32][24];        // dGh tile, gate-major (exchange; 48-B rows)
   __shared__ __attribute__((aligned(16))) u16 sgT[4][16][40];         // dGh^T gates r,z,n + dGi_n^T (padded rows)
   __shared__ __attribute__((aligned(16))) float red[6][16][33];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -553,35 +567,41 @@ static int resident_blocks(K kernel) {
   return ncu * per;
 }
 
-static bool fwd_kernel_for(int H, const void** k) {
-  switch (H) {
-    case 256: *k = (const void*)gru_fwd_seq_kernel<1>; return true;
-    case 512: *k = (const void*)gru_fwd_seq_kernel<2>; return true;
-    case 1024: *k = (const void*)gru_fwd_seq_kernel<4>; return true;
-    default: return false;
-  }
+// row-tile split: RS = 2 up to H = 512 (H=512 forward kernel 77.5 -> 72.5 us, per step 2.16 ->
+// 2.00 us); RS = 1 at H = 1024, where the K/4 slice's 16 producers per wave measured no better
+// (profiles/r1_fwd_row_split_ab.json).  GK_FWD_RS=1/2 forces one.
+static int fwd_rs(int H) {
+  static const int forced = [] {
+    const char* e = std::getenv("GK_FWD_RS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2) return forced;
+  return H <= 512 ? 2 : 1;
 }
 
+#define FWD_VARIANTS(X) X(256, 1, 1) X(256, 2, 2) X(512, 2, 1) X(512, 4, 2) X(1024, 4, 1) X(1024, 8, 2)
+
 bool gru_fwd_seq_supported(int H, int Bp) {
-  const void* k;
-  if (!fwd_kernel_for(H, &k) || Bp % 32) return false;
-  int cap = 0;
-  switch (H) {
-    case 256: cap = resident_blocks(gru_fwd_seq_kernel<1>); break;
-    case 512: cap = resident_blocks(gru_fwd_seq_kernel<2>); break;
-    default: cap = resident_blocks(gru_fwd_seq_kernel<4>); break;
-  }
-  return (H / 16) * (Bp / 32) <= cap;
+  if (Bp % 32) return false;
+  const int rs = fwd_rs(H);
+  int cap = -1;
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS>);
+  FWD_VARIANTS(X)
+#undef X
+  return cap >= (H / 16) * (Bp / 32);
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
-  switch (a.H) {
-    case 256: hipLaunchKernelGGL(gru_fwd_seq_kernel<1>, grid, block, 0, s, a); break;
-    case 512: hipLaunchKernelGGL(gru_fwd_seq_kernel<2>, grid, block, 0, s, a); break;
-    case 1024: hipLaunchKernelGGL(gru_fwd_seq_kernel<4>, grid, block, 0, s, a); break;
-    default: break;
+  const int rs = fwd_rs(a.H);
+#define X(HH, NK, RS)                                                        \
+  if (a.H == HH && rs == RS) {                                              \
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS>), grid, block, 0, s, a); \
+    return;                                                                  \
   }
+  FWD_VARIANTS(X)
+#undef X
+  throw std::runtime_error("gru_fwd_seq: no kernel variant for this shape");
 }
 
 // fused-variant table: (H, fuse dW_hh, fuse dP) -> kernel
