@@ -24,17 +24,28 @@ DEV int xcd_remap_s(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// NCH > 1 (K-slices of NCH x 512): the slice is streamed as NCH bursts of 8 blocks through the same
+// LDS (one memory latency per 512-deep chunk instead of one per 64-deep k-tile).
 template <int NKB, bool BIAS, bool ROWSUM>
-DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)[2][64 * 64]) {
+DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)[2][64 * 64], int nch = 1) {
   const int tn = id % ntn, tm = (id / ntn) % ntm, sp = id / (ntn * ntm);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int lr = lane & 15, lq = lane >> 4;
   const int row0 = tm * 64, col0 = tn * 64;
-  const int kbeg = sp * NKB * 64;
   const int srow = lane >> 3, sslot = lane & 7;
 
-  // the whole K-slice in one burst: per 64-deep block, wave w stages rows 16w .. 16w+15 of A and B
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_rs = ROWSUM && tn == 0 && wn == 0;
+  float rs[2] = {0.f, 0.f};
+  for (int ch = 0; ch < nch; ++ch) {
+  const int kbeg = (sp * nch + ch) * NKB * 64;
+  if (ch) __syncthreads();   // every wave is done reading the previous chunk
+  // the whole chunk in one burst: per 64-deep block, wave w stages rows 16w .. 16w+15 of A and B
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -50,13 +61,6 @@ DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_rs = ROWSUM && tn == 0 && wn == 0;
-  float rs[2] = {0.f, 0.f};
 #pragma unroll
   for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
@@ -80,6 +84,7 @@ DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)
           for (int e = 0; e < 8; ++e) rs[t] += (float)af[t][e];
       }
     }
+  }
 
   float* C = a.C + (size_t)sp * a.M * a.ldc;
 #pragma unroll
@@ -108,9 +113,9 @@ DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)
 }
 
 template <int NKB, bool BIAS, bool ROWSUM>
-__global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_kernel(GemmArgs a, int ntn, int ntm) {
+__global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_kernel(GemmArgs a, int ntn, int ntm, int nch) {
   __shared__ __attribute__((aligned(16))) u16 lds[NKB][2][64 * 64];
-  gemm_small_body<NKB, BIAS, ROWSUM>(a, xcd_remap_s(blockIdx.x, gridDim.x), ntn, ntm, lds);
+  gemm_small_body<NKB, BIAS, ROWSUM>(a, xcd_remap_s(blockIdx.x, gridDim.x), ntn, ntm, lds, nch);
 }
 
 struct SmallGroup { GemmArgs job[4]; int start[5]; int ntn[4], ntm[4]; int n; };
@@ -127,25 +132,33 @@ __global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_group_kernel
 // + trailing blocks running the batch transpose (gemm_with_prep in gemm_lds.hip)
 template <int NKB, bool BIAS>
 __global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_prep_kernel(GemmArgs a, int ntn, int ntm,
-                                                                                   PrepJob pj, int nprep) {
+                                                                                   PrepJob pj, int nprep, int nch) {
   __shared__ __attribute__((aligned(16))) u16 lds[NKB][2][64 * 64];
   const int ng = ntn * ntm * a.splits;
   if ((int)blockIdx.x >= ng) {
     prep_batch_body(pj, (int)blockIdx.x - ng, nprep);
     return;
   }
-  gemm_small_body<NKB, BIAS, false>(a, xcd_remap_s(blockIdx.x, ng), ntn, ntm, lds);
+  gemm_small_body<NKB, BIAS, false>(a, xcd_remap_s(blockIdx.x, ng), ntn, ntm, lds, nch);
 }
 
-int gemm_small_kblocks(const GemmArgs& a) {
+// 64-deep blocks per chunk (0 = unsupported); *nch = chunks per K-slice (slices of n x 512 stream)
+static int small_blocks(const GemmArgs& a, int* nch) {
+  *nch = 1;
   if (a.onehot_ids || a.M % 64 || a.N % 64 || a.K % a.splits) return 0;
   const int kper = a.K / a.splits;
   if (kper % 64) return 0;
-  const int nkb = kper / 64;
+  int nkb = kper / 64;
+  if (nkb > 8 && nkb % 8 == 0 && nkb <= 32) { *nch = nkb / 8; nkb = 8; }
   if (nkb != 2 && nkb != 3 && nkb != 4 && nkb != 8) return 0;
   if ((a.lda % 8) || (a.ldb % 8)) return 0;
   if ((reinterpret_cast<uintptr_t>(a.A) | reinterpret_cast<uintptr_t>(a.B)) & 15) return 0;
   return nkb;
+}
+int gemm_small_kblocks(const GemmArgs& a) {
+  int nch = 1;
+  const int nkb = small_blocks(a, &nch);
+  return nkb * nch;
 }
 
 template <class Launch>
@@ -161,9 +174,9 @@ static void dispatch_nkb(int nkb, bool bias, bool rs, const Launch& L) {
 }
 
 struct SmallLaunch {
-  const GemmArgs& a; int ntn, ntm; hipStream_t s;
+  const GemmArgs& a; int ntn, ntm, nch; hipStream_t s;
   template <int N, bool B, bool R> void go() const {
-    hipLaunchKernelGGL((gemm_small_kernel<N, B, R>), dim3(ntn * ntm * a.splits), dim3(256), 0, s, a, ntn, ntm);
+    hipLaunchKernelGGL((gemm_small_kernel<N, B, R>), dim3(ntn * ntm * a.splits), dim3(256), 0, s, a, ntn, ntm, nch);
   }
 };
 struct SmallGroupLaunch {
@@ -174,21 +187,23 @@ struct SmallGroupLaunch {
 };
 
 void gemm_small(const GemmArgs& a, hipStream_t s) {
-  const int nkb = gemm_small_kblocks(a);
+  int nch = 1;
+  const int nkb = small_blocks(a, &nch);
   if (!nkb) throw std::runtime_error("gemm_small: unsupported shape");
-  dispatch_nkb(nkb, a.bias && a.splits == 1, a.rowsumA != nullptr, SmallLaunch{a, a.N / 64, a.M / 64, s});
+  dispatch_nkb(nkb, a.bias && a.splits == 1, a.rowsumA != nullptr, SmallLaunch{a, a.N / 64, a.M / 64, nch, s});
 }
 
 void gemm_small_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
-  const int nkb = gemm_small_kblocks(a);
+  int nch = 1;
+  const int nkb = small_blocks(a, &nch);
   if (!nkb || a.rowsumA) throw std::runtime_error("gemm_small_with_prep: unsupported shape");
   const int ntn = a.N / 64, ntm = a.M / 64, nprep = prep_batch_blocks(p.T, p.Bp);
   const dim3 grid(ntn * ntm * a.splits + nprep), block(256);
   const bool bias = a.bias && a.splits == 1;
 #define GP_CASE(N)                                                                                        \
   case N:                                                                                                 \
-    if (bias) hipLaunchKernelGGL((gemm_small_prep_kernel<N, true>), grid, block, 0, s, a, ntn, ntm, p, nprep); \
-    else hipLaunchKernelGGL((gemm_small_prep_kernel<N, false>), grid, block, 0, s, a, ntn, ntm, p, nprep);     \
+    if (bias) hipLaunchKernelGGL((gemm_small_prep_kernel<N, true>), grid, block, 0, s, a, ntn, ntm, p, nprep, nch); \
+    else hipLaunchKernelGGL((gemm_small_prep_kernel<N, false>), grid, block, 0, s, a, ntn, ntm, p, nprep, nch);     \
     return;
   switch (nkb) { GP_CASE(2) GP_CASE(3) GP_CASE(4) GP_CASE(8) default: break; }
 #undef GP_CASE
@@ -199,8 +214,10 @@ void gemm_small_group(const GemmArgs* jobs, int n, hipStream_t s) {
   SmallGroup g;
   g.n = n;
   int tot = 0;
-  const int nkb = gemm_small_kblocks(jobs[0]);
+  int nch0 = 1;
+  const int nkb = small_blocks(jobs[0], &nch0);
   const bool bias = jobs[0].bias && jobs[0].splits == 1, rs = jobs[0].rowsumA != nullptr;
+  if (nch0 != 1) throw std::runtime_error("gemm_small_group: K-slices up to 512 only");
   for (int k = 0; k < n; ++k) {
     const GemmArgs& a = jobs[k];
     if (!nkb || gemm_small_kblocks(a) != nkb || (a.bias && a.splits == 1) != bias || (a.rowsumA != nullptr) != rs)

@@ -27,14 +27,14 @@ def rnd(*shape, scale=1.0, seed=0):
     return (torch.randn(*shape, generator=g) * scale).to(DEV)
 
 
-@pytest.mark.parametrize("algo", [1, 2, 3])   # 3: one-shot 64x64 small GEMM (K-slice 128/192/256/512)
+@pytest.mark.parametrize("algo", [1, 2, 3])   # 3: one-shot 64x64 small GEMM (K-slice <= 512, or n x 512 chunks)
 @pytest.mark.parametrize("M,N,K,splits", [(64, 64, 32, 1), (128, 192, 256, 1), (256, 512, 1024, 4), (192, 128, 512, 2),
                                           (384, 256, 768, 3), (128, 128, 128, 1), (256, 1536, 512, 1),
-                                          (256, 512, 8192, 16)])
+                                          (256, 512, 8192, 16), (256, 3072, 1024, 1), (128, 256, 3072, 2)])
 def test_gemm_nt(ext, algo, M, N, K, splits):
     if algo == 2 and (M % 128 or N % 128 or (K // splits) % 64 or K // splits < 128):
         pytest.skip("shape not supported by the LDS kernel")
-    if algo == 3 and (M % 64 or N % 64 or K % splits or K // splits not in (128, 192, 256, 512)):
+    if algo == 3 and (M % 64 or N % 64 or K % splits or K // splits not in (128, 192, 256, 512, 1024, 1536)):
         pytest.skip("shape not supported by the one-shot kernel")
     A, B = bf(rnd(M, K, seed=1)), bf(rnd(N, K, seed=2) + 0.1 * torch.arange(K, device=DEV) / K)
     bias = rnd(N, seed=3) if splits == 1 else None
