@@ -147,7 +147,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // latency per workgroup and half the slabs of the 32-way 128 x 128 split
     static const int kslice = [] {
       const char* e = std::getenv("GK_FC_SMALL_K");
-      return e ? std::atoi(e) : 0;   // 0: 128x128 split-K (measured equal, profiles/r1_small_gemm_ab.jsonl)
+      // 1024: 8 slabs, summed inside the Adam launch (0.2362 -> 0.2338 ms at h512,
+      // profiles/r1_fc_kslice_ab.jsonl; 512 measured equal to 128x128 split-K, r1_small_gemm_ab.jsonl)
+      return e ? std::atoi(e) : 1024;
     }();
     if (kslice > 0 && tok % kslice == 0 && tok / kslice <= kFcSplitsMax) {
       GemmArgs ws = w;

@@ -107,31 +107,29 @@ DEV float4 sum_slabs4(const float* __restrict__ src, long n, int splits, size_t 
 }
 
 __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
-  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)
+  __shared__ u16 tile[16][72];   // 144-B rows: the transposed reads (one column, 8 rows) spread over banks
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   if (j.bump && b == 0 && threadIdx.x == 0) *j.bump += 1;
   const SlabJob& J = j.job[k];
-  if (J.bf || J.bfT) {   // 64x64 tile: slab sum -> fp32 / bf16 / bf16 transposed
+  if (J.bf || J.bfT) {   // 16x64 tile (one float4 per thread): slab sum -> fp32 / bf16 / bf16 transposed
+    // 16-row tiles: 4x the workgroups of 64x64 ones, so the slab loads of a 256 x 1536 dP reach
+    // every CU (96 blocks of 64x64 left most of the chip idle)
     const int tiles_c = J.C / 64, t = b - j.blk_start[k];
-    const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+    const int r0 = (t / tiles_c) * 16, c0 = (t % tiles_c) * 64;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const size_t o = (size_t)(r0 + ty + 16 * q) * J.C + c0 + 4 * tx;
-      const float4 acc = sum_slabs4(J.src, J.n, J.splits, o);
-      if (J.dst) *reinterpret_cast<float4*>(J.dst + o) = acc;
-      uint2 w;
-      w.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
-      w.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
-      if (J.bf) *reinterpret_cast<uint2*>(J.bf + o) = w;
-      *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w;
-    }
+    const size_t o = (size_t)(r0 + ty) * J.C + c0 + 4 * tx;
+    const float4 acc = sum_slabs4(J.src, J.n, J.splits, o);
+    if (J.dst) *reinterpret_cast<float4*>(J.dst + o) = acc;
+    uint2 w;
+    w.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
+    w.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
+    if (J.bf) *reinterpret_cast<uint2*>(J.bf + o) = w;
     if (!J.bfT) return;
+    *reinterpret_cast<uint2*>(&tile[ty][4 * tx]) = w;
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int piece = threadIdx.x + 256 * q, col = piece >> 3, seg = piece & 7;
+    if (threadIdx.x < 128) {   // 64 columns x 2 pieces of 8 rows (16 B)
+      const int col = threadIdx.x >> 1, seg = threadIdx.x & 1;
       u16 v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
@@ -167,8 +165,8 @@ void reduce_slabs_multi(SlabJobs& j, hipStream_t s) {
     const SlabJob& J = j.job[k];
     j.blk_start[k] = tot;
     if (J.bf || J.bfT) {
-      if (J.R % 64 || J.C % 64) throw std::runtime_error("reduce_slabs_multi: cast job needs R, C % 64 == 0");
-      tot += (J.R / 64) * (J.C / 64);
+      if (J.R % 16 || J.C % 64) throw std::runtime_error("reduce_slabs_multi: cast job needs R % 16, C % 64 == 0");
+      tot += (J.R / 16) * (J.C / 64);
       continue;
     }
     long b = (J.n / 4 + 255) / 256;
