@@ -50,7 +50,7 @@ def save_checkpoint(tr, path: str, fmt: str = "gen") -> None:
     cfg = tr.cfg
     params = tr.state_dict()
     if hasattr(tr, "t"):                    # HipTrainer
-        m, v, step = tr.m.cpu(), tr.v.cpu(), tr.t.get_step()
+        (m, v), step = tr.opt_state(), tr.t.get_step()
     else:
         from .models.params import to_flat
         m, v, step = to_flat(cfg, tr.opt.m), to_flat(cfg, tr.opt.v), tr.opt.step_n
@@ -69,8 +69,7 @@ def load_checkpoint(tr, path: str) -> int:
     if hasattr(tr, "t"):
         tr.load_state(params)
         if st is not None:
-            tr.m.copy_(st["m"].to(tr.m.device))
-            tr.v.copy_(st["v"].to(tr.v.device))
+            tr.load_opt_state(st["m"], st["v"])
             tr.t.set_step(int(st["step"][0]))
     else:
         for k in tr.params:

@@ -25,7 +25,7 @@ import torch
 
 from ..config import GRUConfig
 from ..models import cpu_ref
-from ..models.params import flat_layout, to_flat
+from ..models.params import flat_layout, pad_config, pad_params, to_flat
 from ..parallel.dist import DistCtx, shard
 
 
@@ -36,10 +36,19 @@ class HipGenerator:
         self.C = load_ext()
         self.cfg = cfg
         self.dev = device or torch.device("cuda", torch.cuda.current_device())
-        self.layout = flat_layout(cfg)
-        self.flat = flat if flat is not None else to_flat(cfg, params).to(self.dev)
+        # E, H off the 64-grid: the exactly equivalent zero-padded model (models/params.py).  The
+        # vocabulary is not padded: the sampler's fallback index is V - 1 (namegensf.cu:333)
+        if cfg.vocab % 64:
+            raise ValueError(f"HIP generator needs vocab % 64 == 0 (got {cfg.vocab})")
+        icfg = pad_config(cfg).replace(vocab=cfg.vocab)
+        if icfg != cfg:
+            if flat is not None:
+                raise ValueError("a shared flat buffer needs embed and hidden to be multiples of 64")
+            params = pad_params(params, cfg, icfg)
+        self.layout = flat_layout(icfg)
+        self.flat = flat if flat is not None else to_flat(icfg, params).to(self.dev)
         offsets = {s.name: s.offset for s in self.layout.segments}
-        dims = dict(V=cfg.vocab, E=cfg.embed, H=cfg.hidden, L=cfg.layers, max_len=cfg.max_len,
+        dims = dict(V=cfg.vocab, E=icfg.embed, H=icfg.hidden, L=cfg.layers, max_len=cfg.max_len,
                     sos=cfg.sos, eos=cfg.eos, max_batch=max_batch)
         self.g = self.C.Generator(dims, self.flat.data_ptr(), offsets)
         self.g.refresh_weights(self._s())

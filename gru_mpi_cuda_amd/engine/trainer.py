@@ -20,7 +20,7 @@ import torch
 
 from ..config import GRUConfig
 from ..models import cpu_ref
-from ..models.params import flat_layout, from_flat, init_params, to_flat
+from ..models.params import flat_layout, from_flat, init_params, pad_config, pad_params, to_flat, unpad_params
 from ..parallel.dist import DistCtx, allreduce_mean_buckets, bucket_bounds
 
 
@@ -41,15 +41,22 @@ class HipTrainer:
         if cfg.batch % self.ctx.world:
             raise ValueError(f"global batch {cfg.batch} not divisible by world size {self.ctx.world}")
         self.local_batch = cfg.batch // self.ctx.world
-        self.layout = flat_layout(cfg)
-        self.params = to_flat(cfg, params if params is not None else init_params(cfg)).to(self.dev)
+        # V, E, H off the 64-grid run on the exactly equivalent zero-padded model (params.py);
+        # params / grads / m / v below are in the padded (internal) layout, the accessors
+        # (state_dict, grad_dict, load_state, opt_state) speak the user's shapes
+        self.icfg = pad_config(cfg)
+        self.padded = self.icfg != cfg
+        self.layout = flat_layout(self.icfg)
+        p0 = params if params is not None else init_params(cfg)
+        self.params = to_flat(self.icfg, self._pad(p0)).to(self.dev)
         self.grads = torch.zeros_like(self.params)
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.comm = comm
-        self.buckets = _bucket_list(cfg, self.layout.total)
+        self.buckets = _bucket_list(self.icfg, self.layout.total)
         offsets = {s.name: s.offset for s in self.layout.segments}
-        dims = dict(V=cfg.vocab, E=cfg.embed, H=cfg.hidden, L=cfg.layers, B=self.local_batch,
+        ic = self.icfg
+        dims = dict(V=ic.vocab, E=ic.embed, H=ic.hidden, L=cfg.layers, B=self.local_batch,
                     T=cfg.seq, chunks=cfg.time_chunks, overlap=int(cfg.overlap))
         opt = dict(lr=cfg.lr, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps,
                    weight_decay=cfg.weight_decay, clip_norm=cfg.clip_norm,
@@ -68,6 +75,12 @@ class HipTrainer:
         self._one_graph = True
         if cfg.watchdog_ms > 0:       # host thread watching each launched step
             self.t.enable_watchdog(int(cfg.watchdog_ms))
+
+    def _pad(self, params: Dict[str, torch.Tensor], masked_bias: bool = True) -> Dict[str, torch.Tensor]:
+        return pad_params(params, self.cfg, self.icfg, masked_bias) if self.padded else params
+
+    def _unpad(self, params: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        return unpad_params(params, self.cfg, self.icfg) if self.padded else params
 
     def check_watchdog(self) -> None:
         """Raise if the collective watchdog fired (step timeout or RCCL async error)."""
@@ -144,15 +157,24 @@ class HipTrainer:
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
         torch.cuda.synchronize(self.dev)
-        return {k: v.cpu() for k, v in from_flat(self.cfg, self.params).items()}
+        return self._unpad({k: v.cpu() for k, v in from_flat(self.icfg, self.params).items()})
 
     def grad_dict(self) -> Dict[str, torch.Tensor]:
         torch.cuda.synchronize(self.dev)
-        return {k: v.cpu() for k, v in from_flat(self.cfg, self.grads).items()}
+        return self._unpad({k: v.cpu() for k, v in from_flat(self.icfg, self.grads).items()})
 
     def load_state(self, params: Dict[str, torch.Tensor]) -> None:
-        self.params.copy_(to_flat(self.cfg, params).to(self.dev))
+        self.params.copy_(to_flat(self.icfg, self._pad(params)).to(self.dev))
         self.t.refresh_weights(self._stream())
+
+    def opt_state(self):
+        """Adam moments as flat fp32 tensors in the user config's layout (checkpoints)."""
+        torch.cuda.synchronize(self.dev)
+        return tuple(to_flat(self.cfg, self._unpad(from_flat(self.icfg, t.cpu()))) for t in (self.m, self.v))
+
+    def load_opt_state(self, m: torch.Tensor, v: torch.Tensor) -> None:
+        for dst, src in ((self.m, m), (self.v, v)):
+            dst.copy_(to_flat(self.icfg, self._pad(from_flat(self.cfg, src.float()), masked_bias=False)).to(self.dev))
 
 
 class CpuTrainer:

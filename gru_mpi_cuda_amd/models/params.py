@@ -122,3 +122,72 @@ def to_flat(cfg: GRUConfig, params: Dict[str, torch.Tensor], device="cpu") -> to
 
 def from_flat(cfg: GRUConfig, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
     return {k: v.detach().clone() for k, v in flat_layout(cfg).views(flat).items()}
+
+
+# ------------------------------------------------------------------ padding to the MFMA tile grid
+# The HIP engine tiles V, E and H by 64.  Other sizes run on a zero-padded model, which is exact:
+# padded hidden units have zero weights and biases, so from h0 = 0 they stay 0 (r = z = 1/2,
+# n = tanh 0 = 0), contribute nothing to real units, and receive zero gradient (their dy and
+# dh are zero); padded embedding columns are zero on both sides of W_ih0; padded vocabulary rows
+# get a logit bias of MASKED_LOGIT, i.e. softmax probability exactly 0 and zero gradient, so Adam
+# never moves any padded entry.
+MASKED_LOGIT = -30000.0
+PAD_MULT = 64
+
+
+def _round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+def pad_config(cfg: GRUConfig, mult: int = PAD_MULT) -> GRUConfig:
+    return cfg.replace(vocab=_round_up(cfg.vocab, mult), embed=_round_up(cfg.embed, mult),
+                       hidden=_round_up(cfg.hidden, mult))
+
+
+def pad_params(params: Dict[str, torch.Tensor], cfg: GRUConfig, pcfg: GRUConfig,
+               masked_bias: bool = True) -> Dict[str, torch.Tensor]:
+    """cfg-shaped tensors -> pcfg-shaped (zero padding per gate block; masked_bias=False pads the
+    FC bias with zeros too, for optimiser moments)."""
+    H, Hp = cfg.hidden, pcfg.hidden
+    out: Dict[str, torch.Tensor] = {}
+    for k, v in params.items():
+        shp = param_shapes(pcfg)[k]
+        if k.startswith(("weight_ih_l", "weight_hh_l")):
+            l = int(k.rsplit("l", 1)[1])
+            inn = cfg.layer_in(l) if k.startswith("weight_ih") else H
+            innp = pcfg.layer_in(l) if k.startswith("weight_ih") else Hp
+            p = v.new_zeros(3, Hp, innp)
+            p[:, :H, :inn] = v.reshape(3, H, inn)
+            out[k] = p.reshape(shp)
+        elif k.startswith(("bias_ih_l", "bias_hh_l")):
+            p = v.new_zeros(3, Hp)
+            p[:, :H] = v.reshape(3, H)
+            out[k] = p.reshape(shp)
+        elif k == "fc.bias":
+            p = v.new_full(shp, MASKED_LOGIT if masked_bias else 0.0)
+            p[:cfg.vocab] = v
+            out[k] = p
+        else:   # embedding [V][E], fc.weight [V][H]
+            p = v.new_zeros(shp)
+            p[:v.shape[0], :v.shape[1]] = v
+            out[k] = p
+    return out
+
+
+def unpad_params(params: Dict[str, torch.Tensor], cfg: GRUConfig, pcfg: GRUConfig) -> Dict[str, torch.Tensor]:
+    """pcfg-shaped tensors -> cfg-shaped (the real entries)."""
+    H, Hp = cfg.hidden, pcfg.hidden
+    out: Dict[str, torch.Tensor] = {}
+    for k, v in params.items():
+        if k.startswith(("weight_ih_l", "weight_hh_l")):
+            l = int(k.rsplit("l", 1)[1])
+            inn = cfg.layer_in(l) if k.startswith("weight_ih") else H
+            innp = pcfg.layer_in(l) if k.startswith("weight_ih") else Hp
+            out[k] = v.reshape(3, Hp, innp)[:, :H, :inn].reshape(3 * H, inn).contiguous()
+        elif k.startswith(("bias_ih_l", "bias_hh_l")):
+            out[k] = v.reshape(3, Hp)[:, :H].reshape(3 * H).contiguous()
+        elif k == "fc.bias":
+            out[k] = v[:cfg.vocab].contiguous()
+        else:
+            out[k] = v[:param_shapes(cfg)[k][0], :param_shapes(cfg)[k][1]].contiguous()
+    return out
