@@ -146,6 +146,24 @@ PYBIND11_MODULE(_C, m) {
     gemm_nt(a, S(s));
     HIP_LAUNCH_CHECK();
   });
+  m.def("cast_multi", [](py::list jobs, uintptr_t s) {
+    CastJobs j;
+    if (jobs.size() > 24) throw std::runtime_error("cast_multi: at most 24 jobs");
+    for (auto h : jobs) {
+      py::dict d = h.cast<py::dict>();
+      j.add(GP(const float, d, "src"), get<int>(d, "R", 0), get<int>(d, "C", 0), GP(u16, d, "dst"),
+            GP(u16, d, "dstT"), GP(u16, d, "dstF"), GP(u16, d, "dstTF"));
+    }
+    cast_multi(j, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("reduce_slabs_cast", [](py::dict d, uintptr_t s) {   // one slab-sum + cast job
+    SlabJobs j;
+    j.add_cast(GP(const float, d, "src"), get<int>(d, "splits", 1), get<int>(d, "R", 0), get<int>(d, "C", 0),
+               GP(float, d, "dst"), GP(u16, d, "bf"), GP(u16, d, "bfT"));
+    reduce_slabs_multi(j, S(s));
+    HIP_LAUNCH_CHECK();
+  });
   m.def("fwd_step", [](py::dict d, uintptr_t s) {
     FwdStepArgs a;
     a.hprev_bf = GP(const u16, d, "hprev_bf"); a.hprev_f = GP(const float, d, "hprev_f");

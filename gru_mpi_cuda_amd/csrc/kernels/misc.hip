@@ -177,16 +177,20 @@ void reduce_slabs_multi(SlabJobs& j, hipStream_t s) {
 }
 
 // fp32 [R][C] -> bf16 [R][C] and/or bf16 [C][R], 64x64 tiles through LDS, many tensors per launch
+// 64-row tiles where an FT copy needs whole 64 x 64 fragment blocks, else 16-row tiles: 4x the
+// workgroups, so a 256 x 1536 tensor (the data-parallel dP cast) reaches every CU
+DEV_HOST_INLINE int cast_tile_rows(const CastJob& J) { return (J.dstF || J.dstTF) ? 64 : 16; }
 __global__ void cast_multi_kernel(CastJobs j) {
   __shared__ float tile[64][65];
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   const CastJob& J = j.job[k];
+  const int th = cast_tile_rows(J);
   const int tiles_c = (J.C + 63) / 64;
   const int t = b - j.blk_start[k];
-  const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+  const int r0 = (t / tiles_c) * th, c0 = (t % tiles_c) * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int y = ty; y < 64; y += 4) {
+  for (int y = ty; y < th; y += 4) {
     const int r = r0 + y, c = c0 + tx;
     const float v = (r < J.R && c < J.C) ? J.src[(size_t)r * J.C + c] : 0.f;
     tile[y][tx] = v;
@@ -194,12 +198,13 @@ __global__ void cast_multi_kernel(CastJobs j) {
   }
   if (!J.dstT && !J.dstF && !J.dstTF) return;
   __syncthreads();
-  if (J.dstT)
-    for (int y = ty; y < 64; y += 4) {
-      const int c = c0 + y, r = r0 + tx;
-      if (c < J.C && r < J.R) J.dstT[(size_t)c * J.R + r] = f2bf(tile[tx][y]);
+  if (J.dstT)   // th consecutive threads write one column's th rows (2 th contiguous bytes)
+    for (int q = threadIdx.x; q < 64 * th; q += 256) {
+      const int y = q / th, x = q % th;
+      const int c = c0 + y, r = r0 + x;
+      if (c < J.C && r < J.R) J.dstT[(size_t)c * J.R + r] = f2bf(tile[x][y]);
     }
-  if (J.R % 64 || J.C % 64) return;   // FT copies: whole 64 x 64 tiles only (checked on the host)
+  if (th != 64) return;   // FT copies: whole 64 x 64 tiles only (checked on the host)
   // 512 16-B pieces per tile: (4 row tiles x 2 k-steps) fragments of 64 lanes
   for (int q = threadIdx.x; q < 512; q += 256) {
     const int fl = q & 63, fr = (q >> 6) & 3, fk = q >> 8;   // lane, 16-row tile, 32-k step
@@ -223,7 +228,8 @@ void cast_multi(CastJobs& j, hipStream_t s) {
     if ((j.job[k].dstF || j.job[k].dstTF) && (j.job[k].R % 64 || j.job[k].C % 64))
       throw std::runtime_error("cast_multi: FT copies need R, C % 64 == 0");
     j.blk_start[k] = tot;
-    tot += ((j.job[k].R + 63) / 64) * ((j.job[k].C + 63) / 64);
+    const int th = cast_tile_rows(j.job[k]);
+    tot += ((j.job[k].R + th - 1) / th) * ((j.job[k].C + 63) / 64);
   }
   j.blk_start[j.n] = tot;
   hipLaunchKernelGGL(cast_multi_kernel, dim3(tot), dim3(256), 0, s, j);

@@ -240,3 +240,40 @@ def test_fc_sample(ext, H):
     assert o[3, step] == 0                       # dead row untouched
     live = [i for i in range(N) if i != 3]
     assert torch.equal(o[live, step].long(), got[live])
+
+
+@pytest.mark.parametrize("R,C,ft", [(256, 1536, False), (100, 72, False), (64, 128, True), (192, 256, True)])
+def test_cast_multi(ext, R, C, ft):
+    """fp32 -> bf16 / bf16 transposed (/ FT copies): 16-row tiles without FT outputs, 64-row with."""
+    from gru_mpi_cuda_amd.ops import ft_layout
+    src = rnd(R, C, seed=R + C)
+    dst = torch.empty(R, C, device=DEV, dtype=torch.bfloat16)
+    dT = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    job = dict(src=src.data_ptr(), R=R, C=C, dst=dst.data_ptr(), dstT=dT.data_ptr())
+    if ft:
+        dF = torch.empty(R * C, device=DEV, dtype=torch.bfloat16)
+        dTF = torch.empty(R * C, device=DEV, dtype=torch.bfloat16)
+        job.update(dstF=dF.data_ptr(), dstTF=dTF.data_ptr())
+    ext.cast_multi([job, dict(job)], S())   # two jobs: the block prefix sum
+    torch.cuda.synchronize()
+    ref = src.bfloat16()
+    assert torch.equal(dst, ref) and torch.equal(dT, ref.T.contiguous())
+    if ft:
+        assert torch.equal(dF, ft_layout(ref)) and torch.equal(dTF, ft_layout(ref.T.contiguous()))
+
+
+@pytest.mark.parametrize("R,C,splits", [(256, 1536, 8), (16, 64, 1), (48, 192, 3)])
+def test_reduce_slabs_cast(ext, R, C, splits):
+    """Slab sum (slab order 0, 1, 2, ...) -> fp32 + bf16 + bf16 transposed, on 16 x 64 tiles."""
+    src = rnd(splits, R, C, seed=splits)
+    dst = torch.empty(R, C, device=DEV)
+    bf = torch.empty(R, C, device=DEV, dtype=torch.bfloat16)
+    bT = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    ext.reduce_slabs_cast(dict(src=src.data_ptr(), splits=splits, R=R, C=C, dst=dst.data_ptr(),
+                               bf=bf.data_ptr(), bfT=bT.data_ptr()), S())
+    torch.cuda.synchronize()
+    ref = src[0].clone()
+    for k in range(1, splits):
+        ref += src[k]
+    assert torch.equal(dst, ref)
+    assert torch.equal(bf, ref.bfloat16()) and torch.equal(bT, ref.bfloat16().T.contiguous())
