@@ -1,0 +1,48 @@
+"""bench.py's output contract (one JSON line from rank 0, K timed steps, whole-job value, max over
+ranks), rehearsed on the CPU path: world 1 directly, world 2 under torch.distributed.run with gloo
+and 127.0.0.1 rendezvous -- the same launcher line the driver uses for N GPUs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lines(cmd, n):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout   # rank 0 only
+    r = json.loads(lines[0])
+    assert KEYS <= set(r), set(r) ^ KEYS
+    assert r["n_gpus"] == n and r["steps"] == 3 and r["warmup"] == 1
+    assert r["higher_is_better"] is True and r["scaling"] == "weak"
+    cfg = r["config"]
+    assert cfg["parallelism"] == f"dp{n}" and cfg["global_batch"] == 4 * n and cfg["seq_len"] == 16
+    # value is the whole-job aggregate: global tokens over the (max-over-ranks) timed span
+    tok = cfg["global_batch"] * cfg["seq_len"] * r["steps"]
+    assert abs(r["value"] - tok / (r["ms_per_step"] * r["steps"] / 1000)) / r["value"] < 0.01
+    return r
+
+
+def test_bench_contract_world1():
+    _lines([sys.executable, "bench.py", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], 1)
+
+
+def test_bench_contract_world2_gloo():
+    _lines([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+            "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], 2)
