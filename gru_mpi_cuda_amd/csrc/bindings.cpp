@@ -189,6 +189,9 @@ PYBIND11_MODULE(_C, m) {
     a.dgiT = GP(u16, d, "dgiT"); a.dgi = GP(u16, d, "dgi");
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
     a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0); a.algo = get<int>(d, "algo", 0);
+    a.sk_part = GP(float, d, "sk_part"); a.sk_part_floats = get<long>(d, "sk_part_floats", 0);
+    a.sk_cnt = GP(unsigned, d, "sk_cnt"); a.sk_cnt_words = get<long>(d, "sk_cnt_words", 0);
+    a.err = GP(unsigned, d, "err");
     if (a.Bp % 32 || a.H % 64) throw std::runtime_error("bwd_step: Bp % 32 and H % 64 required");
     gru_bwd_step(a, S(s));
     HIP_LAUNCH_CHECK();
@@ -197,6 +200,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
+  m.def("bwd_step_sk_splits", &gru_bwd_step_sk_splits);
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
     SeqFwdArgs a;

@@ -87,6 +87,14 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     if (seq_[l].bwd) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
   }
   size_t o_pP = seq_[0].fuse_p ? R((size_t)nrb * V * 3 * H * 4) : 0;
+  // per-step backward on the split-K LDS kernel: partial tiles + monotonic arrival counters
+  // (shared by all layers: their step kernels run one after another on one stream)
+  int sk = 0;
+  for (int l = 0; l < L; ++l)
+    if (!seq_[l].bwd) sk = gru_bwd_step_sk_splits(H, B);
+  sk_part_floats_ = sk ? (long)H * B * sk : 0;
+  sk_cnt_words_ = sk ? (long)(H / 128) * (B / 128) * 16 : 0;
+  size_t o_skp = sk ? R((size_t)sk_part_floats_ * 4) : 0, o_skc = sk ? R((size_t)sk_cnt_words_ * 4) : 0;
   (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
@@ -99,6 +107,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     seq_[l].dbih_part = seq_[l].bwd ? arena_.get<float>(o_pbi[l]) : nullptr;
   }
   dP_part_ = seq_[0].fuse_p ? arena_.get<float>(o_pP) : nullptr;
+  sk_part_ = sk ? arena_.get<float>(o_skp) : nullptr;
+  sk_cnt_ = sk ? arena_.get<unsigned>(o_skc) : nullptr;
 
   ids_ = arena_.get<int>(o_ids); labels_ = arena_.get<int>(o_lab); inv_count_ = arena_.get<float>(o_inv);
   Ptab_ = arena_.get<float>(o_P); loss_part_ = arena_.get<float>(o_lp); loss_ = arena_.get<float>(o_loss);
@@ -306,6 +316,8 @@ void Trainer::bwd_step(int l, int t, hipStream_t s) {
   a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = T * B; a.colT = t * B;
   a.dgi = y.dgi ? y.dgi + (size_t)t * B * 3 * H : nullptr;
   a.Bp = B; a.H = H; a.algo = step_algo_;
+  a.sk_part = sk_part_; a.sk_part_floats = sk_part_floats_; a.sk_cnt = sk_cnt_; a.sk_cnt_words = sk_cnt_words_;
+  a.err = err_;
   gru_bwd_step(a, s);
 }
 

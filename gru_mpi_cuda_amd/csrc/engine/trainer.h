@@ -160,6 +160,9 @@ class Trainer {
   std::vector<SeqPlan> seq_;
   int splits_ = 8;
   unsigned *cnt_ = nullptr, *err_ = nullptr;
+  float* sk_part_ = nullptr;         // split-K backward step kernel workspace (gru_step_lds.hip)
+  unsigned* sk_cnt_ = nullptr;
+  long sk_part_floats_ = 0, sk_cnt_words_ = 0;
   int xcd_local_ = 1;          // persistent kernels may use the L2-local hand-off (GK_XCD_LOCAL=0: never)
   u16* xbuf_ = nullptr;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;

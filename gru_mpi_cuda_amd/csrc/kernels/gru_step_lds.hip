@@ -600,6 +600,205 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_lds8_kernel(BwdStepArgs a
   }
 }
 
+// ==================================================================== backward, split-K
+// Large-batch backward step (B = 512, H = 2048: dh = dGh_{t+1} · W_hh is 512 x 2048 x 6144).  The
+// 64 x 64 kernel above streams (64 + 64) x 3H operands per workgroup: 1.5 MB at H = 2048, bound
+// by the per-CU L2 read rate.  Here a workgroup owns a 128 x 128 tile over a 1/S slice of K (half
+// the operand bytes per output), S workgroups per tile fill the chip, and they meet through
+// global memory: each writes its fp32 partial tile write-through (sc1), drains, bumps the tile's
+// arrival counter, and waits until all S have arrived; then workgroup s sums the S partials in
+// slab order 0, 1, ... (deterministic, whoever runs it) for its share of the tile's rows and runs
+// the gate-gradient epilogue there.  All workgroups are co-resident (the host checks occupancy),
+// other kernels' workgroups never wait, so every spin ends; it is bounded anyway (error word).
+// Counters are monotonic: launch k of a tile leaves them at k*S, so no reset node is needed.
+namespace {
+typedef unsigned int sk_u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t sk_rsrc_t;
+DEV sk_rsrc_t sk_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+constexpr int SKNS = 4;                       // LDS ring: 4 x 32 KiB
+constexpr unsigned kSkSpinLimit = 1u << 21;   // x s_sleep(1): far beyond any real wait
+}
+
+template <int S>
+__global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[SKNS][256 * 64];
+  const int H = a.H, H3 = 3 * a.H;
+  // block -> (tile, split): the S splits of a tile are 8 blocks apart (one XCD under the
+  // dispatcher's round-robin placement: a speed choice, the exchange does not depend on it)
+  const int bid = blockIdx.x;
+  const int split = (bid >> 3) % S, tile = (bid / (8 * S)) * 8 + (bid & 7);
+  const int ntu = H / 128;
+  const int j0 = (tile % ntu) * 128, b0 = (tile / ntu) * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;             // K loop: wave = 64 rows x 32 units
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+  constexpr int NQ = 4 / S;                       // epilogue quarters (32 rows) per workgroup
+  constexpr int PIECE = 8 * 4 * 2 * 64;           // f32x4 per partial tile: [wave][i][jn][lane]
+  const bool kloop = a.dgh_next != nullptr;
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const sk_rsrc_t rP = sk_rsrc(a.sk_part, (unsigned)(a.sk_part_floats * 4));
+  const size_t tile_base = (size_t)tile * S * PIECE;   // f32x4 units
+  if (kloop) {
+    const int nk = H3 / 64 / S, kt0 = split * nk;
+    // 32 DMA pieces (8 rows x 128 B) per k-tile, 4 per wave: image rows 0..127 = A (dGh_{t+1}),
+    // 128..255 = B (W_hh^T)
+    const u16* src[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = (4 * w + q) * 8 + srow, rr = r & 127;
+      const u16* base = r < 128 ? a.dgh_next + (size_t)(b0 + rr) * H3 : a.WhhT + (size_t)(j0 + rr) * H3;
+      src[q] = base + swz(rr, sslot) * 8 + (size_t)kt0 * 64;
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(4 * w + q) * 8 * 64]), 16, 0, 0);
+    };
+    ring_loop<SKNS, 4>(nk, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 128 * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[4], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ra = wm * 64 + i * 16 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int rb = wn * 32 + j * 16 + lr;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    });
+    // publish this split's partial tile (write-through), drain, arrive, wait for all S
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const size_t o = tile_base + (size_t)split * PIECE + ((w * 4 + i) * 2 + j) * 64 + lane;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, acc[i][j]), rP, (unsigned)(o * 16), 0, 16);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* cnt = a.sk_cnt + (size_t)tile * 16;
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (old / S + 1) * S;
+      unsigned spins = 0;
+      while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kSkSpinLimit) {
+          if (a.err) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: quarter sq = rows 32 sq .. 32 sq + 31 of the tile; thread piece P = w + 8 pp
+  // covers partial fragment (wave wm_q*4 + P/4, i = 2(sq&1) + (P/2)&1, jn = P&1) of every slab:
+  // 4 rows x 1 unit per piece, 8 items per thread.  Transposed staging [4 kinds][128 units][40].
+  u16* st = lds[0];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) {
+    const int sq = split + S * qq;
+    const int wmq = sq >> 1, ib = 2 * (sq & 1);
+    if (qq) __syncthreads();   // the previous quarter's transposed reads are done with st
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int P = w + 8 * pp;
+      const int wnp = P >> 2, ii = (P >> 1) & 1, jn = P & 1, i = ib + ii;
+      f32x4 ps = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (kloop) {
+#pragma unroll
+        for (int s2 = 0; s2 < S; ++s2) {
+          const size_t o = tile_base + (size_t)s2 * PIECE + (((wmq * 4 + wnp) * 4 + i) * 2 + jn) * 64 + lane;
+          ps += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rP, (unsigned)(o * 16), 0, 16));
+        }
+      }
+      const int ut = wnp * 32 + jn * 16 + lr;   // unit within the tile
+      const int j = j0 + ut;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rq = ii * 16 + lq * 4 + e;    // row within the quarter
+        const int b = b0 + 32 * sq + rq;
+        const size_t o = (size_t)b * H + j;
+        const float dh = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f) + ps[e];
+        const float r = a.r[o], z = a.z[o], n = a.n[o];
+        const float dn = dh * (1.f - z);
+        const float dz = dh * (a.hprev[o] - n);
+        const float dan = dn * (1.f - n * n);
+        const float dar = dan * a.ghn[o] * r * (1.f - r);
+        const float daz = dz * z * (1.f - z);
+        a.carry_out[o] = z * dh;
+        const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
+        const size_t og = (size_t)b * H3 + j;
+        a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
+        if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
+        st[(0 * 128 + ut) * 40 + rq] = br;
+        st[(1 * 128 + ut) * 40 + rq] = bz;
+        st[(2 * 128 + ut) * 40 + rq] = bn;
+        st[(3 * 128 + ut) * 40 + rq] = bi;
+      }
+    }
+    __syncthreads();
+    // 4 kinds x 128 units x 32 rows = 2048 pieces of 8 rows (16 B), 4 per thread
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int q = tid + p * 512;
+      const int kind = q >> 9, rem = q & 511, unit = rem >> 2, seg = rem & 3;
+      const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 128 + unit) * 40 + seg * 8]);
+      const int g = kind < 3 ? kind : 2;
+      const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + 32 * sq + seg * 8;
+      if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
+      if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+    }
+  }
+}
+
+static int sk_capacity(const void* kernel) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 512, 0) != hipSuccess) return 0;
+  return per * cus;
+}
+
+int gru_bwd_step_sk_splits(int H, int Bp) {
+  static const bool on = [] {
+    const char* e = std::getenv("GK_BWD_SK");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || H % 128 || Bp % 128) return 0;
+  const int tiles = (H / 128) * (Bp / 128);
+  if (tiles % 8) return 0;
+  static const int cap4 = sk_capacity((const void*)gru_bwd_step_sk_kernel<4>);
+  static const int cap2 = sk_capacity((const void*)gru_bwd_step_sk_kernel<2>);
+  // only where the 64 x 64 kernel's per-workgroup operand stream is the bound: H = 2048 (K = 6144)
+  // 40.3 -> 35.4 us per step; at H = 1024 (K = 3072) the exchange costs more than it saves
+  // (9.50 -> 9.62 ms per h1024_l2 step at B = 1024), profiles/r1_bwd_step_sk_ab.jsonl
+  if (H < 2048) return 0;
+  if ((3 * H / 64) % 4 == 0 && tiles * 4 <= cap4 && tiles * 4 >= 192) return 4;
+  if ((3 * H / 64) % 2 == 0 && tiles * 2 <= cap2 && tiles * 2 >= 192) return 2;
+  return 0;
+}
+
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
@@ -627,6 +826,14 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   }
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
+  if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
+    const int tiles = (a.H / 128) * (a.Bp / 128);
+    if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
+      if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, a);
+      return;
+    }
+  }
   static const bool eight = [] {
     const char* e = std::getenv("GK_BWD_LDS8");
     return !(e && e[0] == '0');

@@ -53,8 +53,18 @@ struct BwdStepArgs {
   u16* dgi = nullptr;              // [Bp][3H] row-major dGi (nullable; needed below layer 0 only)
   int ldT = 0, colT = 0, Bp = 0, H = 0;
   int algo = 0;                    // as FwdStepArgs::algo
+  // split-K LDS kernel (gru_step_lds.hip): fp32 partial tiles, per-tile arrival counters (64-B
+  // lines, zeroed once, monotonic across launches) and the error word of its bounded spin
+  float* sk_part = nullptr;
+  long sk_part_floats = 0;
+  unsigned* sk_cnt = nullptr;
+  long sk_cnt_words = 0;
+  unsigned* err = nullptr;
 };
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
+// split-K count the backward LDS step kernel would use for (H, Bp): 0 = the 64 x 64 kernel;
+// workspace: H * Bp * splits fp32 partials, (H/128)(Bp/128) * 16 counter words
+int gru_bwd_step_sk_splits(int H, int Bp);
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
 bool gru_step_lds_ok(int H, int Bp);
 // which per-step kernel gru_fwd_step/gru_bwd_step pick for (algo, H, Bp) without fused input

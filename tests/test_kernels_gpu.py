@@ -128,8 +128,12 @@ def test_fwd_step(ext, mode, H, Bp, algo):
 
 
 @pytest.mark.parametrize("first", [False, True])
-@pytest.mark.parametrize("H,Bp,algo", [(128, 64, 1), (1024, 128, 1), (1024, 128, 2), (1024, 256, 2), (512, 128, 2)])
-def test_bwd_step(ext, first, H, Bp, algo):
+@pytest.mark.parametrize("H,Bp,algo,sk", [(128, 64, 1, 0), (1024, 128, 1, 0), (1024, 128, 2, 0), (1024, 256, 2, 0),
+                                          (512, 128, 2, 0), (2048, 512, 2, 0), (2048, 512, 2, 1),
+                                          (2048, 1024, 2, 1)])
+def test_bwd_step(ext, first, H, Bp, algo, sk):
+    """sk = 1: the split-K LDS kernel (128 x 128 tiles, S workgroups per tile meeting through
+    fp32 partials and monotonic arrival counters), launched three times on one workspace."""
     T = 4
     t = 1
     dgn = bf(rnd(Bp, 3 * H, scale=0.1, seed=1))
@@ -149,8 +153,27 @@ def test_bwd_step(ext, first, H, Bp, algo):
              dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), dgi=dgi.data_ptr(), ldT=T * Bp, colT=t * Bp, Bp=Bp, H=H, algo=algo)
     if not first:
         d.update(dgh_next=dgn.data_ptr(), carry_in=carry.data_ptr())
-    ext.bwd_step(d, S())
-    torch.cuda.synchronize()
+    launches = 1
+    if sk:
+        S_ = ext.bwd_step_sk_splits(H, Bp)
+        assert S_ in (2, 4), S_
+        part = torch.empty(H * Bp * S_, device=DEV)
+        cnt = torch.zeros((H // 128) * (Bp // 128) * 16, device=DEV, dtype=torch.int32)
+        err = torch.zeros(1, device=DEV, dtype=torch.int32)
+        d.update(sk_part=part.data_ptr(), sk_part_floats=part.numel(), sk_cnt=cnt.data_ptr(),
+                 sk_cnt_words=cnt.numel(), err=err.data_ptr())
+        launches = 3
+    outs = []
+    for _ in range(launches):
+        ext.bwd_step(d, S())
+        torch.cuda.synchronize()
+        outs.append((cout.clone(), dgh.clone()))
+    if sk:
+        assert int(err.item()) == 0
+        if not first:
+            assert int(cnt[0].item()) == 3 * S_   # monotonic: every launch adds S per tile
+        for c2, g2 in outs[1:]:
+            assert torch.equal(c2, outs[0][0]) and torch.equal(g2, outs[0][1])   # deterministic
     dh = dy.clone()
     if not first:
         dh += dgn.float() @ WhhT.float().T + carry
