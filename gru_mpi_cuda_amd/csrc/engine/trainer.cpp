@@ -653,7 +653,8 @@ float Trainer::read_loss() {
   float v = 0.f;
   if (read_error())
     throw std::runtime_error("[rank " + std::to_string(global_rank()) +
-                             "] persistent sequence kernel hit its spin limit (workgroups not co-resident?)");
+                             "] a cross-workgroup wait hit its spin limit (persistent sequence kernel: error bit 1, "
+                             "split-K backward step kernel: bit 2; workgroups not co-resident?)");
   HIP_CHECK(hipMemcpy(&v, loss_, 4, hipMemcpyDeviceToHost));
   return v;
 }

@@ -67,19 +67,22 @@ def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
         assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
 
 
-@pytest.mark.parametrize("layers,B", [(1, 128), (2, 256)])
-def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B):
-    """Per-step schedule on the LDS-staged big-tile step kernels (the large-H path)."""
+@pytest.mark.parametrize("layers,B,H", [(1, 128, 1024), (2, 256, 1024), (1, 512, 2048)])
+def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H):
+    """Per-step schedule on the LDS-staged big-tile step kernels (the large-H path; H = 2048 with
+    B = 512 takes the split-K backward step kernel)."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     monkeypatch.setenv("GK_PERSIST", "0")
     monkeypatch.setenv("GK_STEP_ALGO", "2")
-    cfg = GRUConfig(vocab=256, embed=128, hidden=1024, layers=layers, batch=B, seq=6, time_chunks=2, seed=5)
+    cfg = GRUConfig(vocab=256, embed=128, hidden=H, layers=layers, batch=B, seq=6 if H < 2048 else 4,
+                    time_chunks=2, seed=5)
     params = init_params(cfg)
     x, y = NameStream(B, cfg.seq, seed=4).next()
     tr = HipTrainer(cfg, params=params)
     plan = tr.t.plan()
     assert "step=lds" in plan, plan
     tr.forward_backward(x, y)
+    assert tr.t.read_error() == 0
     g = tr.grad_dict()
     p64 = {k: v.double() for k, v in params.items()}
     ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
