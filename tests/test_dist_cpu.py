@@ -84,7 +84,7 @@ def _train_worker(rank, world, port, outdir, steps):
     gdist.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_training_equals_single_rank(tmp_path, world):
     ctx = mp.get_context("spawn")
     for w in (1, world):
