@@ -26,7 +26,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 KERNELS = ["kernels/gru_step.hip", "kernels/gru_seq.hip", "kernels/fc.hip", "kernels/gemm.hip",
            "kernels/gemm_lds.hip", "kernels/gemm_small.hip", "kernels/gru_step_lds.hip", "kernels/misc.hip"]
-ENGINE = ["engine/trainer.cpp", "engine/trainer_seq.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp",
+ENGINE = ["runtime/blaslt.cpp", "engine/trainer.cpp", "engine/trainer_seq.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp",
           "comm/watchdog.cpp", "data/name_loader.cpp"]
 PYBIND = ["bindings.cpp"]
 CAPI = ["capi/namegen_api.cpp", "capi/ckpt_reader.cpp"]
@@ -115,15 +115,15 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     with ThreadPoolExecutor(jobs) as ex:
         objs = dict(zip(srcs, ex.map(lambda s: _compile(s, force, hdr), srcs)))
     core = [objs[s] for s in KERNELS + ENGINE]
-    _link(core + [objs[s] for s in PYBIND], ext_path(), libs=["-lrccl", "-lrocprofiler-sdk-roctx"])
+    _link(core + [objs[s] for s in PYBIND], ext_path(), libs=["-lrccl", "-lhipblaslt", "-lrocprofiler-sdk-roctx"])
     capi_objs = [objs[s] for s in CAPI if s in objs]
     if capi_objs:
         lib = os.path.join(HERE, "bin", "libnamegen.so")
-        _link(core + capi_objs, lib, libs=["-lrccl", "-lrocprofiler-sdk-roctx"])
+        _link(core + capi_objs, lib, libs=["-lrccl", "-lhipblaslt", "-lrocprofiler-sdk-roctx"])
         drv = [objs[s] for s in DRIVER if s in objs]
         if drv:
             _link(drv, os.path.join(HERE, "bin", "namegen"), shared=False,
-                  libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl", "-lrocprofiler-sdk-roctx",
+                  libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl", "-lhipblaslt", "-lrocprofiler-sdk-roctx",
                         f"-Wl,-rpath,{os.path.join(HERE, 'bin')}", "-Wl,-rpath,$ORIGIN"])
     build_host_tools(force)
     if verbose:

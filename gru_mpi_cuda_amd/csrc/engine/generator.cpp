@@ -1,5 +1,6 @@
 #include "generator.h"
 #include "../runtime/trace.h"
+#include "../runtime/blaslt.h"
 
 #include <algorithm>
 
@@ -11,6 +12,7 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
     : d_(d), params_(params), off_(offsets) {
   if (d_.V % 64 || d_.E % 64 || d_.H % 64)
     throw std::runtime_error("HIP generator needs vocab, embed and hidden to be multiples of 64");
+  blaslt_init();   // before any graph capture (large prep GEMMs may go to the library)
   Bmax_ = rup(std::max(32, d_.max_batch), 64);
   const int V = d_.V, E = d_.E, H = d_.H, L = d_.L, B = Bmax_;
   std::vector<size_t> ohf, ohb, oWhh, oWih;

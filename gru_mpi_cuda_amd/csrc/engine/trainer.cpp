@@ -1,5 +1,6 @@
 #include "trainer.h"
 #include "../runtime/trace.h"
+#include "../runtime/blaslt.h"
 
 #include <cstring>
 #include <algorithm>
@@ -13,6 +14,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     : d_(d), o_(o), params_(params), grads_(grads), m_(m), v_(v), nflat_(nflat), off_(offsets) {
   if (d_.V % 64 || d_.E % 64 || d_.H % 64)
     throw std::runtime_error("HIP engine needs vocab, embed and hidden to be multiples of 64");
+  blaslt_init();   // library handle + workspace now, never inside the step-graph capture
   Bp_ = round_up(std::max(d_.B, 1), 64);
   C_ = std::max(1, d_.chunks);
   while (C_ > 1 && d_.T % C_) --C_;

@@ -18,6 +18,17 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
   // split K only as deep as it takes to give the chip ~256 workgroups: every extra split costs a
   // full M x N fp32 slab written and read again (8 slabs of dW_hh at H=1024 = 100 MB).  With no
   // split the GEMM writes the gradient (and the bias row sums) directly.
+  {
+    // large products (H >= 2048 over B*T tokens): one unsplit hipBLASLt GEMM straight into the
+    // gradient (+ a row-sum kernel for the bias) -- no slabs to write and reduce
+    GemmArgs w;
+    w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
+    w.M = M; w.N = N; w.K = K;
+    if (gemm_library_wanted(w) && gemm_library_ok(w)) {
+      gemm_nt(w, s);
+      return;
+    }
+  }
   const int tiles = std::max(1, (M / 128) * (N / 128));
   auto can_split = [&](int s2) { return s2 <= splits_ && K % s2 == 0 && (K / s2) % 128 == 0; };
   int sp = 1;

@@ -15,6 +15,7 @@
 #include <stdexcept>
 #include "kernels.h"
 #include "mma_tile.h"
+#include "../runtime/blaslt.h"
 
 namespace gk {
 
@@ -116,7 +117,54 @@ __global__ void __launch_bounds__(256) gemm_nt_kernel(GemmArgs a, int ntn, int n
   }
 }
 
+// Row sums of a bf16 [M][K] matrix (the bias gradient that rides along a library GEMM): one
+// 256-thread workgroup per row, 16-B loads four deep, fixed-order wave + LDS reduction
+// (deterministic).  Needs K % 8 == 0, lda % 8 == 0 and a 16-B aligned A.
+__global__ void __launch_bounds__(256) rowsum_bf16_kernel(const u16* __restrict__ A, int lda, int K,
+                                                          float* __restrict__ out) {
+  const uint4* row = reinterpret_cast<const uint4*>(A + (size_t)blockIdx.x * lda);
+  const int n8 = K / 8;
+  float acc = 0.f;
+  int i = threadIdx.x;
+  auto add8 = [&](uint4 q) {
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc += __uint_as_float(w[e] << 16) + __uint_as_float(w[e] & 0xffff0000u);
+  };
+  for (; i + 3 * 256 < n8; i += 4 * 256) {
+    const uint4 q0 = row[i], q1 = row[i + 256], q2 = row[i + 512], q3 = row[i + 768];
+    add8(q0); add8(q1); add8(q2); add8(q3);
+  }
+  for (; i < n8; i += 256) add8(row[i]);
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+bool gemm_library_ok(const GemmArgs& a) {
+  if (a.onehot_ids || a.bias || a.splits != 1 || !a.A || !a.B || !a.C) return false;
+  if (a.rowsumA && (a.K % 8 || a.lda % 8 || reinterpret_cast<uintptr_t>(a.A) % 16)) return false;
+  return a.M > 0 && a.N > 0 && a.K > 0;
+}
+
+bool gemm_library_wanted(const GemmArgs& a) {
+  return a.algo == 4 ||
+         (a.algo == 0 && blaslt_enabled() && 2.0 * a.M * a.N * (double)a.K >= blaslt_min_gflop() * 1e9);
+}
+
+static bool gemm_library(const GemmArgs& a, hipStream_t s) {
+  if (!gemm_library_ok(a)) return false;
+  if (!blaslt_gemm_nt(a.A, a.lda, a.B, a.ldb, a.C, a.ldc, a.M, a.N, a.K, a.accumulate != 0, s)) return false;
+  if (a.rowsumA) hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.lda, a.K, a.rowsumA);
+  return true;
+}
+
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
+  // large plain products: hipBLASLt (bf16 in, fp32 out), when it has an algorithm for the shape
+  if (gemm_library_wanted(a) && gemm_library(a, s)) return;
+  if (a.algo == 4) throw std::runtime_error("gemm_nt: library GEMM requested but not available for this shape");
   if (a.algo == 3) {
     if (!gemm_small_kblocks(a)) throw_gemm_shape();
     gemm_small(a, s);

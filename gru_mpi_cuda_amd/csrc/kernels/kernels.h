@@ -186,8 +186,11 @@ struct GemmArgs {
   int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
   int accumulate = 0;              // C += result instead of C = result
   int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
-                                   // 3 one-shot 64x64 (gemm_small)
+                                   // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel)
 };
+// algo 0 sends plain (no one-hot, no bias, unsplit) products of >= GK_BLASLT_MIN_GFLOP to hipBLASLt
+bool gemm_library_ok(const GemmArgs& a);
+bool gemm_library_wanted(const GemmArgs& a);
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
 // several independent LDS-GEMM problems in ONE launch (fills the chip with small products);

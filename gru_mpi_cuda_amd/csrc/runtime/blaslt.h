@@ -1,0 +1,24 @@
+// hipBLASLt for the large *plain* GEMMs (no one-hot A operand, no fused bias): the weight-gradient
+// products over B*T tokens at H >= 2048 and the FC backward dH.  Measured on MI355X
+// (scripts/probe_blaslt.cpp, profiles/r1_blaslt_probe.jsonl): 1.38 PFLOP/s on dW_hh at H = 2048
+// against 0.89 for the engine's LDS kernel.  Everything fused (persistent recurrence, GRU
+// epilogues, one-hot dP, FC + softmax-xent) stays on the hand-written kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gk {
+
+using u16 = unsigned short;
+
+// Create the handle and the workspace (call before any stream capture; idempotent).
+void blaslt_init();
+// Smallest GEMM (2*M*N*K, in GFLOP) routed to the library under algo 0; env GK_BLASLT_MIN_GFLOP,
+// default 60; GK_BLASLT=0 disables the library entirely.
+double blaslt_min_gflop();
+bool blaslt_enabled();
+// C[M][N] (ldc) = A[M][K] (lda) . B[N][K]^T (ldb), fp32 out, fp32 accumulation (C += with
+// accumulate).  Returns false (and launches nothing) when the library has no algorithm for it.
+bool blaslt_gemm_nt(const u16* A, int lda, const u16* B, int ldb, float* C, int ldc, int M, int N, int K,
+                    bool accumulate, hipStream_t s);
+
+}  // namespace gk

@@ -67,13 +67,17 @@ def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
         assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
 
 
+@pytest.mark.parametrize("blaslt", ["default", "all"])
 @pytest.mark.parametrize("layers,B,H", [(1, 128, 1024), (2, 256, 1024), (1, 512, 2048)])
-def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H):
+def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H, blaslt):
     """Per-step schedule on the LDS-staged big-tile step kernels (the large-H path; H = 2048 with
-    B = 512 takes the split-K backward step kernel)."""
+    B = 512 takes the split-K backward step kernel).  blaslt=all: every plain GEMM the engine may
+    hand to hipBLASLt goes there (weight gradients with the row-sum bias kernel, FC dH)."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     monkeypatch.setenv("GK_PERSIST", "0")
     monkeypatch.setenv("GK_STEP_ALGO", "2")
+    if blaslt == "all":
+        monkeypatch.setenv("GK_BLASLT_MIN_GFLOP", "0")
     cfg = GRUConfig(vocab=256, embed=128, hidden=H, layers=layers, batch=B, seq=6 if H < 2048 else 4,
                     time_chunks=2, seed=5)
     params = init_params(cfg)

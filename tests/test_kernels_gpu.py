@@ -52,6 +52,26 @@ def test_gemm_nt(ext, algo, M, N, K, splits):
     torch.testing.assert_close(rs.sum(0), A.float().sum(1), atol=1e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K,lda_pad,accumulate", [(256, 512, 1024, 0, 0), (6144 // 4, 512, 4096, 64, 0),
+                                                      (512, 384, 2048, 0, 1), (1024, 2048, 256, 0, 0)])
+def test_gemm_library(ext, M, N, K, lda_pad, accumulate):
+    """algo 4: hipBLASLt (bf16 in, fp32 out, TN) + the bf16 row-sum kernel for the bias gradient,
+    against fp32 torch; lda_pad exercises a strided A view (the engine's HT + B operand)."""
+    lda = K + lda_pad
+    A_full = bf(rnd(M, lda, seed=11))
+    A = A_full[:, lda_pad:]
+    B = bf(rnd(N, K, seed=12))
+    C0 = rnd(M, N, seed=13)
+    C = C0.clone() if accumulate else torch.full((M, N), float("nan"), device=DEV)
+    rs = torch.full((M,), float("nan"), device=DEV)
+    ext.gemm_nt(dict(A=A.data_ptr(), lda=lda, B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=M, N=N, K=K,
+                     rowsumA=rs.data_ptr(), accumulate=accumulate, algo=4), S())
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().T + (C0 if accumulate else 0)
+    torch.testing.assert_close(C, ref, atol=2e-3 * K ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(rs, A.float().sum(1), atol=1e-3 * K ** 0.5, rtol=1e-4)
+
+
 @pytest.mark.parametrize("N,K,splits,algo", [(192, 512, 1, 1), (384, 1024, 1, 2), (256, 2048, 4, 2)])
 def test_gemm_onehot(ext, N, K, splits, algo):
     """algo 2: the one-hot A tile is synthesised into the swizzled LDS image of the LDS GEMM."""
