@@ -150,8 +150,14 @@ bool gemm_library_ok(const GemmArgs& a) {
 }
 
 bool gemm_library_wanted(const GemmArgs& a) {
-  return a.algo == 4 ||
-         (a.algo == 0 && blaslt_enabled() && 2.0 * a.M * a.N * (double)a.K >= blaslt_min_gflop() * 1e9);
+  if (a.algo == 4) return true;
+  if (a.algo != 0 || !blaslt_enabled() || 2.0 * a.M * a.N * (double)a.K < blaslt_min_gflop() * 1e9) return false;
+  // with the bias row sum the library pays a second pass over A (5.5 TB/s): worth it only where
+  // the LDS kernel's split-K slabs get big -- dW_hh at H = 2048 (6144 x 2048: 1.90 -> 1.25 + 0.15 ms);
+  // at H = 1024 (3072 x 1024, K = 65536) the two GEMMs tie and the row sum is pure loss
+  // (profiles/r1_blaslt_ab.jsonl).  GK_BLASLT_MIN_GFLOP=0 lifts this too (tests).
+  if (a.rowsumA && (double)a.M * a.N < 8e6 && blaslt_min_gflop() > 0) return false;
+  return true;
 }
 
 static bool gemm_library(const GemmArgs& a, hipStream_t s) {
