@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
 #include <vector>
 
 #define CK(x) do { auto e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
@@ -89,14 +90,18 @@ static double run(hipblasLtHandle_t h, int M, int N, int K, bool rowsum, int* na
   return best;
 }
 
-int main() {
+int main(int argc, char** argv) {
   hipblasLtHandle_t h;
   if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) { printf("create failed\n"); return 1; }
   struct S { const char* name; int M, N, K; } shapes[] = {
       {"h2048.dW_hh", 6144, 2048, 65536}, {"h2048.dW_ih", 6144, 512, 65536}, {"h2048.dH", 65536, 2048, 256},
       {"h1024.dWhh", 3072, 1024, 8192}, {"h1024.Gi", 8192, 3072, 1024}, {"sq4096", 4096, 4096, 4096}};
-  for (auto& sh : shapes)
-    for (int rs = 0; rs < 2; ++rs) {
+  // optional: M N K triples on the command line (no row-sum variant)
+  std::vector<S> custom;
+  for (int i = 1; i + 2 < argc; i += 3) custom.push_back({"custom", atoi(argv[i]), atoi(argv[i + 1]), atoi(argv[i + 2])});
+  std::vector<S> list = custom.empty() ? std::vector<S>(std::begin(shapes), std::end(shapes)) : custom;
+  for (auto& sh : list)
+    for (int rs = 0; rs < (custom.empty() ? 2 : 1); ++rs) {
       int na = 0; double err = 0, rserr = 0;
       const double us = run(h, sh.M, sh.N, sh.K, rs, &na, &err, &rserr);
       const double tf = us > 0 ? 2.0 * sh.M * sh.N * (double)sh.K / us / 1e6 : 0;
