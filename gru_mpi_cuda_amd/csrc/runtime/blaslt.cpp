@@ -14,6 +14,9 @@ namespace gk {
 namespace {
 
 constexpr size_t kWorkspace = 64ull << 20;
+// one workspace per stream that calls the library: the trainer's overlapped schedule records
+// library GEMMs on two streams that run concurrently inside one graph
+constexpr int kSlots = 4;
 
 struct Plan {
   bool ok = false;
@@ -26,7 +29,10 @@ struct State {
   std::mutex mu;
   int device = -1;
   hipblasLtHandle_t h = nullptr;
-  void* ws = nullptr;
+  void* ws[kSlots] = {};
+  hipStream_t ws_stream[kSlots] = {};
+  unsigned long ws_used[kSlots] = {};   // 0 = free, else last-use tick
+  unsigned long tick = 0;
   std::map<std::tuple<int, int, int, int, int, int, int>, Plan> plans;
 };
 
@@ -46,7 +52,8 @@ void init_locked(State& s) {
   if (s.h && s.device == dev) return;
   if (s.h) throw std::runtime_error("blaslt: one device per process (got a second device)");
   check(hipblasLtCreate(&s.h), "create");
-  if (hipMalloc(&s.ws, kWorkspace) != hipSuccess) throw std::runtime_error("blaslt: workspace hipMalloc failed");
+  for (int i = 0; i < kSlots; ++i)
+    if (hipMalloc(&s.ws[i], kWorkspace) != hipSuccess) throw std::runtime_error("blaslt: workspace hipMalloc failed");
   s.device = dev;
 }
 
@@ -75,6 +82,20 @@ Plan make_plan(State& s, int M, int N, int K, int lda, int ldb, int ldc) {
     p.algo = res[0].algo;
   }
   return p;
+}
+
+void* workspace_for(State& s, hipStream_t stream) {
+  // least-recently-used slot when a new stream shows up (engines come and go in one process;
+  // at most two of their streams run library GEMMs at the same time)
+  ++s.tick;
+  int lru = 0;
+  for (int i = 0; i < kSlots; ++i) {
+    if (s.ws_used[i] && s.ws_stream[i] == stream) { s.ws_used[i] = s.tick; return s.ws[i]; }
+    if (s.ws_used[i] < s.ws_used[lru]) lru = i;
+  }
+  s.ws_stream[lru] = stream;
+  s.ws_used[lru] = s.tick;
+  return s.ws[lru];
 }
 
 }  // namespace
@@ -108,7 +129,7 @@ bool blaslt_gemm_nt(const u16* A, int lda, const u16* B, int ldb, float* C, int 
   const Plan& p = it->second;
   if (!p.ok) return false;
   const float alpha = 1.f, beta = accumulate ? 1.f : 0.f;
-  check(hipblasLtMatmul(s.h, p.op, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo, s.ws, kWorkspace,
+  check(hipblasLtMatmul(s.h, p.op, &alpha, B, p.la, A, p.lb, &beta, C, p.lc, C, p.lc, &p.algo, workspace_for(s, stream), kWorkspace,
                         stream),
         "matmul");
   return true;

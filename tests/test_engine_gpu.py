@@ -303,3 +303,11 @@ def test_trainer_odd_shapes_match_cpu(layers, V, E, H, B, T):
         torch.cuda.synchronize()
         again = to_flat(tr.icfg, tr._pad(tr.state_dict()))
         assert torch.equal(again, tr.params.cpu())
+
+
+@pytest.mark.parametrize("sched", ["overlap", "perstep", "persistent"])
+def test_trainer_grads_library_gemms(monkeypatch, sched):
+    """Every eligible GEMM on hipBLASLt (threshold 0), incl. the overlapped schedule whose two
+    streams run library GEMMs concurrently (one workspace per stream)."""
+    monkeypatch.setenv("GK_BLASLT_MIN_GFLOP", "0")
+    test_trainer_grads_match_cpu(monkeypatch, sched, 2, 128, 128, 4, 96)
