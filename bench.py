@@ -7,6 +7,12 @@ with fp32 master weights, synthetic name sequences, random-init weights.
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+Without a launcher (no WORLD_SIZE in the environment) and --gpus N > 1, this process starts the N
+rank processes itself (parallel/launch.py, one per GPU, 127.0.0.1 rendezvous) before anything
+touches the GPU, and only relays their exit code; rank 0's JSON line is the output.  Under a
+launcher, WORLD_SIZE must equal --gpus, and the RCCL communicator's own rank count
+(ncclCommCount) is checked against it and reported as ``rccl_ranks``.
+
 Rank 0 prints ONE JSON line; `value` is the whole-job aggregate (tokens/s over all ranks),
 timed over exactly K steps bracketed by barrier + device synchronize, max over ranks.
 """
@@ -41,7 +47,18 @@ def main() -> int:
                     help="at 1 GPU, still record the gradient collectives (1-rank RCCL communicator) "
                          "to time the data-parallel step structure")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: become the launcher (before any GPU call -- the parent never touches it)
+        from gru_mpi_cuda_amd.parallel.launch import run
+        return run(args.gpus, [os.path.abspath(__file__), *sys.argv[1:]], timeout=args.launch_timeout)
+    if env_world is not None and int(env_world) != args.gpus and "--gpus" in " ".join(sys.argv):
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -51,6 +68,9 @@ def main() -> int:
 
     ctx = gdist.init(use_gpu=torch.cuda.is_available())
     world = ctx.world
+    if ctx.device.type == "cuda" and world > torch.cuda.device_count():
+        print(f"bench.py: {world} ranks but only {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+        return 2
     base = preset(args.preset)
     per_gpu = args.per_gpu_batch or base.batch
     cfg = base.replace(batch=per_gpu * world)
@@ -72,6 +92,9 @@ def main() -> int:
             from gru_mpi_cuda_amd.ops import load_ext
             C = load_ext()
             comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1)
+        if comm is not None and comm.count() != world:
+            print(f"bench.py: RCCL communicator has {comm.count()} ranks, expected {world}", file=sys.stderr)
+            return 2
         tr = make_trainer(cfg, ctx, comm=comm)
         if args.no_graph and hasattr(tr, "t"):
             tr.t.set_use_graph(False)
@@ -79,6 +102,7 @@ def main() -> int:
         final_loss = lambda: tr.loss()                  # noqa: E731
         plan = tr.t.plan() if hasattr(tr, "t") else "cpu"
     else:
+        comm = None
         step, final_loss = _torch_gru_step(cfg, ctx, pool)
         plan = "torch.nn.GRU (MIOpen)"
 
@@ -118,6 +142,8 @@ def main() -> int:
                        "overlap": cfg.overlap, "plan": plan,
                        "collectives": (len(tr.t.allreduce_log()) if args.impl == "hip" and comm is not None
                                        and hasattr(tr, "t") else 0)},
+            "rccl_ranks": comm.count() if comm is not None else (world if ctx.backend != "none" else 1),
+            "comm_backend": "rccl" if comm is not None else ctx.backend,
             "final_loss": round(float(loss), 4),
         }
         print(json.dumps(out), flush=True)

@@ -27,7 +27,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 KERNELS = ["kernels/gru_step.hip", "kernels/gru_seq.hip", "kernels/fc.hip", "kernels/gemm.hip",
            "kernels/gemm_lds.hip", "kernels/gemm_small.hip", "kernels/gru_step_lds.hip", "kernels/misc.hip"]
 ENGINE = ["runtime/blaslt.cpp", "engine/trainer.cpp", "engine/trainer_seq.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp",
-          "comm/watchdog.cpp", "data/name_loader.cpp"]
+          "comm/watchdog.cpp", "comm/bootstrap.cpp", "data/name_loader.cpp"]
 PYBIND = ["bindings.cpp"]
 CAPI = ["capi/namegen_api.cpp", "capi/ckpt_reader.cpp"]
 DRIVER = ["capi/namegen_main.cpp"]

@@ -18,6 +18,7 @@ import json
 import os
 import sys
 import time
+from typing import Optional
 
 import numpy as np
 
@@ -59,13 +60,47 @@ def save_checkpoint(tr, path: str, fmt: str = "gen") -> None:
               opt_state={"m": m, "v": v, "step": torch.tensor([step], dtype=torch.int64)})
 
 
-def load_checkpoint(tr, path: str) -> int:
-    """Restore weights (+ optimiser state when present) into a trainer; returns the step."""
+def _read_checkpoint(tr, path: Optional[str]):
+    """(params dict, opt-state dict or None).  Data-parallel: only rank 0 opens the file; the
+    flat weights, Adam moments and step go to the other ranks by broadcast (SURVEY §5.4 -- the
+    reference has every rank read the blob, namegensf.cu:368-372, §2.7 item 4), so ranks > 0
+    need neither the file nor a shared filesystem."""
     import torch
-    from .models.params import from_flat, to_flat
+    from .models.params import flat_layout, from_flat, to_flat
     from .utils import ckpt
-    _, params = ckpt.load(path, tr.cfg)
-    st = ckpt.load_opt_state(path)
+    ctx = getattr(tr, "ctx", None)
+    if ctx is None or ctx.world <= 1:
+        _, params = ckpt.load(path, tr.cfg)
+        return params, ckpt.load_opt_state(path)
+    import torch.distributed as dist
+    dev = ctx.device if ctx.backend == "nccl" else torch.device("cpu")
+    n = flat_layout(tr.cfg).total
+    hdr = torch.zeros(2, dtype=torch.int64, device=dev)   # [has optimiser state, step]
+    flat = torch.zeros(3 * n, dtype=torch.float32, device=dev)
+    if ctx.is_main:
+        _, params = ckpt.load(path, tr.cfg)
+        st = ckpt.load_opt_state(path)
+        flat[:n] = to_flat(tr.cfg, params).to(dev)
+        if st is not None:
+            flat[n:2 * n] = st["m"].float().to(dev)
+            flat[2 * n:] = st["v"].float().to(dev)
+            hdr[0], hdr[1] = 1, int(st["step"][0])
+    dist.broadcast(hdr, 0)
+    dist.broadcast(flat, 0)
+    flat, hdr = flat.cpu(), hdr.cpu()
+    params = from_flat(tr.cfg, flat[:n])
+    st = None
+    if int(hdr[0]):
+        st = {"m": flat[n:2 * n].clone(), "v": flat[2 * n:].clone(),
+              "step": torch.tensor([int(hdr[1])], dtype=torch.int64)}
+    return params, st
+
+
+def load_checkpoint(tr, path: Optional[str]) -> int:
+    """Restore weights (+ optimiser state when present) into a trainer; returns the step.
+    ``path`` is only read on rank 0 (may be None elsewhere)."""
+    from .models.params import from_flat
+    params, st = _read_checkpoint(tr, path)
     if hasattr(tr, "t"):
         tr.load_state(params)
         if st is not None:

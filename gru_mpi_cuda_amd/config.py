@@ -44,7 +44,10 @@ class GRUConfig:
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
     overlap: bool = False       # True: chunked side-stream schedule; False: single stream built on
                                 # the persistent sequence kernels (faster on MI355X, profiles/)
-    watchdog_ms: int = 0        # >0: abort the RCCL communicator when a step is not done in time
+    watchdog_ms: int = -1       # host watchdog thread per trainer: >0 aborts the RCCL
+                                # communicator when a step is not done in time; 0 only watches the
+                                # communicator's async errors and the step error word; -1 = auto
+                                # (120 s deadline when data-parallel, 0 at one rank); < -1 = off
 
     def __post_init__(self):
         if self.layers < 1:

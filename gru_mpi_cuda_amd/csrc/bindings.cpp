@@ -9,6 +9,7 @@
 #include "engine/trainer.h"
 #include "engine/generator.h"
 #include "comm/rccl_comm.h"
+#include "comm/bootstrap.h"
 #include "data/name_loader.h"
 
 namespace py = pybind11;
@@ -111,6 +112,7 @@ PYBIND11_MODULE(_C, m) {
       .def("uses_persistent", &Trainer::uses_persistent)
       .def("read_error", &Trainer::read_error)
       .def("enable_watchdog", &Trainer::enable_watchdog)
+      .def("inject_error", &Trainer::inject_error)
       .def("watchdog_status", &Trainer::watchdog_status)
       .def("watchdog_message", &Trainer::watchdog_message)
       .def("buffer", &Trainer::buffer);
@@ -234,7 +236,10 @@ PYBIND11_MODULE(_C, m) {
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
     a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
-    if (!gru_bwd_seq_supported(a.H, a.Bp, a.dWhh_part != nullptr, a.dP_part != nullptr))
+    // "unchecked": skip the co-residency query and go straight to the dispatch table (tests its
+    // unmatched-variant error without launching anything)
+    if (!get<int>(d, "unchecked", 0) &&
+        !gru_bwd_seq_supported(a.H, a.Bp, a.dWhh_part != nullptr, a.dP_part != nullptr))
       throw std::runtime_error("bwd_seq: shape not supported");
     gru_bwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
@@ -280,6 +285,14 @@ PYBIND11_MODULE(_C, m) {
   });
 
   // ---------------------------------------------------------------- RCCL communicator
+  m.def("bootstrap_key", &bootstrap_key);
+  m.def("bootstrap_path", &bootstrap_path);
+  m.def("file_exchange_uid", [](int rank, const std::string& path, const std::string& key, py::bytes uid,
+                                int timeout_ms) {
+    std::string u = uid;
+    py::gil_scoped_release nogil;
+    return py::bytes(file_exchange_uid(rank, path, key, u, timeout_ms));
+  });
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int rank, int world) {
         std::string s = uid;
@@ -298,6 +311,13 @@ PYBIND11_MODULE(_C, m) {
       .def("allgather_u8", [](RcclComm& c, uintptr_t send, uintptr_t recv, long n, uintptr_t s) {
         c.allgather_u8(Pp<const unsigned char>(send), Pp<unsigned char>(recv), n, S(s));
       })
+      .def("reduce_scatter_avg_f32", [](RcclComm& c, uintptr_t send, uintptr_t recv, long n, uintptr_t s) {
+        c.reduce_scatter_avg_f32(Pp<const float>(send), Pp<float>(recv), n, S(s));
+      })
+      .def("allgather_f32", [](RcclComm& c, uintptr_t send, uintptr_t recv, long n, uintptr_t s) {
+        c.allgather_f32(Pp<const float>(send), Pp<float>(recv), n, S(s));
+      })
+      .def("count", &RcclComm::count)
       .def("check_async_error", &RcclComm::check_async_error)
       .def("abort", &RcclComm::abort)
       .def("aborted", &RcclComm::aborted)

@@ -22,6 +22,7 @@
 #include "../runtime/runtime.h"
 #include "../engine/generator.h"
 #include "../comm/rccl_comm.h"
+#include "../comm/bootstrap.h"
 #include "ckpt_reader.h"
 
 namespace {
@@ -43,37 +44,6 @@ std::unique_ptr<State> S;
 int env_int(const char* k, int dflt) {
   const char* v = std::getenv(k);
   return v && *v ? std::atoi(v) : dflt;
-}
-
-std::string bootstrap_path() {
-  const char* f = std::getenv("GK_BOOTSTRAP_FILE");
-  if (f && *f) return f;
-  const char* port = std::getenv("MASTER_PORT");
-  return std::string("/tmp/gk_namegen_") + (port ? port : "default") + ".uid";
-}
-
-// rank 0 publishes the 128-byte ncclUniqueId through a file (atomic rename); others poll it
-std::string exchange_uid(int rank, const std::string& path) {
-  if (rank == 0) {
-    const std::string uid = RcclComm::unique_id();
-    const std::string tmp = path + ".tmp." + std::to_string(getpid());
-    {
-      std::ofstream o(tmp, std::ios::binary);
-      o.write(uid.data(), (std::streamsize)uid.size());
-    }
-    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("namegen: cannot publish " + path);
-    return uid;
-  }
-  for (int i = 0; i < 12000; ++i) {   // up to 120 s
-    std::ifstream in(path, std::ios::binary);
-    if (in) {
-      std::string uid(128, '\0');
-      in.read(&uid[0], 128);
-      if (in.gcount() == 128) return uid;
-    }
-    std::this_thread::sleep_for(std::chrono::milliseconds(10));
-  }
-  throw std::runtime_error("namegen: rank " + std::to_string(rank) + " timed out waiting for " + path);
 }
 
 void shard(int n, int rank, int world, int* start, int* count) {
@@ -102,8 +72,11 @@ static void init_impl(int N, int rng_seed, char* parameter_fname) {
   std::fflush(stdout);
 
   if (st.world > 1) {
-    st.uid_file = bootstrap_path();
-    st.comm.reset(new RcclComm(exchange_uid(st.rank, st.uid_file), st.rank, st.world));
+    // job-unique file exchange of the ncclUniqueId (comm/bootstrap.h)
+    const std::string key = bootstrap_key();
+    st.uid_file = bootstrap_path(key);
+    const std::string uid = st.rank == 0 ? RcclComm::unique_id() : std::string();
+    st.comm.reset(new RcclComm(file_exchange_uid(st.rank, st.uid_file, key, uid), st.rank, st.world));
   }
   // dims: rank 0's view (sidecar / env / defaults), broadcast so every rank agrees
   int dims[8] = {0};

@@ -55,6 +55,20 @@ void RcclComm::broadcast_f32(float* p, long n, int root, hipStream_t s) {
 void RcclComm::allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s) {
   RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclUint8, C(live()), s));
 }
+void RcclComm::reduce_scatter_avg_f32(const float* send, float* recv, long n, hipStream_t s) {
+  RCCL_CHECK(ncclReduceScatter(send, recv, (size_t)n, ncclFloat32, ncclAvg, C(live()), s));
+}
+void RcclComm::allgather_u16(const unsigned short* send, unsigned short* recv, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclBfloat16, C(live()), s));
+}
+void RcclComm::allgather_f32(const float* send, float* recv, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclFloat32, C(live()), s));
+}
+int RcclComm::count() const {
+  int n = 0;
+  RCCL_CHECK(ncclCommCount(C(live()), &n));
+  return n;
+}
 void RcclComm::check_async_error() {
   ncclResult_t r = ncclSuccess;
   RCCL_CHECK(ncclCommGetAsyncError(C(live()), &r));

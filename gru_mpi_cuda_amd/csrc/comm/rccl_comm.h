@@ -22,6 +22,12 @@ class RcclComm {
   void allreduce_sum_f32(float* p, long n, hipStream_t s);
   void broadcast_f32(float* p, long n, int root, hipStream_t s);
   void allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s);
+  // sharded optimiser (ZeRO-1 style): recv[n] = mean over ranks of send[rank*n .. rank*n+n)
+  void reduce_scatter_avg_f32(const float* send, float* recv, long n, hipStream_t s);
+  // recv[world*n] = concat over ranks of send[n]; bf16 payload moved as 16-bit words
+  void allgather_u16(const unsigned short* send, unsigned short* recv, long n, hipStream_t s);
+  void allgather_f32(const float* send, float* recv, long n, hipStream_t s);
+  int count() const;                  // ncclCommCount: ranks the communicator really has
   // watchdog hook: raises if the communicator reported an asynchronous error
   void check_async_error();
   void abort();                       // thread-safe (the watchdog calls it)

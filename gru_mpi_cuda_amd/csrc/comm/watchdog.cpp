@@ -51,6 +51,19 @@ void Watchdog::run() {
         continue;
       }
     }
+    // a persistent / split-K kernel hit its cross-workgroup spin limit: the step was not applied
+    // (OptimArgs::err); stop the job before the other ranks wait on this one forever
+    if (err_word_ && *err_word_) {
+      msg_ = "[rank " + std::to_string(comm_ ? comm_->rank() : global_rank()) +
+             "] a cross-workgroup wait hit its spin limit (error word " + std::to_string(*err_word_) +
+             "); the step's update was skipped";
+      status_ = kStepError;
+      ev_ = nullptr;
+      trace_mark("watchdog: step error word set");
+      if (comm_) comm_->abort();
+      std::fprintf(stderr, "[gk watchdog] %s\n", msg_.c_str());
+      continue;
+    }
     if (!ev_) continue;
     const hipError_t q = hipEventQuery(ev_);
     if (q == hipSuccess) { ev_ = nullptr; continue; }
@@ -61,7 +74,7 @@ void Watchdog::run() {
     }
     const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
                         std::chrono::steady_clock::now() - armed_at_).count();
-    if (ms > timeout_ms_) {
+    if (timeout_ms_ > 0 && ms > timeout_ms_) {
       msg_ = "[rank " + std::to_string(comm_ ? comm_->rank() : global_rank()) + "] training step not done after " +
              std::to_string(ms) + " ms (timeout " + std::to_string(timeout_ms_) + " ms)";
       status_ = kTimeout;

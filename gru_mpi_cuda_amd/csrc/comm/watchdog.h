@@ -19,8 +19,14 @@ namespace gk {
 
 class Watchdog {
  public:
-  enum Status { kOk = 0, kTimeout = 1, kCommError = 2 };
+  enum Status { kOk = 0, kTimeout = 1, kCommError = 2, kStepError = 3 };
+  // timeout_ms 0: no step deadline (still watches the communicator and the step error word)
   Watchdog(RcclComm* comm, int timeout_ms, int poll_ms = 20);
+  // host-mapped mirror of the device step error word (written by the optimiser kernel)
+  void set_error_word(const volatile unsigned* w) {
+    std::lock_guard<std::mutex> g(mu_);
+    err_word_ = w;
+  }
   ~Watchdog();
   // arm: the work recorded before `ev` must complete within the timeout from now
   void watch(hipEvent_t ev);
@@ -30,6 +36,7 @@ class Watchdog {
  private:
   void run();
   RcclComm* comm_;
+  const volatile unsigned* err_word_ = nullptr;
   int timeout_ms_, poll_ms_, device_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;

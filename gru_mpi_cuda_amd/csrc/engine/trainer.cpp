@@ -160,6 +160,9 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
     HIP_CHECK(hipEventRecord(e, s0_));
   }
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(err_host_, 0, 64);
+  HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_host_dev_), err_host_, 0));
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
   overlap_ = d_.overlap != 0;
@@ -171,7 +174,9 @@ Trainer::~Trainer() {
   g_opt_.reset();
   for (auto& e : events_) (void)hipEventDestroy(e);
   for (auto& e : stage_done_) if (e) (void)hipEventDestroy(e);
+  wd_.reset();   // the watchdog thread reads err_host_
   if (h_stage_) (void)hipHostFree(h_stage_);
+  if (err_host_) (void)hipHostFree(err_host_);
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
   if (sc_) (void)hipStreamDestroy(sc_);
@@ -469,6 +474,7 @@ void Trainer::record_opt(hipStream_t s) {
   OptimArgs a;
   a.p = params_; a.g = grads_; a.m = m_; a.v = v_; a.n = nflat_; a.step = step_;
   a.gscale = o_.clip > 0.f ? gscale_ : nullptr;
+  a.err = err_; a.err_host = err_host_dev_;
   a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
   const int V = d_.V, E = d_.E, H = d_.H;
   if (V % 64 == 0 && E % 64 == 0 && H % 64 == 0) {
@@ -604,7 +610,10 @@ void Trainer::record_allreduce(hipStream_t s) {
 
 void Trainer::enable_watchdog(int timeout_ms) {
   wd_.reset();
-  if (timeout_ms > 0) wd_ = std::make_unique<Watchdog>(comm_, timeout_ms);
+  if (timeout_ms >= 0) {   // 0: no step deadline, still the communicator and the step error word
+    wd_ = std::make_unique<Watchdog>(comm_, timeout_ms);
+    wd_->set_error_word(err_host_);
+  }
 }
 
 void Trainer::step(hipStream_t s) {

@@ -130,7 +130,10 @@ class Trainer {
   // collectives recorded into the last captured step graph (tests / plan printing)
   const std::vector<std::pair<long, long>>& allreduce_log() const { return ar_log_; }
   void step(hipStream_t s);      // whole training step as one graph replay
-  // collective watchdog over the launched steps (needs set_comm first; 0 disables)
+  // test hook: set the device step error word (fault injection)
+  void inject_error(unsigned bits) { HIP_CHECK(hipMemcpy(err_, &bits, 4, hipMemcpyHostToDevice)); }
+  // watchdog over the launched steps (call after set_comm): timeout_ms > 0 aborts a step that
+  // is not done in time, 0 only watches the communicator and the step error word, < 0 disables
   void enable_watchdog(int timeout_ms);
   int watchdog_status() const { return wd_ ? wd_->status() : 0; }
   std::string watchdog_message() { return wd_ ? wd_->message() : std::string(); }
@@ -160,6 +163,7 @@ class Trainer {
   std::vector<SeqPlan> seq_;
   int splits_ = 8;
   unsigned *cnt_ = nullptr, *err_ = nullptr;
+  unsigned *err_host_ = nullptr, *err_host_dev_ = nullptr;   // host-mapped mirror of *err_ (watchdog)
   float* sk_part_ = nullptr;         // split-K backward step kernel workspace (gru_step_lds.hip)
   unsigned* sk_cnt_ = nullptr;
   long sk_part_floats_ = 0, sk_cnt_words_ = 0;

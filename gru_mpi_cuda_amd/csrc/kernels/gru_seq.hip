@@ -630,6 +630,9 @@ void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
   }
   BWD_VARIANTS(X)
 #undef X
+  // an unmatched (H, fuse dW_hh, fuse dP) must not silently leave the gradients untouched
+  throw std::runtime_error("gru_bwd_seq: no kernel variant for H=" + std::to_string(a.H) +
+                           " fuse_w=" + std::to_string(fw) + " fuse_p=" + std::to_string(fp));
 }
 
 }  // namespace gk

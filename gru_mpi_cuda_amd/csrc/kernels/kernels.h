@@ -218,6 +218,11 @@ struct OptimArgs {
   long n = 0;
   int* step = nullptr;             // device step counter (graph-replay safe), incremented by caller kernel
   const float* gscale = nullptr;   // device scalar gradient scale (clip); nullable = 1
+  // step error word (cross-workgroup spin limit in the persistent / split-K kernels): when set,
+  // the update is skipped (no garbage gradient reaches the weights) and the word is mirrored to
+  // host-mapped memory (err_host) where the host watchdog sees it without a device sync
+  const unsigned* err = nullptr;
+  unsigned* err_host = nullptr;
   float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f;
   int sgd = 0;
 };

@@ -235,7 +235,16 @@ void cast_multi(CastJobs& j, hipStream_t s) {
   hipLaunchKernelGGL(cast_multi_kernel, dim3(tot), dim3(256), 0, s, j);
 }
 
+// true when the step must not be applied (see OptimArgs::err); uniform over the block
+DEV bool step_failed(const OptimArgs& a) {
+  if (!a.err) return false;
+  const unsigned e = *a.err;
+  if (a.err_host && blockIdx.x == 0 && threadIdx.x == 0) *a.err_host = e;
+  return e != 0u;
+}
+
 __global__ void adam_kernel(OptimArgs a) {
+  if (step_failed(a)) return;
   const int t = *a.step;
   const float sc = a.gscale ? *a.gscale : 1.f;
   const float bc1 = 1.f - powf(a.b1, (float)t), bc2 = 1.f - powf(a.b2, (float)t);
@@ -361,6 +370,7 @@ __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   const OptCastJob& J = j.job[k];
   const int t = b - j.blk_start[k];
+  if (step_failed(a)) return;
   const AdamCoef co = adam_coef(a);
   if (J.R == 0) {   // flat job: 1024 elements per block
     const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;

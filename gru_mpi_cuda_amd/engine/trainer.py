@@ -73,8 +73,13 @@ class HipTrainer:
                             max(1024, int(cfg.bucket_mb * (1 << 20) / 4)))
         self.t.refresh_weights(self._stream())
         self._one_graph = True
-        if cfg.watchdog_ms > 0:       # host thread watching each launched step
-            self.t.enable_watchdog(int(cfg.watchdog_ms))
+        # host thread watching each launched step, the communicator and the step
+        # error word (a persistent kernel's spin limit: that step's update is skipped on device)
+        wd = int(cfg.watchdog_ms)
+        if wd == -1:
+            wd = 120_000 if self.ctx.world > 1 else 0
+        if wd >= 0:
+            self.t.enable_watchdog(wd)
 
     def _pad(self, params: Dict[str, torch.Tensor], masked_bias: bool = True) -> Dict[str, torch.Tensor]:
         return pad_params(params, self.cfg, self.icfg, masked_bias) if self.padded else params
@@ -83,7 +88,7 @@ class HipTrainer:
         return unpad_params(params, self.cfg, self.icfg) if self.padded else params
 
     def check_watchdog(self) -> None:
-        """Raise if the collective watchdog fired (step timeout or RCCL async error)."""
+        """Raise if the watchdog fired (step timeout, RCCL async error or step error word)."""
         if self.t.watchdog_status():
             raise RuntimeError(f"watchdog: {self.t.watchdog_message()}")
 

@@ -44,6 +44,7 @@ def rank_env(rank: int, world: int, addr: str, port: int, base: Optional[Dict[st
     env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                LOCAL_WORLD_SIZE=str(world), MASTER_ADDR=addr, MASTER_PORT=str(port))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL peer buffers
+    env.setdefault("GK_RUN_ID", f"{os.getpid()}-{port}")   # job key of the C API's id exchange
     return env
 
 

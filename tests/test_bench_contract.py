@@ -20,8 +20,9 @@ def _port():
     return p
 
 
-def _lines(cmd, n):
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+def _lines(cmd, n, env=None):
+    env = dict(env if env is not None else os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -46,3 +47,20 @@ def test_bench_contract_world2_gloo():
     _lines([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
             "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
             "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], 2)
+
+
+def test_bench_self_launches_world2():
+    """``bench.py --gpus 2`` with no launcher starts its own 2 ranks (parallel/launch.py) and still
+    prints exactly one JSON line with n_gpus 2 (--gpus must not be a no-op)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = _lines([sys.executable, "bench.py", "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3",
+                "--warmup", "1"], 2, env=env)
+    assert r["rccl_ranks"] == 2 and r["comm_backend"] == "gloo"
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--preset", "cpu_tiny", "--steps", "1",
+                        "--warmup", "0"], env=env, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr

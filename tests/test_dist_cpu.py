@@ -114,3 +114,48 @@ def test_shard_and_buckets():
     b = bucket_bounds(1000, 300, [0, 100, 350, 900])
     assert b[0][0] == 0 and b[-1][1] == 1000
     assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+
+
+def _resume_worker(rank, world, port, path, outdir):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    from gru_mpi_cuda_amd.cli import load_checkpoint
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=16, hidden=16, layers=2, batch=6, seq=6)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=50 + rank))
+    # only rank 0 is given (and may open) the checkpoint; the others get it by broadcast
+    step = load_checkpoint(tr, path if rank == 0 else None)
+    torch.save({"p": tr.state_dict(), "m": dict(tr.opt.m), "step": step},
+               os.path.join(outdir, f"resume_{rank}.pt"))
+    gdist.shutdown()
+
+
+def test_dp_resume_rank0_reads_and_broadcasts(tmp_path):
+    """DP resume: rank 0 reads the checkpoint, weights + Adam moments + step
+    reach every rank by broadcast; ranks > 0 never touch the file."""
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    from gru_mpi_cuda_amd.cli import save_checkpoint
+    cfg = GRUConfig(vocab=256, embed=16, hidden=16, layers=2, batch=6, seq=6)
+    src = CpuTrainer(cfg, params=init_params(cfg, seed=3))
+    ds = NameStream(cfg.batch, cfg.seq, seed=2)
+    for _ in range(2):
+        src.step(*ds.next())
+    path = str(tmp_path / "ck.bin")
+    save_checkpoint(src, path)
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_resume_worker, args=(r, world, port, path, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    want = src.state_dict()
+    for r in range(world):
+        got = torch.load(tmp_path / f"resume_{r}.pt", weights_only=True)
+        assert got["step"] == 2
+        for k in want:
+            torch.testing.assert_close(got["p"][k], want[k], atol=0, rtol=0)
+            torch.testing.assert_close(got["m"][k], src.opt.m[k], atol=0, rtol=0)

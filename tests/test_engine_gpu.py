@@ -215,6 +215,35 @@ def test_watchdog_detects_stalled_step():
         bad.step(x, y)
 
 
+def test_step_error_word_skips_update_and_trips_watchdog():
+    """Fault injection: with the step error word set (what a persistent kernel's
+    cross-workgroup spin limit does) the optimiser kernel leaves weights and moments untouched,
+    mirrors the word to host memory, and the default watchdog (no deadline at one rank) reports
+    it, so the next step raises instead of applying garbage gradients."""
+    import time
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=3)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=1).next()
+    tr = HipTrainer(cfg)
+    tr.step(x, y)
+    torch.cuda.synchronize()
+    assert tr.t.watchdog_status() == 0
+    p0, m0 = tr.params.clone(), tr.m.clone()
+    tr.t.inject_error(1)
+    tr.step(x, y)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(tr.params, p0, atol=0, rtol=0)
+    torch.testing.assert_close(tr.m, m0, atol=0, rtol=0)
+    for _ in range(50):
+        if tr.t.watchdog_status():
+            break
+        time.sleep(0.02)
+    assert tr.t.watchdog_status() == 3, tr.t.watchdog_message()
+    assert "spin limit" in tr.t.watchdog_message()
+    with pytest.raises(RuntimeError, match="watchdog"):
+        tr.step(x, y)
+
+
 @pytest.mark.parametrize("sched", ["persistent", "perstep", "overlap"])
 @pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 128, 64)])
 def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
