@@ -17,7 +17,8 @@ start ranks without the exec-after-GPU-init hazard.
     python -m gru_mpi_cuda_amd.parallel.launch --nproc 8 -- -m gru_mpi_cuda_amd.cli train --preset h512_dp8
     python -m gru_mpi_cuda_amd.parallel.launch --nproc 2 --log-dir run/logs -- bench.py --gpus 2
 
-Arguments after ``--`` go to ``python`` (a script path or ``-m module``).
+Arguments after ``--`` go to ``python`` (a script path or ``-m module``), or with ``--no-python``
+form the command itself (``--no-python -- gru_mpi_cuda_amd/bin/namegen model.bin out.txt 1000``).
 """
 from __future__ import annotations
 
@@ -70,8 +71,9 @@ def _stop(procs: List[subprocess.Popen], grace: float) -> None:
 
 def run(nproc: int, argv: Sequence[str], addr: str = "127.0.0.1", port: Optional[int] = None,
         timeout: float = 0.0, grace: float = 10.0, log_dir: Optional[str] = None,
-        poll_s: float = 0.1) -> int:
-    """Start ``nproc`` ranks of ``python argv...``; return 0 or the first failing rank's code.
+        poll_s: float = 0.1, python: bool = True) -> int:
+    """Start ``nproc`` ranks of ``python argv...`` (``argv...`` itself with python=False, e.g. the
+    native bin/namegen driver); return 0 or the first failing rank's code.
 
     A rank killed by a signal reports 128 + signal number; a ``timeout`` ends the job with 124.
     """
@@ -87,7 +89,8 @@ def run(nproc: int, argv: Sequence[str], addr: str = "127.0.0.1", port: Optional
                 os.makedirs(log_dir, exist_ok=True)
                 out = open(os.path.join(log_dir, f"rank{r}.log"), "wb")
                 logs.append(out)
-            procs.append(subprocess.Popen([sys.executable, *argv], env=rank_env(r, nproc, addr, port),
+            procs.append(subprocess.Popen([sys.executable, *argv] if python else list(argv),
+                                          env=rank_env(r, nproc, addr, port),
                                           stdout=out, stderr=subprocess.STDOUT if out else None,
                                           start_new_session=True))
         t0 = time.monotonic()
@@ -129,6 +132,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     ap.add_argument("--timeout", type=float, default=0.0, help="wall-clock limit for the job in s (0 = none)")
     ap.add_argument("--grace", type=float, default=10.0, help="SIGTERM -> SIGKILL delay in s")
     ap.add_argument("--log-dir", default=None, help="per-rank logs rank<r>.log instead of the terminal")
+    ap.add_argument("--no-python", action="store_true",
+                    help="the program after -- is an executable (e.g. gru_mpi_cuda_amd/bin/namegen), not python args")
     a = ap.parse_args(own)
     if not child:
         ap.error("nothing to run: give the program after --")
@@ -136,7 +141,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     if n is None:
         import torch   # device_count() does not initialise the GPU on this image
         n = max(1, torch.cuda.device_count())
-    return run(n, child, a.master_addr, a.master_port, a.timeout, a.grace, a.log_dir)
+    return run(n, child, a.master_addr, a.master_port, a.timeout, a.grace, a.log_dir, python=not a.no_python)
 
 
 if __name__ == "__main__":

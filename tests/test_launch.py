@@ -79,3 +79,19 @@ def test_cli_train_under_launcher(tmp_path):
     logs = "".join((tmp_path / "logs" / f"rank{r}.log").read_text() for r in range(2))
     assert rc == 0, logs
     assert (tmp_path / "m.jsonl").exists()
+
+
+def test_no_python_runs_an_executable(tmp_path):
+    """--no-python starts the command itself once per rank (the native bin/namegen driver's way
+    in), each with its own RANK / WORLD_SIZE."""
+    import subprocess
+    import sys
+    out = tmp_path / "ranks"
+    out.mkdir()
+    cmd = [sys.executable, "-m", "gru_mpi_cuda_amd.parallel.launch", "--nproc", "3", "--no-python", "--",
+           "/bin/sh", "-c", f'echo "$WORLD_SIZE $GK_RUN_ID" > {out}/r$RANK']
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    got = sorted(f.read_text().split()[0] for f in out.iterdir())
+    assert got == ["3", "3", "3"]
+    assert len({f.read_text().split()[1] for f in out.iterdir()}) == 1   # one job key for all ranks
