@@ -224,6 +224,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
     a.dy = GP(const float, d, "dy");
+    a.dl = GP(const u16, d, "dl"); a.WfcT = GP(const u16, d, "WfcT");
+    if (a.dl && get<int>(d, "V", 0) != 256) throw std::runtime_error("bwd_seq: in-kernel dH needs V = 256");
     a.sr = GP(const float, d, "sr"); a.sz = GP(const float, d, "sz"); a.sn = GP(const float, d, "sn");
     a.sghn = GP(const float, d, "sghn"); a.HSf = GP(const float, d, "HSf");
     a.HT = GP(const u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0); a.WhhT = GP(const u16, d, "WhhT");

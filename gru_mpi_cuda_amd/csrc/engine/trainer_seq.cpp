@@ -13,6 +13,11 @@
 
 namespace gk {
 
+static bool env_flag(const char* name, bool dflt) {
+  const char* v = std::getenv(name);
+  return v && v[0] ? v[0] != '0' : dflt;
+}
+
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
   // split K only as deep as it takes to give the chip ~256 workgroups: every extra split costs a
@@ -114,6 +119,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // ------------------------------------------------------------------ FC + loss + dH
   Layer& top = Ls_[L - 1];
   SlabJobs tail;   // reductions deferred to the last multi-tensor reduce (layer 0's)
+  // dH of the top layer inside its persistent backward kernel (dy = dl · W_fc on the MFMA pipe the
+  // recurrence leaves idle): fc_xent writes bf16 dl and skips the W_fc^T stream + fp32 dy store.
+  // Off by default: fc_xent 16.3 -> 11.4 us but the backward kernel +7..10 us at h512 (its step
+  // 2.6 -> 2.8 us, every phase a little longer; profiles/r2_bwd_dh_ab.jsonl).  GK_BWD_DH=1 turns it on.
+  static const bool bwd_dh_env = env_flag("GK_BWD_DH", false);
+  const bool bwd_dh = bwd_dh_env && seq_[L - 1].bwd && V == 256 && fc_xent_fused_ok(V, H, (int)tok);
   {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
@@ -132,6 +143,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
       g.M = (int)tok; g.N = H; g.K = V;
       gemm_nt(g, s);
+    } else if (bwd_dh) {
+      f.dl = dl_; f.Wf = WfcF;
+      fc_xent(f, s);
     } else if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
       f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
@@ -178,7 +192,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     const std::string k = std::to_string(l);
     if (q.bwd) {
       SeqBwdArgs a;
-      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+      a.dy = y.dy; a.sr = y.sr;
+      if (l == L - 1 && bwd_dh) { a.dy = nullptr; a.dl = dl_; a.WfcT = WfcT; } a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
       a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;

@@ -228,7 +228,10 @@ DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WTf, int n0, int lane) {
     for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WTf + ((size_t)((n0 / 16 + c) * 8 + kk) * 64 + lane) * 8);
 }
 
-template <int HH>
+// DH = false (the persistent backward path): no dH here -- the backward sequence kernel computes
+// dy = dl · W_fc itself from the row-major bf16 dl this kernel writes (its MFMA pipe is idle while
+// it waits on the recurrence), so the W_fc^T stream, the dH MFMAs and the fp32 dy store go away.
+template <int HH, bool DH>
 __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int nst = 0;
@@ -296,7 +299,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   STAMP();
   const int per = H / NW;                 // dH columns of this wave (a multiple of 64)
   bf16x8 bt[8][4];
-  fc2_load_wt(bt, a.WTf, w * per, lane);
+  if constexpr (DH) fc2_load_wt(bt, a.WTf, w * per, lane);
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -367,8 +370,15 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
         *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
   }
   STAMP();
+  if constexpr (!DH) {   // row-major dl: 32 rows x 512 B, whole 16-B pieces
+    for (int q = tid; q < FROWS * V / 8; q += 512) {
+      const int r2 = q / (V / 8), c8 = q % (V / 8);
+      *reinterpret_cast<uint4*>(a.dl + (size_t)(m0 + r2) * V + c8 * 8) =
+          *reinterpret_cast<const uint4*>(dlr + r2 * LDR + c8 * 8);
+    }
+  }
   // ---- dH = dl · W_fc: 32 rows x this wave's columns, 64 per pass, K = V = 256
-  for (int n0 = w * per; n0 < (w + 1) * per; n0 += 64) {
+  if constexpr (DH) for (int n0 = w * per; n0 < (w + 1) * per; n0 += 64) {
     if (n0 != w * per) fc2_load_wt(bt, a.WTf, n0, lane);
     f32x4 dacc[2][4];
     zero_acc(dacc);
@@ -650,8 +660,10 @@ void softmax_xent(const float* logits, const FcXentArgs& a, hipStream_t s) {
 
 bool fc_xent_fused_ok(int V, int H, int M) { return V == 256 && (H == 512 || H == 1024) && M % FROWS == 0; }
 
+// the 8-wave V = 256 kernel: fused dH (dy + W_fc^T FT copy, no row-major dl), or dl only (no dy)
 static bool fc_xent_v256_ok(const FcXentArgs& a) {
-  return a.V == 256 && a.dy && a.Wf && a.WTf && !a.dl && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
+  const bool dh = a.dy && a.WTf && !a.dl, dl_only = !a.dy && a.dl;
+  return a.V == 256 && a.Wf && (dh || dl_only) && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
          !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');
 }
 
@@ -661,12 +673,19 @@ void fc_xent(const FcXentArgs& a, hipStream_t s) {
                        (size_t)FROWS * (256 + 8) * 2 + FROWS * 4;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)fc_xent_v256_kernel<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* k : {(const void*)fc_xent_v256_kernel<512, true>, (const void*)fc_xent_v256_kernel<1024, true>,
+                            (const void*)fc_xent_v256_kernel<512, false>, (const void*)fc_xent_v256_kernel<1024, false>})
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr = true;
     }
-    if (a.H == 512) hipLaunchKernelGGL(fc_xent_v256_kernel<512>, dim3(a.M / FROWS), dim3(512), shm, s, a);
-    else hipLaunchKernelGGL(fc_xent_v256_kernel<1024>, dim3(a.M / FROWS), dim3(512), shm, s, a);
+    const dim3 g(a.M / FROWS), blk(512);
+    if (a.dy) {
+      if (a.H == 512) hipLaunchKernelGGL((fc_xent_v256_kernel<512, true>), g, blk, shm, s, a);
+      else hipLaunchKernelGGL((fc_xent_v256_kernel<1024, true>), g, blk, shm, s, a);
+    } else {
+      if (a.H == 512) hipLaunchKernelGGL((fc_xent_v256_kernel<512, false>), g, blk, shm, s, a);
+      else hipLaunchKernelGGL((fc_xent_v256_kernel<1024, false>), g, blk, shm, s, a);
+    }
     return;
   }
   const int NW = a.V / 64;

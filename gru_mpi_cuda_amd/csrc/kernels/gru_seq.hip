@@ -342,7 +342,8 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 // NKW3: k-steps per wave of the dh GEMM (K = 3H split over 8 waves)
 // NTW : 16-col tiles per wave of the fused dW_hh accumulator (H / 128); 0 = not fused
 // NTP : 16-col tiles per wave of the fused dP accumulator (V / 128); 0 = not fused
-template <int NKW3, int NTW, int NTP>
+// DL   : top layer's dy = dl · W_fc computed here (SeqBwdArgs::dl) instead of read from a.dy
+template <int NKW3, int NTW, int NTP, bool DL>
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][2][256];      // 16 KB
   __shared__ __attribute__((aligned(16))) u16 srow[3][32][24];        // dGh tile, gate-major (exchange; 48-B rows)
@@ -385,10 +386,44 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
   // next poll they would delay it (vmcnt retires in order), and they have a whole step to land
   float sv[6];
+  int svid = 0;
+  // the step's 32 row ids for the fused dP one-hot: staged through LDS by the epilogue threads of
+  // unit column 0 and read back right before use (8 ids held in registers across the barriers and
+  // the publish pushed the register file over the limit)
+  __shared__ __attribute__((aligned(16))) int idsL[NTP > 0 ? 32 : 1];
+  // top layer with a.dl: this wave's K = 32 slice (logits 32w..32w+31) of dy = dl · W_fc for the
+  // 16 units, into the same accumulators as the recurrent dh GEMM (summed over the waves).  No
+  // registers held across steps (the fused variants' file is full): the W_fc^T fragment sits
+  // lane-linear in LDS like bwL, and the step's two dl fragments go global -> LDS directly
+  // (buffer_load ... lds, 16 B per lane; each wave reads back only what it loaded itself, so no
+  // barrier).  The copy for step t-NB is issued at the END of step t, after its last barrier: the
+  // compiler makes every barrier wait for outstanding LDS-DMA (issued with the saves it put a load
+  // latency on each step's critical path: +0.3 us/step, probe_seq_bwd.py), and the exchange poll's
+  // own vmcnt(0) waits for it too (vmcnt retires in order), so it must be a whole step old by then:
+  // two buffers (NB = 2; one at H = 1024, where LDS is full).
+  constexpr bool fdl = DL;
+  __shared__ __attribute__((aligned(16))) bf16x8 bfcL[DL ? 512 : 1];
+  constexpr int NB = NKW3 >= 12 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) bf16x8 dlL[DL ? NB : 1][2][DL ? 512 : 1];   // [buf][row tile][wave*64+lane]
+  if constexpr (fdl) bfcL[tid] = ld8(a.WfcT + (size_t)(j0 + lr) * 256 + w * 32 + lk);
+  // buffer addressing: one per-lane 32-bit offset, the step and row tile in the scalar offset
+  const rsrc_t rDL = make_rsrc(a.dl, fdl ? (unsigned)((size_t)T * Bp * 256 * 2) : 0u);
+  const unsigned dl_lane = (unsigned)((lr * 256 + w * 32 + lk) * 2);
+  auto load_dl = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rDL, (__attribute__((address_space(3))) void*)(&dlL[t % NB][r][w * 64]), 16,
+                                               dl_lane, (int)(((size_t)t * Bp + b0 + r * 16) * 512), 0, 0);
+  };
+  if constexpr (fdl) {
+    load_dl(T - 1);
+    if (NB > 1 && T > 1) load_dl(T - 2);
+  }
   auto load_saves = [&](int t) {
     const size_t o = ((size_t)t * Bp + b) * H + j;
-    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[0] = fdl ? 0.f : a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
     sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
+    if constexpr (NTP > 0) svid = a.ids[(size_t)t * Bp + b];   // this thread's row id (fused dP)
   };
   load_saves(T - 1);
 
@@ -420,6 +455,14 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
         for (int r = 0; r < 2; ++r) acc[r] = mfma16(af[kk][r], bk, acc[r]);
       }
     }
+    if constexpr (fdl) {
+      // after the exchange loads have been waited on this wait is free (the copy is older)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const bf16x8 bfc = bfcL[tid];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[r] = mfma16(dlL[t % NB][r][tid], bfc, acc[r]);
+    }
+    const int idc = svid;
     const float dy = sv[0], sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4], hprev = sv[5];
     if (t > 0) load_saves(t - 1);
     // operands of the fused weight-gradient MFMAs (independent of other workgroups): issued after
@@ -435,13 +478,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
         for (int nt = 0; nt < NTW; ++nt)
           hB[nt] = ld8(a.HT + (size_t)(w * NTW * 16 + nt * 16 + lr) * a.ldT + (size_t)t * Bp + b0 + lk);
       }
-    }
-    int idv[8];
-    if constexpr (NTP > 0) {
-      const int4 i0 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk);
-      const int4 i1 = *reinterpret_cast<const int4*>(a.ids + (size_t)t * Bp + b0 + lk + 4);
-      idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
-      idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)
@@ -463,6 +499,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dhn), bi = f2bf(dan);
     srow[0][row][col] = br; srow[1][row][col] = bz; srow[2][row][col] = bn;
     sgT[0][col][row] = br; sgT[1][col][row] = bz; sgT[2][col][row] = bn; sgT[3][col][row] = bi;
+    if constexpr (NTP > 0) {
+      if (col == 0) idsL[row] = idc;
+    }
     __syncthreads();
     stamp(a.dbg, s, 3);
     if (w == 0) {
@@ -510,6 +549,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       }
       if constexpr (NTP > 0) {
         ga[2] = *reinterpret_cast<const bf16x8*>(&sgT[3][lr][lk]);   // dGi: n gate without r
+        int idv[8];
+        const int4 i0 = *reinterpret_cast<const int4*>(&idsL[lk]), i1 = *reinterpret_cast<const int4*>(&idsL[lk + 4]);
+        idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
+        idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
 #pragma unroll
         for (int nt = 0; nt < NTP; ++nt) {
           const int v = (w * NTP + nt) * 16 + lr;
@@ -520,6 +563,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
           for (int g = 0; g < 3; ++g) accP[g][nt] = mfma16(ga[g], oh, accP[g][nt]);
         }
       }
+    }
+    if constexpr (fdl) {   // dl image of step t - NB into the buffer this step just consumed
+      if (t >= NB) load_dl(t - NB);
     }
   }
 
@@ -613,8 +659,11 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
   if (Bp % 32) return false;
   int cap = -1;
-#define X(HH, NK, NW, NP)                                                                      \
-  if (H == HH && (NW > 0) == fuse_w && (NP > 0) == fuse_p) cap = resident_blocks(gru_bwd_seq_kernel<NK, NW, NP>);
+  // both the dy-reading and the in-kernel-dH (DL) instantiation must fit (more LDS with DL)
+#define X(HH, NK, NW, NP)                                                                       \
+  if (H == HH && (NW > 0) == fuse_w && (NP > 0) == fuse_p)                                      \
+    cap = std::min(resident_blocks(gru_bwd_seq_kernel<NK, NW, NP, false>),                      \
+                   resident_blocks(gru_bwd_seq_kernel<NK, NW, NP, true>));
   BWD_VARIANTS(X)
 #undef X
   return cap >= (H / 16) * (Bp / 32);
@@ -623,10 +672,12 @@ bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
-#define X(HH, NK, NW, NP)                                                        \
-  if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                          \
-    hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP>), grid, block, 0, s, a); \
-    return;                                                                      \
+  if (a.dl && (!a.WfcT || a.dy)) throw std::runtime_error("gru_bwd_seq: in-kernel dH takes dl + W_fc^T and no dy");
+#define X(HH, NK, NW, NP)                                                                   \
+  if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                                     \
+    if (a.dl) hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP, true>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP, false>), grid, block, 0, s, a);     \
+    return;                                                                                 \
   }
   BWD_VARIANTS(X)
 #undef X

@@ -107,6 +107,10 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
+  // top layer alternative to dy (V = 256): dy = dl · W_fc computed in the kernel from the
+  // row-major bf16 dlogits [T][Bp][V] and W_fc^T [H][V] (fc_xent then skips its dH)
+  const u16* dl = nullptr;
+  const u16* WfcT = nullptr;
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)

@@ -211,9 +211,12 @@ def test_bwd_step(ext, first, H, Bp, algo, sk):
     torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
 
 
-@pytest.mark.parametrize("fused_dh", [False, True])
+@pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256"])
 @pytest.mark.parametrize("H", [256, 320, 512, 1024])
-def test_fc_xent(ext, fused_dh, H):
+def test_fc_xent(ext, mode, H):
+    fused_dh = mode == "fused_dh"
+    if mode == "dl_v256" and H % 512:
+        pytest.skip("the 8-wave kernel is for H in (512, 1024)")
     M, V = 128, 256
     X = bf(rnd(M, H, seed=1))
     W = bf(rnd(V, H, scale=H ** -0.5, seed=2))
@@ -234,6 +237,10 @@ def test_fc_xent(ext, fused_dh, H):
         Wf, WTf = ft_layout(W), ft_layout(WT)
         d.update(WT=WT.data_ptr(), dy=dy.data_ptr(), Wf=Wf.data_ptr(), WTf=WTf.data_ptr())
         del d["dl"]
+    if mode == "dl_v256":   # persistent-backward path: 8-wave kernel, row-major dl, no dH
+        from gru_mpi_cuda_amd.ops import ft_layout
+        Wf = ft_layout(W)
+        d.update(Wf=Wf.data_ptr())
     ext.fc_xent(d, S())
     torch.cuda.synchronize()
     if fused_dh:
