@@ -111,7 +111,7 @@ def main() -> int:
     ap.add_argument("--names", type=int, default=4096)
     ap.add_argument("--ref-names", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="engine,torch,ref-schedule")
+    ap.add_argument("--modes", default="engine,engine_fp32,torch,ref-schedule")
     args = ap.parse_args()
 
     from gru_mpi_cuda_amd.config import preset
@@ -138,13 +138,18 @@ def main() -> int:
         return (time.perf_counter() - t0) / reps, o
 
     modes = args.modes.split(",")
-    if "engine" in modes:
+    for prec in ("bf16", "fp32"):
+        key = "engine" if prec == "bf16" else "engine_fp32"
+        if key not in modes and not (prec == "bf16" and "engine" in modes):
+            continue
+        # engine = bf16 MFMA fast mode; engine_fp32 = fp32-faithful mode (the C API default)
         from gru_mpi_cuda_amd.engine.generator import HipGenerator
-        g = HipGenerator(cfg, params, max_batch=args.names, device=dev)
+        g = HipGenerator(cfg, params, max_batch=args.names, device=dev, precision=prec)
         dt, o = timed(lambda: g.generate_device(rf_dev, args.names), args.reps)
         o = o.cpu().numpy()
-        res["engine"] = {"s": round(dt, 5), "chars_per_s": round(_emitted(o) / dt, 1),
-                         "names_per_s": round(args.names / dt, 1)}
+        res[key] = {"precision": prec, "s": round(dt, 5), "chars_per_s": round(_emitted(o) / dt, 1),
+                    "names_per_s": round(args.names / dt, 1)}
+        del g
     if "torch" in modes:
         dt, o = timed(lambda: torch_batched(gparams, cfg, rf_dev), args.reps)
         o = o.cpu().numpy()

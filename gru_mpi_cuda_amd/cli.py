@@ -182,7 +182,7 @@ def cmd_generate(args) -> int:
         cfg.max_len if fmt == "ref" else ckpt.load(args.ckpt, None, "gen")[0].max_len)
     rf = random_floats(N, ml, seed=args.seed)
     t0 = time.perf_counter()
-    G.namegen_initialize(N, args.seed, args.ckpt, cfg, fmt)
+    G.namegen_initialize(N, args.seed, args.ckpt, cfg, fmt, precision=args.precision)
     out = np.zeros(N * (ml + 1), dtype=np.uint8)
     t1 = time.perf_counter()
     G.namegen(N, rf, out)
@@ -237,6 +237,8 @@ def main(argv=None) -> int:
     g.add_argument("-n", type=int, default=10)
     g.add_argument("--out", default=None, help="names, one per line (non-printables escaped)")
     g.add_argument("--raw-out", default=None, help="raw N x (MAX_LEN+1) output bytes")
+    g.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                   help="fp32: faithful to the reference's fp32 arithmetic (default); bf16: MFMA fast mode")
     g.add_argument("--preset", default="ref", help="dims for --fmt ref (headerless blob)")
     _add_model_args(g)
     g.set_defaults(seed=0)

@@ -123,6 +123,7 @@ PYBIND11_MODULE(_C, m) {
         d.V = get<int>(dims, "V", 256); d.E = get<int>(dims, "E", 512); d.H = get<int>(dims, "H", 1024);
         d.L = get<int>(dims, "L", 2); d.max_len = get<int>(dims, "max_len", 10); d.sos = get<int>(dims, "sos", 0);
         d.eos = get<int>(dims, "eos", 0); d.max_batch = get<int>(dims, "max_batch", 4096);
+        d.fp32 = get<int>(dims, "fp32", 0);
         return new Generator(d, Pp<const float>(params), offsets);
       }))
       .def("refresh_weights", [](Generator& g, uintptr_t s) { g.refresh_weights(S(s)); })

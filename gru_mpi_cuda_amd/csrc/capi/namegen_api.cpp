@@ -109,6 +109,10 @@ static void init_impl(int N, int rng_seed, char* parameter_fname) {
   g.V = st.d.V; g.E = st.d.E; g.H = st.d.H; g.L = st.d.L; g.max_len = st.d.max_len;
   g.sos = st.d.sos; g.eos = st.d.eos;
   g.max_batch = std::max(64, std::min(8192, (N + st.world - 1) / std::max(1, st.world)));
+  // the reference's arithmetic is fp32 (namegensf.cu:233-242, 294-333): fp32-faithful by default,
+  // GK_GEN_PRECISION=bf16 selects the bf16 MFMA fast mode
+  const char* prec = std::getenv("GK_GEN_PRECISION");
+  g.fp32 = !(prec && std::string(prec) == "bf16");
   st.gen.reset(new Generator(g, st.params, offsets));
   st.gen->refresh_weights(st.s);
   HIP_CHECK(hipStreamSynchronize(st.s));   // the reference's MPI_Barrier (namegensf.cu:615)

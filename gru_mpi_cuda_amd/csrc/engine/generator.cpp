@@ -26,7 +26,14 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
+  size_t ogh = 0, ogi = 0, olg = 0;
+  if (d_.fp32) {
+    ogh = arena_.reserve((size_t)B * 3 * H * 4);
+    ogi = arena_.reserve((size_t)B * 3 * H * 4);
+    olg = arena_.reserve((size_t)B * V * 4);
+  }
   arena_.commit();
+  if (d_.fp32) { gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg); }
   for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
   for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
   Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); WfcF_ = arena_.get<u16>(oWfcF);
@@ -46,6 +53,14 @@ Generator::~Generator() {
 
 void Generator::refresh_weights(hipStream_t s) {
   const int V = d_.V, E = d_.E, H = d_.H;
+  if (d_.fp32) {   // fp32 layer-0 table P = Emb · W_ih0^T + b_ih0 from the master weights
+    GemmF32Args g;
+    g.A = P("embedding"); g.lda = E; g.B = P("weight_ih_l0"); g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
+    g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;
+    gemm_f32_nt(g, s);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
   CastJobs j;
   j.add(P("embedding"), V, E, Emb_, nullptr);
   for (int l = 0; l < d_.L; ++l) {
@@ -95,6 +110,50 @@ void Generator::record_steps(int n, hipStream_t s) {
   HIP_LAUNCH_CHECK();
 }
 
+// fp32-faithful step: per layer gh = h W_hh^T + b_hh (and gi = x W_ih^T + b_ih above layer 0) as
+// fp32 MFMA GEMMs on the master weights, the gates in IEEE fp32, then logits = h W_fc^T + b_fc and
+// the fp32 softmax sampler -- the reference's per-char arithmetic (namegensf.cu:669-876) batched
+void Generator::record_steps_f32(int n, hipStream_t s) {
+  const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
+  const int Bp = rup(n, 64);
+  for (int l = 0; l < L; ++l) HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * H * 4, s));
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
+  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
+  HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (ML + 1), s));
+  for (int st = 0; st < ML; ++st) {
+    const int cur = st & 1, nxt = cur ^ 1;
+    for (int l = 0; l < L; ++l) {
+      const std::string k = std::to_string(l);
+      GemmF32Args g;
+      g.A = hf_[2 * l + cur]; g.lda = H; g.B = P("weight_hh_l" + k); g.ldb = H; g.C = gh_; g.ldc = 3 * H;
+      g.bias = P("bias_hh_l" + k); g.M = Bp; g.N = 3 * H; g.K = H;
+      gemm_f32_nt(g, s);
+      GruGatesF32Args a;
+      if (l == 0) {
+        a.P = Ptab_; a.ids = ids_;
+      } else {
+        GemmF32Args x;
+        x.A = hf_[2 * (l - 1) + nxt]; x.lda = H; x.B = P("weight_ih_l" + k); x.ldb = H; x.C = gi_; x.ldc = 3 * H;
+        x.bias = P("bias_ih_l" + k); x.M = Bp; x.N = 3 * H; x.K = H;
+        gemm_f32_nt(x, s);
+        a.Gi = gi_;
+      }
+      a.Gh = gh_; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt]; a.Bp = Bp; a.H = H;
+      gru_gates_f32(a, s);
+    }
+    GemmF32Args f;
+    f.A = hf_[2 * (L - 1) + nxt]; f.lda = H; f.B = P("fc.weight"); f.ldb = H; f.C = logits_; f.ldc = V;
+    f.bias = P("fc.bias"); f.M = Bp; f.N = V; f.K = H;
+    gemm_f32_nt(f, s);
+    SampleF32Args q;
+    q.logits = logits_; q.rf = rf_; q.ids = ids_; q.out = out_; q.alive = alive_;
+    q.probs = (st == ML - 1) ? probe_ : nullptr;
+    q.N = n; q.V = V; q.step = st; q.max_len = ML; q.eos = d_.eos;
+    sample_f32(q, s);
+  }
+  HIP_LAUNCH_CHECK();
+}
+
 void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t s) {
   GK_TRACE("gk.generate");
   const int ML = d_.max_len;
@@ -106,12 +165,12 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
       if (!g) {
         g.reset(new Graph());
         g->begin(cap_);
-        record_steps(n, cap_);
+        if (d_.fp32) record_steps_f32(n, cap_); else record_steps(n, cap_);
         g->end(cap_);
       }
       g->launch(s);
     } else {
-      record_steps(n, s);
+      if (d_.fp32) record_steps_f32(n, s); else record_steps(n, s);
     }
     HIP_CHECK(hipMemcpyAsync(out + (size_t)start * (ML + 1), out_, (size_t)n * (ML + 1), hipMemcpyDeviceToDevice, s));
   }

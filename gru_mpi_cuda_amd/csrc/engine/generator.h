@@ -19,6 +19,9 @@ namespace gk {
 
 struct GenDims {
   int V = 256, E = 512, H = 1024, L = 2, max_len = 10, sos = 0, eos = 0, max_batch = 4096;
+  // 1: fp32-faithful (the reference's arithmetic: fp32 MFMA GEMMs on the fp32 master weights, IEEE
+  // gates and softmax, gen_f32.hip); 0: bf16 MFMA fast mode
+  int fp32 = 0;
 };
 
 class Generator {
@@ -34,6 +37,7 @@ class Generator {
 
  private:
   void record_steps(int n_active, hipStream_t s);
+  void record_steps_f32(int n_active, hipStream_t s);
   const float* P(const std::string& n) const { return params_ + off_.at(n); }
 
   GenDims d_;
@@ -54,6 +58,7 @@ class Generator {
   float *Ptab_, *rf_;
   int *ids_, *alive_;
   unsigned char* out_;
+  float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
 };
 
 }  // namespace gk

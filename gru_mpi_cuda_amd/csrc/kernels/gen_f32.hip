@@ -1,0 +1,170 @@
+// fp32-faithful generation kernels (Generator precision "fp32", the C API's default).
+//
+// The reference computes every generation step in fp32: the matvecs (/root/reference/namegensf.cu:
+// 233-242), sigmoid / tanh / Hadamard gates (:676-854), softmax (:294-300, intended semantics
+// :302-313) and the inverse-CDF sampler over fp32 probabilities (:322-333).  The bf16 fast mode
+// rounds the weights and hidden states to bf16, which moves CDF boundaries by ~1e-3 and flips a
+// few percent of names; this path keeps fp32 end to end on the master weights (no copies):
+//   * gemm_f32_nt: C = A · B^T (+ bias) on v_mfma_f32_16x16x4_f32 (true fp32 products, fp32
+//     accumulate), 64 x 64 tiles of 4 waves, 16-deep k-tiles double-buffered through LDS;
+//   * gru_gates_f32: r, z, n gates and h' = (1 - z) n + z h with IEEE expf / tanhf (not the fast
+//     intrinsics), layer 0's input projection gathered from the fp32 table P = Emb W_ih0^T + b_ih0;
+//   * sample_f32: max-subtracted fp32 softmax and the `psum > r` rule (first index whose running
+//     sum exceeds r, else V - 1), EOS written then the name stops (namegensf.cu:877-882).
+#include "kernels.h"
+#include "common.h"
+
+namespace gk {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+namespace {
+constexpr int kT = 64, kBK = 16, kLd = kBK + 4;   // tile, k-tile, padded LDS row (16-B aligned rows)
+}
+
+__global__ void __launch_bounds__(256) gemm_f32_nt_kernel(GemmF32Args g) {
+  __shared__ __attribute__((aligned(16))) float As[2][kT][kLd];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kT][kLd];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * kT, n0 = blockIdx.x * kT;
+  const int lrow = t >> 2, lk = (t & 3) * 4;          // this thread's 16 B of each operand k-tile
+  const float* pa = g.A + (size_t)(m0 + lrow) * g.lda + lk;
+  const float* pb = g.B + (size_t)(n0 + lrow) * g.ldb + lk;
+  float4 ra = *reinterpret_cast<const float4*>(pa);
+  float4 rb = *reinterpret_cast<const float4*>(pb);
+  *reinterpret_cast<float4*>(&As[0][lrow][lk]) = ra;
+  *reinterpret_cast<float4*>(&Bs[0][lrow][lk]) = rb;
+  __syncthreads();
+  f32x4v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fk = lane >> 4;           // MFMA operand: row / column, k within 4
+  const int nk = g.K / kBK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {                                 // next k-tile in flight during the MFMAs
+      ra = *reinterpret_cast<const float4*>(pa + (kt + 1) * kBK);
+      rb = *reinterpret_cast<const float4*>(pb + (kt + 1) * kBK);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kBK / 4; ++kk) {
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[cur][wm * 32 + i * 16 + fr][kk * 4 + fk];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[cur][wn * 32 + j * 16 + fr][kk * 4 + fk];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      *reinterpret_cast<float4*>(&As[cur ^ 1][lrow][lk]) = ra;
+      *reinterpret_cast<float4*>(&Bs[cur ^ 1][lrow][lk]) = rb;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + fr;
+    const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + fk * 4 + r;
+        g.C[(size_t)row * g.ldc + col] = acc[i][j][r] + bias;
+      }
+  }
+}
+
+void gemm_f32_nt(const GemmF32Args& g, hipStream_t s) {
+  if (g.M % kT || g.N % kT || g.K % kBK || g.lda % 4 || g.ldb % 4)
+    throw std::runtime_error("gemm_f32_nt: needs M, N % 64 == 0, K % 16 == 0 and 16-B aligned rows");
+  hipLaunchKernelGGL(gemm_f32_nt_kernel, dim3(g.N / kT, g.M / kT), dim3(256), 0, s, g);
+}
+
+DEV float sigmoid_ieee(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ void gru_gates_f32_kernel(GruGatesF32Args a) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)a.Bp * a.H) return;
+  const int b = (int)(i / a.H), j = (int)(i % a.H), H = a.H;
+  const float* gi = a.P ? a.P + (size_t)a.ids[b] * 3 * H : a.Gi + (size_t)b * 3 * H;
+  const float* gh = a.Gh + (size_t)b * 3 * H;
+  const float r = sigmoid_ieee(gi[j] + gh[j]);
+  const float z = sigmoid_ieee(gi[H + j] + gh[H + j]);
+  const float n = tanhf(gi[2 * H + j] + r * gh[2 * H + j]);
+  a.hout[i] = (1.f - z) * n + z * a.hprev[i];
+}
+
+void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s) {
+  const long n = (long)a.Bp * a.H;
+  hipLaunchKernelGGL(gru_gates_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// One wave per row: lane owns V/64 consecutive logits.  Softmax statistics by wave reductions,
+// then the inclusive CDF (lane-local sums in index order + a wave scan of the lane totals) and
+// the lowest index whose running sum exceeds r.
+__global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
+  const int b = blockIdx.x, lane = threadIdx.x, per = a.V / 64;
+  if (b >= a.N) return;
+  const float* x = a.logits + (size_t)b * a.V + lane * per;
+  // (fixed-bound loops guarded by `per`: the arrays stay in registers)
+  float xv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xv[e] = e < per ? x[e] : -INFINITY;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) mx = fmaxf(mx, xv[e]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float se = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (e < per) se += expf(xv[e] - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+  float p[8];                                       // V <= 512
+  float loc = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    p[e] = e < per ? expf(xv[e] - mx) / se : 0.f;
+    loc += p[e];
+    if (a.probs && e < per) a.probs[(size_t)b * a.V + lane * per + e] = p[e];
+  }
+  float inc = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  const float rnd = a.rf[(size_t)b * a.max_len + a.step];
+  float psum = inc - loc;
+  int hit = a.V;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    psum += p[e];
+    if (e < per && hit == a.V && psum > rnd) hit = lane * per + e;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) hit = min(hit, __shfl_xor(hit, o, 64));
+  if (lane == 0) {
+    const int sel = hit >= a.V ? a.V - 1 : hit;
+    if (a.alive[b]) {
+      a.out[(size_t)b * (a.max_len + 1) + a.step] = (unsigned char)sel;
+      if (sel == a.eos) a.alive[b] = 0;
+    }
+    a.ids[b] = sel;
+  }
+}
+
+void sample_f32(const SampleF32Args& a, hipStream_t s) {
+  if (a.V % 64 || a.V > 512) throw std::runtime_error("sample_f32: needs V % 64 == 0 and V <= 512");
+  if (a.N > 0) hipLaunchKernelGGL(sample_f32_kernel, dim3(a.N), dim3(64), 0, s, a);
+}
+
+}  // namespace gk

@@ -177,6 +177,32 @@ struct FcSampleArgs {              // generation: logits -> softmax -> inverse-C
 };
 void fc_sample(const FcSampleArgs& a, hipStream_t s);
 
+// ------------------------------------------------------------------ fp32-faithful generation (gen_f32.hip)
+struct GemmF32Args {               // C[M][N] = A[M][K] · B[N][K]^T (+ bias[N]), fp32 MFMA
+  const float* A = nullptr; int lda = 0;
+  const float* B = nullptr; int ldb = 0;
+  float* C = nullptr; int ldc = 0;
+  const float* bias = nullptr;
+  int M = 0, N = 0, K = 0;         // M, N % 64 == 0, K % 16 == 0
+};
+void gemm_f32_nt(const GemmF32Args& g, hipStream_t s);
+struct GruGatesF32Args {           // h' = GRU gates from gi (or P[ids]) and gh = h W_hh^T + b_hh
+  const float* P = nullptr; const int* ids = nullptr;   // layer 0: gi row = P[ids[b]] ([V][3H])
+  const float* Gi = nullptr;       // layers >= 1: [Bp][3H] (with b_ih)
+  const float* Gh = nullptr;       // [Bp][3H] (with b_hh)
+  const float* hprev = nullptr; float* hout = nullptr;   // [Bp][H]
+  int Bp = 0, H = 0;
+};
+void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s);
+struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sample (same I/O as fc_sample)
+  const float* logits = nullptr;   // [Bp][V]
+  const float* rf = nullptr;
+  int* ids = nullptr; unsigned char* out = nullptr; int* alive = nullptr;
+  float* probs = nullptr;
+  int N = 0, V = 0, step = 0, max_len = 0, eos = 0;
+};
+void sample_f32(const SampleF32Args& a, hipStream_t s);
+
 // ------------------------------------------------------------------ generic GEMM
 // C[M][N] (+)= A[M][K] · B[N][K]^T  (bf16 in, fp32 accumulate), both operands K-contiguous.
 struct GemmArgs {

@@ -29,9 +29,20 @@ from ..models.params import flat_layout, pad_config, pad_params, to_flat
 from ..parallel.dist import DistCtx, shard
 
 
+PRECISIONS = ("fp32", "bf16")
+
+
 class HipGenerator:
+    """precision "fp32" (default): fp32-faithful -- fp32 MFMA GEMMs on the fp32 master weights,
+    IEEE gates and softmax, the reference's arithmetic (namegensf.cu:233-242, 294-333);
+    "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies)."""
+
     def __init__(self, cfg: GRUConfig, params: Dict[str, torch.Tensor], max_batch: int = 4096,
-                 device: Optional[torch.device] = None, flat: Optional[torch.Tensor] = None):
+                 device: Optional[torch.device] = None, flat: Optional[torch.Tensor] = None,
+                 precision: str = "fp32"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}")
+        self.precision = precision
         from ..ops import load_ext
         self.C = load_ext()
         self.cfg = cfg
@@ -49,7 +60,7 @@ class HipGenerator:
         self.flat = flat if flat is not None else to_flat(icfg, params).to(self.dev)
         offsets = {s.name: s.offset for s in self.layout.segments}
         dims = dict(V=cfg.vocab, E=icfg.embed, H=icfg.hidden, L=cfg.layers, max_len=cfg.max_len,
-                    sos=cfg.sos, eos=cfg.eos, max_batch=max_batch)
+                    sos=cfg.sos, eos=cfg.eos, max_batch=max_batch, fp32=int(precision == "fp32"))
         self.g = self.C.Generator(dims, self.flat.data_ptr(), offsets)
         self.g.refresh_weights(self._s())
 
@@ -84,8 +95,9 @@ _S: Optional[_State] = None
 
 
 def namegen_initialize(N: int, rng_seed: int, parameter_fname: str, cfg: Optional[GRUConfig] = None,
-                       fmt: str = "auto", ctx: Optional[DistCtx] = None) -> None:
-    """namegensf.cu:359-618.  ``rng_seed`` is accepted and unused, as in the reference."""
+                       fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "fp32") -> None:
+    """namegensf.cu:359-618.  ``rng_seed`` is accepted and unused, as in the reference.
+    ``precision``: "fp32" (faithful, default) or "bf16" (fast mode) on the GPU path."""
     global _S
     from ..parallel import dist as gdist
     from ..utils import ckpt
@@ -109,7 +121,7 @@ def namegen_initialize(N: int, rng_seed: int, parameter_fname: str, cfg: Optiona
         if s.comm is not None:
             s.comm.broadcast_f32(flat.data_ptr(), lay.total, 0, torch.cuda.current_stream().cuda_stream)
         s.gen = HipGenerator(s.cfg, {}, device=s.ctx.device, flat=flat,
-                             max_batch=max(64, min(8192, N // max(1, s.ctx.world) + 1)))
+                             max_batch=max(64, min(8192, N // max(1, s.ctx.world) + 1)), precision=precision)
     else:
         lay = flat_layout(s.cfg)
         flat = to_flat(s.cfg, params) if params is not None else torch.zeros(lay.total)

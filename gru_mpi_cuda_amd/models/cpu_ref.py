@@ -176,7 +176,8 @@ class Adam:
 def sample_inverse_cdf(prob: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     """The reference's ``random_select`` (namegensf.cu:322-333): first i with an fp32
     running sum ``psum > r`` in index order, else n-1.  prob [N, V], r [N]."""
-    cs = torch.cumsum(prob.to(torch.float32), dim=-1)        # sequential fp32 prefix on CPU
+    # sequential prefix on CPU: fp32 like the reference, or fp64 for the exact-math oracle
+    cs = torch.cumsum(prob if prob.dtype == torch.float64 else prob.to(torch.float32), dim=-1)
     hit = cs > r.unsqueeze(-1)
     idx = hit.to(torch.int64).argmax(-1)
     return torch.where(hit.any(-1), idx, torch.full_like(idx, prob.shape[-1] - 1))
@@ -210,8 +211,8 @@ def generate(params: Params, cfg: GRUConfig, rfloats: np.ndarray, start: int = 0
             hs[k], _ = _gates(gi, gh, hs[k])
             inp = hs[k]
         logits = inp @ params["fc.weight"].T + params["fc.bias"]
-        prob = torch.softmax(logits.to(torch.float32), -1)
-        sel = sample_inverse_cdf(prob, rf[:, l])
+        prob = torch.softmax(logits if dt == torch.float64 else logits.to(torch.float32), -1)
+        sel = sample_inverse_cdf(prob, rf[:, l].to(prob.dtype))
         out[alive.numpy(), l] = sel[alive].numpy().astype(np.uint8)
         alive &= sel != cfg.eos
         cur = sel
