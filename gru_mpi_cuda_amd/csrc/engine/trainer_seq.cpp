@@ -10,6 +10,7 @@
 // co-resident (gru_*_seq_supported), so any config still runs -- just slower.
 #include "trainer.h"
 #include <algorithm>
+#include <string>
 
 namespace gk {
 
@@ -18,8 +19,53 @@ static bool env_flag(const char* name, bool dflt) {
   return v && v[0] ? v[0] != '0' : dflt;
 }
 
+// Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
+// split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
+// 128 x 128 split-K path only.  GK_WGRAD_GEMM overrides the default.
+static int wgrad_engine() {   // read at record time (tests switch it per trainer)
+  const char* v = std::getenv("GK_WGRAD_GEMM");
+  if (!v || !*v) return 256;
+  if (std::string(v) == "lib") return 1;
+  if (std::string(v) == "128") return 128;
+  return 256;
+}
+
+// split-K depth for gemm256: the one that fills whole waves of 256 workgroups best (ties: the
+// shallower, fewer slabs), K-slices at least 2048 deep
+static int gemm256_splits(int M, int N, int K) {
+  const int tiles = (M / 256) * (N / 256);
+  int best = 0;
+  double best_fill = 0.0;
+  for (int sp = 1; sp <= 8; sp *= 2) {
+    if (K % sp || (K / sp) % 64 || (sp > 1 && K / sp < 2048)) continue;
+    const int wg = tiles * sp, rounds = (wg + 255) / 256;
+    const double fill = (double)wg / (rounds * 256);
+    if (fill > best_fill + 1e-9) { best_fill = fill; best = sp; }
+  }
+  return best_fill >= 0.7 ? best : 0;
+}
+
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
+  if (wgrad_engine() == 256) {
+    GemmArgs w;
+    w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.M = M; w.N = N; w.K = K;
+    const int sp = gemm256_splits(M, N, K);
+    w.splits = std::max(sp, 1);
+    w.C = sp == 1 ? dst : slab_w_; w.ldc = N;
+    if (rowsum_dst) w.rowsumA = sp == 1 ? rowsum_dst : rs_w_;   // bias gradient fused (row sums of A)
+    if (sp && sp <= splits_ && gemm256_ok(w)) {
+      w.algo = 5;
+      gemm_nt(w, s);
+      if (sp > 1) {
+        SlabJobs j;
+        j.add(slab_w_, sp, (long)M * N, dst);
+        if (rowsum_dst) j.add(rs_w_, sp, M, rowsum_dst);
+        reduce_slabs_multi(j, s);
+      }
+      return;
+    }
+  }
   // split K only as deep as it takes to give the chip ~256 workgroups: every extra split costs a
   // full M x N fp32 slab written and read again (8 slabs of dW_hh at H=1024 = 100 MB).  With no
   // split the GEMM writes the gradient (and the bias row sums) directly.
@@ -29,7 +75,7 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
     GemmArgs w;
     w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
     w.M = M; w.N = N; w.K = K;
-    if (gemm_library_wanted(w) && gemm_library_ok(w)) {
+    if (wgrad_engine() != 128 && gemm_library_wanted(w) && gemm_library_ok(w)) {
       gemm_nt(w, s);
       return;
     }

@@ -160,6 +160,10 @@ bool gemm_library_wanted(const GemmArgs& a) {
   return true;
 }
 
+void rowsum_bf16(const u16* A, int lda, int M, int K, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(M), dim3(256), 0, s, A, lda, K, out);
+}
+
 static bool gemm_library(const GemmArgs& a, hipStream_t s) {
   if (!gemm_library_ok(a)) return false;
   if (!blaslt_gemm_nt(a.A, a.lda, a.B, a.ldb, a.C, a.ldc, a.M, a.N, a.K, a.accumulate != 0, s)) return false;
@@ -171,9 +175,19 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
   // large plain products: hipBLASLt (bf16 in, fp32 out), when it has an algorithm for the shape
   if (gemm_library_wanted(a) && gemm_library(a, s)) return;
   if (a.algo == 4) throw std::runtime_error("gemm_nt: library GEMM requested but not available for this shape");
+  if (a.algo == 5) {
+    if (!gemm256_ok(a)) throw_gemm_shape();
+    gemm256(a, s);
+    return;
+  }
   if (a.algo == 3) {
     if (!gemm_small_kblocks(a)) throw_gemm_shape();
     gemm_small(a, s);
+    return;
+  }
+  // large plain products (a full wave of 256 x 256 tiles): the 256 x 256 LDS kernel
+  if (a.algo == 0 && a.splits == 1 && gemm256_ok(a) && (a.M / 256) * (a.N / 256) >= 256 && a.K >= 256) {
+    gemm256(a, s);
     return;
   }
   // latency-bound regime (fewer than one 128 x 128 workgroup per CU): the one-shot small kernel

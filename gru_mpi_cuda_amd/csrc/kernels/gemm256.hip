@@ -1,0 +1,207 @@
+// 256 x 256 x 64 bf16 MFMA GEMM for the large plain products (the weight gradients over B*T tokens
+// at H >= 1024, the hoisted input projections, FC dH at large H):
+//     C[M][N] (+)= A[M][K] · B[N][K]^T (+ bias[N]),  fp32 accumulate, optional split-K slabs.
+//
+// gfx950 structure (cdna_hip_programming.md §5, the 256² geometry):
+//   * one 512-thread workgroup per CU (128 KiB LDS), 8 waves as 2 (M) x 4 (N), each wave a 128 x 64
+//     output of 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators (128 VGPRs), 64 MFMAs per wave per
+//     64-deep k-tile -- 4x the MFMA work per staged byte of the 128² kernel (gemm_lds.hip);
+//   * staging global -> LDS with global_load_lds_dwordx4 only (no VGPR round trip): a k-tile is four
+//     16 KiB half-tiles (A rows 0-127 / 128-255, B rows 0-127 / 128-255), each a lane-linear
+//     [128][64] image filled by 2 wave-instructions per wave; the bank swizzle (16-B chunk c of row
+//     r in slot c ^ ((r >> 1) & 7), conflict-free ds_read_b128 fragment reads, docs/DESIGN.md) is
+//     applied on the per-lane SOURCE address and on the read;
+//   * two k-tile buffers: tile t+1 is issued at the top of tile t and lands under its 64 MFMAs per
+//     wave (~2k cycles per SIMD); one vmcnt(0) + barrier per k-tile;
+//   * per k-tile the wave runs four groups of 16 MFMAs (k-step x row half) with the fragments of
+//     the next group read under the current one (register double buffer, order pinned);
+//   * bijective XCD-aware block remap, then a grouped raster (4 tile-rows x all columns) so an
+//     XCD's resident workgroups share A and B panels in its L2.
+// Measured (scripts/bench_gemm.py, random operands, profiles/r2_gemm256.jsonl): 4096^3 1172 TF,
+// 8192^3 1287 TF (hipBLASLt on the same box 1190 / 1441); the 128^2 kernel 906 / 893.
+#include <stdexcept>
+#include <string>
+#include "kernels.h"
+#include "common.h"
+
+namespace gk {
+
+typedef __attribute__((address_space(3))) void lds256_t;
+
+namespace {
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+}
+
+DEV int xcd_remap256(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// acc + sum of the 8 bf16 of v: four v_dot2c_f32_bf16 against (1, 1) -- a quarter of the VALU
+// issue of eight converts + adds, which beside the MFMAs slowed the row-sum waves' workgroups 8 %
+DEV float add_sum8(const bf16x8& v, float acc) {
+  const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{v[2 * i], v[2 * i + 1]}, one, acc, false);
+  return acc;
+}
+
+// RS: also the row sums of A (the bias gradient of a weight-gradient product) into
+// rowsumA[split][M], from the A fragments already in registers -- by the waves of the first column
+// tile that read each row (wave column 0 of tile column 0), instead of a second pass over A
+template <bool BIAS, bool ACC, bool RS>
+__global__ void __launch_bounds__(512, 1) gemm256_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  // [buffer][A | B][half][128 rows x 64 bf16]: one array (a second __shared__ object can make
+  // hipcc drain vmcnt before every ds_read, cdna_hip_programming.md §5 item 4a)
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][2][128 * 64];
+  const int id = xcd_remap256(blockIdx.x, gridDim.x);
+  // grouped raster inside each split: runs of kGroupM tile-rows, column-major within the run, so an
+  // XCD's ~32 resident workgroups cover a 4 x 8 block of tiles (4 A panels + 8 B panels in its L2)
+  // instead of 1 x 32 (1 + 32 panels)
+  constexpr int kGroupM = 4;
+  const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
+  const int per_group = kGroupM * ntn, first_m = (pid / per_group) * kGroupM;
+  const int gm = min(ntm - first_m, kGroupM);
+  const int tm = first_m + (pid % per_group) % gm, tn = (pid % per_group) / gm;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int row0 = tm * kBM, col0 = tn * kBN;
+  const int kbeg = sp * kper, nk = kper / kBK;
+
+  // staging: wave w's instruction q of a half-tile covers rows (2w + q) * 8 .. + 7
+  const int srow = lane >> 3, sslot = lane & 7;
+  const u16* src[2][2][2];   // [A | B][half][q]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (2 * w + q) * 8 + srow;
+      const int c = sslot ^ ((r >> 1) & 7);
+      src[0][h][q] = a.A + (size_t)(row0 + h * 128 + r) * a.lda + kbeg + c * 8;
+      src[1][h][q] = a.B + (size_t)(col0 + h * 128 + r) * a.ldb + kbeg + c * 8;
+    }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int op = 0; op < 2; ++op)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          __builtin_amdgcn_global_load_lds(src[op][h][q] + kt * kBK, (lds256_t*)(&lds[buf][op][h][(2 * w + q) * 8 * 64]),
+                                           16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int bh = wc >> 1, bo = (wc & 1) * 64;   // this wave's B half and row offset inside it
+  // fragment reads: A row tile i (0..7) / B column tile j (0..3) at k-step ks of buffer buf
+  auto rdA = [&](int buf, int i, int ks) {
+    const int r = i * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][0][wr][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  auto rdB = [&](int buf, int j, int ks) {
+    const int r = bo + j * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][1][bh][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  // A k-tile is 4 groups g = (k-step g >> 1, row half g & 1) of 16 MFMAs; the fragments of group
+  // g + 1 are read BEFORE the MFMAs of group g (register double buffer), so every LDS read has a
+  // 16-MFMA group (~256 cycles) to land instead of stalling the next MFMA.
+  bf16x8 a0[4], a1[4], b0[4], b1[4];
+  const bool do_rs = RS && tn == 0 && wc == 0;   // wave-uniform
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#define GK_RDA(dst, buf, g) { for (int i = 0; i < 4; ++i) dst[i] = rdA(buf, ((g) & 1) * 4 + i, (g) >> 1); }
+#define GK_RDB(dst, buf, g) { for (int j = 0; j < 4; ++j) dst[j] = rdB(buf, j, (g) >> 1); }
+#define GK_MMA(ga, gb, g) { for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) \
+    acc[((g) & 1) * 4 + i][j] = mfma16(ga[i], gb[j], acc[((g) & 1) * 4 + i][j]); \
+    if (do_rs) for (int i = 0; i < 4; ++i) rs[((g) & 1) * 4 + i] = add_sum8(ga[i], rs[((g) & 1) * 4 + i]); }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    // (sched_barrier pins the block order: left alone, hipcc sinks each read to just before its
+    // first use and waits lgkmcnt(0) there)
+    // (sched_barrier pins the block order: left alone, hipcc sinks each read to just before its
+    // first use and waits lgkmcnt(0) there.  Measured and not kept: a third A set + setprio(1)
+    // around each MFMA group, within noise of this order -- profiles/r2_gemm256.jsonl)
+    GK_RDA(a0, cur, 0); GK_RDB(b0, cur, 0);
+    GK_RDA(a1, cur, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(a0, b0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_RDA(a0, cur, 2); GK_RDB(b1, cur, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(a1, b0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_RDA(a1, cur, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(a0, b1, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(a1, b1, 3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef GK_RDA
+#undef GK_RDB
+#undef GK_MMA
+
+  if (do_rs) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float v = rs[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + wr * 128 + t * 16 + lane] = v;
+    }
+  }
+  float* C = a.C + (size_t)sp * a.M * a.ldc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + wc * 64 + j * 16 + lr;
+    const float bb = BIAS ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + wr * 128 + i * 16 + lq * 4 + e;
+        float* dst = C + (size_t)row * a.ldc + col;
+        const float v = acc[i][j][e] + bb;
+        if (ACC) *dst += v; else *dst = v;
+      }
+  }
+}
+
+bool gemm256_ok(const GemmArgs& a) {
+  if (a.onehot_ids || !a.A) return false;
+  if (a.M % kBM || a.N % kBN || a.splits < 1 || a.K % a.splits) return false;
+  const int kper = a.K / a.splits;
+  if (kper % kBK || a.lda % 8 || a.ldb % 8) return false;
+  if (a.splits > 1 && (a.bias || a.accumulate || a.ldc != a.N)) return false;
+  if (a.rowsumA && (a.bias || a.accumulate)) return false;
+  return true;
+}
+
+void gemm256(const GemmArgs& a, hipStream_t s) {
+  if (!gemm256_ok(a)) throw std::runtime_error("gemm256: unsupported shape");
+  const int ntn = a.N / kBN, ntm = a.M / kBM, kper = a.K / a.splits;
+  const dim3 grid(ntn * ntm * a.splits), block(512);
+#define GK_L(B_, A_, R_) hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper)
+  if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate
+    if (a.bias || a.accumulate) throw std::runtime_error("gemm256: row sums only without bias / accumulate");
+    GK_L(false, false, true);
+  } else if (a.bias) {
+    if (a.accumulate) GK_L(true, true, false); else GK_L(true, false, false);
+  } else {
+    if (a.accumulate) GK_L(false, true, false); else GK_L(false, false, false);
+  }
+#undef GK_L
+}
+
+}  // namespace gk

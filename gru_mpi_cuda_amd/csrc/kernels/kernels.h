@@ -216,13 +216,18 @@ struct GemmArgs {
   int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
   int accumulate = 0;              // C += result instead of C = result
   int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
-                                   // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel)
+                                   // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel),
+                                   // 5 LDS-staged 256x256 (gemm256.hip)
 };
 // algo 0 sends plain (no one-hot, no bias, unsplit) products of >= GK_BLASLT_MIN_GFLOP to hipBLASLt
 bool gemm_library_ok(const GemmArgs& a);
 bool gemm_library_wanted(const GemmArgs& a);
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
+bool gemm256_ok(const GemmArgs& a);
+void gemm256(const GemmArgs& a, hipStream_t s);
+// out[m] = sum_k A[m][k] (bf16 A, fp32 sums; the bias gradient beside a GEMM without row sums)
+void rowsum_bf16(const u16* A, int lda, int M, int K, float* out, hipStream_t s);
 // several independent LDS-GEMM problems in ONE launch (fills the chip with small products);
 // all jobs gemm_lds_ok, with the same bias / row-sum flags; n <= 4
 void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s);

@@ -1,5 +1,7 @@
-"""GEMM microbenchmark: register-direct 64x64 kernel vs LDS-staged 128x128 kernel vs torch
-(hipBLASLt) on the engine's shapes.  Random uniform [-1,1) bf16 operands (guide rule 25)."""
+"""GEMM microbenchmark on the engine's shapes: register-direct 64x64 kernel (algo 1), LDS-staged
+128x128 (algo 2), hipBLASLt through the engine's wrapper (algo 4), LDS-staged 256x256 (algo 5, at
+several split-K depths) and torch (hipBLASLt).  Random uniform [-1,1) bf16 operands (guide rule 25).
+GEMM_SHAPES=name1,name2 restricts the run."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -21,7 +23,14 @@ SHAPES = [  # (name, M, N, K, splits)
     ("h2048.dW_hh", 6144, 2048, 65536, 8),
     ("h2048.dH", 65536, 2048, 256, 1),
     ("sq4096", 4096, 4096, 4096, 1),
+    ("sq8192", 8192, 8192, 8192, 1),
+    ("h2048.step_fwd", 512, 6144, 2048, 1),
+    ("h2048.step_bwd", 512, 2048, 6144, 1),
+    ("h1024.step_bwd_b1024", 1024, 1024, 3072, 1),
 ]
+if os.environ.get("GEMM_SHAPES"):
+    keep = set(os.environ["GEMM_SHAPES"].split(","))
+    SHAPES = [s for s in SHAPES if s[0] in keep]
 
 
 def timeit(fn, n=20):
@@ -45,19 +54,23 @@ for name, M, N, K, sp in SHAPES:
     flop = 2.0 * M * N * K
     row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp}
     ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 34 else None
-    for algo in (1, 2):
+    variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
+    for algo, ks in variants:
+        if ks > 1 and Cs.shape[0] < ks:
+            Cs = torch.empty(ks, M, N, device=dev)
         d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,
-                 splits=sp, algo=algo)
+                 splits=ks, algo=algo)
+        tag = f"algo{algo}" + (f"s{ks}" if algo == 5 else "")
         try:
             us = timeit(lambda: C.gemm_nt(d, s))
         except RuntimeError as e:
-            row[f"algo{algo}"] = str(e)[:60]
+            row[tag] = str(e)[:60]
             continue
-        row[f"algo{algo}_us"] = round(us, 1)
-        row[f"algo{algo}_tflops"] = round(flop / us / 1e6, 1)
+        row[f"{tag}_us"] = round(us, 1)
+        row[f"{tag}_tflops"] = round(flop / us / 1e6, 1)
         if ref is not None:
-            err = float((Cs.sum(0) - ref).abs().max() / ref.abs().max())
-            row[f"algo{algo}_relerr"] = float(f"{err:.2e}")
+            err = float((Cs[:ks].sum(0) - ref).abs().max() / ref.abs().max())
+            row[f"{tag}_relerr"] = float(f"{err:.2e}")
     us = timeit(lambda: A @ B.T)
     row["torch_us"] = round(us, 1)
     row["torch_tflops"] = round(flop / us / 1e6, 1)

@@ -327,3 +327,35 @@ def test_reduce_slabs_cast(ext, R, C, splits):
         ref += src[k]
     assert torch.equal(dst, ref)
     assert torch.equal(bf, ref.bfloat16()) and torch.equal(bT, ref.bfloat16().T.contiguous())
+
+
+@pytest.mark.parametrize("M,N,K,splits,bias,accumulate,lda_pad,rowsum", [
+    (256, 256, 64, 1, True, False, 0, False), (512, 768, 1024, 1, True, False, 0, False),
+    (768, 512, 2048, 4, False, False, 0, True), (1024, 1024, 3072, 1, False, True, 0, False),
+    (512, 256, 4096, 8, False, False, 64, True), (2304, 1280, 576, 1, True, True, 32, False),
+    (1536, 512, 8192, 4, False, False, 0, True), (512, 768, 1024, 1, False, False, 0, True)])
+def test_gemm256(ext, M, N, K, splits, bias, accumulate, lda_pad, rowsum):
+    """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
+    operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
+    bias gradient of a weight-gradient product, one partial per split)."""
+    lda = K + lda_pad
+    Af = bf(rnd(M, lda, seed=4))
+    A, B = Af[:, :K], bf(rnd(N, K, seed=5) + 0.1 * torch.arange(K, device=DEV) / K)
+    bv = rnd(N, seed=6) if bias else None
+    C0 = rnd(M, N, seed=7)
+    C = torch.full((splits, M, N), float("nan"), device=DEV)
+    if accumulate:
+        C[0] = C0
+    d = dict(A=Af.data_ptr(), lda=lda, B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=M, N=N, K=K,
+             splits=splits, algo=5, accumulate=int(accumulate))
+    if bv is not None:
+        d["bias"] = bv.data_ptr()
+    rs = torch.full((splits, M), float("nan"), device=DEV)
+    if rowsum:
+        d["rowsumA"] = rs.data_ptr()
+    ext.gemm_nt(d, S())
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().T + (bv if bv is not None else 0) + (C0 if accumulate else 0)
+    torch.testing.assert_close(C.sum(0), ref, atol=2e-3 * K ** 0.5, rtol=1e-3)
+    if rowsum:
+        torch.testing.assert_close(rs.sum(0), A.float().sum(1), atol=1e-2, rtol=1e-3)
