@@ -585,6 +585,12 @@ long Trainer::group_end(int l) const {
 void Trainer::ar_flush(hipStream_t s, bool force) {
   const long n = ar_ready_ - ar_launched_;
   if (n <= 0 || (!force && n < min_bucket_)) return;
+  if (!env_on("GK_AR_FORK", true)) {   // A/B switch: the collective in line on the step stream
+    comm_->allreduce_avg_f32(grads_ + ar_launched_, n, s);
+    ar_log_.push_back({ar_launched_, n});
+    ar_launched_ = ar_ready_;
+    return;
+  }
   hipEvent_t e = ev();
   HIP_CHECK(hipEventRecord(e, s));          // fork: everything recorded on s so far
   HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
@@ -635,6 +641,7 @@ void Trainer::step(hipStream_t s) {
       if (dp_overlap()) {
         // readiness-ordered collectives on the comm stream, overlapped with the rest of the
         // backward; joined before the optimiser (the embedding-side tail runs after the join)
+        deferred_.n = 0;
         record_fb_seq(s0_, /*dp=*/true);
       } else {
         deferred_.n = 0;

@@ -336,7 +336,13 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients
-  if (dp) record_emb_tail(s, dP_target());          // from the averaged dP
+  if (dp) {
+    // from the averaged dP; its dEmb slabs are already global (after the collective), so like the
+    // single-GPU step they are summed inside the Adam launch (one reduce launch fewer)
+    defer_slabs_ = o_.clip <= 0.f && env_flag("GK_DEFER_SLABS", true);
+    record_emb_tail(s, dP_target());
+    defer_slabs_ = false;
+  }
   else record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
   HIP_LAUNCH_CHECK();
 }

@@ -127,8 +127,6 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(GemmArgs a, int ntn, in
     const int cur = kt & 1;
     if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
     // (sched_barrier pins the block order: left alone, hipcc sinks each read to just before its
-    // first use and waits lgkmcnt(0) there)
-    // (sched_barrier pins the block order: left alone, hipcc sinks each read to just before its
     // first use and waits lgkmcnt(0) there.  Measured and not kept: a third A set + setprio(1)
     // around each MFMA group, within noise of this order -- profiles/r2_gemm256.jsonl)
     GK_RDA(a0, cur, 0); GK_RDB(b0, cur, 0);
