@@ -148,7 +148,7 @@ def main() -> int:
         dt, o = timed(lambda: g.generate_device(rf_dev, args.names), args.reps)
         o = o.cpu().numpy()
         res[key] = {"precision": prec, "s": round(dt, 5), "chars_per_s": round(_emitted(o) / dt, 1),
-                    "names_per_s": round(args.names / dt, 1)}
+                    "names_per_s": round(args.names / dt, 1), "error_word": int(g.g.read_error())}
         del g
     if "torch" in modes:
         dt, o = timed(lambda: torch_batched(gparams, cfg, rf_dev), args.reps)

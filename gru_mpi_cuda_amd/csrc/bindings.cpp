@@ -131,6 +131,7 @@ PYBIND11_MODULE(_C, m) {
         g.generate(Pp<const float>(rf), N, Pp<unsigned char>(out), S(s));
       })
       .def("set_use_graph", &Generator::set_use_graph)
+      .def("read_error", &Generator::read_error)
       .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); });
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)

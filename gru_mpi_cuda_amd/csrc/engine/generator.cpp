@@ -3,6 +3,8 @@
 #include "../runtime/blaslt.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 namespace gk {
 
@@ -26,13 +28,14 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
-  size_t ogh = 0, ogi = 0, olg = 0;
+  size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256);
   if (d_.fp32) {
     ogh = arena_.reserve((size_t)B * 3 * H * 4);
     ogi = arena_.reserve((size_t)B * 3 * H * 4);
     olg = arena_.reserve((size_t)B * V * 4);
   }
   arena_.commit();
+  err_ = arena_.get<unsigned>(oerr);
   if (d_.fp32) { gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg); }
   for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
   for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
@@ -77,17 +80,26 @@ void Generator::refresh_weights(hipStream_t s) {
   HIP_LAUNCH_CHECK();
 }
 
+// Per-batch state reset as one kernel node.  Replays of a graph whose reset was five memset
+// nodes (h, ids, alive, out) left stale and garbage ids in the padded rows of the fp32 path and
+// made replays disagree (scripts/repro_gen_fp32.py with SYNC_FIRST=1: error word 16, replays not
+// identical); a kernel node is ordered like every other node of the chain.
+void Generator::reset_batch(int Bp, bool bf16, hipStream_t s) {
+  GenResetArgs r;
+  r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
+  for (int l = 0; l < d_.L; ++l) {
+    r.hf[l] = hf_[2 * l];
+    r.hb[l] = bf16 ? hb_[2 * l] : nullptr;
+  }
+  r.ids = ids_; r.alive = alive_; r.out = out_;
+  gen_reset(r, s);
+}
+
 void Generator::record_steps(int n, hipStream_t s) {
   const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
   const int Bp = rup(n, 32);
   // per-batch init (part of the graph): h = 0, input = SOS, alive = 1, output rows = NUL
-  for (int l = 0; l < L; ++l) {
-    HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * H * 4, s));
-    HIP_CHECK(hipMemsetAsync(hb_[2 * l], 0, (size_t)Bp * H * 2, s));
-  }
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
-  HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (ML + 1), s));
+  reset_batch(Bp, true, s);
   for (int st = 0; st < ML; ++st) {
     const int cur = st & 1, nxt = cur ^ 1;
     for (int l = 0; l < L; ++l) {
@@ -116,10 +128,7 @@ void Generator::record_steps(int n, hipStream_t s) {
 void Generator::record_steps_f32(int n, hipStream_t s) {
   const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
   const int Bp = rup(n, 64);
-  for (int l = 0; l < L; ++l) HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * H * 4, s));
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
-  HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
-  HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (ML + 1), s));
+  reset_batch(Bp, false, s);
   for (int st = 0; st < ML; ++st) {
     const int cur = st & 1, nxt = cur ^ 1;
     for (int l = 0; l < L; ++l) {
@@ -139,6 +148,7 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
         a.Gi = gi_;
       }
       a.Gh = gh_; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt]; a.Bp = Bp; a.H = H;
+      a.V = V; a.err = err_;
       gru_gates_f32(a, s);
     }
     GemmF32Args f;
@@ -174,6 +184,15 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
     }
     HIP_CHECK(hipMemcpyAsync(out + (size_t)start * (ML + 1), out_, (size_t)n * (ML + 1), hipMemcpyDeviceToDevice, s));
   }
+}
+
+unsigned Generator::read_error() {
+  unsigned e[4] = {0, 0, 0, 0};
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(e, err_, 16, hipMemcpyDeviceToHost));
+  if (e[0] && std::getenv("GK_GEN_DEBUG"))
+    std::fprintf(stderr, "[generator] error word %u: id %d (0x%08x) at row %u\n", e[0], (int)e[1], e[1], e[2]);
+  return e[0];
 }
 
 }  // namespace gk

@@ -34,10 +34,12 @@ class Generator {
   void set_use_graph(bool g) { use_graph_ = g; }
   // optional: device [Bp][V] softmax of the last generated step (tests)
   void set_probe(float* probs) { probe_ = probs; graphs_.clear(); }
+  unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
 
  private:
   void record_steps(int n_active, hipStream_t s);
   void record_steps_f32(int n_active, hipStream_t s);
+  void reset_batch(int Bp, bool bf16, hipStream_t s);
   const float* P(const std::string& n) const { return params_ + off_.at(n); }
 
   GenDims d_;
@@ -59,6 +61,7 @@ class Generator {
   int *ids_, *alive_;
   unsigned char* out_;
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
+  unsigned* err_ = nullptr;
 };
 
 }  // namespace gk

@@ -156,7 +156,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
       if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
-      if (!seq_[l].bwd) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
+      // (zeroed by a kernel node, not a memset node: memset nodes misbehaved on graph replay in
+      // the generator, see Generator::reset_batch)
+      if (!seq_[l].bwd) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       gru_fwd_seq(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
@@ -249,7 +251,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
-      if (!persist_fwd_) HIP_CHECK(hipMemsetAsync(a.cnt, 0, (size_t)fw * 4, s));
+      if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       gru_bwd_seq(a, s);
     } else {
       for (int t = T - 1; t >= 0; --t) bwd_step(l, t, s);

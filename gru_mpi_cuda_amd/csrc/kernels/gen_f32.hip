@@ -93,7 +93,19 @@ __global__ void gru_gates_f32_kernel(GruGatesF32Args a) {
   const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (i >= (long)a.Bp * a.H) return;
   const int b = (int)(i / a.H), j = (int)(i % a.H), H = a.H;
-  const float* gi = a.P ? a.P + (size_t)a.ids[b] * 3 * H : a.Gi + (size_t)b * 3 * H;
+  const float* gi = a.Gi + (size_t)b * 3 * H;
+  if (a.P) {
+    int id = a.ids[b];
+    if (id < 0 || id >= a.V) {   // never expected: flag it instead of reading outside the table
+      if (a.err && j == 0) {
+        atomicOr(a.err, 16u);
+        a.err[1] = (unsigned)id;   // diagnostics: the offending value and row
+        a.err[2] = (unsigned)b;
+      }
+      id = 0;
+    }
+    gi = a.P + (size_t)id * 3 * H;
+  }
   const float* gh = a.Gh + (size_t)b * 3 * H;
   const float r = sigmoid_ieee(gi[j] + gh[j]);
   const float z = sigmoid_ieee(gi[H + j] + gh[H + j]);
@@ -160,6 +172,25 @@ __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
     }
     a.ids[b] = sel;
   }
+}
+
+__global__ void gen_reset_kernel(GenResetArgs a) {
+  const long n = (long)a.Bp * a.H, stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      if (l < a.L) {
+        a.hf[l][i] = 0.f;
+        if (a.hb[l]) a.hb[l][i] = 0;
+      }
+    }
+    if (i < a.Bp) { a.ids[i] = a.sos; a.alive[i] = 1; }
+    if (i < (long)a.Bp * (a.ML + 1)) a.out[i] = 0;
+  }
+}
+void gen_reset(const GenResetArgs& a, hipStream_t s) {
+  if (a.L > 4 || a.H < a.ML + 1) throw std::runtime_error("gen_reset: at most 4 layers, H > max_len");
+  hipLaunchKernelGGL(gen_reset_kernel, dim3(256), dim3(256), 0, s, a);
 }
 
 void sample_f32(const SampleF32Args& a, hipStream_t s) {

@@ -191,7 +191,8 @@ struct GruGatesF32Args {           // h' = GRU gates from gi (or P[ids]) and gh 
   const float* Gi = nullptr;       // layers >= 1: [Bp][3H] (with b_ih)
   const float* Gh = nullptr;       // [Bp][3H] (with b_hh)
   const float* hprev = nullptr; float* hout = nullptr;   // [Bp][H]
-  int Bp = 0, H = 0;
+  int Bp = 0, H = 0, V = 0;
+  unsigned* err = nullptr;         // layer 0: bit 4 set (and the row clamped) on a char id outside [0, V)
 };
 void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s);
 struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sample (same I/O as fc_sample)
@@ -202,6 +203,15 @@ struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sampl
   int N = 0, V = 0, step = 0, max_len = 0, eos = 0;
 };
 void sample_f32(const SampleF32Args& a, hipStream_t s);
+// per-batch generation reset as ONE kernel node (instead of memset nodes): h slot 0 of every layer
+// (fp32 and, if given, bf16) = 0, ids = sos, alive = 1, output rows = NUL
+struct GenResetArgs {
+  float* hf[4] = {nullptr, nullptr, nullptr, nullptr};
+  unsigned short* hb[4] = {nullptr, nullptr, nullptr, nullptr};
+  int* ids = nullptr; int* alive = nullptr; unsigned char* out = nullptr;
+  int L = 0, Bp = 0, H = 0, ML = 0, sos = 0;
+};
+void gen_reset(const GenResetArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ generic GEMM
 // C[M][N] (+)= A[M][K] · B[N][K]^T  (bf16 in, fp32 accumulate), both operands K-contiguous.

@@ -387,3 +387,26 @@ def test_trainer_grads_library_gemms(monkeypatch, sched):
     monkeypatch.setenv("GK_WGRAD_GEMM", "lib")
     monkeypatch.setenv("GK_BLASLT_MIN_GFLOP", "0")
     test_trainer_grads_match_cpu(monkeypatch, sched, 2, 128, 128, 4, 96)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_generator_graph_replays_identical(precision):
+    """Regression (round 2): replays of a captured generation graph must be identical, including
+    the padded rows of a batch (32 names in a 64-row fp32 batch).  With the per-batch reset as five
+    memset nodes, replays after a host sync read garbage char ids in the padded rows (an
+    out-of-range gather that faulted the GPU once) and disagreed; the reset is now one kernel node
+    and an out-of-range id is clamped and flagged in the generator's error word."""
+    from gru_mpi_cuda_amd.engine.generator import HipGenerator
+    from gru_mpi_cuda_amd.utils.data import random_floats
+    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=2, max_len=10, sos=0, eos=0, seed=4)
+    params = init_params(cfg)
+    n = 32
+    rf = torch.from_numpy(random_floats(n, cfg.max_len, seed=9).reshape(n, cfg.max_len)).cuda()
+    g = HipGenerator(cfg, params, max_batch=n, precision=precision)
+    outs = [g.generate_device(rf, n)]
+    torch.cuda.synchronize()
+    outs += [g.generate_device(rf, n) for _ in range(5)]
+    torch.cuda.synchronize()
+    assert g.g.read_error() == 0
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
