@@ -29,10 +29,11 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
   size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256);
-  if (d_.fp32) {
-    ogh = arena_.reserve((size_t)B * 3 * H * 4);
-    ogi = arena_.reserve((size_t)B * 3 * H * 4);
-    olg = arena_.reserve((size_t)B * V * 4);
+  if (d_.fp32) {   // room for split-K slabs of small batches (f32_splits): kF32SlabRows rows
+    const size_t rows = std::max<size_t>(B, kF32SlabRows);
+    ogh = arena_.reserve(rows * 3 * H * 4);
+    ogi = arena_.reserve(rows * 3 * H * 4);
+    olg = arena_.reserve(rows * V * 4);
   }
   arena_.commit();
   err_ = arena_.get<unsigned>(oerr);
@@ -125,9 +126,22 @@ void Generator::record_steps(int n, hipStream_t s) {
 // fp32-faithful step: per layer gh = h W_hh^T + b_hh (and gi = x W_ih^T + b_ih above layer 0) as
 // fp32 MFMA GEMMs on the master weights, the gates in IEEE fp32, then logits = h W_fc^T + b_fc and
 // the fp32 softmax sampler -- the reference's per-char arithmetic (namegensf.cu:669-876) batched
+// Split-K depth of a small-batch fp32 GEMM: enough 64 x 64 tiles x slabs to fill the chip
+// (<= 512 workgroups), K-slices >= 64 deep, slabs within the buffer; 1 for big batches.
+static int f32_splits(int M, int N, int K, int rows_cap) {
+  const int tiles = (M / 64) * (N / 64);
+  int sp = 1;
+  while (sp < 32 && tiles * sp * 2 <= 512 && K % (sp * 2) == 0 && (K / (sp * 2)) % 16 == 0 &&
+         K / (sp * 2) >= 64 && M * sp * 2 <= rows_cap)
+    sp *= 2;
+  return sp;
+}
+
 void Generator::record_steps_f32(int n, hipStream_t s) {
   const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
   const int Bp = rup(n, 64);
+  const int cap = std::max(Bmax_, kF32SlabRows);
+  const int sh = f32_splits(Bp, 3 * H, H, cap), sf = f32_splits(Bp, V, H, cap);
   reset_batch(Bp, false, s);
   for (int st = 0; st < ML; ++st) {
     const int cur = st & 1, nxt = cur ^ 1;
@@ -136,6 +150,7 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
       GemmF32Args g;
       g.A = hf_[2 * l + cur]; g.lda = H; g.B = P("weight_hh_l" + k); g.ldb = H; g.C = gh_; g.ldc = 3 * H;
       g.bias = P("bias_hh_l" + k); g.M = Bp; g.N = 3 * H; g.K = H;
+      g.splits = sh; g.slab = (long)Bp * 3 * H;
       gemm_f32_nt(g, s);
       GruGatesF32Args a;
       if (l == 0) {
@@ -144,19 +159,21 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
         GemmF32Args x;
         x.A = hf_[2 * (l - 1) + nxt]; x.lda = H; x.B = P("weight_ih_l" + k); x.ldb = H; x.C = gi_; x.ldc = 3 * H;
         x.bias = P("bias_ih_l" + k); x.M = Bp; x.N = 3 * H; x.K = H;
+        x.splits = sh; x.slab = (long)Bp * 3 * H;
         gemm_f32_nt(x, s);
-        a.Gi = gi_;
+        a.Gi = gi_; a.gi_splits = sh; a.gi_slab = (long)Bp * 3 * H;
       }
-      a.Gh = gh_; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt]; a.Bp = Bp; a.H = H;
+      a.Gh = gh_; a.gh_splits = sh; a.gh_slab = (long)Bp * 3 * H; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt]; a.Bp = Bp; a.H = H;
       a.V = V; a.err = err_;
       gru_gates_f32(a, s);
     }
     GemmF32Args f;
     f.A = hf_[2 * (L - 1) + nxt]; f.lda = H; f.B = P("fc.weight"); f.ldb = H; f.C = logits_; f.ldc = V;
     f.bias = P("fc.bias"); f.M = Bp; f.N = V; f.K = H;
+    f.splits = sf; f.slab = (long)Bp * V;
     gemm_f32_nt(f, s);
     SampleF32Args q;
-    q.logits = logits_; q.rf = rf_; q.ids = ids_; q.out = out_; q.alive = alive_;
+    q.logits = logits_; q.splits = sf; q.slab = (long)Bp * V; q.rf = rf_; q.ids = ids_; q.out = out_; q.alive = alive_;
     q.probs = (st == ML - 1) ? probe_ : nullptr;
     q.N = n; q.V = V; q.step = st; q.max_len = ML; q.eos = d_.eos;
     sample_f32(q, s);

@@ -62,6 +62,7 @@ class Generator {
   unsigned char* out_;
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
+  static constexpr int kF32SlabRows = 2048;   // fp32 split-K slab capacity (rows x 3H)
 };
 
 }  // namespace gk

@@ -27,10 +27,11 @@ __global__ void __launch_bounds__(256) gemm_f32_nt_kernel(GemmF32Args g) {
   __shared__ __attribute__((aligned(16))) float Bs[2][kT][kLd];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * kT, n0 = blockIdx.x * kT;
+  const int m0 = blockIdx.y * kT, n0 = blockIdx.x * kT, sp = blockIdx.z;
+  const int kper = g.K / g.splits;
   const int lrow = t >> 2, lk = (t & 3) * 4;          // this thread's 16 B of each operand k-tile
-  const float* pa = g.A + (size_t)(m0 + lrow) * g.lda + lk;
-  const float* pb = g.B + (size_t)(n0 + lrow) * g.ldb + lk;
+  const float* pa = g.A + (size_t)(m0 + lrow) * g.lda + (size_t)sp * kper + lk;
+  const float* pb = g.B + (size_t)(n0 + lrow) * g.ldb + (size_t)sp * kper + lk;
   float4 ra = *reinterpret_cast<const float4*>(pa);
   float4 rb = *reinterpret_cast<const float4*>(pb);
   *reinterpret_cast<float4*>(&As[0][lrow][lk]) = ra;
@@ -42,7 +43,7 @@ __global__ void __launch_bounds__(256) gemm_f32_nt_kernel(GemmF32Args g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fk = lane >> 4;           // MFMA operand: row / column, k within 4
-  const int nk = g.K / kBK;
+  const int nk = kper / kBK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {                                 // next k-tile in flight during the MFMAs
@@ -70,21 +71,23 @@ __global__ void __launch_bounds__(256) gemm_f32_nt_kernel(GemmF32Args g) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = n0 + wn * 32 + j * 16 + fr;
-    const float bias = g.bias ? g.bias[col] : 0.f;
+    const float bias = (g.bias && sp == 0) ? g.bias[col] : 0.f;
+    float* C = g.C + (size_t)sp * g.slab;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 32 + i * 16 + fk * 4 + r;
-        g.C[(size_t)row * g.ldc + col] = acc[i][j][r] + bias;
+        C[(size_t)row * g.ldc + col] = acc[i][j][r] + bias;
       }
   }
 }
 
 void gemm_f32_nt(const GemmF32Args& g, hipStream_t s) {
-  if (g.M % kT || g.N % kT || g.K % kBK || g.lda % 4 || g.ldb % 4)
-    throw std::runtime_error("gemm_f32_nt: needs M, N % 64 == 0, K % 16 == 0 and 16-B aligned rows");
-  hipLaunchKernelGGL(gemm_f32_nt_kernel, dim3(g.N / kT, g.M / kT), dim3(256), 0, s, g);
+  if (g.M % kT || g.N % kT || g.splits < 1 || g.K % g.splits || (g.K / g.splits) % kBK || g.lda % 4 || g.ldb % 4 ||
+      (g.splits > 1 && g.slab < (long)g.M * g.ldc))
+    throw std::runtime_error("gemm_f32_nt: needs M, N % 64 == 0, (K / splits) % 16 == 0 and 16-B aligned rows");
+  hipLaunchKernelGGL(gemm_f32_nt_kernel, dim3(g.N / kT, g.M / kT, g.splits), dim3(256), 0, s, g);
 }
 
 DEV float sigmoid_ieee(float x) { return 1.f / (1.f + expf(-x)); }
@@ -107,9 +110,18 @@ __global__ void gru_gates_f32_kernel(GruGatesF32Args a) {
     gi = a.P + (size_t)id * 3 * H;
   }
   const float* gh = a.Gh + (size_t)b * 3 * H;
-  const float r = sigmoid_ieee(gi[j] + gh[j]);
-  const float z = sigmoid_ieee(gi[H + j] + gh[H + j]);
-  const float n = tanhf(gi[2 * H + j] + r * gh[2 * H + j]);
+  float xi[3], xh[3];   // pre-activations: split-K slabs summed in slab order (deterministic)
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    xh[q] = gh[q * H + j];
+    for (int s2 = 1; s2 < a.gh_splits; ++s2) xh[q] += gh[s2 * a.gh_slab + q * H + j];
+    xi[q] = gi[q * H + j];
+    if (!a.P)
+      for (int s2 = 1; s2 < a.gi_splits; ++s2) xi[q] += gi[s2 * a.gi_slab + q * H + j];
+  }
+  const float r = sigmoid_ieee(xi[0] + xh[0]);
+  const float z = sigmoid_ieee(xi[1] + xh[1]);
+  const float n = tanhf(xi[2] + r * xh[2]);
   a.hout[i] = (1.f - z) * n + z * a.hprev[i];
 }
 
@@ -128,7 +140,15 @@ __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
   // (fixed-bound loops guarded by `per`: the arrays stay in registers)
   float xv[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) xv[e] = e < per ? x[e] : -INFINITY;
+  for (int e = 0; e < 8; ++e) {
+    if (e < per) {
+      float v = x[e];
+      for (int s2 = 1; s2 < a.splits; ++s2) v += x[s2 * a.slab + e];   // split-K slabs, fixed order
+      xv[e] = v;
+    } else {
+      xv[e] = -INFINITY;
+    }
+  }
   float mx = -INFINITY;
 #pragma unroll
   for (int e = 0; e < 8; ++e) mx = fmaxf(mx, xv[e]);

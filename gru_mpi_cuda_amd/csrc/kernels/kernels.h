@@ -184,12 +184,16 @@ struct GemmF32Args {               // C[M][N] = A[M][K] · B[N][K]^T (+ bias[N])
   float* C = nullptr; int ldc = 0;
   const float* bias = nullptr;
   int M = 0, N = 0, K = 0;         // M, N % 64 == 0, K % 16 == 0
+  int splits = 1;                  // split-K: slab s (K range s*K/splits ..) at C + s*slab; bias in slab 0
+  long slab = 0;
 };
 void gemm_f32_nt(const GemmF32Args& g, hipStream_t s);
 struct GruGatesF32Args {           // h' = GRU gates from gi (or P[ids]) and gh = h W_hh^T + b_hh
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: gi row = P[ids[b]] ([V][3H])
   const float* Gi = nullptr;       // layers >= 1: [Bp][3H] (with b_ih)
   const float* Gh = nullptr;       // [Bp][3H] (with b_hh)
+  int gi_splits = 1, gh_splits = 1;   // split-K slabs of Gi / Gh, summed here in fixed order
+  long gi_slab = 0, gh_slab = 0;
   const float* hprev = nullptr; float* hout = nullptr;   // [Bp][H]
   int Bp = 0, H = 0, V = 0;
   unsigned* err = nullptr;         // layer 0: bit 4 set (and the row clamped) on a char id outside [0, V)
@@ -197,6 +201,7 @@ struct GruGatesF32Args {           // h' = GRU gates from gi (or P[ids]) and gh 
 void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s);
 struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sample (same I/O as fc_sample)
   const float* logits = nullptr;   // [Bp][V]
+  int splits = 1; long slab = 0;   // split-K slabs of the logits, summed in fixed order
   const float* rf = nullptr;
   int* ids = nullptr; unsigned char* out = nullptr; int* alive = nullptr;
   float* probs = nullptr;
