@@ -19,6 +19,12 @@ static bool env_flag(const char* name, bool dflt) {
   return v && v[0] ? v[0] != '0' : dflt;
 }
 
+// data-parallel: a layer group's collective stays open across the next persistent backward kernel
+static bool ar_span() {
+  static const bool on = env_flag("GK_AR_SPAN", true);
+  return on;
+}
+
 // Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
 // split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
 // 128 x 128 split-K path only.  GK_WGRAD_GEMM overrides the default.
@@ -328,13 +334,21 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
                  G("bias_ih_l" + k), s);
       if (dp) {
         ar_ready_ = group_end(l);   // FC (if l is the top layer) + this layer's four gradients
-        if (!seq_[l - 1].bwd) ar_flush(s, false);   // next backward is per-step: overlap it now
-        else ar_join(s);   // (no-op unless an earlier flush is still open) before the persistent kernel
+        // span (default): the group goes out now and its collective stays open across the next
+        // persistent backward kernel (joined before the embedding tail).  Neither waits on the
+        // other -- the RCCL kernel only on its peers, the sequence kernel only on its own
+        // workgroups -- so if the collective's workgroups cannot co-reside they run after it
+        // (no overlap, no deadlock).  GK_AR_SPAN=0: joined before the persistent kernel.
+        // The fork comes after the dX GEMM below, so the collective starts beside the sequence
+        // kernel rather than beside that bandwidth-bound GEMM.
+        if (!seq_[l - 1].bwd) ar_flush(s, false);
+        else if (!ar_span()) ar_join(s);   // (no-op unless an earlier flush is still open)
       }
       GemmArgs dx;  // dy of the layer below = dGi · W_ih
       dx.A = y.dgi; dx.lda = H3; dx.B = y.WihT; dx.ldb = H3;
       dx.C = Ls_[l - 1].dy; dx.ldc = H; dx.M = (int)tok; dx.N = H; dx.K = H3;
       gemm_nt(dx, s);
+      if (dp && seq_[l - 1].bwd && ar_span()) ar_flush(s, false);
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients

@@ -19,3 +19,16 @@ for r in seg:
 print(f"step span {(t1 - t0) / 1e3:.1f} us, kernels {len(seg)}, union-busy {busy:.1f} us")
 for k, (n, us) in sorted(agg.items(), key=lambda x: -x[1][1]):
     print(f"  {k:60s} n={n:4d} total={us:8.1f} us avg={us / n:7.2f}")
+if "--overlap" in sys.argv:   # kernels that ran concurrently (e.g. an RCCL kernel beside a sequence kernel)
+    iv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("void ", "")[:50] or "<unnamed>")
+          for r in seg]
+    for i, (s1, e1, k1) in enumerate(iv):
+        for s2, e2, k2 in iv[i + 1:]:
+            ov = min(e1, e2) - max(s1, s2)
+            if ov > 0:
+                print(f"  overlap {ov / 1e3:8.1f} us: {k1} [{(s1 - t0) / 1e3:.1f}, {(e1 - t0) / 1e3:.1f}] "
+                      f"| {k2} [{(s2 - t0) / 1e3:.1f}, {(e2 - t0) / 1e3:.1f}]")
+if "--timeline" in sys.argv:
+    for r in seg:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        print(f"  {(s - t0) / 1e3:9.1f} {(e - t0) / 1e3:9.1f}  {r['Kernel_Name'].split('(')[0][:70] or '<unnamed>'}")
