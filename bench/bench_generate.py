@@ -108,11 +108,20 @@ def ref_schedule(params, cfg, rf_host: np.ndarray, dev) -> np.ndarray:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="ref")
-    ap.add_argument("--names", type=int, default=4096)
+    ap.add_argument("--names", default="4096", help="comma list: one JSON line per batch size")
     ap.add_argument("--ref-names", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="engine,engine_fp32,torch,ref-schedule")
+    ap.add_argument("--modes", default="engine,engine_fp32,torch,ref-schedule",
+                    help="engine (bf16), engine_fp32 (fp32, persistent kernel at <= 64 names), "
+                         "engine_fp32_batched (fp32, per-char graph), torch, ref-schedule")
     args = ap.parse_args()
+    for n in [int(x) for x in str(args.names).split(",")]:
+        args.n = n
+        run(args)
+    return 0
+
+
+def run(args) -> None:
 
     from gru_mpi_cuda_amd.config import preset
     from gru_mpi_cuda_amd.models.params import init_params
@@ -123,10 +132,10 @@ def main() -> int:
     gparams = {k: v.to(dev) for k, v in params.items()}
     ML = cfg.max_len
     rng = np.random.default_rng(7)
-    rf = rng.random((args.names, ML), dtype=np.float32)
+    rf = rng.random((args.n, ML), dtype=np.float32)
     rf_dev = torch.from_numpy(rf).to(dev)
     res = {"preset": args.preset, "model": f"GRU L={cfg.layers} H={cfg.hidden} E={cfg.embed} V={cfg.vocab}",
-           "max_len": ML, "names": args.names, "data": "random-init weights, seeded uniforms"}
+           "max_len": ML, "names": args.n, "data": "random-init weights, seeded uniforms"}
 
     def timed(fn, reps):
         fn()
@@ -138,27 +147,30 @@ def main() -> int:
         return (time.perf_counter() - t0) / reps, o
 
     modes = args.modes.split(",")
-    for prec in ("bf16", "fp32"):
-        key = "engine" if prec == "bf16" else "engine_fp32"
-        if key not in modes and not (prec == "bf16" and "engine" in modes):
+    from gru_mpi_cuda_amd.engine.generator import HipGenerator
+    # engine = bf16 MFMA fast mode; engine_fp32 = fp32-faithful mode (the C API default: one
+    # persistent launch at <= 64 names); engine_fp32_batched = fp32 with the per-char graph forced
+    for key, prec, persist in (("engine", "bf16", True), ("engine_fp32", "fp32", True),
+                               ("engine_fp32_batched", "fp32", False)):
+        if key not in modes:
             continue
-        # engine = bf16 MFMA fast mode; engine_fp32 = fp32-faithful mode (the C API default)
-        from gru_mpi_cuda_amd.engine.generator import HipGenerator
-        g = HipGenerator(cfg, params, max_batch=args.names, device=dev, precision=prec)
-        dt, o = timed(lambda: g.generate_device(rf_dev, args.names), args.reps)
+        g = HipGenerator(cfg, params, max_batch=args.n, device=dev, precision=prec)
+        g.g.set_persist(persist)
+        dt, o = timed(lambda: g.generate_device(rf_dev, args.n), args.reps)
         o = o.cpu().numpy()
         res[key] = {"precision": prec, "s": round(dt, 5), "chars_per_s": round(_emitted(o) / dt, 1),
-                    "names_per_s": round(args.names / dt, 1), "error_word": int(g.g.read_error())}
+                    "names_per_s": round(args.n / dt, 1), "us_per_char_step": round(dt / ML * 1e6, 2),
+                    "persistent": bool(g.g.uses_persist(args.n)), "error_word": int(g.g.read_error())}
         del g
     if "torch" in modes:
         dt, o = timed(lambda: torch_batched(gparams, cfg, rf_dev), args.reps)
         o = o.cpu().numpy()
         res["torch"] = {"s": round(dt, 5), "chars_per_s": round(_emitted(o) / dt, 1),
-                        "names_per_s": round(args.names / dt, 1)}
+                        "names_per_s": round(args.n / dt, 1)}
         if "engine" in res:
             res["engine"]["speedup_vs_torch"] = round(res["torch"]["s"] / res["engine"]["s"], 2)
     if "ref-schedule" in modes:
-        nr = min(args.ref_names, args.names)
+        nr = min(args.ref_names, args.n)
         ref_schedule(gparams, cfg, rf[:1], dev)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -169,7 +181,6 @@ def main() -> int:
             res["engine"]["speedup_vs_ref_schedule"] = round(
                 res["engine"]["chars_per_s"] / res["ref_schedule"]["chars_per_s"], 1)
     print(json.dumps(res), flush=True)
-    return 0
 
 
 if __name__ == "__main__":

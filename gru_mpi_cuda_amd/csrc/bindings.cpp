@@ -132,7 +132,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("set_use_graph", &Generator::set_use_graph)
       .def("read_error", &Generator::read_error)
-      .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); });
+      .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); })
+      .def("set_persist", &Generator::set_persist)
+      .def("uses_persist", &Generator::uses_persist);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)
   m.def("gemm_nt", [](py::dict d, uintptr_t s) {

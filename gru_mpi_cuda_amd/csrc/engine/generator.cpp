@@ -28,8 +28,10 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
-  size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256);
-  if (d_.fp32) {   // room for split-K slabs of small batches (f32_splits): kF32SlabRows rows
+  size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256), opws = 0, opsync = 0;
+  if (d_.fp32) {
+    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V) * 4);
+    opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);   // room for split-K slabs of small batches (f32_splits): kF32SlabRows rows
     const size_t rows = std::max<size_t>(B, kF32SlabRows);
     ogh = arena_.reserve(rows * 3 * H * 4);
     ogi = arena_.reserve(rows * 3 * H * 4);
@@ -37,7 +39,10 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   }
   arena_.commit();
   err_ = arena_.get<unsigned>(oerr);
-  if (d_.fp32) { gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg); }
+  if (d_.fp32) {
+    gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg);
+    pws_ = arena_.get<float>(opws); psync_ = arena_.get<unsigned>(opsync);
+  }
   for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
   for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
   Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); WfcF_ = arena_.get<u16>(oWfcF);
@@ -48,6 +53,13 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);   // 0 auto, 1 reg, 2 LDS
+  const char* gp = std::getenv("GK_GEN_PERSIST");
+  if (gp && gp[0] == '0') persist_ = false;
+  if (const char* pm = std::getenv("GK_GEN_PERSIST_MAX")) persist_max_ = std::atoi(pm);
+}
+
+bool Generator::uses_persist(int n) const {
+  return d_.fp32 && persist_ && n <= persist_max_ && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
 }
 
 Generator::~Generator() {
@@ -187,7 +199,18 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);
     HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
-    if (use_graph_) {
+    if (uses_persist(n)) {   // one launch for the whole batch: no graph needed
+      GenPersistArgs a;
+      for (int l = 0; l < d_.L; ++l) {
+        const std::string k = std::to_string(l);
+        a.Whh[l] = P("weight_hh_l" + k); a.bhh[l] = P("bias_hh_l" + k);
+        if (l > 0) { a.Wih[l] = P("weight_ih_l" + k); a.bih[l] = P("bias_ih_l" + k); }
+      }
+      a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab_; a.rf = rf_; a.out = out_; a.probs = probe_;
+      a.ws = pws_; a.sync = psync_; a.err = err_;
+      a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
+      gen_persist_f32(a, s);
+    } else if (use_graph_) {
       auto& g = graphs_[n];
       if (!g) {
         g.reset(new Graph());

@@ -34,6 +34,11 @@ class Generator {
   void set_use_graph(bool g) { use_graph_ = g; }
   // optional: device [Bp][V] softmax of the last generated step (tests)
   void set_probe(float* probs) { probe_ = probs; graphs_.clear(); }
+  // fp32 mode, small batches (<= GK_GEN_PERSIST_MAX names, default 32, at most 64): one persistent
+  // launch per batch (gen_persist.hip) instead of the per-char graph.  On by default;
+  // GK_GEN_PERSIST=0 or set_persist(false) turns it off.
+  void set_persist(bool on) { persist_ = on; }
+  bool uses_persist(int n) const;
   unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
 
  private:
@@ -62,6 +67,10 @@ class Generator {
   unsigned char* out_;
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
+  bool persist_ = true;
+  int persist_max_ = 32;        // names per batch up to which the persistent launch is used
+  float* pws_ = nullptr;        // persistent path: exchange buffers
+  unsigned* psync_ = nullptr;   // persistent path: flags + done counter (self-cleaning, arena-zeroed)
   static constexpr int kF32SlabRows = 2048;   // fp32 split-K slab capacity (rows x 3H)
 };
 

@@ -13,6 +13,7 @@
 //     sum exceeds r, else V - 1), EOS written then the name stops (namegensf.cu:877-882).
 #include "kernels.h"
 #include "common.h"
+#include "gen_sample.h"
 
 namespace gk {
 
@@ -130,9 +131,7 @@ void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s) {
   hipLaunchKernelGGL(gru_gates_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
 }
 
-// One wave per row: lane owns V/64 consecutive logits.  Softmax statistics by wave reductions,
-// then the inclusive CDF (lane-local sums in index order + a wave scan of the lane totals) and
-// the lowest index whose running sum exceeds r.
+// One wave per row: lane owns V/64 consecutive logits (softmax + CDF search: gen_sample.h).
 __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
   const int b = blockIdx.x, lane = threadIdx.x, per = a.V / 64;
   if (b >= a.N) return;
@@ -149,43 +148,9 @@ __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
       xv[e] = -INFINITY;
     }
   }
-  float mx = -INFINITY;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) mx = fmaxf(mx, xv[e]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  float se = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-    if (e < per) se += expf(xv[e] - mx);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
-  float p[8];                                       // V <= 512
-  float loc = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    p[e] = e < per ? expf(xv[e] - mx) / se : 0.f;
-    loc += p[e];
-    if (a.probs && e < per) a.probs[(size_t)b * a.V + lane * per + e] = p[e];
-  }
-  float inc = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }
   const float rnd = a.rf[(size_t)b * a.max_len + a.step];
-  float psum = inc - loc;
-  int hit = a.V;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    psum += p[e];
-    if (e < per && hit == a.V && psum > rnd) hit = lane * per + e;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) hit = min(hit, __shfl_xor(hit, o, 64));
+  const int sel = softmax_sample_wave(xv, per, a.V, rnd, a.probs ? a.probs + (size_t)b * a.V : nullptr);
   if (lane == 0) {
-    const int sel = hit >= a.V ? a.V - 1 : hit;
     if (a.alive[b]) {
       a.out[(size_t)b * (a.max_len + 1) + a.step] = (unsigned char)sel;
       if (sel == a.eos) a.alive[b] = 0;

@@ -1,0 +1,377 @@
+// Persistent fp32 generation for small batches (<= 64 names): ONE launch runs every char.
+//
+// The batched fp32 path (gen_f32.hip) launches ~3L + 2 kernels per char, and each one streams fp32
+// weights from memory. At 32 names that is 69 us per char, almost all of it launch gaps and
+// weight reads of a few rows of work (profiles/r2_generate_modes_splitk.jsonl). Here the weights
+// are read once per launch and stay in VGPRs.
+//
+//   * grid = 256 workgroups of 512 threads, one per CU, all co-resident (checked on the host).
+//   * Workgroup b owns units [b U, b U + U) (U = H / 256) of every recurrent matrix (W_hh of each
+//     layer, W_ih of layers >= 1) and FC rows [b VR, b VR + VR) (VR = V / 256). That is 2L row
+//     tiles of 16 rows (3U gate rows used; VR rows for the FC tile).
+//   * Wave w keeps the K-slice [w H/8, (w + 1) H/8) of every tile in registers as fp32 MFMA
+//     A-fragments (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulate). Lane (row r,
+//     quad q) holds W[r][w H/8 + q H/32 + j] for j < H/32, so its B-fragments of the hidden states
+//     are H/32 contiguous floats per name (float4 loads). The 8 wave partials of a 16 x 16
+//     (rows x names) tile meet in LDS and are summed in wave order.
+//   * Per char t:
+//       - Sample char t-1 from the logits of all 256 workgroups. Every workgroup does this
+//         redundantly and identically; it needs the id for layer 0's input.
+//       - Layer 0: gi = P[id] (the workgroup's slice of the fp32 table, in LDS), then the gates.
+//       - Each layer l >= 1: gi_l = h_{l-1}(t) W_ih_l^T + b_ih_l, then the gates.
+//       - FC: logits = h_{L-1}(t) W_fc^T + b_fc.
+//     The recurrent products gh_l = h_l(t) W_hh_l^T + b_hh_l are only needed by the next char.
+//     They ride on the loads of the product that consumes h_l(t) anyway (gi_{l+1}, or the
+//     logits), so every exchanged state is read once per char. Those reads, 256 workgroups x
+//     names x H floats each, are what a char costs.
+//     That is L + 1 hand-offs per char, each an all-to-all of tiny slices (U or VR floats per
+//     name per producer). A producer's wave 0 publishes them with write-through (sc1) stores,
+//     drains them (vmcnt(0)) and stores its epoch flag. A consumer wave polls only the 32
+//     producers of its K-slice (all 256 for the logits), then reads with sc1 loads: the hand-off
+//     protocol of the persistent training kernels (gru_seq.hip). States and logits are
+//     double-buffered by char parity; a producer can be at most one char ahead of any consumer.
+//     Data-tagged 8-byte granules (no flag) measured slower here: every waiting lane re-reads its
+//     whole set of granules, 44.6 against 28 us per char at 8 names
+//     (profiles/r2_generate_persistent.jsonl).
+//   * Gates use IEEE expf / tanhf, and sampling uses the batched sampler's code (gen_sample.h),
+//     i.e. the same arithmetic as the batched fp32 path. Only the order of the fp32 partial sums
+//     of each dot product differs.
+//   * Spins are bounded. On a timeout, error bit 32 is set and every later wait returns
+//     immediately, so the grid drains. The last workgroup to finish zeroes the flags for the next
+//     launch.
+// Reference: the per-char loop of /root/reference/namegensf.cu:661-884, for all names at once.
+#include <stdexcept>
+#include "kernels.h"
+#include "common.h"
+#include "gen_sample.h"
+
+namespace gk {
+
+namespace {
+constexpr int kG = 256;        // workgroups
+constexpr int kNmax = 64;      // names per launch
+constexpr int kFS = 16;        // flag stride in uints (own 64-B line)
+constexpr int kVmax = 1024;
+constexpr unsigned kSpin = 1u << 21;   // x s_sleep(1) polls: ~0.3 s
+constexpr unsigned kErrBit = 32u;
+}
+
+typedef __amdgpu_buffer_rsrc_t prsrc_t;
+typedef unsigned int pu32x4 __attribute__((ext_vector_type(4)));
+
+DEV prsrc_t prsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, bytes, 0x00020000);
+}
+DEV unsigned flag_load(const unsigned* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave-level wait: every producer in [lo, lo + cnt) has published epoch `ep` of `kind`.
+DEV void pwait(const unsigned* flags, int kind, int lo, int cnt, unsigned ep, unsigned* err) {
+  const int lane = threadIdx.x & 63;
+  const unsigned* f = flags + (size_t)kind * kG * kFS;
+  unsigned spins = 0;
+  for (;;) {
+    bool ok = true;
+    for (int q = lane; q < cnt; q += 64) ok = ok && flag_load(f + (size_t)(lo + q) * kFS) >= ep;
+    if (__all(ok)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255) == 0 && (flag_load(err) & kErrBit)) break;   // another workgroup gave up
+    if (spins > kSpin) {
+      if (lane == 0) __hip_atomic_fetch_or(err, kErrBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the payload loads below the poll
+}
+DEV void st_sc1(prsrc_t r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 16);   // aux 16 = sc1
+}
+
+// one wave's partials of two 16 x 16 (rows x names) tiles over its K-slice: x = this lane's KJ
+// floats of its name (sc1 b128 loads at byte offset off; a padded name, !valid, is not read), A
+// values aval(j) -> pa, and Wb -> pb when do_b.  Two accumulator chains per tile.
+template <int KJ, class AVal>
+DEV void load_mm2(AVal&& aval, const float (&Wb)[KJ], bool do_b, prsrc_t r, unsigned off, bool valid, f32x4& pa,
+                  f32x4& pb) {
+  float x[KJ];
+#pragma unroll
+  for (int j = 0; j < KJ; j += 4) {
+    pu32x4 v = {0u, 0u, 0u, 0u};
+    if (valid) v = __builtin_amdgcn_raw_buffer_load_b128(r, off + j * 4, 0, 16);
+    x[j] = __uint_as_float(v.x); x[j + 1] = __uint_as_float(v.y);
+    x[j + 2] = __uint_as_float(v.z); x[j + 3] = __uint_as_float(v.w);
+  }
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+#pragma unroll
+  for (int j = 0; j < KJ; j += 2) {
+    a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(aval(j), x[j], a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aval(j + 1), x[j + 1], a1, 0, 0, 0);
+  }
+  if (do_b) {
+#pragma unroll
+    for (int j = 0; j < KJ; j += 2) {
+      b0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wb[j], x[j], b0, 0, 0, 0);
+      b1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wb[j + 1], x[j + 1], b1, 0, 0, 0);
+    }
+  }
+  pa = a0 + a1;
+  pb = b0 + b1;
+}
+
+DEV float sig_ieee(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int V_> struct ic { static constexpr int value = V_; };
+template <int B_, int E_, class F> DEV void static_for(F&& f) {
+  if constexpr (B_ < E_) { f(ic<B_>{}); static_for<B_ + 1, E_>(f); }
+}
+
+template <int KJ, int L>
+__global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
+  constexpr int U = KJ / 8, H = 32 * KJ, KW = H / 8, NT = 2 * L - 1, R3 = 3 * U;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, q4 = lane >> 4;
+  const int V = a.V, VR = V / kG, N = a.N, Np = (N + 15) & ~15, nnt = Np / 16, ML = a.ML;
+
+  __shared__ float sP[kVmax * R3];            // P[v][g H + b U + u] -> sP[v][g U + u]
+  __shared__ float red[2][8][256];            // wave partials of two tiles
+  __shared__ float sgh[L][16][kNmax];         // gh rows (incl. b_hh) x names
+  __shared__ float sgi[16][kNmax];            // gi rows (incl. b_ih) / logits
+  __shared__ float sh[L][kNmax][U];           // own units' hidden states
+  __shared__ float sbh[L][16], sbi[L][16], sbf[16];
+  __shared__ __attribute__((aligned(16))) float sWf[kVmax / kG][H];   // this workgroup's FC rows
+  __shared__ int sid[kNmax], sal[kNmax];
+  __shared__ int s_last, s_live;
+
+  // exchange buffers: X_l[par][name][H], then LG[par][name][V]
+  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * 2 * kNmax * H + 2 * kNmax * V) * 4));
+  const unsigned lg0 = (unsigned)((size_t)L * 2 * kNmax * H * 4);
+  auto xoff = [&](int l, int par, int n, int col) -> unsigned {
+    return (unsigned)((((size_t)(l * 2 + par) * kNmax + n) * H + col) * 4);
+  };
+  unsigned* flags = a.sync;
+  unsigned* done = a.sync + (size_t)(L + 1) * kG * kFS;
+  auto publish_flag = [&](int kind, int t) {   // wave 0, after its payload stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(flags + ((size_t)kind * kG + b) * kFS, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  // ---- resident weights: tile ti < L: W_hh_ti; L <= ti < 2L-1: W_ih_(ti-L+1).  The FC rows (VR of
+  // the 16 rows of its tile) live in LDS.
+  float Wr[NT][KJ];
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) {
+    const float* M = ti < L ? a.Whh[ti] : a.Wih[ti - L + 1];
+    const bool valid = fr < R3;
+    const int row = (fr / U) * H + b * U + fr % U;
+    const float* src = M + (size_t)(valid ? row : 0) * H + w * KW + q4 * KJ;
+#pragma unroll
+    for (int j = 0; j < KJ; j += 4) {
+      float4 v = valid ? *reinterpret_cast<const float4*>(src + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      Wr[ti][j] = v.x; Wr[ti][j + 1] = v.y; Wr[ti][j + 2] = v.z; Wr[ti][j + 3] = v.w;
+    }
+  }
+  for (int i = tid; i < VR * H; i += 512) sWf[i / H][i % H] = a.Wfc[(size_t)(b * VR + i / H) * H + i % H];
+  for (int i = tid; i < V * R3; i += 512) {
+    const int v = i / R3, c = i % R3;
+    sP[i] = a.P[(size_t)v * 3 * H + (c / U) * H + b * U + c % U];
+  }
+  if (tid < 16) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      sbh[l][tid] = tid < R3 ? a.bhh[l][(tid / U) * H + b * U + tid % U] : 0.f;
+      sbi[l][tid] = (l > 0 && tid < R3) ? a.bih[l][(tid / U) * H + b * U + tid % U] : 0.f;
+    }
+    sbf[tid] = tid < VR ? a.bfc[b * VR + tid] : 0.f;
+  }
+  for (int i = tid; i < L * kNmax * U; i += 512) (&sh[0][0][0])[i] = 0.f;
+  if (tid < kNmax) { sid[tid] = a.sos; sal[tid] = tid < N ? 1 : 0; }
+  if (b == 0)
+    for (int i = tid; i < N * (ML + 1); i += 512) a.out[i] = 0;
+  __syncthreads();
+
+  // cross-wave sum of tile partials -> dst[row][name tile nt] (+ bias), rows < nrows
+  auto reduce_to = [&](float (*dst)[kNmax], int slot, int nt, const float* bias, int nrows) {
+    if (tid < 256) {
+      const int row = tid >> 4, n = tid & 15;
+      float s = red[slot][0][tid];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) s += red[slot][k][tid];
+      if (row < nrows) dst[row][nt * 16 + n] = s + bias[row];
+    }
+  };
+  auto stash = [&](int slot, const f32x4& acc) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[slot][w][(4 * q4 + r) * 16 + fr] = acc[r];
+  };
+  // gates of layer l for all names -> sh[l], then wave 0 publishes h_l(t) and its flag
+  auto gates_publish = [&](int l, int t) {
+    for (int i = tid; i < Np * U; i += 512) {
+      const int n = i / U, u = i % U;
+      float gi[3], gh[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        gh[g] = sgh[l][g * U + u][n];
+        gi[g] = l == 0 ? sP[sid[n] * R3 + g * U + u] : sgi[g * U + u][n];
+      }
+      const float r = sig_ieee(gi[0] + gh[0]);
+      const float z = sig_ieee(gi[1] + gh[1]);
+      const float nn = tanhf(gi[2] + r * gh[2]);
+      sh[l][n][u] = (1.f - z) * nn + z * sh[l][n][u];
+    }
+    __syncthreads();
+    if (w == 0) {
+      if (lane < Np) {
+        if constexpr (U == 4) {
+          const pu32x4 v = {__float_as_uint(sh[l][lane][0]), __float_as_uint(sh[l][lane][1]),
+                            __float_as_uint(sh[l][lane][2]), __float_as_uint(sh[l][lane][3])};
+          __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoff(l, t & 1, lane, b * U), 0, 16);
+        } else {
+          for (int u = 0; u < U; ++u) st_sc1(xr, xoff(l, t & 1, lane, b * U + u), sh[l][lane][u]);
+        }
+      }
+      publish_flag(l, t);
+    }
+  };
+
+  // gh_l = h_l W_hh_l^T + b_hh_l is only needed by the next char's gates: it is computed beside the
+  // product that consumes h_l(t) anyway (gi_{l+1}, or the logits for the top layer), so each
+  // exchanged state is read once per char.  At t = 0 (h = 0) it is the bias.
+  for (int i = tid; i < L * 16 * kNmax; i += 512) {
+    const int l = i / (16 * kNmax), row = (i / kNmax) % 16;
+    (&sgh[0][0][0])[i] = sbh[l][row];
+  }
+  __syncthreads();
+  // x = h_src(t) (this wave's K-slice, name tile nt) times W tile TA (-> dst rows < nrows, + bias)
+  // and, unless this is the last char, times W_hh_src (-> sgh[src] for the next char)
+  auto product = [&](auto ta_tag, auto src_tag, int t, float (*dst)[kNmax], const float* bias, int nrows) {
+    constexpr int TA = decltype(ta_tag)::value, SRC = decltype(src_tag)::value;   // TA = NT: the FC rows
+    const bool gh = t + 1 < ML;
+    const int kw0 = w * KW + q4 * KJ;
+    for (int nt = 0; nt < nnt; ++nt) {
+      f32x4 pa, pb;
+      auto aval = [&](int j) -> float {
+        if constexpr (TA == NT) return fr < VR ? sWf[fr < VR ? fr : 0][kw0 + j] : 0.f;
+        else return Wr[TA][j];
+      };
+      if (nt == 0) pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
+      load_mm2<KJ>(aval, Wr[SRC], gh, xr, xoff(SRC, t & 1, nt * 16 + fr, kw0), nt * 16 + fr < N, pa, pb);
+      stash(0, pa);
+      if (gh) stash(1, pb);
+      __syncthreads();
+      reduce_to(dst, 0, nt, bias, nrows);
+      if (gh) reduce_to(sgh[SRC], 1, nt, sbh[SRC], R3);
+      __syncthreads();
+    }
+  };
+
+  for (int t = 0; t <= ML; ++t) {
+    if (t == ML && b != 0) break;   // only workgroup 0 samples the last char
+    // ---- sample char t-1 from the logits of every workgroup
+    if (t > 0) {
+      if (w == 0) pwait(flags, L, 0, kG, (unsigned)t, a.err);
+      __syncthreads();
+      const int per = V / 64;
+      for (int n = w; n < Np; n += 8) {
+        float xv[16];
+        const unsigned base = lg0 + (unsigned)((((t - 1) & 1) * kNmax + n) * V + lane * per) * 4;
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          xv[e] = e >= per ? -INFINITY
+                  : n < N ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, base + 4 * e, 0, 16))
+                          : 0.f;   // (a padded name: a uniform draw nobody reads)
+        const float rnd = n < N ? a.rf[(size_t)n * ML + (t - 1)] : 0.5f;
+        float* prow = (b == 0 && a.probs && t == ML && n < N) ? a.probs + (size_t)n * V : nullptr;
+        const int sel = softmax_sample_wave(xv, per, V, rnd, prow);
+        if (lane == 0) {
+          if (sal[n]) {
+            if (b == 0) a.out[(size_t)n * (ML + 1) + (t - 1)] = (unsigned char)sel;
+            if (sel == a.eos) sal[n] = 0;
+          }
+          sid[n] = sel;
+        }
+      }
+      __syncthreads();
+      if (t == ML) break;
+      if (!a.probs) {   // every name ended: all workgroups see the same ids and stop together
+        if (tid == 0) {
+          int live = 0;
+          for (int n = 0; n < N; ++n) live |= sal[n];
+          s_live = live;
+        }
+        __syncthreads();
+        if (!s_live) break;
+      }
+    }
+    // ---- layer 0: gi = P[id]
+    gates_publish(0, t);
+    // ---- layers >= 1: gi_l = h_{l-1}(t) W_ih_l^T + b_ih_l  (+ gh_{l-1} of the next char)
+    static_for<1, L>([&](auto lt) {
+      constexpr int l = decltype(lt)::value;
+      product(ic<L + l - 1>{}, ic<l - 1>{}, t, sgi, sbi[l], R3);
+      gates_publish(l, t);
+    });
+    // ---- FC: logits rows b VR .. b VR + VR  (+ gh_{L-1} of the next char)
+    product(ic<NT>{}, ic<L - 1>{}, t, sgi, sbf, VR);
+    if (w == 0) {
+      if (lane < Np)
+        for (int r = 0; r < VR; ++r)
+          st_sc1(xr, lg0 + (unsigned)(((t & 1) * kNmax + lane) * V + b * VR + r) * 4, sgi[r][lane]);
+      publish_flag(L, t);
+    }
+  }
+
+  // ---- the last workgroup out zeroes the flags for the next launch (nobody polls them any more)
+  __syncthreads();
+  if (tid == 0) s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == kG - 1;
+  __syncthreads();
+  if (s_last) {
+    for (long i = tid; i < (long)(L + 1) * kG * kFS; i += 512) flags[i] = 0u;
+    if (tid == 0) *done = 0u;
+  }
+}
+
+#define GP_VARIANTS(X) X(8, 1) X(8, 2) X(8, 3) X(8, 4) X(16, 1) X(16, 2) X(16, 3) X(16, 4) X(32, 1) X(32, 2)
+
+// resident workgroups of the variant on the whole device (0 on any query failure: unsupported)
+static int gp_resident(int KJ, int L) {
+  int dev = 0, cus = 0, nb = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+#define X(K, LL) \
+  if (KJ == K && L == LL && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, gen_persist_kernel<K, LL>, 512, 0) != hipSuccess) return 0;
+  GP_VARIANTS(X)
+#undef X
+  return cus >= kG ? cus * nb : 0;   // one workgroup per CU is the layout; fewer CUs: unsupported
+}
+
+bool gen_persist_supported(int H, int L, int V, int N, int ML) {
+  if (N < 1 || N > kNmax || L < 1 || L > 4 || H % 256 || V % kG || V > kVmax || ML < 1) return false;
+  const int KJ = H / 32;
+  if (KJ != 8 && KJ != 16 && KJ != 32) return false;
+  if (2 * L * KJ > 128) return false;   // resident weight registers per lane
+  return gp_resident(KJ, L) >= kG;
+}
+
+long gen_persist_ws_floats(int H, int L, int V) { return (long)L * 2 * kNmax * H + 2L * kNmax * V; }
+long gen_persist_sync_words(int L) { return (long)(L + 1) * kG * kFS + 16; }
+
+void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
+  if (!gen_persist_supported(a.H, a.L, a.V, a.N, a.ML))
+    throw std::runtime_error("gen_persist_f32: unsupported shape or device (see gen_persist_supported)");
+  if (!a.ws || !a.sync || !a.err || !a.P || !a.Wfc || !a.bfc || !a.rf || !a.out)
+    throw std::runtime_error("gen_persist_f32: missing buffer");
+  for (int l = 0; l < a.L; ++l)
+    if (!a.Whh[l] || !a.bhh[l] || (l > 0 && (!a.Wih[l] || !a.bih[l])))
+      throw std::runtime_error("gen_persist_f32: missing layer weights");
+  const int KJ = a.H / 32;
+#define X(K, LL) \
+  if (KJ == K && a.L == LL) { hipLaunchKernelGGL((gen_persist_kernel<K, LL>), dim3(kG), dim3(512), 0, s, a); return; }
+  GP_VARIANTS(X)
+#undef X
+  throw std::runtime_error("gen_persist_f32: no variant");
+}
+
+}  // namespace gk

@@ -217,6 +217,26 @@ struct GenResetArgs {
   int L = 0, Bp = 0, H = 0, ML = 0, sos = 0;
 };
 void gen_reset(const GenResetArgs& a, hipStream_t s);
+// Persistent fp32 generation for small batches (gen_persist.hip): ONE launch runs every char of up to
+// 64 names with the fp32 recurrent weights resident in VGPRs across 256 workgroups (exchange
+// buffers in `ws`).
+struct GenPersistArgs {
+  const float* Whh[4] = {}; const float* Wih[4] = {};   // [3H][H] (Wih[0] unused: folded into P)
+  const float* bhh[4] = {}; const float* bih[4] = {};   // [3H]
+  const float* Wfc = nullptr; const float* bfc = nullptr;   // [V][H], [V]
+  const float* P = nullptr;        // [V][3H] layer-0 table Emb W_ih0^T + b_ih0
+  const float* rf = nullptr;       // [N][ML] uniforms
+  unsigned char* out = nullptr;    // [N][ML + 1]
+  float* probs = nullptr;          // nullable [Npad][V]: softmax of the last step (tests)
+  float* ws = nullptr;             // gen_persist_ws_floats(): exchange buffers
+  unsigned* sync = nullptr;        // gen_persist_sync_words(): epoch flags + arrival count (zeroed once, self-cleaning)
+  unsigned* err = nullptr;         // bit 32: a cross-workgroup wait hit its spin limit
+  int N = 0, H = 0, L = 0, V = 0, ML = 0, sos = 0, eos = 0;
+};
+bool gen_persist_supported(int H, int L, int V, int N, int ML);
+long gen_persist_ws_floats(int H, int L, int V);
+long gen_persist_sync_words(int L);
+void gen_persist_f32(const GenPersistArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ generic GEMM
 // C[M][N] (+)= A[M][K] · B[N][K]^T  (bf16 in, fp32 accumulate), both operands K-contiguous.
