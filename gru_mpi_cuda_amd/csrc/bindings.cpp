@@ -134,6 +134,7 @@ PYBIND11_MODULE(_C, m) {
       .def("read_error", &Generator::read_error)
       .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); })
       .def("set_persist", &Generator::set_persist)
+      .def("set_persist_max", &Generator::set_persist_max)
       .def("uses_persist", &Generator::uses_persist);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)

@@ -38,6 +38,7 @@ class Generator {
   // launch per batch (gen_persist.hip) instead of the per-char graph.  On by default;
   // GK_GEN_PERSIST=0 or set_persist(false) turns it off.
   void set_persist(bool on) { persist_ = on; }
+  void set_persist_max(int n) { persist_max_ = n; }
   bool uses_persist(int n) const;
   unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
 

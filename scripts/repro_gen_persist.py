@@ -15,6 +15,7 @@ for L, E, H, N in [(2, 256, 256, 32), (1, 128, 512, 32), (1, 128, 1024, 32), (2,
     params = init_params(cfg)
     rf = random_floats(N, cfg.max_len, seed=9)
     g = HipGenerator(cfg, params, precision="fp32")
+    g.g.set_persist_max(64)
     outs = [g.generate(rf) for _ in range(4)]
     err = g.g.read_error()
     g.g.set_persist(False)

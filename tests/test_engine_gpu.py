@@ -182,6 +182,7 @@ def test_generator_persistent_fp32(L, E, H, N):
     params = init_params(cfg)
     rf = random_floats(N, cfg.max_len, seed=9)
     gen = HipGenerator(cfg, params, precision="fp32")
+    gen.g.set_persist_max(64)   # (default 32: the per-char graph is faster at 64 names)
     assert gen.g.uses_persist(N)
     got = gen.generate(rf)
     again = gen.generate(rf)
