@@ -138,6 +138,16 @@ PYBIND11_MODULE(_C, m) {
       .def("uses_persist", &Generator::uses_persist);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)
+  m.def("gemm_f32", [](py::dict d, uintptr_t s) {   // fp32 MFMA GEMM of the fp32 generation path
+    GemmF32Args a;
+    a.A = GP(const float, d, "A"); a.lda = get<int>(d, "lda", 0);
+    a.B = GP(const float, d, "B"); a.ldb = get<int>(d, "ldb", 0);
+    a.C = GP(float, d, "C"); a.ldc = get<int>(d, "ldc", 0);
+    a.bias = GP(const float, d, "bias");
+    a.M = get<int>(d, "M", 0); a.N = get<int>(d, "N", 0); a.K = get<int>(d, "K", 0);
+    a.splits = get<int>(d, "splits", 1); a.slab = get<long>(d, "slab", 0);
+    gemm_f32_nt(a, S(s));
+  });
   m.def("gemm_nt", [](py::dict d, uintptr_t s) {
     GemmArgs a;
     a.A = GP(const u16, d, "A"); a.lda = get<int>(d, "lda", 0);

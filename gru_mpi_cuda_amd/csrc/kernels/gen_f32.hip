@@ -11,6 +11,7 @@
 //     intrinsics), layer 0's input projection gathered from the fp32 table P = Emb W_ih0^T + b_ih0;
 //   * sample_f32: max-subtracted fp32 softmax and the `psum > r` rule (first index whose running
 //     sum exceeds r, else V - 1), EOS written then the name stops (namegensf.cu:877-882).
+#include <cstdlib>
 #include "kernels.h"
 #include "common.h"
 #include "gen_sample.h"
@@ -84,10 +85,84 @@ __global__ void __launch_bounds__(256) gemm_f32_nt_kernel(GemmF32Args g) {
   }
 }
 
+// Big products (batched generation: 4096 names x 3H x H per layer and char): 128 x 128 tiles, each
+// wave 64 x 64 = 4 x 4 MFMA tiles (16 independent accumulator chains), half the LDS reads and
+// operand traffic per MFMA of the 64 x 64 kernel; next k-tile's global loads issued before the MFMAs.
+constexpr int kT2 = 128;
+__global__ void __launch_bounds__(256) gemm_f32_nt128_kernel(GemmF32Args g) {
+  __shared__ __attribute__((aligned(16))) float As[2][kT2][kLd];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kT2][kLd];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * kT2, n0 = blockIdx.x * kT2;
+  const int lrow = t >> 2, lk = (t & 3) * 4;          // rows lrow and lrow + 64, 16 B each
+  const float* pa = g.A + (size_t)(m0 + lrow) * g.lda + lk;
+  const float* pb = g.B + (size_t)(n0 + lrow) * g.ldb + lk;
+  const size_t a64 = (size_t)64 * g.lda, b64 = (size_t)64 * g.ldb;
+  float4 ra0 = *reinterpret_cast<const float4*>(pa), ra1 = *reinterpret_cast<const float4*>(pa + a64);
+  float4 rb0 = *reinterpret_cast<const float4*>(pb), rb1 = *reinterpret_cast<const float4*>(pb + b64);
+  *reinterpret_cast<float4*>(&As[0][lrow][lk]) = ra0;
+  *reinterpret_cast<float4*>(&As[0][lrow + 64][lk]) = ra1;
+  *reinterpret_cast<float4*>(&Bs[0][lrow][lk]) = rb0;
+  *reinterpret_cast<float4*>(&Bs[0][lrow + 64][lk]) = rb1;
+  __syncthreads();
+  f32x4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fk = lane >> 4;
+  const int nk = g.K / kBK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      const int o = (kt + 1) * kBK;
+      ra0 = *reinterpret_cast<const float4*>(pa + o); ra1 = *reinterpret_cast<const float4*>(pa + a64 + o);
+      rb0 = *reinterpret_cast<const float4*>(pb + o); rb1 = *reinterpret_cast<const float4*>(pb + b64 + o);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kBK / 4; ++kk) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = As[cur][wm * 64 + i * 16 + fr][kk * 4 + fk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = Bs[cur][wn * 64 + j * 16 + fr][kk * 4 + fk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      *reinterpret_cast<float4*>(&As[cur ^ 1][lrow][lk]) = ra0;
+      *reinterpret_cast<float4*>(&As[cur ^ 1][lrow + 64][lk]) = ra1;
+      *reinterpret_cast<float4*>(&Bs[cur ^ 1][lrow][lk]) = rb0;
+      *reinterpret_cast<float4*>(&Bs[cur ^ 1][lrow + 64][lk]) = rb1;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + fr;
+    const float bias = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + fk * 4 + r;
+        g.C[(size_t)row * g.ldc + col] = acc[i][j][r] + bias;
+      }
+  }
+}
+
 void gemm_f32_nt(const GemmF32Args& g, hipStream_t s) {
   if (g.M % kT || g.N % kT || g.splits < 1 || g.K % g.splits || (g.K / g.splits) % kBK || g.lda % 4 || g.ldb % 4 ||
       (g.splits > 1 && g.slab < (long)g.M * g.ldc))
     throw std::runtime_error("gemm_f32_nt: needs M, N % 64 == 0, (K / splits) % 16 == 0 and 16-B aligned rows");
+  static const bool big_ok = [] { const char* e = std::getenv("GK_F32_GEMM128"); return !e || e[0] != '0'; }();
+  if (big_ok && g.splits == 1 && g.M % kT2 == 0 && g.N % kT2 == 0 && (g.M / kT2) * (g.N / kT2) >= 256) {
+    hipLaunchKernelGGL(gemm_f32_nt128_kernel, dim3(g.N / kT2, g.M / kT2), dim3(256), 0, s, g);
+    return;
+  }
   hipLaunchKernelGGL(gemm_f32_nt_kernel, dim3(g.N / kT, g.M / kT, g.splits), dim3(256), 0, s, g);
 }
 

@@ -359,3 +359,18 @@ def test_gemm256(ext, M, N, K, splits, bias, accumulate, lda_pad, rowsum):
     torch.testing.assert_close(C.sum(0), ref, atol=2e-3 * K ** 0.5, rtol=1e-3)
     if rowsum:
         torch.testing.assert_close(rs.sum(0), A.float().sum(1), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(4096, 3072, 1024, 1), (2048, 2048, 512, 1), (64, 3072, 1024, 8),
+                                          (128, 256, 1024, 4), (256, 256, 512, 1)])
+def test_gemm_f32(ext, M, N, K, splits):
+    """fp32 generation GEMM (gen_f32.hip: v_mfma_f32_16x16x4_f32, exact fp32 products): the 128 x 128
+    kernel (>= 256 tiles, unsplit) and the 64 x 64 split-K kernel against an fp64 torch product;
+    split-K slabs summed here, the bias in slab 0 only."""
+    A, B, bv = rnd(M, K, seed=4), rnd(N, K, seed=5), rnd(N, seed=6)
+    C = torch.full((splits, M, N), float("nan"), device=DEV)
+    ext.gemm_f32(dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, bias=bv.data_ptr(),
+                      M=M, N=N, K=K, splits=splits, slab=M * N), S())
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().T + bv.double()
+    torch.testing.assert_close(C.double().sum(0), ref, atol=1e-5 * K ** 0.5, rtol=1e-5)
