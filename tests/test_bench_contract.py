@@ -1,11 +1,13 @@
 """bench.py's output contract (one JSON line from rank 0, K timed steps, whole-job value, max over
-ranks), rehearsed on the CPU path: world 1 directly, world 2 under torch.distributed.run with gloo
-and 127.0.0.1 rendezvous -- the same launcher line the driver uses for N GPUs."""
+ranks), rehearsed on the CPU path: world 1 directly, worlds 2 and 8 under torch.distributed.run with
+gloo and 127.0.0.1 rendezvous -- the same launcher line the driver uses for N GPUs."""
 import json
 import os
 import socket
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
@@ -43,10 +45,14 @@ def test_bench_contract_world1():
     _lines([sys.executable, "bench.py", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], 1)
 
 
-def test_bench_contract_world2_gloo():
-    _lines([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
-            "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], 2)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_contract_torchrun_gloo(world):
+    """The driver's multi-GPU form (torchrun, one rank per device, up to a whole 8-GPU node),
+    rehearsed on CPU with gloo: one JSON line from rank 0 with n_gpus == world."""
+    r = _lines([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+                "--gpus", str(world), "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"], world)
+    assert r["rccl_ranks"] == world
 
 
 def test_bench_self_launches_world2():
