@@ -113,7 +113,8 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="engine,engine_fp32,torch,ref-schedule",
                     help="engine (bf16), engine_fp32 (fp32, persistent kernel at <= 64 names), "
-                         "engine_fp32_batched (fp32, per-char graph), torch, ref-schedule")
+                         "engine_fp32_batched (fp32, per-char graph), engine_bf16x3 (split-bf16 products), "
+                         "torch, ref-schedule")
     args = ap.parse_args()
     for n in [int(x) for x in str(args.names).split(",")]:
         args.n = n
@@ -151,7 +152,7 @@ def run(args) -> None:
     # engine = bf16 MFMA fast mode; engine_fp32 = fp32-faithful mode (the C API default: one
     # persistent launch at <= 64 names); engine_fp32_batched = fp32 with the per-char graph forced
     for key, prec, persist in (("engine", "bf16", True), ("engine_fp32", "fp32", True),
-                               ("engine_fp32_batched", "fp32", False)):
+                               ("engine_fp32_batched", "fp32", False), ("engine_bf16x3", "bf16x3", True)):
         if key not in modes:
             continue
         g = HipGenerator(cfg, params, max_batch=args.n, device=dev, precision=prec)

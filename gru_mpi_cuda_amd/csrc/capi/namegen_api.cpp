@@ -110,9 +110,9 @@ static void init_impl(int N, int rng_seed, char* parameter_fname) {
   g.sos = st.d.sos; g.eos = st.d.eos;
   g.max_batch = std::max(64, std::min(8192, (N + st.world - 1) / std::max(1, st.world)));
   // the reference's arithmetic is fp32 (namegensf.cu:233-242, 294-333): fp32-faithful by default,
-  // GK_GEN_PRECISION=bf16 selects the bf16 MFMA fast mode
+  // GK_GEN_PRECISION=bf16 selects the bf16 MFMA fast mode, bf16x3 the split-bf16 products
   const char* prec = std::getenv("GK_GEN_PRECISION");
-  g.fp32 = !(prec && std::string(prec) == "bf16");
+  g.fp32 = !prec ? 1 : std::string(prec) == "bf16" ? 0 : std::string(prec) == "bf16x3" ? 2 : 1;
   st.gen.reset(new Generator(g, st.params, offsets));
   st.gen->refresh_weights(st.s);
   HIP_CHECK(hipStreamSynchronize(st.s));   // the reference's MPI_Barrier (namegensf.cu:615)

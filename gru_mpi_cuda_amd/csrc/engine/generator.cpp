@@ -18,20 +18,23 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   Bmax_ = rup(std::max(32, d_.max_batch), 64);
   const int V = d_.V, E = d_.E, H = d_.H, L = d_.L, B = Bmax_;
   std::vector<size_t> ohf, ohb, oWhh, oWih;
-  for (int i = 0; i < 2 * L; ++i) { ohf.push_back(arena_.reserve((size_t)B * H * 4)); ohb.push_back(arena_.reserve((size_t)B * H * 2)); }
+  // bf16x3: the bf16 weight / state copies hold split rows ([hi | lo | hi] / [hi | hi | lo], 3x wide)
+  const size_t xw = d_.fp32 == 2 ? 3 : 1;
+  for (int i = 0; i < 2 * L; ++i) { ohf.push_back(arena_.reserve((size_t)B * H * 4)); ohb.push_back(arena_.reserve((size_t)B * H * 2 * xw)); }
   for (int l = 0; l < L; ++l) {
-    oWhh.push_back(arena_.reserve((size_t)3 * H * H * 2));
-    oWih.push_back(arena_.reserve((size_t)3 * H * (l == 0 ? E : H) * 2));
+    oWhh.push_back(arena_.reserve((size_t)3 * H * H * 2 * xw));
+    oWih.push_back(arena_.reserve((size_t)3 * H * (l == 0 ? E : H) * 2 * xw));
   }
-  size_t oEmb = arena_.reserve((size_t)V * E * 2), oWfc = arena_.reserve((size_t)V * H * 2);
+  size_t oEmb = arena_.reserve((size_t)V * E * 2), oWfc = arena_.reserve((size_t)V * H * 2 * xw);
   size_t oWfcF = arena_.reserve((size_t)V * H * 2);   // fragment-tiled copy for the 8-wave sampler
   size_t oP = arena_.reserve((size_t)V * 3 * H * 4), orf = arena_.reserve((size_t)B * d_.max_len * 4);
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
   size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256), opws = 0, opsync = 0;
   if (d_.fp32) {
-    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V) * 4);
-    opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);   // room for split-K slabs of small batches (f32_splits): kF32SlabRows rows
+    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V) * 4);   // persistent small-batch path
+    opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);
+    // room for split-K slabs of small batches (f32_splits / split3_splits): kF32SlabRows rows
     const size_t rows = std::max<size_t>(B, kF32SlabRows);
     ogh = arena_.reserve(rows * 3 * H * 4);
     ogi = arena_.reserve(rows * 3 * H * 4);
@@ -74,6 +77,14 @@ void Generator::refresh_weights(hipStream_t s) {
     g.A = P("embedding"); g.lda = E; g.B = P("weight_ih_l0"); g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
     g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;
     gemm_f32_nt(g, s);
+    if (split3()) {   // the products' weight operands: [hi | lo | hi] rows
+      for (int l = 0; l < d_.L; ++l) {
+        const std::string k = std::to_string(l);
+        split_bf16x3(P("weight_hh_l" + k), 3 * H, H, Whh_[l], s);
+        if (l > 0) split_bf16x3(P("weight_ih_l" + k), 3 * H, H, Wih_[l], s);
+      }
+      split_bf16x3(P("fc.weight"), V, H, Wfc_, s);
+    }
     HIP_LAUNCH_CHECK();
     return;
   }
@@ -100,9 +111,10 @@ void Generator::refresh_weights(hipStream_t s) {
 void Generator::reset_batch(int Bp, bool bf16, hipStream_t s) {
   GenResetArgs r;
   r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
+  r.hb_cols = split3() ? 3 * d_.H : d_.H;
   for (int l = 0; l < d_.L; ++l) {
     r.hf[l] = hf_[2 * l];
-    r.hb[l] = bf16 ? hb_[2 * l] : nullptr;
+    r.hb[l] = (bf16 || split3()) ? hb_[2 * l] : nullptr;
   }
   r.ids = ids_; r.alive = alive_; r.out = out_;
   gen_reset(r, s);
@@ -149,43 +161,86 @@ static int f32_splits(int M, int N, int K, int rows_cap) {
   return sp;
 }
 
+// bf16x3 split-K depth: unsplit when the LDS-staged kernels get a grid (>= 128 tiles of 128 x 128),
+// else the one-shot small GEMM over the smallest K-slice count that gives ~256 workgroups (slices
+// it supports: 2-4 or 8 k-blocks of 64, or whole multiples of 8 up to 32); slabs within rows_cap
+static int split3_splits(int M, int N, int K3, int rows_cap) {
+  if (M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= 128) return 1;
+  const int tiles = (M / 64) * (N / 64);
+  int last = 1;
+  for (int sp = 2; sp <= 32; ++sp) {
+    if (K3 % sp || (K3 / sp) % 64 || M * sp > rows_cap) continue;
+    const int nkb = K3 / sp / 64;
+    if (!(nkb == 2 || nkb == 3 || nkb == 4 || nkb == 8 || (nkb % 8 == 0 && nkb <= 32))) continue;
+    last = sp;
+    if (tiles * sp >= 256) return sp;
+  }
+  return last;
+}
+
+int Generator::product_f32(const float* A32, const u16* A3, const std::string& w, const float* bias, int M, int N,
+                           float* C, hipStream_t s) {
+  const int H = d_.H;
+  const int cap = std::max(Bmax_, kF32SlabRows);
+  if (!split3()) {
+    GemmF32Args g;
+    g.A = A32; g.lda = H; g.B = P(w); g.ldb = H; g.C = C; g.ldc = N;
+    g.bias = bias; g.M = M; g.N = N; g.K = H;
+    g.splits = f32_splits(M, N, H, cap); g.slab = (long)M * N;
+    gemm_f32_nt(g, s);
+    return g.splits;
+  }
+  const u16* W3 = w == "fc.weight" ? Wfc_ : (w.rfind("weight_hh_l", 0) == 0 ? Whh_[std::stoi(w.substr(11))]
+                                                                            : Wih_[std::stoi(w.substr(11))]);
+  GemmArgs g;
+  g.A = A3; g.lda = 3 * H; g.B = W3; g.ldb = 3 * H; g.C = C; g.ldc = N;
+  g.M = M; g.N = N; g.K = 3 * H;
+  g.splits = split3_splits(M, N, 3 * H, cap);
+  if (g.splits == 1) {
+    g.bias = bias;   // split: the consumer adds the bias after the slab sum
+    // the 256 x 256 kernel from 3/4 of a wave of its tiles (4096 names x 3H: 192 tiles), where the
+    // 128 x 128 kernel's 1.5 rounds of 512 slots leave as much idle
+    static const bool big = [] { const char* e = std::getenv("GK_X3_GEMM256"); return !e || e[0] != '0'; }();
+    if (big && M % 256 == 0 && N % 256 == 0 && (M / 256) * (N / 256) >= 192) g.algo = 5;
+  } else {
+    g.algo = 3;
+  }
+  gemm_nt(g, s);
+  return g.splits;
+}
+
 void Generator::record_steps_f32(int n, hipStream_t s) {
   const int H = d_.H, L = d_.L, V = d_.V, ML = d_.max_len;
   const int Bp = rup(n, 64);
-  const int cap = std::max(Bmax_, kF32SlabRows);
-  const int sh = f32_splits(Bp, 3 * H, H, cap), sf = f32_splits(Bp, V, H, cap);
+  const bool x3 = split3();
   reset_batch(Bp, false, s);
   for (int st = 0; st < ML; ++st) {
     const int cur = st & 1, nxt = cur ^ 1;
     for (int l = 0; l < L; ++l) {
       const std::string k = std::to_string(l);
-      GemmF32Args g;
-      g.A = hf_[2 * l + cur]; g.lda = H; g.B = P("weight_hh_l" + k); g.ldb = H; g.C = gh_; g.ldc = 3 * H;
-      g.bias = P("bias_hh_l" + k); g.M = Bp; g.N = 3 * H; g.K = H;
-      g.splits = sh; g.slab = (long)Bp * 3 * H;
-      gemm_f32_nt(g, s);
+      const float* bh = P("bias_hh_l" + k);
+      const int sh = product_f32(hf_[2 * l + cur], hb_[2 * l + cur], "weight_hh_l" + k, bh, Bp, 3 * H, gh_, s);
       GruGatesF32Args a;
       if (l == 0) {
         a.P = Ptab_; a.ids = ids_;
       } else {
-        GemmF32Args x;
-        x.A = hf_[2 * (l - 1) + nxt]; x.lda = H; x.B = P("weight_ih_l" + k); x.ldb = H; x.C = gi_; x.ldc = 3 * H;
-        x.bias = P("bias_ih_l" + k); x.M = Bp; x.N = 3 * H; x.K = H;
-        x.splits = sh; x.slab = (long)Bp * 3 * H;
-        gemm_f32_nt(x, s);
-        a.Gi = gi_; a.gi_splits = sh; a.gi_slab = (long)Bp * 3 * H;
+        const float* bi = P("bias_ih_l" + k);
+        const int si = product_f32(hf_[2 * (l - 1) + nxt], hb_[2 * (l - 1) + nxt], "weight_ih_l" + k, bi, Bp, 3 * H,
+                                   gi_, s);
+        a.Gi = gi_; a.gi_splits = si; a.gi_slab = (long)Bp * 3 * H;
+        if (x3 && si > 1) a.bgi = bi;
       }
-      a.Gh = gh_; a.gh_splits = sh; a.gh_slab = (long)Bp * 3 * H; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt]; a.Bp = Bp; a.H = H;
-      a.V = V; a.err = err_;
+      a.Gh = gh_; a.gh_splits = sh; a.gh_slab = (long)Bp * 3 * H; a.hprev = hf_[2 * l + cur]; a.hout = hf_[2 * l + nxt];
+      if (x3 && sh > 1) a.bgh = bh;
+      if (x3) a.hsplit = hb_[2 * l + nxt];
+      a.Bp = Bp; a.H = H; a.V = V; a.err = err_;
       gru_gates_f32(a, s);
     }
-    GemmF32Args f;
-    f.A = hf_[2 * (L - 1) + nxt]; f.lda = H; f.B = P("fc.weight"); f.ldb = H; f.C = logits_; f.ldc = V;
-    f.bias = P("fc.bias"); f.M = Bp; f.N = V; f.K = H;
-    f.splits = sf; f.slab = (long)Bp * V;
-    gemm_f32_nt(f, s);
+    const float* bf = P("fc.bias");
+    const int sf = product_f32(hf_[2 * (L - 1) + nxt], hb_[2 * (L - 1) + nxt], "fc.weight", bf, Bp, V, logits_, s);
     SampleF32Args q;
     q.logits = logits_; q.splits = sf; q.slab = (long)Bp * V; q.rf = rf_; q.ids = ids_; q.out = out_; q.alive = alive_;
+    if (x3 && sf > 1) q.bias = bf;
     q.probs = (st == ML - 1) ? probe_ : nullptr;
     q.N = n; q.V = V; q.step = st; q.max_len = ML; q.eos = d_.eos;
     sample_f32(q, s);

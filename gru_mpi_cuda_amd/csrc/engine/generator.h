@@ -20,7 +20,8 @@ namespace gk {
 struct GenDims {
   int V = 256, E = 512, H = 1024, L = 2, max_len = 10, sos = 0, eos = 0, max_batch = 4096;
   // 1: fp32-faithful (the reference's arithmetic: fp32 MFMA GEMMs on the fp32 master weights, IEEE
-  // gates and softmax, gen_f32.hip); 0: bf16 MFMA fast mode
+  // gates and softmax, gen_f32.hip); 0: bf16 MFMA fast mode; 2: bf16x3 -- the fp32 path with its
+  // products as bf16 MFMA GEMMs over split operands (hi*hi + hi*lo + lo*hi, ~2^-16 relative error)
   int fp32 = 0;
 };
 
@@ -45,6 +46,10 @@ class Generator {
  private:
   void record_steps(int n_active, hipStream_t s);
   void record_steps_f32(int n_active, hipStream_t s);
+  // one product of the fp32 / bf16x3 path: C = h W^T (+ bias) -> splits (slabs of M x N at C)
+  int product_f32(const float* A32, const u16* A3, const std::string& w, const float* bias, int M, int N, float* C,
+                  hipStream_t s);
+  bool split3() const { return d_.fp32 == 2; }
   void reset_batch(int Bp, bool bf16, hipStream_t s);
   const float* P(const std::string& n) const { return params_ + off_.at(n); }
 

@@ -11,6 +11,7 @@
 //     intrinsics), layer 0's input projection gathered from the fp32 table P = Emb W_ih0^T + b_ih0;
 //   * sample_f32: max-subtracted fp32 softmax and the `psum > r` rule (first index whose running
 //     sum exceeds r, else V - 1), EOS written then the name stops (namegensf.cu:877-882).
+#include <algorithm>
 #include <cstdlib>
 #include "kernels.h"
 #include "common.h"
@@ -195,10 +196,37 @@ __global__ void gru_gates_f32_kernel(GruGatesF32Args a) {
     if (!a.P)
       for (int s2 = 1; s2 < a.gi_splits; ++s2) xi[q] += gi[s2 * a.gi_slab + q * H + j];
   }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (a.bgh) xh[q] += a.bgh[q * H + j];
+    if (a.bgi && !a.P) xi[q] += a.bgi[q * H + j];
+  }
   const float r = sigmoid_ieee(xi[0] + xh[0]);
   const float z = sigmoid_ieee(xi[1] + xh[1]);
   const float n = tanhf(xi[2] + r * xh[2]);
-  a.hout[i] = (1.f - z) * n + z * a.hprev[i];
+  const float h = (1.f - z) * n + z * a.hprev[i];
+  a.hout[i] = h;
+  if (a.hsplit) {
+    const u16 hi = f2bf(h), lo = f2bf(h - bf2f(hi));
+    u16* d = a.hsplit + (size_t)b * 3 * H + j;
+    d[0] = hi; d[H] = hi; d[2 * H] = lo;
+  }
+}
+
+// fp32 [R][K] -> bf16 [R][3K] = [hi | lo | hi] (the weight side of a bf16x3 product)
+__global__ void split_bf16x3_kernel(const float* __restrict__ src, int R, int K, u16* __restrict__ dst) {
+  const long n = (long)R * K, stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const long r = i / K, k = i - r * K;
+    const float x = src[i];
+    const u16 hi = f2bf(x), lo = f2bf(x - bf2f(hi));
+    u16* d = dst + r * 3 * K + k;
+    d[0] = hi; d[K] = lo; d[2 * K] = hi;
+  }
+}
+void split_bf16x3(const float* src, int R, int K, u16* dst, hipStream_t s) {
+  const long n = (long)R * K;
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 4096)), dim3(256), 0, s, src, R, K, dst);
 }
 
 void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s) {
@@ -218,6 +246,7 @@ __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
     if (e < per) {
       float v = x[e];
       for (int s2 = 1; s2 < a.splits; ++s2) v += x[s2 * a.slab + e];   // split-K slabs, fixed order
+      if (a.bias) v += a.bias[lane * per + e];
       xv[e] = v;
     } else {
       xv[e] = -INFINITY;
@@ -236,12 +265,14 @@ __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
 
 __global__ void gen_reset_kernel(GenResetArgs a) {
   const long n = (long)a.Bp * a.H, stride = (long)gridDim.x * blockDim.x;
+  const int hbm = a.hb_cols ? a.hb_cols / a.H : 1;   // bf16 copies per row: 1, or 3 (bf16x3 split)
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       if (l < a.L) {
         a.hf[l][i] = 0.f;
-        if (a.hb[l]) a.hb[l][i] = 0;
+        if (a.hb[l])
+          for (int c = 0; c < hbm; ++c) a.hb[l][(i / a.H) * (long)hbm * a.H + c * a.H + i % a.H] = 0;
       }
     }
     if (i < a.Bp) { a.ids[i] = a.sos; a.alive[i] = 1; }
@@ -250,6 +281,7 @@ __global__ void gen_reset_kernel(GenResetArgs a) {
 }
 void gen_reset(const GenResetArgs& a, hipStream_t s) {
   if (a.L > 4 || a.H < a.ML + 1) throw std::runtime_error("gen_reset: at most 4 layers, H > max_len");
+  if (a.hb_cols && a.hb_cols != a.H && a.hb_cols != 3 * a.H) throw std::runtime_error("gen_reset: hb_cols must be H or 3H");
   hipLaunchKernelGGL(gen_reset_kernel, dim3(256), dim3(256), 0, s, a);
 }
 

@@ -197,6 +197,10 @@ struct GruGatesF32Args {           // h' = GRU gates from gi (or P[ids]) and gh 
   const float* hprev = nullptr; float* hout = nullptr;   // [Bp][H]
   int Bp = 0, H = 0, V = 0;
   unsigned* err = nullptr;         // layer 0: bit 4 set (and the row clamped) on a char id outside [0, V)
+  // bf16x3 mode: biases not folded into split-K slabs (nullable), and the bf16 split copy of h'
+  // written as the next products' A operand: hsplit[b] = [hi | hi | lo] of h'[b] ([Bp][3H])
+  const float* bgh = nullptr; const float* bgi = nullptr;
+  unsigned short* hsplit = nullptr;
 };
 void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s);
 struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sample (same I/O as fc_sample)
@@ -206,13 +210,19 @@ struct SampleF32Args {             // softmax of fp32 logits + inverse-CDF sampl
   int* ids = nullptr; unsigned char* out = nullptr; int* alive = nullptr;
   float* probs = nullptr;
   int N = 0, V = 0, step = 0, max_len = 0, eos = 0;
+  const float* bias = nullptr;     // nullable: added after the slab sum (bf16x3 split-K logits)
 };
 void sample_f32(const SampleF32Args& a, hipStream_t s);
+// bf16x3 operands: an fp32 value x = hi + lo with hi = bf16(x), lo = bf16(x - hi).  Weights become
+// [R][3K] = [hi | lo | hi] rows and activations [hi | hi | lo] rows, so ONE bf16 MFMA GEMM over 3K
+// accumulates hi*hi + hi*lo + lo*hi in fp32 (the lo*lo term, ~2^-16 relative, is dropped).
+void split_bf16x3(const float* src, int R, int K, unsigned short* dst, hipStream_t s);
 // per-batch generation reset as ONE kernel node (instead of memset nodes): h slot 0 of every layer
 // (fp32 and, if given, bf16) = 0, ids = sos, alive = 1, output rows = NUL
 struct GenResetArgs {
   float* hf[4] = {nullptr, nullptr, nullptr, nullptr};
   unsigned short* hb[4] = {nullptr, nullptr, nullptr, nullptr};
+  int hb_cols = 0;                 // columns of hb rows: H (bf16 copy) or 3H (bf16x3 split copy); 0 = H
   int* ids = nullptr; int* alive = nullptr; unsigned char* out = nullptr;
   int L = 0, Bp = 0, H = 0, ML = 0, sos = 0;
 };

@@ -29,13 +29,18 @@ from ..models.params import flat_layout, pad_config, pad_params, to_flat
 from ..parallel.dist import DistCtx, shard
 
 
-PRECISIONS = ("fp32", "bf16")
+PRECISIONS = ("fp32", "bf16", "bf16x3")
+_MODE = {"bf16": 0, "fp32": 1, "bf16x3": 2}   # GenDims::fp32
 
 
 class HipGenerator:
     """precision "fp32" (default): fp32-faithful -- fp32 MFMA GEMMs on the fp32 master weights,
     IEEE gates and softmax, the reference's arithmetic (namegensf.cu:233-242, 294-333);
-    "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies)."""
+    "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies);
+    "bf16x3": the fp32 path with its products as bf16 MFMA GEMMs over split operands
+    (x = hi + lo, hi*hi + hi*lo + lo*hi in fp32: ~2^-16 relative error per product instead of fp32's
+    2^-24, at the bf16 MFMA rate x 1/3).  Batches of <= 32 names run the exact fp32 persistent
+    kernel in both fp32 modes."""
 
     def __init__(self, cfg: GRUConfig, params: Dict[str, torch.Tensor], max_batch: int = 4096,
                  device: Optional[torch.device] = None, flat: Optional[torch.Tensor] = None,
@@ -60,7 +65,7 @@ class HipGenerator:
         self.flat = flat if flat is not None else to_flat(icfg, params).to(self.dev)
         offsets = {s.name: s.offset for s in self.layout.segments}
         dims = dict(V=cfg.vocab, E=icfg.embed, H=icfg.hidden, L=cfg.layers, max_len=cfg.max_len,
-                    sos=cfg.sos, eos=cfg.eos, max_batch=max_batch, fp32=int(precision == "fp32"))
+                    sos=cfg.sos, eos=cfg.eos, max_batch=max_batch, fp32=_MODE[precision])
         self.g = self.C.Generator(dims, self.flat.data_ptr(), offsets)
         self.g.refresh_weights(self._s())
 
