@@ -303,6 +303,12 @@ PYBIND11_MODULE(_C, m) {
 
   // ---------------------------------------------------------------- RCCL communicator
   m.def("bootstrap_key", &bootstrap_key);
+  m.def("launch_env", [] {
+    const LaunchEnv e = launch_env();
+    py::dict d;
+    d["rank"] = e.rank; d["world"] = e.world; d["local"] = e.local; d["launcher"] = e.launcher;
+    return d;
+  });
   m.def("bootstrap_path", &bootstrap_path);
   m.def("file_exchange_uid", [](int rank, const std::string& path, const std::string& key, py::bytes uid,
                                 int timeout_ms) {

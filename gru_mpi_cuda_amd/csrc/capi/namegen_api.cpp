@@ -41,11 +41,6 @@ struct State {
 };
 std::unique_ptr<State> S;
 
-int env_int(const char* k, int dflt) {
-  const char* v = std::getenv(k);
-  return v && *v ? std::atoi(v) : dflt;
-}
-
 void shard(int n, int rank, int world, int* start, int* count) {
   const int base = n / world, rem = n % world;
   *count = base + (rank < rem ? 1 : 0);
@@ -58,9 +53,10 @@ static void init_impl(int N, int rng_seed, char* parameter_fname) {
   (void)rng_seed;   // unused, as in the reference (namegensf.cu:359)
   S.reset(new State());
   State& st = *S;
-  st.rank = env_int("RANK", 0);
-  st.world = env_int("WORLD_SIZE", 1);
-  st.local = env_int("LOCAL_RANK", st.rank);
+  const LaunchEnv le = launch_env();   // torchrun, mpirun (Open MPI / Hydra) or srun
+  st.rank = le.rank;
+  st.world = le.world;
+  st.local = le.local;
   global_rank() = st.rank;
   int ndev = 0;
   HIP_CHECK(hipGetDeviceCount(&ndev));
@@ -166,8 +162,8 @@ static void finalize_impl() {
   S.reset();
 }
 
-extern "C" int namegen_rank(void) { return S ? S->rank : env_int("RANK", 0); }
-extern "C" int namegen_world(void) { return S ? S->world : env_int("WORLD_SIZE", 1); }
+extern "C" int namegen_rank(void) { return S ? S->rank : launch_env().rank; }
+extern "C" int namegen_world(void) { return S ? S->world : launch_env().world; }
 extern "C" int namegen_max_len(void) { return S ? S->d.max_len : 0; }
 
 // C boundary: like the reference's CUDA_CALL, report and exit instead of unwinding into C

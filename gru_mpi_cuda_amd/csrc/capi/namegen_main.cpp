@@ -3,8 +3,10 @@
 //
 //   namegen <parameter_file> <output_file> <N> [rng_seed]
 //
-// One process per GPU under any launcher that sets RANK / WORLD_SIZE / LOCAL_RANK (and
-// MASTER_PORT or GK_BOOTSTRAP_FILE for the RCCL unique-id exchange).  Rank 0 draws
+// One process per GPU under torchrun / parallel.launch (RANK, WORLD_SIZE, LOCAL_RANK), Open MPI or
+// MPICH `mpirun -np P`, or Slurm `srun` -- the reference's launch line works unchanged (the rank
+// variables of each are read by comm/bootstrap.cpp launch_env; the RCCL unique id travels through a
+// job-unique file).  Rank 0 draws
 // N*MAX_LEN uniforms in [0,1) from rng_seed (splitmix64; the reference's generator is not in
 // its repo), writes one name per line to output_file and prints the generation throughput.
 #include <chrono>

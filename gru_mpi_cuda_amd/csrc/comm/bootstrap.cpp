@@ -16,10 +16,46 @@ namespace gk {
 static const char kMagic[8] = {'G', 'K', 'U', 'I', 'D', '0', '0', '1'};
 static constexpr size_t kUidBytes = 128;
 
+static const char* env_str(const char* k) {
+  const char* v = std::getenv(k);
+  return v && *v ? v : nullptr;
+}
+
+LaunchEnv launch_env() {
+  struct Scheme { const char *rank, *world, *local, *name; };
+  static const Scheme schemes[] = {
+      {"RANK", "WORLD_SIZE", "LOCAL_RANK", "torchrun"},
+      {"OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK", "openmpi"},
+      {"PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID", "hydra"},
+      {"SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID", "slurm"},
+  };
+  LaunchEnv e;
+  for (const Scheme& sc : schemes) {
+    const char* r = env_str(sc.rank);
+    const char* w = env_str(sc.world);
+    if (!r || !w) continue;
+    e.rank = std::atoi(r);
+    e.world = std::atoi(w);
+    const char* l = env_str(sc.local);
+    e.local = l ? std::atoi(l) : e.rank;
+    e.launcher = sc.name;
+    if (e.world < 1 || e.rank < 0 || e.rank >= e.world)
+      throw std::runtime_error(std::string("launch_env: inconsistent ") + sc.rank + "/" + sc.world);
+    return e;
+  }
+  return e;
+}
+
 std::string bootstrap_key() {
   if (const char* r = std::getenv("GK_RUN_ID"); r && *r) return std::string("run:") + r;
   if (const char* t = std::getenv("TORCHELASTIC_RUN_ID"); t && *t && std::strcmp(t, "none") != 0)
     return std::string("te:") + t;
+  if (const char* p = env_str("PMIX_NAMESPACE")) return std::string("pmix:") + p;
+  if (const char* o = env_str("OMPI_MCA_ess_base_jobid")) return std::string("ompi:") + o;
+  if (const char* j = env_str("SLURM_JOB_ID")) {
+    const char* st = env_str("SLURM_STEP_ID");
+    return std::string("slurm:") + j + "." + (st ? st : "0");
+  }
   const char* port = std::getenv("MASTER_PORT");
   return "ppid:" + std::to_string((long)getppid()) + ":" + (port ? port : "0");
 }
