@@ -135,6 +135,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_probe", [](Generator& g, uintptr_t p) { g.set_probe(Pp<float>(p)); })
       .def("set_persist", &Generator::set_persist)
       .def("set_persist_max", &Generator::set_persist_max)
+      .def("set_persist_dbg", [](Generator& g, uintptr_t p) { g.set_persist_dbg(reinterpret_cast<unsigned long long*>(p)); })
       .def("uses_persist", &Generator::uses_persist);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)

@@ -32,7 +32,7 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
   size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256), opws = 0, opsync = 0;
   if (d_.fp32) {
-    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V) * 4);   // persistent small-batch path
+    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V, d_.max_len) * 4);   // persistent small-batch path
     opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);
     // room for split-K slabs of small batches (f32_splits / split3_splits): kF32SlabRows rows
     const size_t rows = std::max<size_t>(B, kF32SlabRows);
@@ -178,20 +178,18 @@ static int split3_splits(int M, int N, int K3, int rows_cap) {
   return last;
 }
 
-int Generator::product_f32(const float* A32, const u16* A3, const std::string& w, const float* bias, int M, int N,
-                           float* C, hipStream_t s) {
+int Generator::product_f32(const float* A32, const u16* A3, const float* W32, const u16* W3, const float* bias, int M,
+                           int N, float* C, hipStream_t s) {
   const int H = d_.H;
   const int cap = std::max(Bmax_, kF32SlabRows);
   if (!split3()) {
     GemmF32Args g;
-    g.A = A32; g.lda = H; g.B = P(w); g.ldb = H; g.C = C; g.ldc = N;
+    g.A = A32; g.lda = H; g.B = W32; g.ldb = H; g.C = C; g.ldc = N;
     g.bias = bias; g.M = M; g.N = N; g.K = H;
     g.splits = f32_splits(M, N, H, cap); g.slab = (long)M * N;
     gemm_f32_nt(g, s);
     return g.splits;
   }
-  const u16* W3 = w == "fc.weight" ? Wfc_ : (w.rfind("weight_hh_l", 0) == 0 ? Whh_[std::stoi(w.substr(11))]
-                                                                            : Wih_[std::stoi(w.substr(11))]);
   GemmArgs g;
   g.A = A3; g.lda = 3 * H; g.B = W3; g.ldb = 3 * H; g.C = C; g.ldc = N;
   g.M = M; g.N = N; g.K = 3 * H;
@@ -219,14 +217,14 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
     for (int l = 0; l < L; ++l) {
       const std::string k = std::to_string(l);
       const float* bh = P("bias_hh_l" + k);
-      const int sh = product_f32(hf_[2 * l + cur], hb_[2 * l + cur], "weight_hh_l" + k, bh, Bp, 3 * H, gh_, s);
+      const int sh = product_f32(hf_[2 * l + cur], hb_[2 * l + cur], P("weight_hh_l" + k), Whh_[l], bh, Bp, 3 * H, gh_, s);
       GruGatesF32Args a;
       if (l == 0) {
         a.P = Ptab_; a.ids = ids_;
       } else {
         const float* bi = P("bias_ih_l" + k);
-        const int si = product_f32(hf_[2 * (l - 1) + nxt], hb_[2 * (l - 1) + nxt], "weight_ih_l" + k, bi, Bp, 3 * H,
-                                   gi_, s);
+        const int si = product_f32(hf_[2 * (l - 1) + nxt], hb_[2 * (l - 1) + nxt], P("weight_ih_l" + k), Wih_[l], bi,
+                                   Bp, 3 * H, gi_, s);
         a.Gi = gi_; a.gi_splits = si; a.gi_slab = (long)Bp * 3 * H;
         if (x3 && si > 1) a.bgi = bi;
       }
@@ -237,7 +235,7 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
       gru_gates_f32(a, s);
     }
     const float* bf = P("fc.bias");
-    const int sf = product_f32(hf_[2 * (L - 1) + nxt], hb_[2 * (L - 1) + nxt], "fc.weight", bf, Bp, V, logits_, s);
+    const int sf = product_f32(hf_[2 * (L - 1) + nxt], hb_[2 * (L - 1) + nxt], P("fc.weight"), Wfc_, bf, Bp, V, logits_, s);
     SampleF32Args q;
     q.logits = logits_; q.splits = sf; q.slab = (long)Bp * V; q.rf = rf_; q.ids = ids_; q.out = out_; q.alive = alive_;
     if (x3 && sf > 1) q.bias = bf;
@@ -262,7 +260,7 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
         if (l > 0) { a.Wih[l] = P("weight_ih_l" + k); a.bih[l] = P("bias_ih_l" + k); }
       }
       a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab_; a.rf = rf_; a.out = out_; a.probs = probe_;
-      a.ws = pws_; a.sync = psync_; a.err = err_;
+      a.ws = pws_; a.sync = psync_; a.err = err_; a.dbg = persist_dbg_;
       a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
       gen_persist_f32(a, s);
     } else if (use_graph_) {

@@ -35,20 +35,22 @@ class Generator {
   void set_use_graph(bool g) { use_graph_ = g; }
   // optional: device [Bp][V] softmax of the last generated step (tests)
   void set_probe(float* probs) { probe_ = probs; graphs_.clear(); }
-  // fp32 mode, small batches (<= GK_GEN_PERSIST_MAX names, default 32, at most 64): one persistent
+  // fp32 modes, small batches (<= GK_GEN_PERSIST_MAX names, default and at most 64): one persistent
   // launch per batch (gen_persist.hip) instead of the per-char graph.  On by default;
   // GK_GEN_PERSIST=0 or set_persist(false) turns it off.
   void set_persist(bool on) { persist_ = on; }
   void set_persist_max(int n) { persist_max_ = n; }
+  void set_persist_dbg(unsigned long long* p) { persist_dbg_ = p; }   // diagnostic stamps (nullable)
   bool uses_persist(int n) const;
   unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
 
  private:
   void record_steps(int n_active, hipStream_t s);
   void record_steps_f32(int n_active, hipStream_t s);
-  // one product of the fp32 / bf16x3 path: C = h W^T (+ bias) -> splits (slabs of M x N at C)
-  int product_f32(const float* A32, const u16* A3, const std::string& w, const float* bias, int M, int N, float* C,
-                  hipStream_t s);
+  // one product of the fp32 / bf16x3 path: C = h W^T (+ bias) -> splits (slabs of M x N at C).  fp32
+  // reads A32 / W32; bf16x3 the split copies A3 ([hi|hi|lo] rows) / W3 ([hi|lo|hi] rows)
+  int product_f32(const float* A32, const u16* A3, const float* W32, const u16* W3, const float* bias, int M, int N,
+                  float* C, hipStream_t s);
   bool split3() const { return d_.fp32 == 2; }
   void reset_batch(int Bp, bool bf16, hipStream_t s);
   const float* P(const std::string& n) const { return params_ + off_.at(n); }
@@ -74,7 +76,8 @@ class Generator {
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
   bool persist_ = true;
-  int persist_max_ = 32;        // names per batch up to which the persistent launch is used
+  int persist_max_ = 64;        // names per batch up to which the persistent launch is used
+  unsigned long long* persist_dbg_ = nullptr;
   float* pws_ = nullptr;        // persistent path: exchange buffers
   unsigned* psync_ = nullptr;   // persistent path: flags + done counter (self-cleaning, arena-zeroed)
   static constexpr int kF32SlabRows = 2048;   // fp32 split-K slab capacity (rows x 3H)

@@ -21,15 +21,16 @@
 //       - Each layer l >= 1: gi_l = h_{l-1}(t) W_ih_l^T + b_ih_l, then the gates.
 //       - FC: logits = h_{L-1}(t) W_fc^T + b_fc.
 //     The recurrent products gh_l = h_l(t) W_hh_l^T + b_hh_l are only needed by the next char.
-//     They ride on the loads of the product that consumes h_l(t) anyway (gi_{l+1}, or the
-//     logits), so every exchanged state is read once per char. Those reads, 256 workgroups x
-//     names x H floats each, are what a char costs.
+//     They reuse the x registers of the product that consumes h_l(t) anyway (gi_{l+1}, or the
+//     logits), after that product's publish, so every exchanged state is read once per char and
+//     the gh MFMAs overlap the next hand-off.  Padded names are neither loaded nor sampled.
 //     That is L + 1 hand-offs per char, each an all-to-all of tiny slices (U or VR floats per
 //     name per producer). A producer's wave 0 publishes them with write-through (sc1) stores,
 //     drains them (vmcnt(0)) and stores its epoch flag. A consumer wave polls only the 32
 //     producers of its K-slice (all 256 for the logits), then reads with sc1 loads: the hand-off
-//     protocol of the persistent training kernels (gru_seq.hip). States and logits are
-//     double-buffered by char parity; a producer can be at most one char ahead of any consumer.
+//     protocol of the persistent training kernels (gru_seq.hip). Every char has its own state and
+//     logits slots, so consumers read with plain loads that the 32 workgroups of an XCD share
+//     through its L2.
 //     Data-tagged 8-byte granules (no flag) measured slower here: every waiting lane re-reads its
 //     whole set of granules, 44.6 against 28 us per char at 8 names
 //     (profiles/r2_generate_persistent.jsonl).
@@ -51,7 +52,8 @@ namespace {
 constexpr int kG = 256;        // workgroups
 constexpr int kNmax = 64;      // names per launch
 constexpr int kFS = 16;        // flag stride in uints (own 64-B line)
-constexpr int kVmax = 1024;
+constexpr int kVmax = 512;     // V = 256 or 512 (the sampler's instances); LDS: sP is V x 3U floats
+constexpr int kLgLds = 64 * 256;   // logits staged through LDS up to names x V = 16 K floats
 constexpr unsigned kSpin = 1u << 21;   // x s_sleep(1) polls: ~0.3 s
 constexpr unsigned kErrBit = 32u;
 }
@@ -88,35 +90,32 @@ DEV void st_sc1(prsrc_t r, unsigned off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 16);   // aux 16 = sc1
 }
 
-// one wave's partials of two 16 x 16 (rows x names) tiles over its K-slice: x = this lane's KJ
-// floats of its name (sc1 b128 loads at byte offset off; a padded name, !valid, is not read), A
-// values aval(j) -> pa, and Wb -> pb when do_b.  Two accumulator chains per tile.
-template <int KJ, class AVal>
-DEV void load_mm2(AVal&& aval, const float (&Wb)[KJ], bool do_b, prsrc_t r, unsigned off, bool valid, f32x4& pa,
-                  f32x4& pb) {
-  float x[KJ];
+// this lane's KJ floats of its name from the exchange buffer (b128 loads at byte offset off; a
+// padded name, !valid, is not read).  PLAIN loads, cacheable in the XCD's L2, so the 32 workgroups
+// of an XCD share one fetch of each line from the last-level cache: every char has its own slots,
+// so no line is read before its producer's write-through store and flag (none can be stale in this
+// launch; the kernel boundary invalidates the caches between launches).
+template <int KJ>
+DEV void load_x(prsrc_t r, unsigned off, bool valid, float (&x)[KJ]) {
 #pragma unroll
   for (int j = 0; j < KJ; j += 4) {
     pu32x4 v = {0u, 0u, 0u, 0u};
-    if (valid) v = __builtin_amdgcn_raw_buffer_load_b128(r, off + j * 4, 0, 16);
+    if (valid) v = __builtin_amdgcn_raw_buffer_load_b128(r, off + j * 4, 0, 0);
     x[j] = __uint_as_float(v.x); x[j + 1] = __uint_as_float(v.y);
     x[j + 2] = __uint_as_float(v.z); x[j + 3] = __uint_as_float(v.w);
   }
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+}
+// one wave's partial of a 16 x 16 (rows x names) tile over its K-slice: A values aval(j), B = x;
+// two accumulator chains
+template <int KJ, class AVal>
+DEV f32x4 tile_mm(AVal&& aval, const float (&x)[KJ]) {
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
 #pragma unroll
   for (int j = 0; j < KJ; j += 2) {
     a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(aval(j), x[j], a0, 0, 0, 0);
     a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aval(j + 1), x[j + 1], a1, 0, 0, 0);
   }
-  if (do_b) {
-#pragma unroll
-    for (int j = 0; j < KJ; j += 2) {
-      b0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wb[j], x[j], b0, 0, 0, 0);
-      b1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Wb[j + 1], x[j + 1], b1, 0, 0, 0);
-    }
-  }
-  pa = a0 + a1;
-  pb = b0 + b1;
+  return a0 + a1;
 }
 
 DEV float sig_ieee(float x) { return 1.f / (1.f + expf(-x)); }
@@ -142,12 +141,14 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   __shared__ __attribute__((aligned(16))) float sWf[kVmax / kG][H];   // this workgroup's FC rows
   __shared__ int sid[kNmax], sal[kNmax];
   __shared__ int s_last, s_live;
+  __shared__ __attribute__((aligned(16))) float sLG[kLgLds];   // staged logits of the last char
+  __shared__ float sRf[kNmax];
 
-  // exchange buffers: X_l[par][name][H], then LG[par][name][V]
-  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * 2 * kNmax * H + 2 * kNmax * V) * 4));
-  const unsigned lg0 = (unsigned)((size_t)L * 2 * kNmax * H * 4);
-  auto xoff = [&](int l, int par, int n, int col) -> unsigned {
-    return (unsigned)((((size_t)(l * 2 + par) * kNmax + n) * H + col) * 4);
+  // one slot per char (no reuse inside a launch: see load_x), X_l[t][name][H] then LG[t][name][V]
+  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * ML * kNmax * H + (size_t)ML * kNmax * V) * 4));
+  const unsigned lg0 = (unsigned)((size_t)L * ML * kNmax * H * 4);
+  auto xoff = [&](int l, int t, int n, int col) -> unsigned {
+    return (unsigned)((((size_t)(l * ML + t) * kNmax + n) * H + col) * 4);
   };
   unsigned* flags = a.sync;
   unsigned* done = a.sync + (size_t)(L + 1) * kG * kFS;
@@ -227,15 +228,23 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
         if constexpr (U == 4) {
           const pu32x4 v = {__float_as_uint(sh[l][lane][0]), __float_as_uint(sh[l][lane][1]),
                             __float_as_uint(sh[l][lane][2]), __float_as_uint(sh[l][lane][3])};
-          __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoff(l, t & 1, lane, b * U), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoff(l, t, lane, b * U), 0, 16);
         } else {
-          for (int u = 0; u < U; ++u) st_sc1(xr, xoff(l, t & 1, lane, b * U + u), sh[l][lane][u]);
+          for (int u = 0; u < U; ++u) st_sc1(xr, xoff(l, t, lane, b * U + u), sh[l][lane][u]);
         }
       }
       publish_flag(l, t);
     }
   };
 
+  // diagnostic phase stamps (100 MHz wall clock), first and last workgroup, thread 0 only:
+  // 0 char start, 1 logits seen, 2 sampled, 3 layer 0 published, 4 + 2(l-1) layer l input seen,
+  // 5 + 2(l-1) layer l published, 6 + 2(L-2) logits input seen, 7 + 2(L-2) logits published;
+  // sampling internals: 8 logits staged, 9 wave 0's first name sampled, 10 wave 0's names done
+  auto stampk = [&](int t, int k) {
+    if (!a.dbg || tid != 0 || (b != 0 && b != kG - 1) || k > 15) return;
+    a.dbg[((size_t)(b == 0 ? 0 : 1) * (ML + 1) + t) * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
   // gh_l = h_l W_hh_l^T + b_hh_l is only needed by the next char's gates: it is computed beside the
   // product that consumes h_l(t) anyway (gi_{l+1}, or the logits for the top layer), so each
   // exchanged state is read once per char.  At t = 0 (h = 0) it is the bias.
@@ -246,45 +255,79 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   __syncthreads();
   // x = h_src(t) (this wave's K-slice, name tile nt) times W tile TA (-> dst rows < nrows, + bias)
   // and, unless this is the last char, times W_hh_src (-> sgh[src] for the next char)
-  auto product = [&](auto ta_tag, auto src_tag, int t, float (*dst)[kNmax], const float* bias, int nrows) {
+  float xk[KJ];   // this wave's x of the last name tile, kept for the gh pass after the publish
+  auto product = [&](auto ta_tag, auto src_tag, int t, float (*dst)[kNmax], const float* bias, int nrows, int sk) {
     constexpr int TA = decltype(ta_tag)::value, SRC = decltype(src_tag)::value;   // TA = NT: the FC rows
-    const bool gh = t + 1 < ML;
     const int kw0 = w * KW + q4 * KJ;
+    auto aval = [&](int j) -> float {
+      if constexpr (TA == NT) return fr < VR ? sWf[fr < VR ? fr : 0][kw0 + j] : 0.f;
+      else return Wr[TA][j];
+    };
     for (int nt = 0; nt < nnt; ++nt) {
-      f32x4 pa, pb;
-      auto aval = [&](int j) -> float {
-        if constexpr (TA == NT) return fr < VR ? sWf[fr < VR ? fr : 0][kw0 + j] : 0.f;
-        else return Wr[TA][j];
-      };
-      if (nt == 0) pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
-      load_mm2<KJ>(aval, Wr[SRC], gh, xr, xoff(SRC, t & 1, nt * 16 + fr, kw0), nt * 16 + fr < N, pa, pb);
-      stash(0, pa);
-      if (gh) stash(1, pb);
+      if (nt == 0) {
+        pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
+        stampk(t, sk);
+      }
+      load_x<KJ>(xr, xoff(SRC, t, nt * 16 + fr, kw0), nt * 16 + fr < N, xk);
+      stash(0, tile_mm<KJ>(aval, xk));
+      // several name tiles: gh here from the same x (re-reading it after the publish cost more)
+      const bool gh = nnt > 1 && t + 1 < ML;
+      if (gh) stash(1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
       __syncthreads();
       reduce_to(dst, 0, nt, bias, nrows);
       if (gh) reduce_to(sgh[SRC], 1, nt, sbh[SRC], R3);
       __syncthreads();
     }
   };
+  // gh_src of the next char from the same h_src(t), after this phase's publish: with one name tile
+  // its MFMAs run while the next hand-off is in flight instead of before the publish (x still in
+  // xk): 22 -> 15.6 us per char at 1 name together with the sampler changes
+  auto product_gh = [&](auto src_tag, int t) {
+    constexpr int SRC = decltype(src_tag)::value;
+    if (t + 1 >= ML || nnt > 1) return;   // (several name tiles: done inside product)
+    stash(1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
+    __syncthreads();
+    reduce_to(sgh[SRC], 1, 0, sbh[SRC], R3);
+    __syncthreads();
+  };
 
   for (int t = 0; t <= ML; ++t) {
     if (t == ML && b != 0) break;   // only workgroup 0 samples the last char
+    stampk(t, 0);
     // ---- sample char t-1 from the logits of every workgroup
     if (t > 0) {
       if (w == 0) pwait(flags, L, 0, kG, (unsigned)t, a.err);
       __syncthreads();
+      stampk(t, 1);
       const int per = V / 64;
-      for (int n = w; n < Np; n += 8) {
-        float xv[16];
-        const unsigned base = lg0 + (unsigned)((((t - 1) & 1) * kNmax + n) * V + lane * per) * 4;
+      const unsigned lgt = lg0 + (unsigned)((size_t)(t - 1) * kNmax * V * 4);
+      const bool staged = N * V <= kLgLds;
+      if (tid < N) sRf[tid] = a.rf[(size_t)tid * ML + (t - 1)];   // this char's uniforms, loaded together
+      if (staged) {   // every name's logits into LDS with all loads in flight: one memory round trip
+        for (int i = tid; i < N * V / 4; i += 512) {
+          const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
+          sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
+          sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
+        }
+      }
+      __syncthreads();
+      stampk(t, 8);
+      for (int n = w; n < N; n += 8) {   // real names only: a padded row keeps sid = sos
+        const float rnd = sRf[n];
+        const unsigned base = lgt + (unsigned)(n * V + lane * per) * 4;
+        float* prow = (b == 0 && a.probs && t == ML) ? a.probs + (size_t)n * V : nullptr;
+        // the sampler instantiated for exactly V / 64 values per lane: a 16-wide instance runs
+        // all 16 IEEE expf / divides as selects (2.9 us per name and wave, probe_gen_persist.py)
+        auto sample = [&](auto per_tag) {
+          constexpr int PER = decltype(per_tag)::value;
+          float xv[PER];
 #pragma unroll
-        for (int e = 0; e < 16; ++e)
-          xv[e] = e >= per ? -INFINITY
-                  : n < N ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, base + 4 * e, 0, 16))
-                          : 0.f;   // (a padded name: a uniform draw nobody reads)
-        const float rnd = n < N ? a.rf[(size_t)n * ML + (t - 1)] : 0.5f;
-        float* prow = (b == 0 && a.probs && t == ML && n < N) ? a.probs + (size_t)n * V : nullptr;
-        const int sel = softmax_sample_wave(xv, per, V, rnd, prow);
+          for (int e = 0; e < PER; ++e)
+            xv[e] = staged ? sLG[n * V + lane * PER + e]
+                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, base + 4 * e, 0, 0));
+          return softmax_sample_wave(xv, PER, V, rnd, prow);
+        };
+        const int sel = per == 4 ? sample(ic<4>{}) : sample(ic<8>{});
         if (lane == 0) {
           if (sal[n]) {
             if (b == 0) a.out[(size_t)n * (ML + 1) + (t - 1)] = (unsigned char)sel;
@@ -292,7 +335,9 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
           }
           sid[n] = sel;
         }
+        if (n == w) stampk(t, 9);
       }
+      stampk(t, 10);
       __syncthreads();
       if (t == ML) break;
       if (!a.probs) {   // every name ended: all workgroups see the same ids and stop together
@@ -305,22 +350,28 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
         if (!s_live) break;
       }
     }
+    stampk(t, 2);
     // ---- layer 0: gi = P[id]
     gates_publish(0, t);
+    stampk(t, 3);
     // ---- layers >= 1: gi_l = h_{l-1}(t) W_ih_l^T + b_ih_l  (+ gh_{l-1} of the next char)
     static_for<1, L>([&](auto lt) {
       constexpr int l = decltype(lt)::value;
-      product(ic<L + l - 1>{}, ic<l - 1>{}, t, sgi, sbi[l], R3);
+      product(ic<L + l - 1>{}, ic<l - 1>{}, t, sgi, sbi[l], R3, 4 + 2 * (l - 1));
       gates_publish(l, t);
+      stampk(t, 5 + 2 * (l - 1));
+      product_gh(ic<l - 1>{}, t);
     });
     // ---- FC: logits rows b VR .. b VR + VR  (+ gh_{L-1} of the next char)
-    product(ic<NT>{}, ic<L - 1>{}, t, sgi, sbf, VR);
+    product(ic<NT>{}, ic<L - 1>{}, t, sgi, sbf, VR, 6 + 2 * (L - 2));
     if (w == 0) {
       if (lane < Np)
         for (int r = 0; r < VR; ++r)
-          st_sc1(xr, lg0 + (unsigned)(((t & 1) * kNmax + lane) * V + b * VR + r) * 4, sgi[r][lane]);
+          st_sc1(xr, lg0 + (unsigned)(((size_t)t * kNmax + lane) * V + b * VR + r) * 4, sgi[r][lane]);
       publish_flag(L, t);
     }
+    stampk(t, 7 + 2 * (L - 2));
+    product_gh(ic<L - 1>{}, t);
   }
 
   // ---- the last workgroup out zeroes the flags for the next launch (nobody polls them any more)
@@ -348,14 +399,14 @@ static int gp_resident(int KJ, int L) {
 }
 
 bool gen_persist_supported(int H, int L, int V, int N, int ML) {
-  if (N < 1 || N > kNmax || L < 1 || L > 4 || H % 256 || V % kG || V > kVmax || ML < 1) return false;
+  if (N < 1 || N > kNmax || L < 1 || L > 4 || H % 256 || (V != 256 && V != 512) || ML < 1) return false;
   const int KJ = H / 32;
   if (KJ != 8 && KJ != 16 && KJ != 32) return false;
   if (2 * L * KJ > 128) return false;   // resident weight registers per lane
   return gp_resident(KJ, L) >= kG;
 }
 
-long gen_persist_ws_floats(int H, int L, int V) { return (long)L * 2 * kNmax * H + 2L * kNmax * V; }
+long gen_persist_ws_floats(int H, int L, int V, int ML) { return ((long)L * kNmax * H + (long)kNmax * V) * ML; }
 long gen_persist_sync_words(int L) { return (long)(L + 1) * kG * kFS + 16; }
 
 void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {

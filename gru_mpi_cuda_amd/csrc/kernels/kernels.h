@@ -241,10 +241,11 @@ struct GenPersistArgs {
   float* ws = nullptr;             // gen_persist_ws_floats(): exchange buffers
   unsigned* sync = nullptr;        // gen_persist_sync_words(): epoch flags + arrival count (zeroed once, self-cleaning)
   unsigned* err = nullptr;         // bit 32: a cross-workgroup wait hit its spin limit
+  unsigned long long* dbg = nullptr;   // diagnostic (nullable): [2 wgs][ML + 1][16] s_memrealtime stamps
   int N = 0, H = 0, L = 0, V = 0, ML = 0, sos = 0, eos = 0;
 };
 bool gen_persist_supported(int H, int L, int V, int N, int ML);
-long gen_persist_ws_floats(int H, int L, int V);
+long gen_persist_ws_floats(int H, int L, int V, int ML);
 long gen_persist_sync_words(int L);
 void gen_persist_f32(const GenPersistArgs& a, hipStream_t s);
 

@@ -183,7 +183,6 @@ def test_generator_persistent_fp32(L, E, H, N):
     params = init_params(cfg)
     rf = random_floats(N, cfg.max_len, seed=9)
     gen = HipGenerator(cfg, params, precision="fp32")
-    gen.g.set_persist_max(64)   # (default 32: the per-char graph is faster at 64 names)
     assert gen.g.uses_persist(N)
     got = gen.generate(rf)
     again = gen.generate(rf)
@@ -217,11 +216,12 @@ def test_generator_bf16x3_big_batch_matches_fp32():
     assert same >= 0.995, same
 
 
-@pytest.mark.parametrize("precision,atol,rtol", [("fp32", 2e-7, 1e-5), ("bf16x3", 2e-5, 1e-3)])
-def test_generator_fp32_probs_match_fp64(precision, atol, rtol):
+@pytest.mark.parametrize("precision,persist,atol,rtol", [("fp32", False, 2e-7, 1e-5), ("bf16x3", False, 2e-5, 1e-3),
+                                                         ("fp32", True, 2e-7, 1e-5)])
+def test_generator_fp32_probs_match_fp64(precision, persist, atol, rtol):
     """Per-step distribution of the fp32 paths: softmax of the last step vs fp64 on the same prefix
-    (teacher-forced through the sampled chars, which agree here).  64 names: the per-char graph
-    (the persistent launch takes <= 32)."""
+    (teacher-forced through the sampled chars, which agree here): the per-char graph in both fp32
+    modes and the persistent small-batch launch."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
     cfg = GRUConfig(vocab=256, embed=128, hidden=256, layers=2, max_len=4, sos=0, eos=255, seed=6)
@@ -229,6 +229,8 @@ def test_generator_fp32_probs_match_fp64(precision, atol, rtol):
     N = 64
     rf = random_floats(N, cfg.max_len, seed=3)
     gen = HipGenerator(cfg, params, precision=precision)
+    gen.g.set_persist(persist)
+    assert gen.g.uses_persist(N) == persist
     probs = torch.zeros(64, cfg.vocab, device="cuda")
     gen.g.set_probe(probs.data_ptr())
     got = gen.generate(rf)
