@@ -234,15 +234,17 @@ void gru_gates_f32(const GruGatesF32Args& a, hipStream_t s) {
   hipLaunchKernelGGL(gru_gates_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
 }
 
-// One wave per row: lane owns V/64 consecutive logits (softmax + CDF search: gen_sample.h).
+// One wave per row: lane owns V/64 consecutive logits (softmax + CDF search: gen_sample.h),
+// instantiated for the exact count when V = 256 (a wider instance computes every slot)
+template <int MAXPER>
 __global__ void __launch_bounds__(64) sample_f32_kernel(SampleF32Args a) {
   const int b = blockIdx.x, lane = threadIdx.x, per = a.V / 64;
   if (b >= a.N) return;
   const float* x = a.logits + (size_t)b * a.V + lane * per;
   // (fixed-bound loops guarded by `per`: the arrays stay in registers)
-  float xv[8];
+  float xv[MAXPER];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
+  for (int e = 0; e < MAXPER; ++e) {
     if (e < per) {
       float v = x[e];
       for (int s2 = 1; s2 < a.splits; ++s2) v += x[s2 * a.slab + e];   // split-K slabs, fixed order
@@ -287,7 +289,9 @@ void gen_reset(const GenResetArgs& a, hipStream_t s) {
 
 void sample_f32(const SampleF32Args& a, hipStream_t s) {
   if (a.V % 64 || a.V > 512) throw std::runtime_error("sample_f32: needs V % 64 == 0 and V <= 512");
-  if (a.N > 0) hipLaunchKernelGGL(sample_f32_kernel, dim3(a.N), dim3(64), 0, s, a);
+  if (a.N <= 0) return;
+  if (a.V == 256) hipLaunchKernelGGL(sample_f32_kernel<4>, dim3(a.N), dim3(64), 0, s, a);
+  else hipLaunchKernelGGL(sample_f32_kernel<8>, dim3(a.N), dim3(64), 0, s, a);
 }
 
 }  // namespace gk
