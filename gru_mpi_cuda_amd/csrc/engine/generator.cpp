@@ -31,9 +31,12 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   size_t oids = arena_.reserve((size_t)B * 4), oal = arena_.reserve((size_t)B * 4);
   size_t oout = arena_.reserve((size_t)B * (d_.max_len + 1));
   size_t ogh = 0, ogi = 0, olg = 0, oerr = arena_.reserve(256), opws = 0, opsync = 0;
+  // persistent small-batch path (every mode): exchange buffers, flags, and in bf16 mode an fp32
+  // layer-0 table of its own (Ptab_ holds the bf16-product one there)
+  opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V, d_.max_len) * 4);
+  opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);
+  const size_t oP32 = d_.fp32 ? 0 : arena_.reserve((size_t)V * 3 * H * 4);
   if (d_.fp32) {
-    opws = arena_.reserve((size_t)gen_persist_ws_floats(H, L, V, d_.max_len) * 4);   // persistent small-batch path
-    opsync = arena_.reserve((size_t)gen_persist_sync_words(L) * 4);
     // room for split-K slabs of small batches (f32_splits / split3_splits): kF32SlabRows rows
     const size_t rows = std::max<size_t>(B, kF32SlabRows);
     ogh = arena_.reserve(rows * 3 * H * 4);
@@ -42,14 +45,13 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   }
   arena_.commit();
   err_ = arena_.get<unsigned>(oerr);
-  if (d_.fp32) {
-    gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg);
-    pws_ = arena_.get<float>(opws); psync_ = arena_.get<unsigned>(opsync);
-  }
+  pws_ = arena_.get<float>(opws); psync_ = arena_.get<unsigned>(opsync);
+  if (d_.fp32) { gh_ = arena_.get<float>(ogh); gi_ = arena_.get<float>(ogi); logits_ = arena_.get<float>(olg); }
   for (int i = 0; i < 2 * L; ++i) { hf_.push_back(arena_.get<float>(ohf[i])); hb_.push_back(arena_.get<u16>(ohb[i])); }
   for (int l = 0; l < L; ++l) { Whh_.push_back(arena_.get<u16>(oWhh[l])); Wih_.push_back(arena_.get<u16>(oWih[l])); }
   Emb_ = arena_.get<u16>(oEmb); Wfc_ = arena_.get<u16>(oWfc); WfcF_ = arena_.get<u16>(oWfcF);
   Ptab_ = arena_.get<float>(oP);
+  Ptab32_ = d_.fp32 ? Ptab_ : arena_.get<float>(oP32);
   rf_ = arena_.get<float>(orf); ids_ = arena_.get<int>(oids); alive_ = arena_.get<int>(oal);
   out_ = arena_.get<unsigned char>(oout);
   HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
@@ -62,7 +64,11 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
 }
 
 bool Generator::uses_persist(int n) const {
-  return d_.fp32 && persist_ && n <= persist_max_ && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
+  // bf16 mode: only where the persistent fp32 launch is faster than the bf16 per-char graph (up to
+  // ~24 names: 21.4 vs 31.7 us per char at 16, 29.4 vs 32.2 at 17 on the reference model,
+  // profiles/r2_generate_persistent.jsonl)
+  const int cap = d_.fp32 ? persist_max_ : std::min(persist_max_, persist_max_bf16_);
+  return persist_ && n <= cap && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
 }
 
 Generator::~Generator() {
@@ -97,6 +103,12 @@ void Generator::refresh_weights(hipStream_t s) {
   }
   j.add(P("fc.weight"), V, H, Wfc_, nullptr, (V % 64 || H % 64) ? nullptr : WfcF_);
   cast_multi(j, s);
+  {   // fp32 table for the persistent small-batch launch (exact fp32 there)
+    GemmF32Args g;
+    g.A = P("embedding"); g.lda = E; g.B = P("weight_ih_l0"); g.ldb = E; g.C = Ptab32_; g.ldc = 3 * H;
+    g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;
+    gemm_f32_nt(g, s);
+  }
   GemmArgs g;   // layer-0 input projection table P = Emb · W_ih0^T + b_ih0  ([V][3H])
   g.A = Emb_; g.lda = E; g.B = Wih_[0]; g.ldb = E; g.C = Ptab_; g.ldc = 3 * H;
   g.bias = P("bias_ih_l0"); g.M = V; g.N = 3 * H; g.K = E;
@@ -259,7 +271,7 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
         a.Whh[l] = P("weight_hh_l" + k); a.bhh[l] = P("bias_hh_l" + k);
         if (l > 0) { a.Wih[l] = P("weight_ih_l" + k); a.bih[l] = P("bias_ih_l" + k); }
       }
-      a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab_; a.rf = rf_; a.out = out_; a.probs = probe_;
+      a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab32_; a.rf = rf_; a.out = out_; a.probs = probe_;
       a.ws = pws_; a.sync = psync_; a.err = err_; a.dbg = persist_dbg_;
       a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
       gen_persist_f32(a, s);

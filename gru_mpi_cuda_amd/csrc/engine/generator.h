@@ -35,9 +35,9 @@ class Generator {
   void set_use_graph(bool g) { use_graph_ = g; }
   // optional: device [Bp][V] softmax of the last generated step (tests)
   void set_probe(float* probs) { probe_ = probs; graphs_.clear(); }
-  // fp32 modes, small batches (<= GK_GEN_PERSIST_MAX names, default and at most 64): one persistent
-  // launch per batch (gen_persist.hip) instead of the per-char graph.  On by default;
-  // GK_GEN_PERSIST=0 or set_persist(false) turns it off.
+  // Small batches (fp32 modes: <= GK_GEN_PERSIST_MAX names, default and at most 64; bf16 mode: <= 24):
+  // one persistent launch per batch (gen_persist.hip, exact fp32) instead of the per-char graph.
+  // On by default; GK_GEN_PERSIST=0 or set_persist(false) turns it off.
   void set_persist(bool on) { persist_ = on; }
   void set_persist_max(int n) { persist_max_ = n; }
   void set_persist_dbg(unsigned long long* p) { persist_dbg_ = p; }   // diagnostic stamps (nullable)
@@ -71,12 +71,14 @@ class Generator {
   u16 *Emb_, *Wfc_, *WfcF_;
   int step_algo_ = 0;
   float *Ptab_, *rf_;
+  float* Ptab32_ = nullptr;     // fp32 layer-0 table of the persistent launch (= Ptab_ in the fp32 modes)
   int *ids_, *alive_;
   unsigned char* out_;
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
   bool persist_ = true;
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
+  int persist_max_bf16_ = 24;   // ... in the bf16 mode (it runs exact fp32, faster up to ~24 names)
   unsigned long long* persist_dbg_ = nullptr;
   float* pws_ = nullptr;        // persistent path: exchange buffers
   unsigned* psync_ = nullptr;   // persistent path: flags + done counter (self-cleaning, arena-zeroed)

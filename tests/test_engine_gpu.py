@@ -200,6 +200,21 @@ def test_generator_persistent_fp32(L, E, H, N):
         assert same_b >= 0.95 and same_r >= 0.95, (same_b, same_r)
 
 
+def test_generator_bf16_mode_small_batch_runs_persistent_fp32():
+    """bf16 mode up to 24 names takes the persistent launch, which is exact fp32 and faster there:
+    same names as the fp32 mode; above it stays on the bf16 per-char graph."""
+    from gru_mpi_cuda_amd.engine.generator import HipGenerator
+    from gru_mpi_cuda_amd.utils.data import random_floats
+    cfg = GRUConfig(vocab=256, embed=512, hidden=1024, layers=2, max_len=10, sos=0, eos=0, seed=4)
+    params = init_params(cfg)
+    fast = HipGenerator(cfg, params, precision="bf16")
+    exact = HipGenerator(cfg, params, precision="fp32")
+    assert fast.g.uses_persist(24) and not fast.g.uses_persist(25)
+    rf = random_floats(16, cfg.max_len, seed=9)
+    assert (fast.generate(rf) == exact.generate(rf)).all()
+    assert fast.g.read_error() == 0
+
+
 def test_generator_bf16x3_big_batch_matches_fp32():
     """bf16x3 at the reference shape and 4096 names, where its products run on the 256 x 256 MFMA
     kernel (192 tiles): same names as the fp32 path (fp64 oracle too slow on the CPU at this size)."""
