@@ -102,7 +102,8 @@ _S: Optional[_State] = None
 def namegen_initialize(N: int, rng_seed: int, parameter_fname: str, cfg: Optional[GRUConfig] = None,
                        fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "fp32") -> None:
     """namegensf.cu:359-618.  ``rng_seed`` is accepted and unused, as in the reference.
-    ``precision``: "fp32" (faithful, default) or "bf16" (fast mode) on the GPU path."""
+    ``precision``: "fp32" (faithful, default), "bf16" (fast mode) or "bf16x3" (split-bf16 products)
+    on the GPU path; the CPU path is the fp32 oracle."""
     global _S
     from ..parallel import dist as gdist
     from ..utils import ckpt
