@@ -220,6 +220,30 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
   m.def("bwd_step_sk_splits", &gru_bwd_step_sk_splits);
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
+  m.def("fwd_seq2", [](py::dict lo, py::dict hi, uintptr_t Wih, uintptr_t bih, uintptr_t s) {
+    auto parse = [](py::dict d) {
+      SeqFwdArgs a;
+      a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+      a.HF = GP(u16, d, "HF"); a.xch = GP(u16, d, "xch");
+      a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
+      a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
+      a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
+      a.h0 = GP(const float, d, "h0");
+      a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
+      a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+      a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+      if (!a.xch || !a.cnt || !a.HSb || !a.HSf || !a.Whh || !a.bhh) throw std::runtime_error("fwd_seq2: HSb/HSf/xch/cnt/Whh/bhh required");
+      return a;
+    };
+    SeqFwd2Args a;
+    a.lo = parse(lo); a.hi = parse(hi);
+    a.Wih = reinterpret_cast<const u16*>(Wih); a.bih = reinterpret_cast<const float*>(bih);
+    if (!a.lo.ids == !a.lo.Gi) throw std::runtime_error("fwd_seq2: lo needs exactly one of P+ids / Gi");
+    if (!gru_fwd_seq2_supported(a.lo.H, a.lo.Bp)) throw std::runtime_error("fwd_seq2: shape not supported");
+    gru_fwd_seq2(a, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fwd_seq2_supported", &gru_fwd_seq2_supported);
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
     SeqFwdArgs a;
     a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);

@@ -61,6 +61,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const char* pe = std::getenv("GK_PERSIST");
   const bool allow = !(pe && pe[0] == '0');
   persist_fwd_ = allow && gru_fwd_seq_supported(H, B);
+  {
+    const char* fw = std::getenv("GK_FWD_WAVE");
+    fwd_wave_ = persist_fwd_ && L >= 2 && !(fw && fw[0] == '0') && gru_fwd_seq2_supported(H, B);
+  }
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);
   if (const char* xl = std::getenv("GK_XCD_LOCAL")) xcd_local_ = std::atoi(xl) != 0;
   if (step_algo_ == 2 && !gru_step_lds_ok(H, B)) step_algo_ = 0;

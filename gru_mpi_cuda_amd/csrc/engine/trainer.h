@@ -159,6 +159,7 @@ class Trainer {
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;
+  bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;
   int splits_ = 8;

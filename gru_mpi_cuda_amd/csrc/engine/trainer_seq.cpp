@@ -142,6 +142,23 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   }
   if (carry_) record_carry(s);
   // ------------------------------------------------------------------ forward
+  auto fwd_args = [&](int l) {
+    Layer& y = Ls_[l];
+    SeqFwdArgs a;
+    a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = seq_[l].HF;
+    a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
+    a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+    a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
+    if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
+    a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
+    if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
+    a.T = T; a.Bp = B; a.H = H;
+    if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
+    // (zeroed by a kernel node, not a memset node: memset nodes misbehaved on graph replay in
+    // the generator, see Generator::reset_batch)
+    if (!seq_[l].bwd) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
+    return a;
+  };
   for (int l = 0; l < L; ++l) {
     Layer& y = Ls_[l];
     if (l > 0) {
@@ -151,21 +168,18 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       g.M = (int)tok; g.N = H3; g.K = H;
       gemm_nt(g, s);
     }
-    if (persist_fwd_) {
-      SeqFwdArgs a;
-      a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = seq_[l].HF;
-      a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
-      a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
-      a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
-      if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
-      a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
-      if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
-      a.T = T; a.Bp = B; a.H = H;
-      if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
-      // (zeroed by a kernel node, not a memset node: memset nodes misbehaved on graph replay in
-      // the generator, see Generator::reset_batch)
-      if (!seq_[l].bwd) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
-      gru_fwd_seq(a, s);
+    if (persist_fwd_ && fwd_wave_ && l + 1 < L) {
+      // layers l and l+1 as one wavefront launch: l+1's input projection runs inside it
+      SeqFwd2Args w2;
+      w2.lo = fwd_args(l);
+      w2.hi = fwd_args(l + 1);
+      w2.hi.Gi = nullptr;
+      w2.hi.xch = xbuf_ + (size_t)T * B * H;   // xbuf_ holds 3 layers' worth of exchange tiles
+      w2.Wih = Ls_[l + 1].Wih; w2.bih = P("bias_ih_l" + std::to_string(l + 1));
+      gru_fwd_seq2(w2, s);
+      ++l;
+    } else if (persist_fwd_) {
+      gru_fwd_seq(fwd_args(l), s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
     }
@@ -410,7 +424,7 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
 }
 
 std::string Trainer::plan() const {
-  std::string p = std::string("fwd=") + (persist_fwd_ ? "persistent" : "per-step");
+  std::string p = std::string("fwd=") + (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

@@ -119,6 +119,48 @@ DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned e
     }
   }
 }
+// Two exchange streams at once (the wavefront forward's h_lo and h_hi): lanes [0, 2NK) poll
+// stream a's producers prod0.., lanes [32, 32 + 2NK) stream b's; k-step kk of a stream is loaded
+// as soon as both of its producers published.  One poll round trip serves both streams.
+template <int NK, class LA, class LB>
+DEV void wave_wait_load2(const unsigned* fa, const unsigned* fb, int prod0, unsigned ea, unsigned eb,
+                         unsigned* err, LA&& loada, LB&& loadb) {
+  static_assert(2 * NK <= 32, "one half-wave of pollers per stream");
+  constexpr unsigned all = (1u << NK) - 1u;
+  const int lane = threadIdx.x & 63;
+  const bool active = (lane & 31) < 2 * NK;
+  const unsigned* f = (lane < 32 ? fa : fb) + (size_t)(prod0 + (lane & 31)) * kFlagStride;
+  const unsigned ep = lane < 32 ? ea : eb;
+  unsigned da = 0, db = 0, spins = 0;
+  for (;;) {
+    bool ok = true;
+    if (active) ok = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ep;
+    const unsigned long long m = __ballot(ok);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      if (!((da >> kk) & 1u) && ((m >> (2 * kk)) & 3ull) == 3ull) {
+        loada(kk);
+        da |= 1u << kk;
+      }
+      if (!((db >> kk) & 1u) && ((m >> (32 + 2 * kk)) & 3ull) == 3ull) {
+        loadb(kk);
+        db |= 1u << kk;
+      }
+    }
+    if (da == all && db == all) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSpinLimit) {
+      if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {   // garbage, flagged: keep the grid draining
+        if (!((da >> kk) & 1u)) loada(kk);
+        if (!((db >> kk) & 1u)) loadb(kk);
+      }
+      break;
+    }
+  }
+}
 DEV void signal_flag(unsigned* flag, unsigned epoch) {
   __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -334,6 +376,281 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     if (a.sr) {
       const size_t so = ((size_t)t * Bp + b) * H + j;
       a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = gh[2];
+    }
+  }
+}
+
+// ==================================================================== two-layer wavefront forward
+// Layer hi at step t depends on layer lo only through h_lo(t) (/root/reference/namegensf.cu:773-854:
+// layer 1's input is layer 0's output for the same char), so one launch runs lo's step s and hi's
+// step s-1 in iteration s = 0..T.  Both operands -- h_lo(s-1) and h_hi(s-2) -- were published by
+// the previous iteration, so one poll loop waits for both (lanes 0-31 poll lo's producers, 32-63
+// hi's).  The h_lo(s-1) K-slice feeds BOTH lo's recurrent product (W_hh,lo) and hi's input product
+// (W_ih,hi): hi needs no Gi GEMM and no Gi buffer.  hi's r/z gates accumulate W_ih x + W_hh h in
+// one MFMA chain; its n gate keeps the two apart (n = tanh(gi_n + r gh_n)).
+//
+// Register/LDS budget (H = 1024, 8 waves, 256 registers each): the three resident weight K-slices
+// (W_hh,lo, W_ih,hi, W_hh,hi over K/8) take 36 * NKW = 144.  The exchange operands are loaded
+// straight into LDS (buffer_load ... lds, 16 B per lane in MFMA fragment order, 16 KB per wave for
+// both streams) and read back per k-step, so they hold no registers across the poll loop.  After
+// its MFMAs a wave writes its 14 K-partial tiles over its own staging area (nothing else reads it
+// by then); the epilogue sums the eight waves' partials.  (A transposed product -- weights as the
+// A operand -- scattered each save store over 16 rows: 1.5 us more per iteration.)  The wave index is read as a scalar so everything derived from it stays in SGPRs.  (Builds that
+// kept the operands in registers spilled 51-110 VGPRs; a 4-wave build fit but ran one wave per
+// SIMD and exposed every LDS and memory latency: 8.9 us per iteration.)
+// Exchange layout, flags, saves and the L2-local hand-off are gru_fwd_seq_kernel's, per layer;
+// lo's tile publishes from wave 0 and hi's from wave 1, so the two drains overlap.
+template <int NKW>   // k-steps per wave: H / 256
+__global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
+  constexpr int NKS = NKW < 4 ? 4 : NKW;   // staging k-steps (>= 4: the area also holds 14 x 256 floats)
+  // [wave][stream lo/hi][k-step][row tile][lane] MFMA B fragments; reused as float partials
+  // [wave][14][256] (lo r,z,n x 2 row tiles | hi r, z (input + recurrent), gi_n, gh_n x 2)
+  __shared__ __attribute__((aligned(16))) bf16x8 stage[8][2][NKS][2][64];
+  __shared__ __attribute__((aligned(16))) u16 stg[2][32][24];
+  __shared__ __attribute__((aligned(16))) u16 stgT[2][16][40];
+  typedef __attribute__((address_space(3))) void lds_void;
+  const SeqFwdArgs& L0 = a.lo;
+  const SeqFwdArgs& L1 = a.hi;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = L0.H, Bp = L0.Bp, T = L0.T;
+  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
+  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const int k0 = w * NKW * 32;
+  const unsigned nunit = (unsigned)(H / 16);
+
+  bf16x8 wh0[NKW][3], wi1[NKW][3], wh1[NKW][3];
+#pragma unroll
+  for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const size_t o = (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk;
+      wh0[kk][g] = ld8(L0.Whh + o);
+      wi1[kk][g] = ld8(a.Wih + o);
+      wh1[kk][g] = ld8(L1.Whh + o);
+    }
+
+  // this thread's epilogue item: row tile q = w / 4, element e = w % 4 of lane `lane`'s accumulator
+  // -> (batch row 16 q + 4 (lane >> 4) + e, unit lane & 15), partial index e * 64 + lane; a wave's
+  // 64 items are 4 rows x 16 consecutive units, so every save store is 4 whole 64-B segments
+  const int q = w >> 2, e = w & 3;
+  const int row = q * 16 + 4 * (lane >> 4) + e, col = lane & 15;
+  const int b = b0 + row, j = j0 + col, pidx = e * 64 + lane;
+  float bh0[3], bh1[3], bi1[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) {
+    bh0[g] = L0.bhh[g * H + j];
+    bh1[g] = L1.bhh[g * H + j];
+    bi1[g] = a.bih[g * H + j];
+  }
+  float hp0 = L0.h0 ? L0.h0[(size_t)b * H + j] : 0.f;
+  float hp1 = L1.h0 ? L1.h0[(size_t)b * H + j] : 0.f;
+  const unsigned hs_bytes = (unsigned)((size_t)(T + 1) * Bp * H * 2), x_bytes = (unsigned)((size_t)T * Bp * H * 2);
+  const rsrc_t rH0 = make_rsrc(L0.HSb, hs_bytes), rX0 = make_rsrc(L0.xch, x_bytes);
+  const rsrc_t rH1 = make_rsrc(L1.HSb, hs_bytes), rX1 = make_rsrc(L1.xch, x_bytes);
+  zero_next_flags(L0.zero_next, L0.zero_words);
+  zero_next_flags(L1.zero_next, L1.zero_words);
+  unsigned* const fl0 = L0.cnt + (size_t)rbk * nunit * kFlagStride;
+  unsigned* const fl1 = L1.cnt + (size_t)rbk * nunit * kFlagStride;
+  const bool loc = L0.allow_local && row_block_local(fl0, ut, (int)nunit, L0.err);
+
+  // k-step kk of stream st (both row tiles) into this wave's staging area, from exchange slot ts
+  // (sc1, after a poll saw the producers) or from the row-major HS[0] (the carried state).  Byte
+  // offsets: one per-lane VGPR for the launch, the rest (slot, k-step, row tile) in the scalar offset.
+  const unsigned xl = (unsigned)((((lk >> 4) * 32 + lr) * 16 + (lk & 15)) * 2);
+  const unsigned hl = (unsigned)((lr * H + lk) * 2);
+  auto stage_x = [&](int st, int kk, int ts) {
+    const rsrc_t rX = st == 0 ? rX0 : rX1;
+    const int so = (int)((((size_t)ts * nrb + rbk) * nunit + (k0 + kk * 32) / 16) * 1024);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(&stage[w][st][kk][r][0]), 16, xl, so + r * 512, 0, 16);
+  };
+  auto stage_h0 = [&](int st) {
+    const rsrc_t rH = st == 0 ? rH0 : rH1;
+#pragma unroll
+    for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rH, (lds_void*)(&stage[w][st][kk][r][0]), 16, hl,
+                                                 (int)((((size_t)b0 + r * 16) * H + k0 + kk * 32) * 2), 0, 16);
+  };
+  float* const mypart = reinterpret_cast<float*>(&stage[w][0][0][0][0]);
+  auto partial = [&](int ww, int set) -> float {
+    return reinterpret_cast<const float*>(&stage[ww][0][0][0][0])[set * 256 + pidx];
+  };
+
+  // lo's input projection for step t, gathered one iteration ahead (off the critical path)
+  auto load_gi0 = [&](int t, float (&gi)[3]) {
+    if (t >= T) return;
+    const float* src = L0.ids ? L0.P + (size_t)L0.ids[(size_t)t * Bp + b] * 3 * H
+                              : L0.Gi + ((size_t)t * Bp + b) * 3 * H;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+  };
+  float gin[3] = {0.f, 0.f, 0.f};
+  load_gi0(0, gin);
+  for (int s = 0; s <= T; ++s) {
+    const bool do0 = s < T, do1 = s > 0;   // lo's step s, hi's step s - 1
+    stamp(L0.dbg, s, 0);
+    float gi0[3] = {gin[0], gin[1], gin[2]};
+    const bool hasA = s > 0 || L0.h0, hasB = do1 && (s > 1 || L1.h0);   // h_lo(s-1), h_hi(s-2)
+    if (s >= 2) {
+      wave_wait_load2<NKW>(fl0, fl1, k0 / 16, (unsigned)s, (unsigned)(s - 1), L0.err,
+                           [&](int kk) { stage_x(0, kk, s - 1); }, [&](int kk) { stage_x(1, kk, s - 2); });
+    } else {
+      if (s == 1) wave_wait_load<NKW>(fl0, lane < 2 * NKW, k0 / 16 + lane, 1u, L0.err, [&](int kk) { stage_x(0, kk, 0); });
+      else if (hasA) stage_h0(0);
+      if (hasB) stage_h0(1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staged operands are in LDS
+    stamp(L0.dbg, s, 5);
+    f32x4 acc0[2][3], acc1[2][4];   // acc1: hi's r, z (input + recurrent), gi_n, gh_n
+    zero_acc(acc0);
+    zero_acc(acc1);
+    if (hasA && hasB) {   // the steady state: every product, no branches between the MFMAs
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const bf16x8 x = stage[w][0][kk][r][lane], y = stage[w][1][kk][r][lane];
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc0[r][g] = mfma16(x, wh0[kk][g], acc0[r][g]);
+#pragma unroll
+          for (int g = 0; g < 3; ++g) acc1[r][g] = mfma16(x, wi1[kk][g], acc1[r][g]);
+          acc1[r][0] = mfma16(y, wh1[kk][0], acc1[r][0]);
+          acc1[r][1] = mfma16(y, wh1[kk][1], acc1[r][1]);
+          acc1[r][3] = mfma16(y, wh1[kk][2], acc1[r][3]);
+        }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          if (hasA) {
+            const bf16x8 x = stage[w][0][kk][r][lane];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) acc0[r][g] = mfma16(x, wh0[kk][g], acc0[r][g]);
+#pragma unroll
+            for (int g = 0; g < 3; ++g) acc1[r][g] = mfma16(x, wi1[kk][g], acc1[r][g]);
+          }
+          if (hasB) {
+            const bf16x8 y = stage[w][1][kk][r][lane];
+            acc1[r][0] = mfma16(y, wh1[kk][0], acc1[r][0]);
+            acc1[r][1] = mfma16(y, wh1[kk][1], acc1[r][1]);
+            acc1[r][3] = mfma16(y, wh1[kk][2], acc1[r][3]);
+          }
+        }
+    }
+    stamp(L0.dbg, s, 1);
+    // partials over this wave's own staging area (its reads above precede these writes in the
+    // wave's in-order LDS queue; no other wave reads it before the barrier)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) mypart[(r * 3 + g) * 256 + i * 64 + lane] = acc0[r][g][i];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) mypart[(6 + r * 4 + g) * 256 + i * 64 + lane] = acc1[r][g][i];
+      }
+    __syncthreads();
+    stamp(L0.dbg, s, 2);
+    float h0v = 0.f, r0 = 0.f, z0 = 0.f, n0 = 0.f, ghn0 = 0.f;
+    float h1v = 0.f, r1 = 0.f, z1 = 0.f, n1 = 0.f, ghn1 = 0.f;
+    if (do0) {
+      float gh[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) sum += partial(ww, q * 3 + g);
+        gh[g] = sum + bh0[g];
+      }
+      r0 = sigmoidf_(gi0[0] + gh[0]);
+      z0 = sigmoidf_(gi0[1] + gh[1]);
+      n0 = tanhf_(gi0[2] + r0 * gh[2]);
+      ghn0 = gh[2];
+      h0v = n0 + z0 * (hp0 - n0);
+      hp0 = h0v;
+      const u16 hb = f2bf(h0v);
+      stg[0][row][col] = hb;
+      stgT[0][col][row] = hb;
+    }
+    if (do1) {
+      float v[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) sum += partial(ww, 6 + q * 4 + g);
+        v[g] = sum;
+      }
+      r1 = sigmoidf_(v[0] + bi1[0] + bh1[0]);
+      z1 = sigmoidf_(v[1] + bi1[1] + bh1[1]);
+      ghn1 = v[3] + bh1[2];
+      n1 = tanhf_(v[2] + bi1[2] + r1 * ghn1);
+      h1v = n1 + z1 * (hp1 - n1);
+      hp1 = h1v;
+      const u16 hb = f2bf(h1v);
+      stg[1][row][col] = hb;
+      stgT[1][col][row] = hb;
+    }
+    __syncthreads();   // also: every partial read before the next iteration's staging overwrites it
+    stamp(L0.dbg, s, 3);
+    load_gi0(s + 1, gin);
+    if (w < 2) {
+      // publish (lo from wave 0, hi from wave 1): the 32x16 bf16 tile, write-through unless the row
+      // block is XCD-local; drain; one signal.  Then the row-major copy for the later GEMMs.
+      const int ly = w, t = s - ly;
+      if (ly == 0 ? do0 : do1) {
+        const SeqFwdArgs& Y = ly == 0 ? L0 : L1;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[ly][lane >> 1][(lane & 1) * 8]);
+        const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
+        unsigned* fl = (ly == 0 ? fl0 : fl1) + (size_t)ut * kFlagStride;
+        const rsrc_t rX = ly == 0 ? rX0 : rX1;
+        if (loc) {
+          st16_plain(rX, xo, v);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) signal_flag_local(fl, (unsigned)(t + 1));
+        } else {
+          st16_sc1(rX, xo, v);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) signal_flag(fl, (unsigned)(t + 1));
+        }
+        if (ly == 0) stamp(L0.dbg, s, 4);
+        *reinterpret_cast<u32x4*>(Y.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
+      }
+    } else if (w < 6) {
+      // waves 2, 3: lo's transposed and fragment-tiled copies; waves 4, 5: hi's
+      const int ly = (w - 2) >> 1, t = s - ly;
+      const SeqFwdArgs& Y = ly == 0 ? L0 : L1;
+      if (ly == 0 ? do0 : do1) {
+        if (((w - 2) & 1) == 0) {
+          if (Y.HT) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[ly][lane >> 2][(lane & 3) * 8]);
+            *reinterpret_cast<u32x4*>(Y.HT + (size_t)(j0 + (lane >> 2)) * Y.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
+          }
+        } else if (Y.HF) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[ly][lane & 15][8 * (lane >> 4)]);
+          *reinterpret_cast<u32x4*>(Y.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
+        }
+      }
+    }
+    // saves for the backward pass after the publishes
+    if (do0) {
+      L0.HSf[((size_t)(s + 1) * Bp + b) * H + j] = h0v;
+      if (L0.sr) {
+        const size_t so = ((size_t)s * Bp + b) * H + j;
+        L0.sr[so] = r0; L0.sz[so] = z0; L0.sn[so] = n0; L0.sghn[so] = ghn0;
+      }
+    }
+    if (do1) {
+      L1.HSf[((size_t)s * Bp + b) * H + j] = h1v;
+      if (L1.sr) {
+        const size_t so = ((size_t)(s - 1) * Bp + b) * H + j;
+        L1.sr[so] = r1; L1.sz[so] = z1; L1.sn[so] = n1; L1.sghn[so] = ghn1;
+      }
     }
   }
 }
@@ -605,11 +922,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
 
 // ==================================================================== host side
 template <class K>
-static int resident_blocks(K kernel) {
+static int resident_blocks(K kernel, int block = 512) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 512, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess) return 0;
   return ncu * per;
 }
 
@@ -648,6 +965,34 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
   FWD_VARIANTS(X)
 #undef X
   throw std::runtime_error("gru_fwd_seq: no kernel variant for this shape");
+}
+
+#define FWD2_VARIANTS(X) X(256, 1) X(512, 2) X(1024, 4)
+
+bool gru_fwd_seq2_supported(int H, int Bp) {
+  if (Bp % 32) return false;
+  int cap = -1;
+#define X(HH, NK) if (H == HH) cap = resident_blocks(gru_fwd_seq2_kernel<NK>);
+  FWD2_VARIANTS(X)
+#undef X
+  return cap >= (H / 16) * (Bp / 32);
+}
+
+void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s) {
+  const SeqFwdArgs& l0 = a.lo;
+  const SeqFwdArgs& l1 = a.hi;
+  if (l1.H != l0.H || l1.Bp != l0.Bp || l1.T != l0.T || !a.Wih || !a.bih || !l1.HSf || !l1.HSb || !l1.xch ||
+      !l1.cnt || l1.xch == l0.xch || l1.cnt == l0.cnt)
+    throw std::runtime_error("gru_fwd_seq2: inconsistent layer arguments");
+  dim3 grid((l0.H / 16) * (l0.Bp / 32)), block(512);
+#define X(HH, NK)                                                           \
+  if (l0.H == HH) {                                                         \
+    hipLaunchKernelGGL((gru_fwd_seq2_kernel<NK>), grid, block, 0, s, a);    \
+    return;                                                                 \
+  }
+  FWD2_VARIANTS(X)
+#undef X
+  throw std::runtime_error("gru_fwd_seq2: no kernel variant for H=" + std::to_string(l0.H));
 }
 
 // fused-variant table: (H, fuse dW_hh, fuse dP) -> kernel

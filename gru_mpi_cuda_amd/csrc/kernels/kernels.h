@@ -105,6 +105,19 @@ inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 
 bool gru_fwd_seq_supported(int H, int Bp);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 
+// Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
+// `lo` at step s and layer `hi` at step s-1 in iteration s = 0..T.  hi's input projection
+// W_ih · h_lo(t) + b_ih is computed in the kernel from the same exchange tiles lo's next step reads
+// (no Gi GEMM, no Gi buffer); lo takes its input projection as SeqFwdArgs does (P table or Gi).
+// hi.Gi is unused; hi.xch and hi.cnt must not alias lo's.
+struct SeqFwd2Args {
+  SeqFwdArgs lo, hi;
+  const u16* Wih = nullptr;     // hi's W_ih [3H][H] bf16
+  const float* bih = nullptr;   // hi's b_ih [3H]
+};
+bool gru_fwd_seq2_supported(int H, int Bp);
+void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s);
+
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
   // top layer alternative to dy (V = 256): dy = dl · W_fc computed in the kernel from the

@@ -23,9 +23,10 @@ def rel(a, b):
 
 
 SCHEDULES = {
-    # name: (GK_PERSIST env, overlap[, GK_XCD_LOCAL env])
+    # name: (GK_PERSIST env, overlap[, GK_XCD_LOCAL env[, GK_FWD_WAVE env]])
     "persistent": ("1", False),
     "persistent_sc1": ("1", False, "0"),   # the placement-independent write-through hand-off only
+    "persistent_nowave": ("1", False, "1", "0"),   # L >= 2: one forward launch per layer
     "perstep": ("0", False),
     "overlap": ("1", True),
 }
@@ -43,6 +44,7 @@ def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
     env, overlap, *xl = SCHEDULES[sched]
     monkeypatch.setenv("GK_PERSIST", env)
     monkeypatch.setenv("GK_XCD_LOCAL", xl[0] if xl else "1")
+    monkeypatch.setenv("GK_FWD_WAVE", xl[1] if len(xl) > 1 else "1")
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=8, time_chunks=chunks, seed=7,
                     overlap=overlap)
     params = init_params(cfg)
@@ -54,6 +56,10 @@ def test_trainer_grads_match_cpu(monkeypatch, sched, layers, H, E, chunks, B):
     plan = tr.t.plan()
     if sched == "persistent" and H >= 256:
         assert "fwd=persistent" in plan and "bwd0=persistent" in plan, plan
+        # two-layer wavefront forward (gru_fwd_seq2) wherever it fits
+        assert ("fwd=persistent+wave" in plan) == (layers >= 2), plan
+    if sched == "persistent_nowave":
+        assert "+wave" not in plan, plan
     if sched == "perstep":
         assert "persistent" not in plan, plan
     tr.forward_backward(x, y)
@@ -356,7 +362,7 @@ def test_step_error_word_skips_update_and_trips_watchdog():
 
 
 @pytest.mark.parametrize("sched", ["persistent", "perstep", "overlap"])
-@pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 128, 64)])
+@pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 128, 64), (2, 256, 64)])
 def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
     """Truncated BPTT (cfg.carry_hidden): the step graph copies HS[T] -> HS[0] of every h copy
     (fp32, bf16, transposed, fragment-tiled), so step k+1 starts from step k's final state; the
