@@ -26,9 +26,12 @@ import numpy as np
 def _add_model_args(ap: argparse.ArgumentParser) -> None:
     for name, typ in (("vocab", int), ("embed", int), ("hidden", int), ("layers", int), ("batch", int),
                       ("seq", int), ("lr", float), ("max_len", int), ("sos", int), ("eos", int),
-                      ("clip_norm", float), ("seed", int), ("bucket_mb", float), ("time_chunks", int)):
+                      ("clip_norm", float), ("seed", int), ("bucket_mb", float), ("time_chunks", int),
+                      ("warmup_steps", int), ("total_steps", int), ("lr_min", float)):
         ap.add_argument("--" + name.replace("_", "-"), dest=name, type=typ, default=None)
     ap.add_argument("--optimizer", choices=["adam", "sgd"], default=None)
+    ap.add_argument("--lr-sched", dest="lr_sched", choices=["const", "cosine", "linear"], default=None,
+                    help="learning-rate decay after --warmup-steps, down to --lr-min at --total-steps")
     ap.add_argument("--carry-hidden", dest="carry_hidden", action="store_const", const=True, default=None,
                     help="truncated BPTT: carry each step's final hidden state into the next step")
 
@@ -127,6 +130,10 @@ def cmd_train(args) -> int:
     from .utils.metrics import MetricsWriter, StepTimer, log
     ctx = gdist.init(use_gpu=torch.cuda.is_available() and not args.cpu, verbose=True)
     cfg = _cfg_from(args)
+    if cfg.lr_sched != "const" and cfg.total_steps <= 0:
+        # decay over this run (a resumed run restores the step counter, so pass --total-steps to
+        # keep one schedule across restarts)
+        cfg = cfg.replace(total_steps=args.steps)
     comm = make_comm(ctx) if ctx.device.type == "cuda" else None
     tr = make_trainer(cfg, ctx, comm=comm)
     start = load_checkpoint(tr, args.resume) if args.resume else 0

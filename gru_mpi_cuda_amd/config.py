@@ -35,6 +35,13 @@ class GRUConfig:
     eps: float = 1e-8
     weight_decay: float = 0.0
     clip_norm: float = 0.0      # 0 = off; global-norm gradient clipping otherwise
+    # learning-rate schedule (applied on the device from the step counter, so graph replay keeps
+    # it): linear warm-up over warmup_steps, then "const", "cosine" or "linear" decay to lr_min at
+    # total_steps (models/cpu_ref.lr_at)
+    lr_sched: str = "const"
+    warmup_steps: int = 0
+    total_steps: int = 0
+    lr_min: float = 0.0
     dtype: str = "bf16"         # compute dtype of the HIP engine (fp32 master weights)
     seed: int = 1234
     carry_hidden: bool = False  # truncated BPTT over a continuous stream: each step starts from the

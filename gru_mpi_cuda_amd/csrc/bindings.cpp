@@ -78,6 +78,8 @@ PYBIND11_MODULE(_C, m) {
         o.lr = get<float>(opt, "lr", 1e-3f); o.b1 = get<float>(opt, "beta1", 0.9f); o.b2 = get<float>(opt, "beta2", 0.999f);
         o.eps = get<float>(opt, "eps", 1e-8f); o.wd = get<float>(opt, "weight_decay", 0.f);
         o.clip = get<float>(opt, "clip_norm", 0.f); o.sgd = get<int>(opt, "sgd", 0);
+        o.sched = get<int>(opt, "lr_sched", 0); o.warmup = get<int>(opt, "warmup_steps", 0);
+        o.total = get<int>(opt, "total_steps", 0); o.lr_min = get<float>(opt, "lr_min", 0.f);
         return new Trainer(d, o, Pp<float>(params), Pp<float>(grads), Pp<float>(mm), Pp<float>(vv), nflat, offsets);
       }))
       .def("refresh_weights", [](Trainer& t, uintptr_t s) { t.refresh_weights(S(s)); })

@@ -480,6 +480,7 @@ void Trainer::record_opt(hipStream_t s) {
   a.gscale = o_.clip > 0.f ? gscale_ : nullptr;
   a.err = err_; a.err_host = err_host_dev_;
   a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
+  a.sched = o_.sched; a.warmup = o_.warmup; a.total = o_.total; a.lr_min = o_.lr_min;
   const int V = d_.V, E = d_.E, H = d_.H;
   if (V % 64 == 0 && E % 64 == 0 && H % 64 == 0) {
     // one launch: update every tensor and write its bf16 (+ transposed) MFMA copies from the

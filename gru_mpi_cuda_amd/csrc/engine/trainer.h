@@ -29,6 +29,8 @@ struct Dims {
 struct OptCfg {
   float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f, clip = 0.f;
   int sgd = 0;
+  int sched = 0, warmup = 0, total = 0;   // OptimArgs::sched / warmup / total
+  float lr_min = 0.f;
 };
 
 class Trainer {

@@ -276,15 +276,20 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   zero_next_flags(a.zero_next, a.zero_words);
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
 
+  // the input projection of step t, gathered one step ahead, after the publish (its latency off
+  // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order)
+  auto load_gi = [&](int t, float (&gi)[3]) {
+    if (t >= T) return;
+    const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H
+                             : a.Gi + ((size_t)t * Bp + b) * 3 * H;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+  };
+  float gin[3] = {0.f, 0.f, 0.f};
+  load_gi(0, gin);
   for (int t = 0; t < T; ++t) {
     stamp(a.dbg, t, 0);
-    float gi[3];
-    {
-      const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H
-                               : a.Gi + ((size_t)t * Bp + b) * 3 * H;
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
-    }
+    const float gi[3] = {gin[0], gin[1], gin[2]};
     f32x4 acc[NR][3];
     zero_acc(acc);
     if (t > 0 || a.h0) {
@@ -372,6 +377,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
     }
     // saves for the backward pass AFTER the publish, so they are not part of wave 0's drain
+    load_gi(t + 1, gin);
     a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
     if (a.sr) {
       const size_t so = ((size_t)t * Bp + b) * H + j;
@@ -598,7 +604,6 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
     }
     __syncthreads();   // also: every partial read before the next iteration's staging overwrites it
     stamp(L0.dbg, s, 3);
-    load_gi0(s + 1, gin);
     if (w < 2) {
       // publish (lo from wave 0, hi from wave 1): the 32x16 bf16 tile, write-through unless the row
       // block is XCD-local; drain; one signal.  Then the row-major copy for the later GEMMs.
@@ -637,7 +642,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
         }
       }
     }
-    // saves for the backward pass after the publishes
+    // next step's input projection and the saves for the backward pass after the publishes (a
+    // load issued before wave 0's drain would be part of it: vmcnt retires in order)
+    load_gi0(s + 1, gin);
     if (do0) {
       L0.HSf[((size_t)(s + 1) * Bp + b) * H + j] = h0v;
       if (L0.sr) {

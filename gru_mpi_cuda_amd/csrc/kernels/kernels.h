@@ -319,6 +319,11 @@ struct OptimArgs {
   unsigned* err_host = nullptr;
   float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, eps = 1e-8f, wd = 0.f;
   int sgd = 0;
+  // learning-rate schedule, evaluated on the device from the step counter (graph-replay safe):
+  // linear warm-up over `warmup` steps, then 0 = constant, 1 = cosine, 2 = linear decay to lr_min
+  // at step `total` (models/cpu_ref.py lr_at is the host twin)
+  int sched = 0, warmup = 0, total = 0;
+  float lr_min = 0.f;
 };
 void adam_step(const OptimArgs& a, hipStream_t s);
 void bump_step(int* step, hipStream_t s);

@@ -243,9 +243,20 @@ DEV bool step_failed(const OptimArgs& a) {
   return e != 0u;
 }
 
+// learning rate of update t (1-based): warm-up, then the decay of OptimArgs::sched
+DEV float sched_lr(const OptimArgs& a, int t) {
+  float lr = a.lr;
+  if (a.warmup > 0 && t <= a.warmup) return lr * (float)t / (float)a.warmup;
+  if (a.sched == 0 || a.total <= a.warmup) return lr;
+  const float p = fminf(1.f, (float)(t - a.warmup) / (float)(a.total - a.warmup));
+  const float f = a.sched == 1 ? 0.5f * (1.f + cosf(3.14159265358979f * p)) : 1.f - p;
+  return a.lr_min + (lr - a.lr_min) * f;
+}
+
 __global__ void adam_kernel(OptimArgs a) {
   if (step_failed(a)) return;
   const int t = *a.step;
+  const float lr = sched_lr(a, t);
   const float sc = a.gscale ? *a.gscale : 1.f;
   const float bc1 = 1.f - powf(a.b1, (float)t), bc2 = 1.f - powf(a.b2, (float)t);
   const float ib1 = 1.f / bc1, ib2 = 1.f / bc2;
@@ -257,7 +268,7 @@ __global__ void adam_kernel(OptimArgs a) {
     const float gv[4] = {g4.x * sc, g4.y * sc, g4.z * sc, g4.w * sc};
     if (a.sgd) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+      for (int e = 0; e < 4; ++e) pv[e] -= lr * (gv[e] + a.wd * pv[e]);
     } else {
       float4 m = reinterpret_cast<float4*>(a.m)[i];
       float4 v = reinterpret_cast<float4*>(a.v)[i];
@@ -268,7 +279,7 @@ __global__ void adam_kernel(OptimArgs a) {
         vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
         float u = (mv[e] * ib1) / (sqrtf(vv[e] * ib2) + a.eps);
         if (a.wd != 0.f) u += a.wd * pv[e];
-        pv[e] -= a.lr * u;
+        pv[e] -= lr * u;
       }
       reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
       reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -281,10 +292,11 @@ void adam_step(const OptimArgs& a, hipStream_t s) {
 }
 
 // Adam/SGD update of 4 consecutive elements (same math as adam_kernel)
-struct AdamCoef { float sc, ib1, ib2; };
+struct AdamCoef { float sc, ib1, ib2, lr; };
 DEV AdamCoef adam_coef(const OptimArgs& a) {
   const int t = *a.step;
-  return AdamCoef{a.gscale ? *a.gscale : 1.f, 1.f / (1.f - powf(a.b1, (float)t)), 1.f / (1.f - powf(a.b2, (float)t))};
+  return AdamCoef{a.gscale ? *a.gscale : 1.f, 1.f / (1.f - powf(a.b1, (float)t)), 1.f / (1.f - powf(a.b2, (float)t)),
+                  sched_lr(a, t)};
 }
 // gradient float4 i (flat index) of job J: from the gradient buffer, or summed from J's slabs
 // (same order as sum_slabs4 in reduce_multi) and written back to the gradient buffer
@@ -302,7 +314,7 @@ DEV float4 adam4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
   const float gv[4] = {g4.x * k.sc, g4.y * k.sc, g4.z * k.sc, g4.w * k.sc};
   if (a.sgd) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+    for (int e = 0; e < 4; ++e) pv[e] -= k.lr * (gv[e] + a.wd * pv[e]);
   } else {
     const float4 m = reinterpret_cast<float4*>(a.m)[i];
     const float4 v = reinterpret_cast<float4*>(a.v)[i];
@@ -313,7 +325,7 @@ DEV float4 adam4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
       vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
       float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
       if (a.wd != 0.f) u += a.wd * pv[e];
-      pv[e] -= a.lr * u;
+      pv[e] -= k.lr * u;
     }
     reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
     reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
@@ -342,7 +354,7 @@ DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
     const float gv[4] = {g[q].x * k.sc, g[q].y * k.sc, g[q].z * k.sc, g[q].w * k.sc};
     if (a.sgd) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pv[e] -= a.lr * (gv[e] + a.wd * pv[e]);
+      for (int e = 0; e < 4; ++e) pv[e] -= k.lr * (gv[e] + a.wd * pv[e]);
     } else {
       float mv[4] = {m[q].x, m[q].y, m[q].z, m[q].w}, vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
@@ -351,7 +363,7 @@ DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
         vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
         float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
         if (a.wd != 0.f) u += a.wd * pv[e];
-        pv[e] -= a.lr * u;
+        pv[e] -= k.lr * u;
       }
       reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
       reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);

@@ -58,9 +58,13 @@ class HipTrainer:
         ic = self.icfg
         dims = dict(V=ic.vocab, E=ic.embed, H=ic.hidden, L=cfg.layers, B=self.local_batch,
                     T=cfg.seq, chunks=cfg.time_chunks, overlap=int(cfg.overlap))
+        from ..models.cpu_ref import LR_SCHEDS
+        if cfg.lr_sched not in LR_SCHEDS:
+            raise ValueError(f"lr_sched must be one of {LR_SCHEDS}, got {cfg.lr_sched!r}")
         opt = dict(lr=cfg.lr, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps,
                    weight_decay=cfg.weight_decay, clip_norm=cfg.clip_norm,
-                   sgd=int(cfg.optimizer == "sgd"))
+                   sgd=int(cfg.optimizer == "sgd"), lr_sched=LR_SCHEDS.index(cfg.lr_sched),
+                   warmup_steps=cfg.warmup_steps, total_steps=cfg.total_steps, lr_min=cfg.lr_min)
         self.t = self.C.Trainer(dims, opt, self.params.data_ptr(), self.grads.data_ptr(),
                                 self.m.data_ptr(), self.v.data_ptr(), self.layout.total, offsets)
         self.t.set_use_graph(use_graph)

@@ -18,6 +18,7 @@ is checked against ``torch.autograd`` in tests/test_cpu_ref.py.
 """
 from __future__ import annotations
 
+import math
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -137,6 +138,24 @@ def autograd_grads(params: Params, cfg: GRUConfig, x: torch.Tensor, y: torch.Ten
 
 
 # --------------------------------------------------------------------------- optimiser
+LR_SCHEDS = ("const", "cosine", "linear")
+
+
+def lr_at(cfg: GRUConfig, t: int) -> float:
+    """Learning rate of update t (1-based): linear warm-up over ``warmup_steps``, then constant,
+    cosine or linear decay from ``lr`` to ``lr_min`` at ``total_steps`` -- the host twin of the
+    device schedule in the Adam kernels (csrc/kernels/misc.hip sched_lr)."""
+    if cfg.lr_sched not in LR_SCHEDS:
+        raise ValueError(f"lr_sched must be one of {LR_SCHEDS}, got {cfg.lr_sched!r}")
+    if cfg.warmup_steps > 0 and t <= cfg.warmup_steps:
+        return cfg.lr * t / cfg.warmup_steps
+    if cfg.lr_sched == "const" or cfg.total_steps <= cfg.warmup_steps:
+        return cfg.lr
+    p = min(1.0, (t - cfg.warmup_steps) / (cfg.total_steps - cfg.warmup_steps))
+    f = 0.5 * (1.0 + math.cos(math.pi * p)) if cfg.lr_sched == "cosine" else 1.0 - p
+    return cfg.lr_min + (cfg.lr - cfg.lr_min) * f
+
+
 class Adam:
     """Functional Adam/SGD on a dict of fp32 tensors -- same update rule as the HIP
     ``optim`` kernel (bias-corrected Adam, decoupled weight decay, optional global
@@ -155,9 +174,10 @@ class Adam:
             norm = torch.sqrt(sum((g.double() ** 2).sum() for g in grads.values())).item()
             scale = min(1.0, c.clip_norm / (norm + 1e-6))
         self.step_n += 1
+        lr = lr_at(c, self.step_n)
         if c.optimizer == "sgd":
             for k in params:
-                params[k] -= c.lr * (grads[k] * scale + c.weight_decay * params[k])
+                params[k] -= lr * (grads[k] * scale + c.weight_decay * params[k])
             return
         b1, b2 = c.beta1, c.beta2
         bc1 = 1 - b1 ** self.step_n
@@ -169,7 +189,7 @@ class Adam:
             upd = (self.m[k] / bc1) / (torch.sqrt(self.v[k] / bc2) + c.eps)
             if c.weight_decay:
                 upd = upd + c.weight_decay * params[k]
-            params[k] -= c.lr * upd
+            params[k] -= lr * upd
 
 
 # --------------------------------------------------------------------------- generation

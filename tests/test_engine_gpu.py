@@ -483,3 +483,34 @@ def test_generator_graph_replays_identical(precision, n):
     assert g.g.read_error() == 0
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+
+
+def test_trainer_lr_schedule_matches_cpu():
+    """Device learning-rate schedule (misc.hip sched_lr, read from the device step counter inside
+    the replayed graph) against the host formula cpu_ref.lr_at: with SGD every update is
+    -lr_t * g_t, so the median of -du/g over large-gradient elements recovers lr_t per step.
+    Adam: the first warm-up step is exactly 1/warmup of the constant-lr first step."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.models.cpu_ref import lr_at
+    cfg = GRUConfig(vocab=256, embed=128, hidden=256, layers=1, batch=64, seq=8, lr=5e-2, seed=2,
+                    optimizer="sgd", lr_sched="cosine", warmup_steps=2, total_steps=6, lr_min=5e-3)
+    params = init_params(cfg)
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    tr = HipTrainer(cfg, params=params)
+    for t in range(1, 8):
+        before = tr.state_dict()
+        tr.step(*ds.next())
+        after, g = tr.state_dict(), tr.grad_dict()
+        k = "weight_hh_l0"
+        gk, du = g[k].double(), (after[k] - before[k]).double()
+        sel = gk.abs() > gk.abs().quantile(0.9)
+        got = float((-du[sel] / gk[sel]).median())
+        assert got == pytest.approx(lr_at(cfg, t), rel=2e-3), (t, got, lr_at(cfg, t))
+    upd = {}
+    for name, c in (("const", cfg.replace(optimizer="adam", lr_sched="const", warmup_steps=0)),
+                    ("warm", cfg.replace(optimizer="adam", lr_sched="linear", warmup_steps=4, total_steps=10))):
+        tr = HipTrainer(c, params=params)
+        tr.step(*NameStream(cfg.batch, cfg.seq, seed=9).next())
+        upd[name] = {k: v - params[k] for k, v in tr.state_dict().items()}
+    for k in upd["const"]:
+        assert rel(upd["warm"][k] * 4, upd["const"][k]) < 1e-3, k

@@ -374,3 +374,75 @@ def test_gemm_f32(ext, M, N, K, splits):
     torch.cuda.synchronize()
     ref = A.double() @ B.double().T + bv.double()
     torch.testing.assert_close(C.double().sum(0), ref, atol=1e-5 * K ** 0.5, rtol=1e-5)
+
+
+def _gru2_ref(P, ids, Whh0, bhh0, Wih1, bih1, Whh1, bhh1, h00, h01):
+    """Two stacked GRU layers in fp32 with the kernels' bf16 rounding of every MFMA operand (h is
+    exchanged as bf16; the gate math and the carried state stay fp32)."""
+    T, B = ids.shape
+    f = lambda t: t.to(torch.bfloat16).float()
+    h0, h1 = h00.clone(), h01.clone()
+    H0, H1, S1 = [], [], []
+    for t in range(T):
+        gi = P[ids[t].long()]
+        gh = f(h0) @ Whh0.float().t() + bhh0
+        gi_r, gi_z, gi_n = torch.chunk(gi, 3, dim=1)
+        gh_r, gh_z, gh_n = torch.chunk(gh, 3, dim=1)
+        r = torch.sigmoid(gi_r + gh_r); z = torch.sigmoid(gi_z + gh_z); n = torch.tanh(gi_n + r * gh_n)
+        h0 = n + z * (h0 - n)
+        gi1 = f(h0) @ Wih1.float().t() + bih1
+        gh1 = f(h1) @ Whh1.float().t() + bhh1
+        gi_r, gi_z, gi_n = torch.chunk(gi1, 3, dim=1)
+        gh_r, gh_z, gh_n = torch.chunk(gh1, 3, dim=1)
+        r = torch.sigmoid(gi_r + gh_r); z = torch.sigmoid(gi_z + gh_z); n = torch.tanh(gi_n + r * gh_n)
+        h1 = n + z * (h1 - n)
+        H0.append(h0); H1.append(h1); S1.append(gh_n)
+    return torch.stack(H0), torch.stack(H1), torch.stack(S1)
+
+
+@pytest.mark.parametrize("H,B", [(256, 64), (512, 64), (1024, 128)])
+@pytest.mark.parametrize("carry", [False, True])
+def test_fwd_seq2_two_layer_wavefront(ext, H, B, carry):
+    """gru_fwd_seq2 (layer 0 at step s, layer 1 at step s-1, layer 1's input projection in-kernel)
+    against a torch fp32 two-layer recurrence on the same bf16 operands."""
+    if not ext.fwd_seq2_supported(H, B):
+        pytest.skip("shape not co-resident")
+    T, V = 8, 256
+    g = torch.Generator(device="cpu").manual_seed(3)
+    R = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)
+    Whh0, Wih1, Whh1 = (bf(R(3 * H, H, sc=H ** -0.5)) for _ in range(3))
+    bhh0, bih1, bhh1 = (R(3 * H, sc=0.1) for _ in range(3))
+    P = R(V, 3 * H, sc=0.5)
+    ids = torch.randint(0, V, (T, B), generator=g, dtype=torch.int32).to(DEV)
+    h00 = R(B, H, sc=0.5) if carry else torch.zeros(B, H, device=DEV)
+    h01 = R(B, H, sc=0.5) if carry else torch.zeros(B, H, device=DEV)
+    err = torch.zeros(16, device=DEV, dtype=torch.int32)
+    bufs, dicts = [], []
+    for Whh, bhh, h0 in ((Whh0, bhh0, h00), (Whh1, bhh1, h01)):
+        b = dict(HSb=torch.zeros(T + 1, B, H, device=DEV, dtype=torch.bfloat16),
+                 xch=torch.zeros(T, B, H, device=DEV, dtype=torch.bfloat16),
+                 HSf=torch.zeros(T + 1, B, H, device=DEV),
+                 HT=torch.zeros(H, (T + 1) * B, device=DEV, dtype=torch.bfloat16),
+                 sv=[torch.zeros(T, B, H, device=DEV) for _ in range(4)],
+                 cnt=torch.zeros(B // 32 * H // 16 * 16 + 64, device=DEV, dtype=torch.int32), h0=h0.contiguous())
+        b["HSb"][0] = h0.to(torch.bfloat16)
+        b["HSf"][0] = h0
+        d = dict(HSb=b["HSb"].data_ptr(), xch=b["xch"].data_ptr(), HSf=b["HSf"].data_ptr(), HT=b["HT"].data_ptr(),
+                 ldT=(T + 1) * B, sr=b["sv"][0].data_ptr(), sz=b["sv"][1].data_ptr(), sn=b["sv"][2].data_ptr(),
+                 sghn=b["sv"][3].data_ptr(), Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), cnt=b["cnt"].data_ptr(),
+                 err=err.data_ptr(), T=T, Bp=B, H=H)
+        if carry:
+            d["h0"] = b["h0"].data_ptr()
+        bufs.append(b); dicts.append(d)
+    dicts[0].update(P=P.data_ptr(), ids=ids.data_ptr())
+    ext.fwd_seq2(dicts[0], dicts[1], Wih1.data_ptr(), bih1.data_ptr(), S())
+    torch.cuda.synchronize()
+    assert int(err[0]) == 0
+    H0, H1, GHN1 = _gru2_ref(P, ids, Whh0, bhh0, Wih1, bih1, Whh1, bhh1, h00, h01)
+    torch.testing.assert_close(bufs[0]["HSf"][1:], H0, atol=5e-3, rtol=0)
+    torch.testing.assert_close(bufs[1]["HSf"][1:], H1, atol=5e-3, rtol=0)
+    torch.testing.assert_close(bufs[1]["sv"][3], GHN1, atol=5e-3, rtol=0)
+    # bf16 copies: row-major HS and the transposed HT of layer 1 (the weight-gradient operands)
+    torch.testing.assert_close(bufs[1]["HSb"][1:].float(), H1, atol=2e-2, rtol=0)
+    HT1 = bufs[1]["HT"].view(H, T + 1, B)[:, 1:].permute(1, 2, 0).float()
+    torch.testing.assert_close(HT1, H1, atol=2e-2, rtol=0)
