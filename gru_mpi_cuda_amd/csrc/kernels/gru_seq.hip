@@ -277,13 +277,15 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
 
   // the input projection of step t, gathered one step ahead, after the publish (its latency off
-  // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order)
+  // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order).
+  // The char id it needs is loaded one step earlier still, so the gather never waits on an id load.
+  int idn = a.ids ? a.ids[b] : 0;   // id of the step whose row load_gi gathers next
   auto load_gi = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
-    const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H
-                             : a.Gi + ((size_t)t * Bp + b) * 3 * H;
+    const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};
   load_gi(0, gin);
@@ -486,13 +488,15 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
     return reinterpret_cast<const float*>(&stage[ww][0][0][0][0])[set * 256 + pidx];
   };
 
-  // lo's input projection for step t, gathered one iteration ahead (off the critical path)
+  // lo's input projection for step t, gathered one iteration ahead (off the critical path), from
+  // a char id loaded one iteration before that (the gather never waits on an id load)
+  int idn = L0.ids ? L0.ids[b] : 0;
   auto load_gi0 = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
-    const float* src = L0.ids ? L0.P + (size_t)L0.ids[(size_t)t * Bp + b] * 3 * H
-                              : L0.Gi + ((size_t)t * Bp + b) * 3 * H;
+    const float* src = L0.ids ? L0.P + (size_t)idn * 3 * H : L0.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    if (L0.ids && t + 1 < T) idn = L0.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};
   load_gi0(0, gin);
