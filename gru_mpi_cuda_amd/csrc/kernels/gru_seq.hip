@@ -37,6 +37,13 @@ DEV bf16x8 ld8_sc1(rsrc_t r, unsigned off) {
   return __builtin_bit_cast(bf16x8, v);
 }
 DEV void st16_sc1(rsrc_t r, unsigned off, u32x4 v) { __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16); }
+// sc1 load with a per-lane offset and a wave-uniform scalar offset: the address math of an
+// unrolled k-loop then needs no VGPR temporaries (in the streaming wait, temporaries that alias a
+// pending load's destination made the compiler drain vmcnt before every k-step's load)
+DEV bf16x8 ld8_sc1s(rsrc_t r, unsigned voff, int soff) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 16);
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 static constexpr unsigned kSpinLimit = 1u << 21;   // x s_sleep(2): ~0.3 s, >> any real wait
 
@@ -677,7 +684,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) u16 srow[3][32][24];        // dGh tile, gate-major (exchange; 48-B rows)
   __shared__ __attribute__((aligned(16))) u16 sgT[4][16][40];         // dGh^T gates r,z,n + dGi_n^T (padded rows)
   __shared__ __attribute__((aligned(16))) float red[6][16][33];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // H = 1024 (NKW3 = 12): scalar wave index and scalar-offset exchange loads (below); the smaller
+  // variants measured slower with them (h512 step 0.2257 -> 0.2327 ms, profiles/r2_bwd_soffset_ab.json)
+  constexpr bool kScalarX = NKW3 >= 12;
+  const int tid = threadIdx.x, lane = tid & 63, w = kScalarX ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int H = a.H, H3 = 3 * a.H, Bp = a.Bp, T = a.T;
   const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
   const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
@@ -709,6 +719,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   zero_acc(accW);
   zero_acc(accP);
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
+  const unsigned xlane = (unsigned)(((lk >> 4) * 3 * 512 + lr * 16 + (lk & 15)) * 2);   // exchange lane offset
   zero_next_flags(a.zero_next, a.zero_words);
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
@@ -766,13 +777,22 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       bf16x8 af[NKW3][2];
       // dGh_{t+1} column c = k0 + 32kk + lk (gate c/H, unit c%H) lives in producer tile (c%H)/16 of
       // slot t+1 at column (c/H)*16 + c%16
+      // 32-column k-steps never straddle a gate (H % 32 == 0): gate c0 / H and producer tile
+      // (c0 % H) / 16 are wave-uniform (scalar offset); the lane part is fixed for the launch
       const size_t slot = ((size_t)(t + 1) * nrb + rbk) * nunit;
       wave_wait_load<NKW3>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3,
                            ((k0 + 16 * lane) % H) / 16, (unsigned)s, a.err, [&](int kk) {
-        const int c = k0 + kk * 32 + lk, u = c % H;
-        const unsigned tb = (unsigned)(((slot + u / 16) * 3 + c / H) * 512 + lr * 16 + (u & 15)) * 2;
+        if constexpr (kScalarX) {
+          const int c0 = k0 + kk * 32;
+          const int so = (int)((((slot + (size_t)((c0 % H) / 16)) * 3 + (size_t)(c0 / H)) * 512) * 2);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 16 * 2));
+          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1s(rX, xlane + (unsigned)(r * 16 * 16 * 2), so);
+        } else {
+          const int c = k0 + kk * 32 + lk, u = c % H;
+          const unsigned tb = (unsigned)(((slot + u / 16) * 3 + c / H) * 512 + lr * 16 + (u & 15)) * 2;
+#pragma unroll
+          for (int r = 0; r < 2; ++r) af[kk][r] = ld8_sc1(rX, tb + (unsigned)(r * 16 * 16 * 2));
+        }
       });
       stamp(a.dbg, s, 1);
 #pragma unroll
