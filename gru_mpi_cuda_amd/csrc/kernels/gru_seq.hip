@@ -280,6 +280,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
   const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
   const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
+  const unsigned sv_bytes = (unsigned)((size_t)T * Bp * H * 4);   // < 4 GB: checked on the host
+  const rsrc_t rHSf = make_rsrc(a.HSf, sv_bytes + (unsigned)(Bp * H * 4));
+  const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
+  const rsrc_t rSn = make_rsrc(a.sn, a.sn ? sv_bytes : 0u), rSg = make_rsrc(a.sghn, a.sghn ? sv_bytes : 0u);
+  const unsigned sv_lane = (unsigned)((b * H + j) * 4);
   zero_next_flags(a.zero_next, a.zero_words);
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
 
@@ -378,6 +383,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       }
       stamp(a.dbg, t, 4);
       *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
+      stamp(a.dbg, t, 5);
     } else if (w == 1 && a.HT) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane >> 2][(lane & 3) * 8]);
       *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
@@ -385,13 +391,20 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane & 15][8 * (lane >> 4)]);
       *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
     }
-    // saves for the backward pass AFTER the publish, so they are not part of wave 0's drain
+    // the next gather, then the saves for the backward pass, AFTER the publish (not part of wave
+    // 0's drain).  Saves as buffer stores: one per-lane offset for the launch, the step in the
+    // scalar offset -- with 64-bit VGPR address math the compiler reused the in-flight gather's
+    // destination as a temporary and waited for it (+0.3 us per step at H = 512).
     load_gi(t + 1, gin);
-    a.HSf[((size_t)(t + 1) * Bp + b) * H + j] = h;
+    const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
     if (a.sr) {
-      const size_t so = ((size_t)t * Bp + b) * H + j;
-      a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = gh[2];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
     }
+    stamp(a.dbg, t, 6);
   }
 }
 
@@ -653,8 +666,8 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
         }
       }
     }
-    // next step's input projection and the saves for the backward pass after the publishes (a
-    // load issued before wave 0's drain would be part of it: vmcnt retires in order)
+    // next step's input gather and the saves for the backward pass after the publishes (a load
+    // issued before wave 0's drain would be part of it: vmcnt retires in order)
     load_gi0(s + 1, gin);
     if (do0) {
       L0.HSf[((size_t)(s + 1) * Bp + b) * H + j] = h0v;
@@ -986,6 +999,8 @@ bool gru_fwd_seq_supported(int H, int Bp) {
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
+  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
+    throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
 #define X(HH, NK, RS)                                                        \
