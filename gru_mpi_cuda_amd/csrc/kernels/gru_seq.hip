@@ -897,7 +897,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       const size_t og = ((size_t)t * Bp + b) * H3 + j;
       a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
     }
-    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS)
+    stamp(a.dbg, s, 5);
+    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS).  Here, between the publish
+    // and the next poll, they are hidden by the flag propagation; deferred into the next step's
+    // exchange-load window they delayed its recurrent MFMAs (0.2199 -> 0.2291 ms,
+    // profiles/r2_rejected_ab.jsonl)
     if constexpr (NTW > 0 || NTP > 0) {
       bf16x8 ga[3];
 #pragma unroll
@@ -928,6 +932,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     if constexpr (fdl) {   // dl image of step t - NB into the buffer this step just consumed
       if (t >= NB) load_dl(t - NB);
     }
+    stamp(a.dbg, s, 6);
   }
 
   // ---- partial weight gradients of this row block

@@ -61,10 +61,11 @@ for mode in ("plain", "dbg"):
         times.append(e0.elapsed_time(e1) * 1000)
     res[mode + "_us"] = round(float(np.median(times[5:])), 1)
 res["err"] = int(err[0])
-st = dbg.view(2, 4096, 8)[:, :T, :5].cpu().numpy().astype(np.float64) * 10.0
+st = dbg.view(2, 4096, 8)[:, :T, :7].cpu().numpy().astype(np.float64) * 10.0
 for wg in (0, 1):
     x = st[wg]
     ph = {"wait": x[1:, 1] - x[1:, 0], "mma": x[1:, 2] - x[1:, 1], "epi": x[1:, 3] - x[1:, 2],
-          "pub": x[1:, 4] - x[1:, 3], "step": x[2:, 0] - x[1:-1, 0]}
+          "pub": x[1:, 4] - x[1:, 3], "dgi": x[1:, 5] - x[1:, 4], "fused": x[1:, 6] - x[1:, 5],
+          "loop": x[2:, 0] - x[1:-1, 6], "step": x[2:, 0] - x[1:-1, 0]}
     res[f"wg{wg}"] = {k: round(float(np.median(v)) / 1000, 3) for k, v in ph.items()}
 print(json.dumps(res))
