@@ -400,14 +400,14 @@ def _gru2_ref(P, ids, Whh0, bhh0, Wih1, bih1, Whh1, bhh1, h00, h01):
     return torch.stack(H0), torch.stack(H1), torch.stack(S1)
 
 
-@pytest.mark.parametrize("H,B", [(256, 64), (512, 64), (1024, 128)])
+@pytest.mark.parametrize("H,B,T", [(256, 64, 8), (512, 64, 8), (1024, 128, 8), (256, 32, 1), (512, 96, 2)])
 @pytest.mark.parametrize("carry", [False, True])
-def test_fwd_seq2_two_layer_wavefront(ext, H, B, carry):
+def test_fwd_seq2_two_layer_wavefront(ext, H, B, T, carry):
     """gru_fwd_seq2 (layer 0 at step s, layer 1 at step s-1, layer 1's input projection in-kernel)
     against a torch fp32 two-layer recurrence on the same bf16 operands."""
     if not ext.fwd_seq2_supported(H, B):
         pytest.skip("shape not co-resident")
-    T, V = 8, 256
+    V = 256
     g = torch.Generator(device="cpu").manual_seed(3)
     R = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)
     Whh0, Wih1, Whh1 = (bf(R(3 * H, H, sc=H ** -0.5)) for _ in range(3))
