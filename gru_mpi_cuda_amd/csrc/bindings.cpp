@@ -221,6 +221,26 @@ PYBIND11_MODULE(_C, m) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
   m.def("bwd_step_sk_splits", &gru_bwd_step_sk_splits);
+  m.def("step_lds_variants", []() {
+    const StepLdsVariants& v = step_lds_variants();
+    py::dict d;
+    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8;
+    d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf;
+    return d;
+  });
+  m.def("set_step_lds_variants", [](py::dict d) {
+    StepLdsVariants& v = step_lds_variants();
+    for (auto kv : d) {
+      const std::string k = py::str(kv.first);
+      const int x = kv.second.cast<int>();
+      if (k == "fwd_ns") v.fwd_ns = x;
+      else if (k == "fwd_nt") v.fwd_nt = x;
+      else if (k == "fwd8") v.fwd8 = x;
+      else if (k == "bwd_sk_ns") v.bwd_sk_ns = x;
+      else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
+      else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
+    }
+  });
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
   m.def("fwd_seq2", [](py::dict lo, py::dict hi, uintptr_t Wih, uintptr_t bih, uintptr_t s) {
     auto parse = [](py::dict d) {

@@ -67,7 +67,11 @@ constexpr int FNS = 4, BNS = 6;
 // NS: LDS ring depth.  4 (112 KiB, one workgroup per CU) when the grid is about one wave of
 // workgroups (training at H = 2048: 256 tiles); 2 (56 KiB, two per CU) for big-batch generation,
 // where several rounds of tiles per CU need the second workgroup to hide latency.
-template <bool FUSED, int NS>
+// NT: saves (fp32 h, r, z, n, gh_n) with nontemporal stores (A/B switch GK_STEP_NT=1): they are
+// re-read only by the backward sweep, after T more steps of traffic.
+template <class T> DEV void save_st(T* p, T v, std::true_type) { __builtin_nontemporal_store(v, p); }
+template <class T> DEV void save_st(T* p, T v, std::false_type) { *p = v; }
+template <bool FUSED, int NS, bool NT = false>
 __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
   const int H = a.H;
@@ -194,10 +198,11 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
       const float n = tanhf_(gin + r * ghn);
       const float h = n + z * (hp[i][e] - n);
       const size_t o = (size_t)b * H + u;
-      a.h_f[o] = h;
+      const std::integral_constant<bool, NT> nt{};
+      save_st(a.h_f + o, h, nt);
       const u16 hb = f2bf(h);
       a.h_bf[o] = hb;
-      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+      if (a.sr) { save_st(a.sr + o, r, nt); save_st(a.sz + o, z, nt); save_st(a.sn + o, n, nt); save_st(a.sghn + o, ghn, nt); }
       st[rr * 32 + wn * 16 + lr] = hb;
     }
   if (a.hT) {
@@ -213,6 +218,147 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
       *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
           *reinterpret_cast<const uint4*>(v);
     }
+  }
+}
+
+// 8-wave forward (A/B switch GK_FWD_LDS8=1): the same 128 x 96 tile, but two wave groups split
+// every 64-deep k-tile by its two 32-deep k-steps (group g does k-step g), as the 8-wave backward
+// kernel does: each wave issues half the LDS-DMA pieces and half the MFMAs, and two waves share a
+// SIMD.  Group 1's partial accumulators join group 0's through LDS; group 0 runs the epilogue.
+// 28 DMA pieces per k-tile: waves 0-3 issue 4, waves 4-7 issue 3 plus a duplicate of their first
+// (same source, same LDS bytes), so every wave's vmcnt arithmetic counts 4 per k-tile.
+template <int NS>
+__global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
+  const int H = a.H;
+  const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 128;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = w >> 2, wl = w & 3;
+  const int wm = wl >> 1, wn = wl & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+  const int u = j0 + wn * 16 + lr;
+
+  float gi[4][4][3], bh[3], hp[4][4];
+  if (grp == 0) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * H + u];
+    const float* src[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) src[i][e] = a.Gi + (size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * 3 * H;
+    if (a.ids) {
+      const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int4 v = id4[i * 4];
+        src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
+        src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+  }
+
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // piece p (image rows 8p..8p+7): A rows (h_{t-1}) for p < 16, B rows (W_hh gate rows) after
+  const u16* src[4];
+  int dst[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int p = w + 8 * q;
+    if (p >= 28) p = w;                       // waves 4-7: duplicate of the first piece
+    const int r = p * 8 + srow;
+    if (p < 16) {
+      src[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
+    } else {
+      const int rb = r - 128;
+      src[q] = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + swz(rb, sslot) * 8;
+    }
+    dst[q] = p * 8 * 64;
+  }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][dst[q]]), 16, 0, 0);
+  };
+  ring_loop<NS, 4>(H / 64, stage, [&](int cur) {
+    const u16* LA = lds[cur];
+    const u16* LB = lds[cur] + 128 * 64;
+    const int c = grp * 4 + lq;
+    bf16x8 af[4], bfr[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wm * 64 + i * 16 + lr;
+      af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const int r = g * 32 + wn * 16 + lr;
+      bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
+  });
+  // group 1 -> LDS -> group 0 (ring_loop ended with a barrier: the ring is free)
+  f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);   // [4 waves][12 tiles][64 lanes] = 48 KiB
+  if (grp == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) red[(wl * 12 + i * 3 + g) * 64 + lane] = acc[i][g];
+  }
+  __syncthreads();
+  u16* st = lds[NS - 1];     // [128 rows][32 units]; NS >= 3 keeps it clear of the 48 KiB above
+  if (grp == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) acc[i][g] += red[(wl * 12 + i * 3 + g) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = wm * 64 + i * 16 + lq * 4 + e;
+        const int b = b0 + rr;
+        const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
+        const float r = sigmoidf_(gi[i][e][0] + ghr);
+        const float z = sigmoidf_(gi[i][e][1] + ghz);
+        const float n = tanhf_(gi[i][e][2] + r * ghn);
+        const float h = n + z * (hp[i][e] - n);
+        const size_t o = (size_t)b * H + u;
+        a.h_f[o] = h;
+        const u16 hb = f2bf(h);
+        a.h_bf[o] = hb;
+        if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+        st[rr * 32 + wn * 16 + lr] = hb;
+      }
+  }
+  if (a.hT) {
+    __syncthreads();
+    // 32 units x 128 rows: 512 x 16-B pieces, 1 per thread
+    const int q = threadIdx.x;
+    const int unit = q >> 4, seg = q & 15;
+    u16 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
+    *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
+        *reinterpret_cast<const uint4*>(v);
   }
 }
 
@@ -621,9 +767,14 @@ constexpr int SKNS = 4;                       // LDS ring: 4 x 32 KiB
 constexpr unsigned kSkSpinLimit = 1u << 21;   // x s_sleep(1): far beyond any real wait
 }
 
-template <int S>
+// NS: LDS ring depth (4 x 32 KiB; 5 fills the 160 KiB LDS: A/B switch GK_BWD_SK_NS=5).
+// PF (default): the epilogue's fp32 operands (dy, carry, saves, h_{t-1}) are loaded before the K
+// loop, so their latency hides under it instead of following the split-K exchange (h2048 step
+// 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl; GK_BWD_SK_PF=0 reverts).
+template <int S, int NS = SKNS, bool PF = false>
 __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[SKNS][256 * 64];
+  static_assert(!PF || S == 4, "prefetch holds one epilogue quarter");
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][256 * 64];
   const int H = a.H, H3 = 3 * a.H;
   // block -> (tile, split): the S splits of a tile are 8 blocks apart (one XCD under the
   // dispatcher's round-robin placement: a speed choice, the exchange does not depend on it)
@@ -644,6 +795,25 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // epilogue element (quarter qq, piece pp, row e) -> offset into the [Bp][H] operands
+  auto epi_off = [&](int qq, int pp, int e) {
+    const int sq = split + S * qq, P = w + 8 * pp;
+    const int wnp = P >> 2, ii = (P >> 1) & 1, jn = P & 1;
+    const int b = b0 + 32 * sq + ii * 16 + lq * 4 + e;
+    return (size_t)b * H + j0 + wnp * 32 + jn * 16 + lr;
+  };
+  float pre[PF ? 2 : 1][4][6];
+  if constexpr (PF) {
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const size_t o = epi_off(0, pp, e);
+        pre[pp][e][0] = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f);
+        pre[pp][e][1] = a.r[o]; pre[pp][e][2] = a.z[o]; pre[pp][e][3] = a.n[o];
+        pre[pp][e][4] = a.hprev[o]; pre[pp][e][5] = a.ghn[o];
+      }
+  }
   const sk_rsrc_t rP = sk_rsrc(a.sk_part, (unsigned)(a.sk_part_floats * 4));
   const size_t tile_base = (size_t)tile * S * PIECE;   // f32x4 units
   if (kloop) {
@@ -662,7 +832,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
       for (int q = 0; q < 4; ++q)
         __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(4 * w + q) * 8 * 64]), 16, 0, 0);
     };
-    ring_loop<SKNS, 4>(nk, stage, [&](int cur) {
+    ring_loop<NS, 4>(nk, stage, [&](int cur) {
       const u16* LA = lds[cur];
       const u16* LB = lds[cur] + 128 * 64;
 #pragma unroll
@@ -739,12 +909,18 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
         const int rq = ii * 16 + lq * 4 + e;    // row within the quarter
         const int b = b0 + 32 * sq + rq;
         const size_t o = (size_t)b * H + j;
-        const float dh = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f) + ps[e];
-        const float r = a.r[o], z = a.z[o], n = a.n[o];
+        float dh, r, z, n, hp, ghn;
+        if constexpr (PF) {
+          dh = pre[pp][e][0] + ps[e]; r = pre[pp][e][1]; z = pre[pp][e][2]; n = pre[pp][e][3];
+          hp = pre[pp][e][4]; ghn = pre[pp][e][5];
+        } else {
+          dh = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f) + ps[e];
+          r = a.r[o]; z = a.z[o]; n = a.n[o]; hp = a.hprev[o]; ghn = a.ghn[o];
+        }
         const float dn = dh * (1.f - z);
-        const float dz = dh * (a.hprev[o] - n);
+        const float dz = dh * (hp - n);
         const float dan = dn * (1.f - n * n);
-        const float dar = dan * a.ghn[o] * r * (1.f - r);
+        const float dar = dan * ghn * r * (1.f - r);
         const float daz = dz * z * (1.f - z);
         a.carry_out[o] = z * dh;
         const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
@@ -799,6 +975,20 @@ int gru_bwd_step_sk_splits(int H, int Bp) {
   return 0;
 }
 
+StepLdsVariants& step_lds_variants() {
+  static StepLdsVariants v = [] {
+    StepLdsVariants d;
+    auto env = [](const char* name, int& f) { if (const char* e = std::getenv(name)) f = std::atoi(e); };
+    env("GK_STEP_LDS_NS", d.fwd_ns);
+    env("GK_STEP_NT", d.fwd_nt);
+    env("GK_FWD_LDS8", d.fwd8);
+    env("GK_BWD_SK_NS", d.bwd_sk_ns);
+    env("GK_BWD_SK_PF", d.bwd_sk_pf);
+    return d;
+  }();
+  return v;
+}
+
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
@@ -815,9 +1005,25 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
     return;
   }
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);
+  const StepLdsVariants& v = step_lds_variants();
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
-  if (const char* e = std::getenv("GK_STEP_LDS_NS")) ns = std::atoi(e) == 2 ? 2 : 4;
-  if (ns == 2) {
+  if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : v.fwd_ns == 5 ? 5 : 4;
+  const bool nt = v.fwd_nt != 0, eight = v.fwd8 != 0;
+  if (ns != 2 && !a.x_bf && eight) {
+    if (ns == 5) hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<5>, grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<FNS>, grid, dim3(512), 0, s, a);
+    return;
+  }
+  if (ns != 2 && !a.x_bf && nt) {
+    if (ns == 5) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 5, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, FNS, true>), grid, block, 0, s, a);
+    return;
+  }
+  if (ns == 5) {
+    // 5-deep ring (140 KiB): four k-tiles in flight instead of three
+    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 5>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 5>), grid, block, 0, s, a);
+  } else if (ns == 2) {
     if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 2>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 2>), grid, block, 0, s, a);
   } else {
@@ -829,7 +1035,13 @@ void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
   if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
-      if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
+      const StepLdsVariants& v = step_lds_variants();
+      const int ns = v.bwd_sk_ns == 5 ? 5 : SKNS;
+      const bool pf = v.bwd_sk_pf != 0;
+      if (S == 4 && ns == 5 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5, true>), dim3(tiles * 4), dim3(512), 0, s, a);
+      else if (S == 4 && ns == 5) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5>), dim3(tiles * 4), dim3(512), 0, s, a);
+      else if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, a);
+      else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
       else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, a);
       return;
     }

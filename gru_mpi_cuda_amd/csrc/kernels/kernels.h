@@ -65,6 +65,17 @@ void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
 // split-K count the backward LDS step kernel would use for (H, Bp): 0 = the 64 x 64 kernel;
 // workspace: H * Bp * splits fp32 partials, (H/128)(Bp/128) * 16 counter words
 int gru_bwd_step_sk_splits(int H, int Bp);
+// Large-H step-kernel variants (gru_step_lds.hip).  Initialised from the environment (GK_STEP_LDS_NS,
+// GK_STEP_NT, GK_FWD_LDS8, GK_BWD_SK_NS, GK_BWD_SK_PF) on first use; settable at run time so the
+// kernel tests cover every variant in one process.  0 / -1 fields mean "automatic".
+struct StepLdsVariants {
+  int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4, 5
+  int fwd_nt = 0;        // forward saves with nontemporal stores
+  int fwd8 = 0;          // 8-wave forward (two wave groups split each k-tile)
+  int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
+  int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
+};
+StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
 bool gru_step_lds_ok(int H, int Bp);
 // which per-step kernel gru_fwd_step/gru_bwd_step pick for (algo, H, Bp) without fused input

@@ -211,6 +211,31 @@ def test_bwd_step(ext, first, H, Bp, algo, sk):
     torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
 
 
+@pytest.fixture
+def step_variants(ext):
+    saved = ext.step_lds_variants()
+    yield ext
+    ext.set_step_lds_variants(saved)
+
+
+# large-H step-kernel variants (StepLdsVariants in kernels.h): each against the same fp32 reference
+@pytest.mark.parametrize("var", [dict(fwd8=1), dict(fwd8=1, fwd_ns=5), dict(fwd_ns=5), dict(fwd_nt=1),
+                                 dict(fwd8=0, fwd_ns=4, fwd_nt=0)])
+@pytest.mark.parametrize("H,Bp", [(1024, 256), (2048, 512)])
+@pytest.mark.parametrize("mode", ["table", "gi"])
+def test_fwd_step_variants(step_variants, mode, H, Bp, var):
+    step_variants.set_step_lds_variants(var)
+    test_fwd_step(step_variants, mode, H, Bp, 2)
+
+
+@pytest.mark.parametrize("var", [dict(bwd_sk_pf=1, bwd_sk_ns=4), dict(bwd_sk_pf=0, bwd_sk_ns=4),
+                                 dict(bwd_sk_pf=1, bwd_sk_ns=5), dict(bwd_sk_pf=0, bwd_sk_ns=5)])
+@pytest.mark.parametrize("first", [False, True])
+def test_bwd_step_sk_variants(step_variants, first, var):
+    step_variants.set_step_lds_variants(var)
+    test_bwd_step(step_variants, first, 2048, 512, 2, 1)
+
+
 @pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256"])
 @pytest.mark.parametrize("H", [256, 320, 512, 1024])
 def test_fc_xent(ext, mode, H):
