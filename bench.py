@@ -47,6 +47,8 @@ def main() -> int:
                     help="at 1 GPU, still record the gradient collectives (1-rank RCCL communicator) "
                          "to time the data-parallel step structure")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--shard-optim", action="store_true",
+                    help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -80,6 +82,8 @@ def main() -> int:
         cfg = cfg.replace(overlap=True)
     if args.bucket_mb:
         cfg = cfg.replace(bucket_mb=args.bucket_mb)
+    if args.shard_optim:
+        cfg = cfg.replace(shard_optim=True)
 
     stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
     pool = [stream.next() for _ in range(8)]
@@ -139,7 +143,7 @@ def main() -> int:
                        "global_batch": cfg.batch, "seq_len": cfg.seq,
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
-                       "overlap": cfg.overlap, "plan": plan,
+                       "overlap": cfg.overlap, "plan": plan, "shard_optim": cfg.shard_optim,
                        "collectives": (len(tr.t.allreduce_log()) if args.impl == "hip" and comm is not None
                                        and hasattr(tr, "t") else 0)},
             "rccl_ranks": comm.count() if comm is not None else (world if ctx.backend != "none" else 1),

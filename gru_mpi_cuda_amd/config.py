@@ -48,6 +48,8 @@ class GRUConfig:
                                 # previous step's final (detached) hidden state
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
+    shard_optim: bool = False   # data-parallel ZeRO-1 step: reduce-scatter the gradient, Adam on the
+                                # owned 1/world slice, all-gather the fp32 masters (Trainer::set_shard_optim)
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
     overlap: bool = False       # True: chunked side-stream schedule; False: single stream built on
                                 # the persistent sequence kernels (faster on MI355X, profiles/)

@@ -114,6 +114,10 @@ PYBIND11_MODULE(_C, m) {
       .def("uses_persistent", &Trainer::uses_persistent)
       .def("read_error", &Trainer::read_error)
       .def("enable_watchdog", &Trainer::enable_watchdog)
+      .def("set_shard_optim", &Trainer::set_shard_optim)
+      .def("shard_optim", &Trainer::shard_optim)
+      .def("shard_chunk", &Trainer::shard_chunk)
+      .def("gather_opt_state", [](Trainer& t, uintptr_t s) { t.gather_opt_state(S(s)); })
       .def("inject_error", &Trainer::inject_error)
       .def("watchdog_status", &Trainer::watchdog_status)
       .def("watchdog_message", &Trainer::watchdog_message)

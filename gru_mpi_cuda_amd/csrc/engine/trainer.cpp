@@ -184,6 +184,7 @@ Trainer::~Trainer() {
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
   if (sc_) (void)hipStreamDestroy(sc_);
+  if (gshard_) (void)hipFree(gshard_);
 }
 
 hipEvent_t Trainer::ev() {
@@ -470,17 +471,69 @@ void Trainer::record_fb(hipStream_t s0) {
   HIP_LAUNCH_CHECK();
 }
 
-void Trainer::record_opt(hipStream_t s) {
-  if (o_.clip > 0.f) {
-    sumsq_partials(grads_, nflat_, norm_parts_, 256, s);
-    clip_scale_finalize(norm_parts_, 256, o_.clip, gscale_, s);
-  }
+OptimArgs Trainer::optim_args() const {
   OptimArgs a;
   a.p = params_; a.g = grads_; a.m = m_; a.v = v_; a.n = nflat_; a.step = step_;
   a.gscale = o_.clip > 0.f ? gscale_ : nullptr;
   a.err = err_; a.err_host = err_host_dev_;
   a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
   a.sched = o_.sched; a.warmup = o_.warmup; a.total = o_.total; a.lr_min = o_.lr_min;
+  return a;
+}
+
+void Trainer::set_shard_optim(bool on) {
+  if (on && !comm_) throw std::runtime_error("set_shard_optim: needs a communicator (call set_comm first)");
+  if (on && o_.clip > 0.f)
+    throw std::runtime_error("set_shard_optim: gradient clipping needs the global norm; not supported sharded");
+  if (on && nflat_ % 4) throw std::runtime_error("set_shard_optim: flat parameter count must be a multiple of 4");
+  shard_opt_ = on;
+  if (on) {
+    const int W = comm_->world();
+    shard_chunk_ = nflat_ / (4L * W) * 4;
+    if (gshard_) { HIP_CHECK(hipFree(gshard_)); gshard_ = nullptr; }
+    HIP_CHECK(hipMalloc(&gshard_, sizeof(float) * (size_t)std::max(4L, shard_chunk_)));
+  }
+  g_step_[0].reset();
+  g_step_[1].reset();
+}
+
+void Trainer::record_sharded_opt(hipStream_t s) {
+  const int r = comm_->rank(), W = comm_->world();
+  const long c = shard_chunk_, tail = nflat_ - (long)W * c;
+  ar_log_.clear();
+  if (c > 0) comm_->reduce_scatter_avg_f32(grads_, gshard_, c, s);
+  if (tail > 0) {
+    comm_->allreduce_avg_f32(grads_ + (long)W * c, tail, s);
+    ar_log_.push_back({(long)W * c, tail});
+  }
+  OptimArgs a = optim_args();
+  if (c > 0) {
+    a.p = params_ + (long)r * c; a.g = gshard_; a.m = m_ + (long)r * c; a.v = v_ + (long)r * c; a.n = c;
+    adam_step(a, s);
+  }
+  if (tail > 0) {   // every rank updates the (identical) tail
+    const long o = (long)W * c;
+    a.p = params_ + o; a.g = grads_ + o; a.m = m_ + o; a.v = v_ + o; a.n = tail;
+    adam_step(a, s);
+  }
+  if (c > 0 && W > 1) comm_->allgather_f32(params_ + (long)r * c, params_, c, s);   // in place
+  refresh_weights(s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::gather_opt_state(hipStream_t s) {
+  if (!shard_opt_ || !comm_ || comm_->world() == 1 || shard_chunk_ == 0) return;
+  const long c = shard_chunk_, o = (long)comm_->rank() * c;
+  comm_->allgather_f32(m_ + o, m_, c, s);
+  comm_->allgather_f32(v_ + o, v_, c, s);
+}
+
+void Trainer::record_opt(hipStream_t s) {
+  if (o_.clip > 0.f) {
+    sumsq_partials(grads_, nflat_, norm_parts_, 256, s);
+    clip_scale_finalize(norm_parts_, 256, o_.clip, gscale_, s);
+  }
+  OptimArgs a = optim_args();
   const int V = d_.V, E = d_.E, H = d_.H;
   if (V % 64 == 0 && E % 64 == 0 && H % 64 == 0) {
     // one launch: update every tensor and write its bf16 (+ transposed) MFMA copies from the
@@ -558,6 +611,7 @@ void Trainer::optimizer_step(hipStream_t s) {
 
 void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets, long min_bucket_floats) {
   comm_ = c;
+  if (!c) shard_opt_ = false;
   buckets_ = buckets;
   min_bucket_ = std::max(1L, min_bucket_floats);
   // the overlapped path relies on the readiness order of the flat layout (models/params.py)
@@ -643,7 +697,13 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
-      if (dp_overlap()) {
+      if (shard_opt_) {
+        // sharded optimiser: whole backward first (slab sums into the flat gradient), then
+        // reduce-scatter -> Adam on the owned slice -> all-gather -> bf16 refresh
+        deferred_.n = 0;
+        if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+        record_sharded_opt(s0_);
+      } else if (dp_overlap()) {
         // readiness-ordered collectives on the comm stream, overlapped with the rest of the
         // backward; joined before the optimiser (the embedding-side tail runs after the join)
         deferred_.n = 0;
@@ -655,7 +715,7 @@ void Trainer::step(hipStream_t s) {
         defer_slabs_ = false;
         record_allreduce(s0_);
       }
-      record_opt(s0_);
+      if (!shard_opt_) record_opt(s0_);
     } catch (...) {
       defer_slabs_ = false;
       deferred_.n = 0;

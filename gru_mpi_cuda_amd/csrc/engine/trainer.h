@@ -125,12 +125,27 @@ class Trainer {
   long min_bucket_ = 0, ar_ready_ = 0, ar_launched_ = 0;
   bool ar_busy_ = false, dP_inplace_ = false;
   std::vector<std::pair<long, long>> ar_log_;   // (offset, floats) of every recorded collective
+  // sharded optimiser (set_shard_optim)
+  bool shard_opt_ = false;
+  long shard_chunk_ = 0;
+  float* gshard_ = nullptr;          // this rank's reduce-scattered gradient slice [shard_chunk_]
+  void record_sharded_opt(hipStream_t s);
+  OptimArgs optim_args() const;
  public:
   void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
   // buckets: plain bucket list; min_bucket_floats: smallest collective of the overlapped path
   void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets, long min_bucket_floats);
   // collectives recorded into the last captured step graph (tests / plan printing)
   const std::vector<std::pair<long, long>>& allreduce_log() const { return ar_log_; }
+  // Sharded optimiser step (ZeRO-1 style, data-parallel only; call after set_comm).  The step graph
+  // reduce-scatters the flat fp32 gradient (rank r owns floats [r*c, (r+1)*c), c = a multiple of 4;
+  // the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the fp32 masters and
+  // moments, all-gathers the updated masters in place and refreshes the bf16 MFMA copies.  Moments
+  // outside the owned slice go stale: gather_opt_state() all-gathers them (checkpoints).
+  void set_shard_optim(bool on);
+  bool shard_optim() const { return shard_opt_; }
+  long shard_chunk() const { return shard_chunk_; }
+  void gather_opt_state(hipStream_t s);
   void step(hipStream_t s);      // whole training step as one graph replay
   // test hook: set the device step error word (fault injection)
   void inject_error(unsigned bits) { HIP_CHECK(hipMemcpy(err_, &bits, 4, hipMemcpyHostToDevice)); }

@@ -221,7 +221,8 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
   }
 }
 
-// 8-wave forward (A/B switch GK_FWD_LDS8=1): the same 128 x 96 tile, but two wave groups split
+// 8-wave forward (default; GK_FWD_LDS8=0 reverts; h2048 step 9.84 -> 9.75-9.78 ms,
+// profiles/r2_h2048_fwd8_ab.jsonl): the same 128 x 96 tile, but two wave groups split
 // every 64-deep k-tile by its two 32-deep k-steps (group g does k-step g), as the 8-wave backward
 // kernel does: each wave issues half the LDS-DMA pieces and half the MFMAs, and two waves share a
 // SIMD.  Group 1's partial accumulators join group 0's through LDS; group 0 runs the epilogue.

@@ -75,6 +75,8 @@ class HipTrainer:
             # bucket_mb on a comm stream, overlapped with the rest of the backward
             self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets],
                             max(1024, int(cfg.bucket_mb * (1 << 20) / 4)))
+            if cfg.shard_optim:
+                self.t.set_shard_optim(True)
         self.t.refresh_weights(self._stream())
         self._one_graph = True
         # host thread watching each launched step, the communicator and the step
@@ -177,7 +179,10 @@ class HipTrainer:
         self.t.refresh_weights(self._stream())
 
     def opt_state(self):
-        """Adam moments as flat fp32 tensors in the user config's layout (checkpoints)."""
+        """Adam moments as flat fp32 tensors in the user config's layout (checkpoints).  Sharded
+        optimiser: every rank first all-gathers the moment slices the other ranks own."""
+        if self.t.shard_optim():
+            self.t.gather_opt_state(self._stream())
         torch.cuda.synchronize(self.dev)
         return tuple(to_flat(self.cfg, self._unpad(from_flat(self.icfg, t.cpu()))) for t in (self.m, self.v))
 
@@ -203,7 +208,18 @@ class CpuTrainer:
         if self.ctx.world > 1:          # identical replicas
             import torch.distributed as dist
             dist.broadcast(self.flat_p, 0)
-        self.opt = cpu_ref.Adam(cfg, self.params)
+        self.shard = None
+        if cfg.shard_optim and self.ctx.world > 1:
+            # ZeRO-1 twin of Trainer::set_shard_optim: rank r owns flat floats [r*c, (r+1)*c) with c a
+            # multiple of 4; the tail past world*c is updated by every rank
+            if cfg.clip_norm > 0:
+                raise ValueError("shard_optim: gradient clipping is not supported with a sharded optimiser")
+            W, r, n = self.ctx.world, self.ctx.rank, self.layout.total
+            c = n // (4 * W) * 4
+            self.shard = (c, {"own": slice(r * c, (r + 1) * c), "tail": slice(W * c, n)})
+            self.opt = cpu_ref.Adam(cfg, {k: self.flat_p[sl] for k, sl in self.shard[1].items()})
+        else:
+            self.opt = cpu_ref.Adam(cfg, self.params)
         self.buckets = _bucket_list(cfg, self.layout.total)
         self._loss = float("nan")
         self._state = None            # carried hidden state (cfg.carry_hidden)
@@ -226,7 +242,15 @@ class CpuTrainer:
         allreduce_mean_buckets(self.flat_g, self.buckets, self.ctx.world)
 
     def optimizer_step(self) -> None:
-        self.opt.step(self.params, self.gviews)
+        if self.shard is None:
+            self.opt.step(self.params, self.gviews)
+            return
+        import torch.distributed as dist
+        c, sl = self.shard
+        self.opt.step({k: self.flat_p[v] for k, v in sl.items()}, {k: self.flat_g[v] for k, v in sl.items()})
+        if c:
+            parts = list(self.flat_p[:self.ctx.world * c].view(self.ctx.world, c).unbind(0))
+            dist.all_gather(parts, self.flat_p[sl["own"]].clone())
 
     def step(self, x, y) -> None:
         self.forward_backward(x, y)

@@ -103,6 +103,47 @@ def test_dp_training_equals_single_rank(tmp_path, world):
         torch.testing.assert_close(a[k], b[k], atol=1e-4, rtol=1e-4)
 
 
+def _shard_worker(rank, world, port, outdir, steps, shard):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=12, hidden=20, layers=2, batch=12, seq=5, lr=1e-2, shard_optim=shard)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1))
+    if shard:
+        c = tr.shard[0]
+        assert c % 4 == 0 and c * world <= tr.layout.total < (c + 4) * world
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    per = cfg.batch // world
+    for _ in range(steps):
+        x, y = ds.next()
+        tr.step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    torch.save(tr.state_dict(), os.path.join(outdir, f"s{int(shard)}_{world}_r{rank}.pt"))
+    gdist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_optimizer_equals_replicated(tmp_path, world):
+    """ZeRO-1 step (cfg.shard_optim; the CPU twin of Trainer::set_shard_optim): Adam on the owned
+    1/world slice + tail, then an all-gather of the masters, is bitwise the replicated step, and every
+    rank ends with the same weights.  world 3 leaves a non-empty tail."""
+    ctx = mp.get_context("spawn")
+    for shard in (False, True):
+        port = _free_port()
+        procs = [ctx.Process(target=_shard_worker, args=(r, world, port, str(tmp_path), 3, shard))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(180)
+            assert p.exitcode == 0
+    ref = torch.load(tmp_path / f"s0_{world}_r0.pt", weights_only=True)
+    for r in range(world):
+        got = torch.load(tmp_path / f"s1_{world}_r{r}.pt", weights_only=True)
+        for k in ref:
+            assert torch.equal(ref[k], got[k]), (r, k)
+
+
 def test_shard_and_buckets():
     from gru_mpi_cuda_amd.parallel.dist import shard, bucket_bounds
     for n in (0, 1, 7, 37, 64):

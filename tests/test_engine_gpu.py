@@ -290,6 +290,37 @@ def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("layers,E,H,opt", [(1, 512, 512, "adam"), (2, 128, 256, "adam"), (1, 256, 256, "sgd")])
+def test_sharded_optimizer_step_world1(layers, E, H, opt):
+    """ZeRO-1 step (Trainer::set_shard_optim) on a 1-rank communicator: reduce-scatter (a copy),
+    Adam on the owned slice (= everything), in-place all-gather skipped, bf16 refresh -- must
+    equal the no-comm step bit for bit (same slab-sum order, same elementwise update), and
+    gather_opt_state must leave the moments intact."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=64, seq=8, seed=3, optimizer=opt,
+                    shard_optim=True)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
+    comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1)
+    a = HipTrainer(cfg, params=init_params(cfg), comm=comm)
+    b = HipTrainer(cfg.replace(shard_optim=False), params=init_params(cfg))
+    assert a.t.shard_optim() and a.t.shard_chunk() == a.layout.total // 4 * 4
+    for _ in range(3):
+        a.step(x, y)
+        b.step(x, y)
+    assert a._one_graph, "in-graph sharded step fell back"
+    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+    ma, va = a.opt_state()
+    mb, vb = b.opt_state()
+    torch.testing.assert_close(ma, mb, atol=0, rtol=0)
+    torch.testing.assert_close(va, vb, atol=0, rtol=0)
+    # the refreshed bf16 compute copies drive the next forward: equal losses
+    a.forward_backward(x, y)
+    b.forward_backward(x, y)
+    assert a.loss() == b.loss()
+
+
 def test_set_batch_device_matches_host():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=48, seq=8, seed=3)

@@ -130,6 +130,13 @@ def test_dp_two_layer_flush_path_equals_one_gpu(tmp_path):
 
 
 @needs2
+def test_dp_sharded_optimizer_equals_one_gpu(tmp_path):
+    """ZeRO-1 step at world 2 (reduce-scatter, SGD on the owned half, all-gather of the fp32
+    masters) equals one GPU on the whole batch."""
+    _compare_dp(tmp_path, 2, dict(H512_CFG, shard_optim=True), 2e-4)
+
+
+@needs2
 def test_bench_dp_step_reports():
     n = 2
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
