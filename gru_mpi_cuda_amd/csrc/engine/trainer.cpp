@@ -184,7 +184,6 @@ Trainer::~Trainer() {
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
   if (sc_) (void)hipStreamDestroy(sc_);
-  if (gshard_) (void)hipFree(gshard_);
 }
 
 hipEvent_t Trainer::ev() {
@@ -490,8 +489,8 @@ void Trainer::set_shard_optim(bool on) {
   if (on) {
     const int W = comm_->world();
     shard_chunk_ = nflat_ / (4L * W) * 4;
-    if (gshard_) { HIP_CHECK(hipFree(gshard_)); gshard_ = nullptr; }
-    HIP_CHECK(hipMalloc(&gshard_, sizeof(float) * (size_t)std::max(4L, shard_chunk_)));
+    if ((long)W * shard_chunk_ > 0 && shard_chunk_ > (1L << 30))
+      throw std::runtime_error("set_shard_optim: shard too large for one optimiser job");
   }
   g_step_[0].reset();
   g_step_[1].reset();
@@ -501,21 +500,18 @@ void Trainer::record_sharded_opt(hipStream_t s) {
   const int r = comm_->rank(), W = comm_->world();
   const long c = shard_chunk_, tail = nflat_ - (long)W * c;
   ar_log_.clear();
-  if (c > 0) comm_->reduce_scatter_avg_f32(grads_, gshard_, c, s);
+  // in-place reduce-scatter: the owned slice's mean lands at grads_ + r*c, where Adam reads it
+  if (c > 0) comm_->reduce_scatter_avg_f32(grads_, grads_ + (long)r * c, c, s);
   if (tail > 0) {
     comm_->allreduce_avg_f32(grads_ + (long)W * c, tail, s);
     ar_log_.push_back({(long)W * c, tail});
   }
-  OptimArgs a = optim_args();
-  if (c > 0) {
-    a.p = params_ + (long)r * c; a.g = gshard_; a.m = m_ + (long)r * c; a.v = v_ + (long)r * c; a.n = c;
-    adam_step(a, s);
-  }
-  if (tail > 0) {   // every rank updates the (identical) tail
-    const long o = (long)W * c;
-    a.p = params_ + o; a.g = grads_ + o; a.m = m_ + o; a.v = v_ + o; a.n = tail;
-    adam_step(a, s);
-  }
+  // the fused optimiser launch's flat path (same update code as the replicated step), no casts:
+  // the bf16 copies are refreshed from the gathered masters below
+  OptCastJobs j;
+  if (c > 0) j.add((long)r * c, 0, (int)c, nullptr, nullptr);
+  if (tail > 0) j.add((long)W * c, 0, (int)tail, nullptr, nullptr);   // every rank: the same tail
+  if (j.n) adam_cast_multi(optim_args(), j, s);
   if (c > 0 && W > 1) comm_->allgather_f32(params_ + (long)r * c, params_, c, s);   // in place
   refresh_weights(s);
   HIP_LAUNCH_CHECK();

@@ -128,7 +128,6 @@ class Trainer {
   // sharded optimiser (set_shard_optim)
   bool shard_opt_ = false;
   long shard_chunk_ = 0;
-  float* gshard_ = nullptr;          // this rank's reduce-scattered gradient slice [shard_chunk_]
   void record_sharded_opt(hipStream_t s);
   OptimArgs optim_args() const;
  public:
@@ -138,8 +137,8 @@ class Trainer {
   // collectives recorded into the last captured step graph (tests / plan printing)
   const std::vector<std::pair<long, long>>& allreduce_log() const { return ar_log_; }
   // Sharded optimiser step (ZeRO-1 style, data-parallel only; call after set_comm).  The step graph
-  // reduce-scatters the flat fp32 gradient (rank r owns floats [r*c, (r+1)*c), c = a multiple of 4;
-  // the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the fp32 masters and
+  // reduce-scatters the flat fp32 gradient in place (rank r owns floats [r*c, (r+1)*c), c a multiple
+  // of 4; the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the masters and
   // moments, all-gathers the updated masters in place and refreshes the bf16 MFMA copies.  Moments
   // outside the owned slice go stale: gather_opt_state() all-gathers them (checkpoints).
   void set_shard_optim(bool on);

@@ -228,7 +228,10 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
 // SIMD.  Group 1's partial accumulators join group 0's through LDS; group 0 runs the epilogue.
 // 28 DMA pieces per k-tile: waves 0-3 issue 4, waves 4-7 issue 3 plus a duplicate of their first
 // (same source, same LDS bytes), so every wave's vmcnt arithmetic counts 4 per k-tile.
-template <int NS>
+// SE (split epilogue, fwd8 = 2): the groups swap half of their partial tiles instead of group 1
+// handing all of them over, and each runs the epilogue for its two 16-row fragments (i = 2 grp,
+// 2 grp + 1) -- eight waves store the outputs instead of four.
+template <int NS, bool SE = false>
 __global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
   const int H = a.H;
@@ -240,13 +243,16 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a
   const int u = j0 + wn * 16 + lr;
 
   float gi[4][4][3], bh[3], hp[4][4];
-  if (grp == 0) {
+  // fragment i's epilogue runs in group 0, or (SE) in group i / 2
+  auto own = [&](int i) { return SE ? (i >> 1) == grp : grp == 0; };
+  if (SE || grp == 0) {
 #pragma unroll
     for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+      if (own(i))
 #pragma unroll
-      for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * H + u];
+        for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * H + u];
     const float* src[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -255,18 +261,20 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a
     if (a.ids) {
       const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int4 v = id4[i * 4];
-        src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
-        src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
-      }
+      for (int i = 0; i < 4; ++i)
+        if (own(i)) {
+          const int4 v = id4[i * 4];
+          src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
+          src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
+        }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+      if (own(i))
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+          for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
   }
 
   f32x4 acc[4][3];
@@ -317,22 +325,24 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a
       for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
   });
   // group 1 -> LDS -> group 0 (ring_loop ended with a barrier: the ring is free)
-  f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);   // [4 waves][12 tiles][64 lanes] = 48 KiB
-  if (grp == 1) {
+  // [4 waves][12 tiles][64 lanes] = 48 KiB; fragment i's tile of wave wl sits at (wl*12 + 3i + g)
+  f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i)
+    if (!own(i))
 #pragma unroll
       for (int g = 0; g < 3; ++g) red[(wl * 12 + i * 3 + g) * 64 + lane] = acc[i][g];
-  }
   __syncthreads();
   u16* st = lds[NS - 1];     // [128 rows][32 units]; NS >= 3 keeps it clear of the 48 KiB above
-  if (grp == 0) {
+  if (SE || grp == 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+      if (own(i))
 #pragma unroll
-      for (int g = 0; g < 3; ++g) acc[i][g] += red[(wl * 12 + i * 3 + g) * 64 + lane];
+        for (int g = 0; g < 3; ++g) acc[i][g] += red[(wl * 12 + i * 3 + g) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
+      if (own(i))
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rr = wm * 64 + i * 16 + lq * 4 + e;
@@ -1011,7 +1021,8 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : v.fwd_ns == 5 ? 5 : 4;
   const bool nt = v.fwd_nt != 0, eight = v.fwd8 != 0;
   if (ns != 2 && !a.x_bf && eight) {
-    if (ns == 5) hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<5>, grid, dim3(512), 0, s, a);
+    if (v.fwd8 == 2) hipLaunchKernelGGL((gru_fwd_step_lds8_kernel<FNS, true>), grid, dim3(512), 0, s, a);
+    else if (ns == 5) hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<5>, grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<FNS>, grid, dim3(512), 0, s, a);
     return;
   }

@@ -71,7 +71,8 @@ int gru_bwd_step_sk_splits(int H, int Bp);
 struct StepLdsVariants {
   int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4, 5
   int fwd_nt = 0;        // forward saves with nontemporal stores
-  int fwd8 = 1;          // 8-wave forward (two wave groups split each k-tile; 0 = 4-wave kernel)
+  int fwd8 = 2;          // 8-wave forward (two wave groups split each k-tile): 2 = split epilogue,
+                         // 1 = group 0 runs the whole epilogue, 0 = the 4-wave kernel
   int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
 };

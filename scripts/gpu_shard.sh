@@ -2,7 +2,7 @@
 # Sharded optimiser (ZeRO-1) on one GPU: engine tests on a 1-rank communicator, then the step cost
 # of the data-parallel structures (--rccl-self) with and without --shard-optim at h512 and h2048.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread -k "sharded or rccl_world1" > gpurun_out/shard_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread -k "sharded or rccl_world1" -s > gpurun_out/shard_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/shard_tests.log; [ $rc -ne 0 ] && exit $rc
 out=gpurun_out/ab_shard.jsonl; : > $out
 run() {  # tag, args...

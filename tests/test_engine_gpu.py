@@ -293,9 +293,10 @@ def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
 @pytest.mark.parametrize("layers,E,H,opt", [(1, 512, 512, "adam"), (2, 128, 256, "adam"), (1, 256, 256, "sgd")])
 def test_sharded_optimizer_step_world1(layers, E, H, opt):
     """ZeRO-1 step (Trainer::set_shard_optim) on a 1-rank communicator: reduce-scatter (a copy),
-    Adam on the owned slice (= everything), in-place all-gather skipped, bf16 refresh -- must
-    equal the no-comm step bit for bit (same slab-sum order, same elementwise update), and
-    gather_opt_state must leave the moments intact."""
+    Adam on the owned slice (= everything, through the fused launch's flat path), in-place
+    all-gather skipped, bf16 refresh -- must equal the no-comm step (same slab-sum order, same
+    update formula; allowed one-ulp-level drift where the compiler contracts the matrix and flat
+    update paths differently), and gather_opt_state must leave the moments intact."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
@@ -310,15 +311,17 @@ def test_sharded_optimizer_step_world1(layers, E, H, opt):
         a.step(x, y)
         b.step(x, y)
     assert a._one_graph, "in-graph sharded step fell back"
-    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+    d = (a.params - b.params).abs().max().item()
+    print(f"sharded vs replicated: max |diff| {d:.3g} (bitwise: {d == 0})")
+    torch.testing.assert_close(a.params, b.params, atol=1e-6, rtol=0)
     ma, va = a.opt_state()
     mb, vb = b.opt_state()
-    torch.testing.assert_close(ma, mb, atol=0, rtol=0)
-    torch.testing.assert_close(va, vb, atol=0, rtol=0)
-    # the refreshed bf16 compute copies drive the next forward: equal losses
+    torch.testing.assert_close(ma, mb, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(va, vb, atol=1e-9, rtol=1e-4)
+    # the refreshed bf16 compute copies drive the next forward
     a.forward_backward(x, y)
     b.forward_backward(x, y)
-    assert a.loss() == b.loss()
+    assert abs(a.loss() - b.loss()) < 1e-4
 
 
 def test_set_batch_device_matches_host():
