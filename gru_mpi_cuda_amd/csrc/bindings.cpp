@@ -228,7 +228,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("step_lds_variants", []() {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
-    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8;
+    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64;
     d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf;
     return d;
   });
@@ -240,6 +240,7 @@ PYBIND11_MODULE(_C, m) {
       if (k == "fwd_ns") v.fwd_ns = x;
       else if (k == "fwd_nt") v.fwd_nt = x;
       else if (k == "fwd8") v.fwd8 = x;
+      else if (k == "fwd64") v.fwd64 = x;
       else if (k == "bwd_sk_ns") v.bwd_sk_ns = x;
       else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);

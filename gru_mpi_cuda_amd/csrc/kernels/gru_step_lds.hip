@@ -221,6 +221,132 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
   }
 }
 
+// 64-row forward (default where the 128-row tile would give one workgroup per CU; GK_FWD_LDS64=0
+// reverts, 2 = 4-deep ring): tile 64 rows x 32 units x 3 gates, 4 waves of 32 rows x 16 units, a
+// 3-deep ring of 20 KiB slots, two workgroups per CU.  At B = 512, H = 2048 that is 512 workgroups:
+// twice the k-tile streams in flight per CU of the 128-row tile, for 1.4x its L2 bytes per FLOP
+// (the W_hh tile is shared by 64 rows instead of 128): h2048 step 9.72-9.74 -> 9.43-9.47 ms
+// (profiles/r2_h2048_fwd64_ab.jsonl).  Training path only (no fused input phase).
+template <int NS>
+__global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs a) {
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][(64 + 96) * 64];
+  const int H = a.H;
+  const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+  const int u = j0 + wn * 16 + lr;
+
+  float gi[2][4][3], bh[3], hp[2][4];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * H + u];
+  {
+    const float* src[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) src[i][e] = a.Gi + (size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * 3 * H;
+    if (a.ids) {
+      const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 32 + lq * 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int4 v = id4[i * 4];
+        src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
+        src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+  }
+
+  f32x4 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 20 DMA pieces per k-tile, 5 per wave: piece p = 5w + q, image rows 8p..8p+7 (A for p < 8)
+  const u16* src[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int p = 5 * w + q, r = p * 8 + srow;
+    if (p < 8) {
+      src[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
+    } else {
+      const int rb = r - 64;
+      src[q] = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + swz(rb, sslot) * 8;
+    }
+  }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(5 * w + q) * 8 * 64]), 16, 0, 0);
+  };
+  ring_loop<NS, 5>(H / 64, stage, [&](int cur) {
+    const u16* LA = lds[cur];
+    const u16* LB = lds[cur] + 64 * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + lq;
+      bf16x8 af[2], bfr[3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wm * 32 + i * 16 + lr;
+        af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+      }
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const int r = g * 32 + wn * 16 + lr;
+        bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
+    }
+  });
+
+  u16* st = lds[0];     // [64 rows][32 units]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rr = wm * 32 + i * 16 + lq * 4 + e;
+      const int b = b0 + rr;
+      const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
+      const float r = sigmoidf_(gi[i][e][0] + ghr);
+      const float z = sigmoidf_(gi[i][e][1] + ghz);
+      const float n = tanhf_(gi[i][e][2] + r * ghn);
+      const float h = n + z * (hp[i][e] - n);
+      const size_t o = (size_t)b * H + u;
+      a.h_f[o] = h;
+      const u16 hb = f2bf(h);
+      a.h_bf[o] = hb;
+      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+      st[rr * 32 + wn * 16 + lr] = hb;
+    }
+  if (a.hT) {
+    __syncthreads();
+    // 32 units x 64 rows: 256 x 16-B pieces, 1 per thread
+    const int q = threadIdx.x;
+    const int unit = q >> 3, seg = q & 7;
+    u16 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
+    *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
+        *reinterpret_cast<const uint4*>(v);
+  }
+}
+
 // 8-wave forward (default; GK_FWD_LDS8=0 reverts; h2048 step 9.84 -> 9.75-9.78 ms,
 // profiles/r2_h2048_fwd8_ab.jsonl): the same 128 x 96 tile, but two wave groups split
 // every 64-deep k-tile by its two 32-deep k-steps (group g does k-step g), as the 8-wave backward
@@ -993,6 +1119,7 @@ StepLdsVariants& step_lds_variants() {
     env("GK_STEP_LDS_NS", d.fwd_ns);
     env("GK_STEP_NT", d.fwd_nt);
     env("GK_FWD_LDS8", d.fwd8);
+    env("GK_FWD_LDS64", d.fwd64);
     env("GK_BWD_SK_NS", d.bwd_sk_ns);
     env("GK_BWD_SK_PF", d.bwd_sk_pf);
     return d;
@@ -1020,6 +1147,11 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
   if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : v.fwd_ns == 5 ? 5 : 4;
   const bool nt = v.fwd_nt != 0, eight = v.fwd8 != 0;
+  if (ns != 2 && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
+    if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<3>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
+    return;
+  }
   if (ns != 2 && !a.x_bf && eight) {
     if (v.fwd8 == 2) hipLaunchKernelGGL((gru_fwd_step_lds8_kernel<FNS, true>), grid, dim3(512), 0, s, a);
     else if (ns == 5) hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<5>, grid, dim3(512), 0, s, a);

@@ -219,8 +219,8 @@ def step_variants(ext):
 
 
 # large-H step-kernel variants (StepLdsVariants in kernels.h): each against the same fp32 reference
-@pytest.mark.parametrize("var", [dict(fwd8=1), dict(fwd8=2), dict(fwd8=1, fwd_ns=5), dict(fwd_ns=5), dict(fwd_nt=1),
-                                 dict(fwd8=0, fwd_ns=4, fwd_nt=0)])
+@pytest.mark.parametrize("var", [dict(fwd8=1, fwd64=0), dict(fwd8=2, fwd64=0), dict(fwd64=1), dict(fwd64=2), dict(fwd8=1, fwd64=0, fwd_ns=5), dict(fwd8=0, fwd64=0, fwd_ns=5), dict(fwd8=0, fwd64=0, fwd_nt=1),
+                                 dict(fwd8=0, fwd64=0, fwd_ns=4, fwd_nt=0)])
 @pytest.mark.parametrize("H,Bp", [(1024, 256), (2048, 512)])
 @pytest.mark.parametrize("mode", ["table", "gi"])
 def test_fwd_step_variants(step_variants, mode, H, Bp, var):
