@@ -99,7 +99,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   for (int l = 0; l < L; ++l)
     if (!seq_[l].bwd) sk = gru_bwd_step_sk_splits(H, B);
   sk_part_floats_ = sk ? (long)H * B * sk : 0;
-  sk_cnt_words_ = sk ? (long)(H / 128) * (B / 128) * 16 : 0;
+  sk_cnt_words_ = sk ? (long)(H / 128) * (B / 64) * 16 : 0;   // 64-row tiles (gru_bwd_step_sk64) need twice the 128-row count
   size_t o_skp = sk ? R((size_t)sk_part_floats_ * 4) : 0, o_skc = sk ? R((size_t)sk_cnt_words_ * 4) : 0;
   (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0

@@ -1085,11 +1085,169 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
   }
 }
 
-static int sk_capacity(const void* kernel) {
+// 64-row split-K backward (A/B switch GK_BWD_SK64=1; rejected: h2048 step 9.37-9.41 -> 10.04-10.05 ms,
+// profiles/r2_h2048_bwd_sk64_ab.jsonl -- unlike the forward, the split-K exchange and the
+// per-workgroup epilogue do not shrink with the tile): tile 64 rows x 128 units over a 1/4 slice of
+// K, 4 waves of 64 rows x 32 units, a 3-deep ring of 24 KiB slots, two workgroups per CU (512 at
+// B = 512, H = 2048: the 64-row forward's trade, twice the k-tile streams in flight per CU).  Same
+// exchange as the 128-row kernel: write-through fp32 partial, monotonic arrival counter, bounded
+// spin; then split s sums the four partials of 16-row group i = s in slab order and runs the
+// gate-gradient epilogue on its 16 x 128 elements (operands loaded before the K loop).
+__global__ void __launch_bounds__(256, 2) gru_bwd_step_sk64_kernel(BwdStepArgs a) {
+  constexpr int S = 4, NS = 3;
+  __shared__ __attribute__((aligned(16))) u16 lds[NS][192 * 64];
+  const int H = a.H, H3 = 3 * a.H;
+  const int bid = blockIdx.x;
+  const int split = (bid >> 3) % S, tile = (bid / (8 * S)) * 8 + (bid & 7);
+  const int ntu = H / 128;
+  const int j0 = (tile % ntu) * 128, b0 = (tile / ntu) * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;   // K loop: wave w = 64 rows x units 32w..
+  const int lr = lane & 15, lq = lane >> 4;
+  const int srow = lane >> 3, sslot = lane & 7;
+  constexpr int PIECE = 4 * 4 * 2 * 64;           // f32x4 per partial tile: [wave][i][jn][lane]
+  const bool kloop = a.dgh_next != nullptr;
+
+  // epilogue element (piece pp, row e): fragment (wave wp = P >> 1, i = split, jn = P & 1), P = w + 4 pp
+  float pre[2][4][6];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int P = w + 4 * pp, wp = P >> 1, jn = P & 1;
+      const size_t o = (size_t)(b0 + split * 16 + lq * 4 + e) * H + j0 + wp * 32 + jn * 16 + lr;
+      pre[pp][e][0] = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f);
+      pre[pp][e][1] = a.r[o]; pre[pp][e][2] = a.z[o]; pre[pp][e][3] = a.n[o];
+      pre[pp][e][4] = a.hprev[o]; pre[pp][e][5] = a.ghn[o];
+    }
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const sk_rsrc_t rP = sk_rsrc(a.sk_part, (unsigned)(a.sk_part_floats * 4));
+  const size_t tile_base = (size_t)tile * S * PIECE;
+  if (kloop) {
+    const int nk = H3 / 64 / S, kt0 = split * nk;
+    // 24 DMA pieces (8 rows x 128 B) per k-tile, 6 per wave: image rows 0..63 = A (dGh_{t+1}),
+    // 64..191 = B (W_hh^T)
+    const u16* src[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int r = (6 * w + q) * 8 + srow;
+      const int rr = r < 64 ? r : r - 64;
+      const u16* base = r < 64 ? a.dgh_next + (size_t)(b0 + rr) * H3 : a.WhhT + (size_t)(j0 + rr) * H3;
+      src[q] = base + swz(rr, sslot) * 8 + (size_t)kt0 * 64;
+    }
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(6 * w + q) * 8 * 64]), 16, 0, 0);
+    };
+    ring_loop<NS, 6>(nk, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 64 * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[4], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ra = i * 16 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int rb = w * 32 + j * 16 + lr;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    });
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const size_t o = tile_base + (size_t)split * PIECE + ((w * 4 + i) * 2 + j) * 64 + lane;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, acc[i][j]), rP, (unsigned)(o * 16), 0, 16);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* cnt = a.sk_cnt + (size_t)tile * 16;
+      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (old / S + 1) * S;
+      unsigned spins = 0;
+      while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kSkSpinLimit) {
+          if (a.err) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: rows 16 split .. 16 split + 15 of the tile; transposed staging [4 kinds][128 units][24]
+  u16* st = lds[0];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int P = w + 4 * pp, wp = P >> 1, jn = P & 1;
+    f32x4 ps = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kloop) {
+#pragma unroll
+      for (int s2 = 0; s2 < S; ++s2) {
+        const size_t o = tile_base + (size_t)s2 * PIECE + ((wp * 4 + split) * 2 + jn) * 64 + lane;
+        ps += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rP, (unsigned)(o * 16), 0, 16));
+      }
+    }
+    const int ut = wp * 32 + jn * 16 + lr;
+    const int j = j0 + ut;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int rq = lq * 4 + e;
+      const int b = b0 + 16 * split + rq;
+      const size_t o = (size_t)b * H + j;
+      const float dh = pre[pp][e][0] + ps[e], r = pre[pp][e][1], z = pre[pp][e][2], n = pre[pp][e][3];
+      const float dn = dh * (1.f - z);
+      const float dz = dh * (pre[pp][e][4] - n);
+      const float dan = dn * (1.f - n * n);
+      const float dar = dan * pre[pp][e][5] * r * (1.f - r);
+      const float daz = dz * z * (1.f - z);
+      a.carry_out[o] = z * dh;
+      const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
+      const size_t og = (size_t)b * H3 + j;
+      a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
+      if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
+      st[(0 * 128 + ut) * 24 + rq] = br;
+      st[(1 * 128 + ut) * 24 + rq] = bz;
+      st[(2 * 128 + ut) * 24 + rq] = bn;
+      st[(3 * 128 + ut) * 24 + rq] = bi;
+    }
+  }
+  __syncthreads();
+  // 4 kinds x 128 units x 16 rows = 1024 pieces of 8 rows (16 B), 4 per thread
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int q = tid + p * 256;
+    const int kind = q >> 8, rem = q & 255, unit = rem >> 1, seg = rem & 1;
+    const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 128 + unit) * 24 + seg * 8]);
+    const int g = kind < 3 ? kind : 2;
+    const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + 16 * split + seg * 8;
+    if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
+    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+  }
+}
+
+static int sk_capacity(const void* kernel, int threads = 512) {
   int dev = 0, cus = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 512, 0) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess) return 0;
   return per * cus;
 }
 
@@ -1120,6 +1278,7 @@ StepLdsVariants& step_lds_variants() {
     env("GK_STEP_NT", d.fwd_nt);
     env("GK_FWD_LDS8", d.fwd8);
     env("GK_FWD_LDS64", d.fwd64);
+    env("GK_BWD_SK64", d.bwd_sk64);
     env("GK_BWD_SK_NS", d.bwd_sk_ns);
     env("GK_BWD_SK_PF", d.bwd_sk_pf);
     return d;
@@ -1176,6 +1335,15 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   }
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
+  if (step_lds_variants().bwd_sk64 && gru_bwd_step_sk_splits(a.H, a.Bp) == 4 && a.Bp % 64 == 0) {
+    static const int cap64 = sk_capacity((const void*)gru_bwd_step_sk64_kernel, 256);
+    const int tiles = (a.H / 128) * (a.Bp / 64);
+    if (tiles % 8 == 0 && tiles * 4 <= cap64 && a.sk_part && a.sk_cnt &&
+        a.sk_part_floats >= (long)a.H * a.Bp * 4 && a.sk_cnt_words >= (long)tiles * 16) {
+      hipLaunchKernelGGL(gru_bwd_step_sk64_kernel, dim3(tiles * 4), dim3(256), 0, s, a);
+      return;
+    }
+  }
   if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {

@@ -76,6 +76,7 @@ struct StepLdsVariants {
   int fwd64 = 1;         // 64-row forward tile, two workgroups per CU (1: 3-deep ring, 2: 4-deep)
   int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
+  int bwd_sk64 = 0;      // split-K backward on 64-row tiles, two workgroups per CU
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection

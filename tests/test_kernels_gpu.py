@@ -178,7 +178,7 @@ def test_bwd_step(ext, first, H, Bp, algo, sk):
         S_ = ext.bwd_step_sk_splits(H, Bp)
         assert S_ in (2, 4), S_
         part = torch.empty(H * Bp * S_, device=DEV)
-        cnt = torch.zeros((H // 128) * (Bp // 128) * 16, device=DEV, dtype=torch.int32)
+        cnt = torch.zeros((H // 128) * (Bp // 64) * 16, device=DEV, dtype=torch.int32)
         err = torch.zeros(1, device=DEV, dtype=torch.int32)
         d.update(sk_part=part.data_ptr(), sk_part_floats=part.numel(), sk_cnt=cnt.data_ptr(),
                  sk_cnt_words=cnt.numel(), err=err.data_ptr())
@@ -228,8 +228,9 @@ def test_fwd_step_variants(step_variants, mode, H, Bp, var):
     test_fwd_step(step_variants, mode, H, Bp, 2)
 
 
-@pytest.mark.parametrize("var", [dict(bwd_sk_pf=1, bwd_sk_ns=4), dict(bwd_sk_pf=0, bwd_sk_ns=4),
-                                 dict(bwd_sk_pf=1, bwd_sk_ns=5), dict(bwd_sk_pf=0, bwd_sk_ns=5)])
+@pytest.mark.parametrize("var", [dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=4), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=4),
+                                 dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=5), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=5),
+                                 dict(bwd_sk64=1)])
 @pytest.mark.parametrize("first", [False, True])
 def test_bwd_step_sk_variants(step_variants, first, var):
     step_variants.set_step_lds_variants(var)
