@@ -49,6 +49,11 @@ def main() -> int:
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--shard-optim", action="store_true",
                     help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
+    ap.add_argument("--min-warmup", type=int, default=100,
+                    help="untimed steps before the timed region are at least this many: W from --warmup plus "
+                         "max(0, N - W) extra, reported as extra_warmup_steps (a fresh box runs its first "
+                         "~20 ms of steps below full clocks: W=5 measured 0.232-0.243 ms/step vs 0.221 after "
+                         "100, profiles/r2_bench_warmup_probe.txt).  Same count on every rank.")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -115,12 +120,13 @@ def main() -> int:
             torch.cuda.synchronize(ctx.device)
         gdist.barrier()
 
-    for i in range(args.warmup):
+    extra = max(0, args.min_warmup - args.warmup) if ctx.device.type == "cuda" else 0   # GPU clock ramp only
+    for i in range(args.warmup + extra):
         step(i)
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(args.warmup + extra + i)
     sync()
     el = time.perf_counter() - t0
     if world > 1:
@@ -135,7 +141,7 @@ def main() -> int:
             "metric": METRIC if args.preset in ("h512", "h512_dp8") else
                       f"char-tokens/sec (whole node) for GRU preset {args.preset}",
             "value": round(value, 1), "unit": "char-tokens/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "extra_warmup_steps": extra,
             "ms_per_step": round(1000 * el / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic name sequences (seeded syllable generator), random-init weights",
