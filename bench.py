@@ -49,7 +49,7 @@ def main() -> int:
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--shard-optim", action="store_true",
                     help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
-    ap.add_argument("--min-warmup", type=int, default=100,
+    ap.add_argument("--min-warmup", type=int, default=300,
                     help="untimed steps before the timed region are at least this many: W from --warmup plus "
                          "max(0, N - W) extra, reported as extra_warmup_steps (a fresh box runs its first "
                          "~20 ms of steps below full clocks: W=5 measured 0.232-0.243 ms/step vs 0.221 after "
