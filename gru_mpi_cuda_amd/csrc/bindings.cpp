@@ -159,6 +159,7 @@ PYBIND11_MODULE(_C, m) {
     GemmArgs a;
     a.A = GP(const u16, d, "A"); a.lda = get<int>(d, "lda", 0);
     a.onehot_ids = GP(const int, d, "onehot_ids");
+    a.B2 = GP(const u16, d, "B2"); a.b2_row = get<int>(d, "b2_row", 0);
     a.B = GP(const u16, d, "B"); a.ldb = get<int>(d, "ldb", 0);
     a.C = GP(float, d, "C"); a.ldc = get<int>(d, "ldc", 0);
     a.bias = GP(const float, d, "bias"); a.rowsumA = GP(float, d, "rowsumA");
@@ -216,6 +217,7 @@ PYBIND11_MODULE(_C, m) {
     a.sk_part = GP(float, d, "sk_part"); a.sk_part_floats = get<long>(d, "sk_part_floats", 0);
     a.sk_cnt = GP(unsigned, d, "sk_cnt"); a.sk_cnt_words = get<long>(d, "sk_cnt_words", 0);
     a.err = GP(unsigned, d, "err");
+    a.dgiT_n_only = get<int>(d, "dgiT_n_only", 0);
     if (a.Bp % 32 || a.H % 64) throw std::runtime_error("bwd_step: Bp % 32 and H % 64 required");
     gru_bwd_step(a, S(s));
     HIP_LAUNCH_CHECK();

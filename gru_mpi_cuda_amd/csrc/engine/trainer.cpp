@@ -68,6 +68,14 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);
   if (const char* xl = std::getenv("GK_XCD_LOCAL")) xcd_local_ = std::atoi(xl) != 0;
   if (step_algo_ == 2 && !gru_step_lds_ok(H, B)) step_algo_ = 0;
+  {
+    // shapes where both one-hot dP call sites (whole sequence, and per time chunk in the overlapped
+    // schedule) are LDS-kernel shapes with 128-aligned gate blocks (gemm_lds_ok with B2)
+    const long tok = (long)d_.T * B, ctok = (long)Tc_ * B;
+    const char* ds = std::getenv("GK_DGIT_SHARE");
+    dgiT_share_ = !(ds && ds[0] == '0') && V % 128 == 0 && H % 128 == 0 && B % 8 == 0 && tok % 128 == 0 &&
+                  ctok % 128 == 0;
+  }
   seq_.resize(L);
   bool any_bwd = false;
   for (int l = 0; l < L; ++l) {
@@ -326,6 +334,7 @@ void Trainer::bwd_step(int l, int t, hipStream_t s) {
   a.dgh = y.dgh[t & 1];
   a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = T * B; a.colT = t * B;
   a.dgi = y.dgi ? y.dgi + (size_t)t * B * 3 * H : nullptr;
+  a.dgiT_n_only = l == 0 && dgiT_share_;
   a.Bp = B; a.H = H; a.algo = step_algo_;
   a.sk_part = sk_part_; a.sk_part_floats = sk_part_floats_; a.sk_cnt = sk_cnt_; a.sk_cnt_words = sk_cnt_words_;
   a.err = err_;
@@ -413,6 +422,7 @@ void Trainer::record_fb(hipStream_t s0) {
       if (l == 0) {
         GemmArgs p;   // dP slab c = onehot(x)^T · dGi   ([V][3H]; gives dEmb, dW_ih0, db_ih0)
         p.onehot_ids = ids_ + t0; p.B = y.dgiT + t0; p.ldb = T * B;
+        if (dgiT_share_) { p.B = y.dghT + t0; p.B2 = y.dgiT + t0; p.b2_row = 2 * H; }
         p.C = slab_P_ + (size_t)c * V * H3; p.ldc = H3; p.M = V; p.N = H3; p.K = Tc * B;
         gemm_nt(p, s1);
       } else {

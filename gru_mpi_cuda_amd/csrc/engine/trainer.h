@@ -185,6 +185,9 @@ class Trainer {
   unsigned* sk_cnt_ = nullptr;
   long sk_part_floats_ = 0, sk_cnt_words_ = 0;
   int xcd_local_ = 1;          // persistent kernels may use the L2-local hand-off (GK_XCD_LOCAL=0: never)
+  // layer 0's per-step backward writes only the n-gate rows of dGi^T; the one-hot dP GEMM reads the
+  // r/z rows from dGh^T, where they are identical (GK_DGIT_SHARE=0: write and read all of dGi^T)
+  bool dgiT_share_ = false;
   u16* xbuf_ = nullptr;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce

@@ -308,6 +308,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
         int sp = splits_;
         while (sp > 1 && (tok % sp || (tok / sp) % 128)) sp >>= 1;
         p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)tok;
+        if (dgiT_share_) { p.B = y.dghT; p.B2 = y.dgiT; p.b2_row = H3 - H; }
         p.C = slab_w_; p.ldc = H3; p.M = V; p.N = H3; p.K = (int)tok; p.splits = sp;
         gemm_nt(p, s);
         float* dPd = dp ? dP_target() : dP_;

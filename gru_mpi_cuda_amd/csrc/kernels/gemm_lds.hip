@@ -55,7 +55,7 @@ DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u1
     const int r = (4 * w + q) * 8 + srow;
     const int c = sslot ^ ((r >> 1) & 7);
     srcA[q] = OH ? nullptr : a.A + (size_t)(row0 + r) * a.lda + kbeg + c * 8;
-    srcB[q] = a.B + (size_t)(col0 + r) * a.ldb + kbeg + c * 8;
+    srcB[q] = (a.B2 && col0 >= a.b2_row ? a.B2 : a.B) + (size_t)(col0 + r) * a.ldb + kbeg + c * 8;
   }
   // one-hot: row r = (4w+q)*8 + srow keeps logical chunk c = sslot ^ (4(q&1) + (srow>>1)) in this
   // lane's slot, so a lane needs the 8 ids of two chunks per k-tile
@@ -217,6 +217,7 @@ bool gemm_lds_ok(const GemmArgs& a) {
   if (a.M % 128 || a.N % 128 || a.K % a.splits) return false;
   const int kper = a.K / a.splits;
   if (kper % 64 || kper < 128) return false;
+  if (a.B2 && (!a.onehot_ids || a.b2_row % 128 || (reinterpret_cast<uintptr_t>(a.B2) & 15))) return false;
   if (a.onehot_ids) {   // synthesised A: 16-B aligned id chunks, no bias / row sums
     return !a.rowsumA && !a.bias && !(a.ldb % 8) && !(reinterpret_cast<uintptr_t>(a.B) & 15) &&
            !(reinterpret_cast<uintptr_t>(a.onehot_ids) & 15);

@@ -210,7 +210,8 @@ __global__ void __launch_bounds__(512) gru_bwd_step_kernel(BwdStepArgs a, int nk
     const size_t off = (size_t)(g * H + j0 + col) * a.ldT + a.colT + b0 + row;
     const u16 vh = st[(g * TUNITS + col) * TROWS + row];
     a.dghT[off] = vh;
-    a.dgiT[off] = (g == 2) ? st[(3 * TUNITS + col) * TROWS + row] : vh;
+    if (g == 2) a.dgiT[off] = st[(3 * TUNITS + col) * TROWS + row];
+    else if (!a.dgiT_n_only) a.dgiT[off] = vh;
   }
 }
 

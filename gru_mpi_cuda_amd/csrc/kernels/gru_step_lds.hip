@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a)
     const int g = kind < 3 ? kind : 2;
     const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + seg * 8;
     if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+    if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
   }
 }
 
@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_lds8_kernel(BwdStepArgs a
     const int g = kind < 3 ? kind : 2;
     const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + seg * 8;
     if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+    if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
   }
 }
 
@@ -1080,7 +1080,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
       const int g = kind < 3 ? kind : 2;
       const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + 32 * sq + seg * 8;
       if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-      if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+      if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
     }
   }
 }
@@ -1239,7 +1239,7 @@ __global__ void __launch_bounds__(256, 2) gru_bwd_step_sk64_kernel(BwdStepArgs a
     const int g = kind < 3 ? kind : 2;
     const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + 16 * split + seg * 8;
     if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-    if (kind != 2 && a.dgiT) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
+    if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
   }
 }
 

@@ -40,6 +40,7 @@ struct FwdStepArgs {
 void gru_fwd_step(const FwdStepArgs& a, hipStream_t s);
 
 struct BwdStepArgs {
+  int dgiT_n_only = 0;             // write only the n-gate rows of dgiT (its r/z rows equal dghT's)
   const u16* dgh_next = nullptr;   // [Bp][3H] dGh_{t+1} (null at t = T-1)
   const u16* WhhT = nullptr;       // [H][3H]
   const float* carry_in = nullptr; // [Bp][H]  z_{t+1} ⊙ dh_{t+1}    (null at t = T-1)
@@ -288,6 +289,9 @@ struct GemmArgs {
   int M = 0, N = 0, K = 0;
   int splits = 1;                  // split-K: slab s written at C + s*M*ldc (ldc == N)
   int accumulate = 0;              // C += result instead of C = result
+  // B rows >= b2_row are read from B2 (same row indexing; one-hot LDS kernel only, b2_row % 128 == 0):
+  // layer 0's dP reads the r/z gate rows of dGi^T from dGh^T, where they are identical
+  const u16* B2 = nullptr; int b2_row = 0;
   int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
                                    // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel),
                                    // 5 LDS-staged 256x256 (gemm256.hip)

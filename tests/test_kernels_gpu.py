@@ -147,11 +147,31 @@ def test_fwd_step(ext, mode, H, Bp, algo):
         torch.testing.assert_close(got, ref, **tol)
 
 
+def test_gemm_onehot_split_b(ext):
+    """B2: rows >= b2_row of the B operand read from a second buffer (layer 0's dP reads the r/z gate
+    rows of dGi^T from dGh^T); equals the one-hot product with the merged operand."""
+    V, H, K, splits = 256, 256, 1024, 2
+    N = 3 * H
+    ids = torch.randint(0, V, (K,), device=DEV, dtype=torch.int32)
+    B = bf(rnd(N, K, seed=5))
+    B2 = bf(rnd(N, K, seed=6))
+    B2[:2 * H] = float("nan")          # rows the kernel must not read from B2
+    B1 = B.clone()
+    B1[2 * H:] = float("nan")          # rows the kernel must not read from B
+    C = torch.zeros(splits, V, N, device=DEV)
+    ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B1.data_ptr(), B2=B2.data_ptr(), b2_row=2 * H, ldb=K,
+                     C=C.data_ptr(), ldc=N, M=V, N=N, K=K, splits=splits, algo=2), S())
+    torch.cuda.synchronize()
+    merged = torch.cat([B[:2 * H], B2[2 * H:]]).float()
+    ref = torch.nn.functional.one_hot(ids.long(), V).float().T @ merged.T
+    torch.testing.assert_close(C.sum(0), ref, atol=1e-3, rtol=1e-3)
+
+
 @pytest.mark.parametrize("first", [False, True])
 @pytest.mark.parametrize("H,Bp,algo,sk", [(128, 64, 1, 0), (1024, 128, 1, 0), (1024, 128, 2, 0), (1024, 256, 2, 0),
                                           (512, 128, 2, 0), (2048, 512, 2, 0), (2048, 512, 2, 1),
                                           (2048, 1024, 2, 1)])
-def test_bwd_step(ext, first, H, Bp, algo, sk):
+def test_bwd_step(ext, first, H, Bp, algo, sk, n_only=False):
     """sk = 1: the split-K LDS kernel (128 x 128 tiles, S workgroups per tile meeting through
     fp32 partials and monotonic arrival counters), launched three times on one workspace."""
     T = 4
@@ -173,6 +193,8 @@ def test_bwd_step(ext, first, H, Bp, algo, sk):
              dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), dgi=dgi.data_ptr(), ldT=T * Bp, colT=t * Bp, Bp=Bp, H=H, algo=algo)
     if not first:
         d.update(dgh_next=dgn.data_ptr(), carry_in=carry.data_ptr())
+    if n_only:
+        d["dgiT_n_only"] = 1
     launches = 1
     if sk:
         S_ = ext.bwd_step_sk_splits(H, Bp)
@@ -208,7 +230,11 @@ def test_bwd_step(ext, first, H, Bp, algo, sk):
     torch.testing.assert_close(dgh.float(), ref_h, atol=2e-3, rtol=1e-2)
     torch.testing.assert_close(dgi.float(), ref_i, atol=2e-3, rtol=1e-2)
     torch.testing.assert_close(dghT[:, t * Bp:(t + 1) * Bp].T, dgh, atol=0, rtol=0)
-    torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
+    if n_only:   # r/z rows untouched (zeros), n rows = dgi's n block
+        assert not dgiT[:2 * H].any()
+        torch.testing.assert_close(dgiT[2 * H:, t * Bp:(t + 1) * Bp].T, dgi[:, 2 * H:], atol=0, rtol=0)
+    else:
+        torch.testing.assert_close(dgiT[:, t * Bp:(t + 1) * Bp].T, dgi, atol=0, rtol=0)
 
 
 @pytest.fixture
@@ -235,6 +261,12 @@ def test_fwd_step_variants(step_variants, mode, H, Bp, var):
 def test_bwd_step_sk_variants(step_variants, first, var):
     step_variants.set_step_lds_variants(var)
     test_bwd_step(step_variants, first, 2048, 512, 2, 1)
+
+
+# dgiT_n_only: every backward step kernel family writes only the n-gate rows of dGi^T
+@pytest.mark.parametrize("H,Bp,algo,sk", [(128, 64, 1, 0), (1024, 128, 2, 0), (2048, 512, 2, 1)])
+def test_bwd_step_dgit_n_only(ext, H, Bp, algo, sk):
+    test_bwd_step(ext, False, H, Bp, algo, sk, n_only=True)
 
 
 @pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256"])
