@@ -292,6 +292,7 @@ struct GemmArgs {
   // B rows >= b2_row are read from B2 (same row indexing; one-hot LDS kernel only, b2_row % 128 == 0):
   // layer 0's dP reads the r/z gate rows of dGi^T from dGh^T, where they are identical
   const u16* B2 = nullptr; int b2_row = 0;
+  int raster = 0;                  // LDS 128x128 kernel tile order: 0 auto (shorter dimension fast), 1 column-fast
   int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
                                    // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel),
                                    // 5 LDS-staged 256x256 (gemm256.hip)
