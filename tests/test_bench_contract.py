@@ -64,6 +64,18 @@ def test_bench_self_launches_world2():
     assert r["rccl_ranks"] == 2 and r["comm_backend"] == "gloo"
 
 
+def test_bench_sharded_optimizer_world2():
+    """``--shard-optim`` through the self-launched 2-rank job: same contract, flag reported, and the
+    same final loss as the replicated optimiser (the CPU twin is bitwise equal)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    args = [sys.executable, "bench.py", "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"]
+    a = _lines(args, 2, env=env)
+    b = _lines(args + ["--shard-optim"], 2, env=env)
+    assert b["config"]["shard_optim"] is True and a["config"]["shard_optim"] is False
+    assert a["final_loss"] == b["final_loss"]
+    assert b["extra_warmup_steps"] == 0     # the GPU clock-ramp warm-up only runs on GPUs
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="",
                HIP_VISIBLE_DEVICES="")
