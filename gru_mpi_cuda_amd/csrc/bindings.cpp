@@ -231,7 +231,7 @@ PYBIND11_MODULE(_C, m) {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
     d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64;
-    d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk64"] = v.bwd_sk64;
+    d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk64"] = v.bwd_sk64; d["bwd_sk_min_h"] = v.bwd_sk_min_h;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -246,6 +246,7 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd_sk_ns") v.bwd_sk_ns = x;
       else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
       else if (k == "bwd_sk64") v.bwd_sk64 = x;
+      else if (k == "bwd_sk_min_h") v.bwd_sk_min_h = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
   });

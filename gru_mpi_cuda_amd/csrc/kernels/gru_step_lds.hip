@@ -1261,10 +1261,11 @@ int gru_bwd_step_sk_splits(int H, int Bp) {
   if (tiles % 8) return 0;
   static const int cap4 = sk_capacity((const void*)gru_bwd_step_sk_kernel<4>);
   static const int cap2 = sk_capacity((const void*)gru_bwd_step_sk_kernel<2>);
-  // only where the 64 x 64 kernel's per-workgroup operand stream is the bound: H = 2048 (K = 6144)
-  // 40.3 -> 35.4 us per step; at H = 1024 (K = 3072) the exchange costs more than it saves
-  // (9.50 -> 9.62 ms per h1024_l2 step at B = 1024), profiles/r1_bwd_step_sk_ab.jsonl
-  if (H < 2048) return 0;
+  // H = 2048 (K = 6144): 40.3 -> 35.4 us per step (profiles/r1_bwd_step_sk_ab.jsonl).  H = 1024 was
+  // a loss before the epilogue operands moved ahead of the K loop (9.50 -> 9.62 ms per h1024_l2 step
+  // at B = 1024); with them it gains: 8.67 -> 8.17-8.19 ms (profiles/r2_h1024l2_b1024_sk_ab.jsonl).
+  // GK_BWD_SK_MIN_H=2048 restores the old bound.
+  if (H < step_lds_variants().bwd_sk_min_h) return 0;
   if ((3 * H / 64) % 4 == 0 && tiles * 4 <= cap4 && tiles * 4 >= 192) return 4;
   if ((3 * H / 64) % 2 == 0 && tiles * 2 <= cap2 && tiles * 2 >= 192) return 2;
   return 0;
@@ -1279,6 +1280,7 @@ StepLdsVariants& step_lds_variants() {
     env("GK_FWD_LDS8", d.fwd8);
     env("GK_FWD_LDS64", d.fwd64);
     env("GK_BWD_SK64", d.bwd_sk64);
+    env("GK_BWD_SK_MIN_H", d.bwd_sk_min_h);
     env("GK_BWD_SK_NS", d.bwd_sk_ns);
     env("GK_BWD_SK_PF", d.bwd_sk_pf);
     return d;

@@ -78,6 +78,7 @@ struct StepLdsVariants {
   int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
   int bwd_sk64 = 0;      // split-K backward on 64-row tiles, two workgroups per CU
+  int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection

@@ -263,6 +263,11 @@ def test_bwd_step_sk_variants(step_variants, first, var):
     test_bwd_step(step_variants, first, 2048, 512, 2, 1)
 
 
+def test_bwd_step_sk_at_h1024(step_variants):
+    step_variants.set_step_lds_variants(dict(bwd_sk_min_h=1024))
+    test_bwd_step(step_variants, False, 1024, 1024, 2, 1)
+
+
 # dgiT_n_only: every backward step kernel family writes only the n-gate rows of dGi^T
 @pytest.mark.parametrize("H,Bp,algo,sk", [(128, 64, 1, 0), (1024, 128, 2, 0), (2048, 512, 2, 1)])
 def test_bwd_step_dgit_n_only(ext, H, Bp, algo, sk):
