@@ -1350,10 +1350,11 @@ void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
       const StepLdsVariants& v = step_lds_variants();
-      const int ns = v.bwd_sk_ns == 5 ? 5 : SKNS;
+      const int ns = v.bwd_sk_ns == 5 ? 5 : v.bwd_sk_ns == 3 ? 3 : SKNS;
       const bool pf = v.bwd_sk_pf != 0;
       if (S == 4 && ns == 5 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5, true>), dim3(tiles * 4), dim3(512), 0, s, a);
       else if (S == 4 && ns == 5) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5>), dim3(tiles * 4), dim3(512), 0, s, a);
+      else if (S == 4 && ns == 3 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 3, true>), dim3(tiles * 4), dim3(512), 0, s, a);
       else if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, a);
       else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
       else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, a);

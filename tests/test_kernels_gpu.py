@@ -256,7 +256,7 @@ def test_fwd_step_variants(step_variants, mode, H, Bp, var):
 
 @pytest.mark.parametrize("var", [dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=4), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=4),
                                  dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=5), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=5),
-                                 dict(bwd_sk64=1)])
+                                 dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=3), dict(bwd_sk64=1)])
 @pytest.mark.parametrize("first", [False, True])
 def test_bwd_step_sk_variants(step_variants, first, var):
     step_variants.set_step_lds_variants(var)
