@@ -227,7 +227,9 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
 // twice the k-tile streams in flight per CU of the 128-row tile, for 1.4x its L2 bytes per FLOP
 // (the W_hh tile is shared by 64 rows instead of 128): h2048 step 9.72-9.74 -> 9.43-9.47 ms
 // (profiles/r2_h2048_fwd64_ab.jsonl).  Training path only (no fused input phase).
-template <int NS>
+// FUSED: layers >= 1 of batched generation -- the input projection as a first K phase (A = x rows,
+// B = W_ih gate rows) ahead of the recurrent one, as in the 128-row kernel.
+template <int NS, bool FUSED = false>
 __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[NS][(64 + 96) * 64];
   const int H = a.H;
@@ -238,14 +240,18 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
   const int srow = lane >> 3, sslot = lane & 7;
   const int u = j0 + wn * 16 + lr;
 
-  float gi[2][4][3], bh[3], hp[2][4];
+  constexpr int NGI = FUSED ? 1 : 2;
+  float gi[NGI][4][3], bh[3], bi[3], hp[2][4];
 #pragma unroll
-  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
+  for (int g = 0; g < 3; ++g) {
+    bh[g] = a.bhh[g * H + u];
+    bi[g] = FUSED ? a.bih[g * H + u] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * H + u];
-  {
+  if constexpr (!FUSED) {
     const float* src[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -265,55 +271,67 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
+        for (int g = 0; g < 3; ++g) gi[FUSED ? 0 : i][e][g] = src[i][e][g * H + u];
   }
 
   f32x4 acc[2][3];
+  f32x4 accN[FUSED ? 2 : 1];   // input part of the n gate (FUSED)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // 20 DMA pieces per k-tile, 5 per wave: piece p = 5w + q, image rows 8p..8p+7 (A for p < 8)
-  const u16* src[5];
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const int p = 5 * w + q, r = p * 8 + srow;
-    if (p < 8) {
-      src[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
-    } else {
-      const int rb = r - 64;
-      src[q] = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + swz(rb, sslot) * 8;
-    }
+    if constexpr (FUSED) accN[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  auto stage = [&](int buf, int kt) {
+
+  // one K phase: A rows b0.. of Am [.][K], B rows (gate, unit) -> Bm row g*H + j0 + unit.
+  // 20 DMA pieces per k-tile, 5 per wave: piece p = 5w + q, image rows 8p..8p+7 (A for p < 8)
+  auto phase = [&](const u16* Am, const u16* Bm, int K, auto input_tag) {
+    constexpr bool input = decltype(input_tag)::value;
+    const u16* src[5];
 #pragma unroll
-    for (int q = 0; q < 5; ++q)
-      __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(5 * w + q) * 8 * 64]), 16, 0, 0);
-  };
-  ring_loop<NS, 5>(H / 64, stage, [&](int cur) {
-    const u16* LA = lds[cur];
-    const u16* LB = lds[cur] + 64 * 64;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + lq;
-      bf16x8 af[2], bfr[3];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = wm * 32 + i * 16 + lr;
-        af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+    for (int q = 0; q < 5; ++q) {
+      const int p = 5 * w + q, r = p * 8 + srow;
+      if (p < 8) {
+        src[q] = Am + (size_t)(b0 + r) * K + swz(r, sslot) * 8;
+      } else {
+        const int rb = r - 64;
+        src[q] = Bm + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * K + swz(rb, sslot) * 8;
       }
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const int r = g * 32 + wn * 16 + lr;
-        bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
     }
-  });
+    auto stage = [&](int buf, int kt) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(5 * w + q) * 8 * 64]), 16, 0, 0);
+    };
+    ring_loop<NS, 5>(K / 64, stage, [&](int cur) {
+      const u16* LA = lds[cur];
+      const u16* LB = lds[cur] + 64 * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + lq;
+        bf16x8 af[2], bfr[3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = wm * 32 + i * 16 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
+        }
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const int r = g * 32 + wn * 16 + lr;
+          bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][0] = mfma16(af[i], bfr[0], acc[i][0]);
+          acc[i][1] = mfma16(af[i], bfr[1], acc[i][1]);
+          if constexpr (FUSED && input) accN[FUSED ? i : 0] = mfma16(af[i], bfr[2], accN[FUSED ? i : 0]);
+          else acc[i][2] = mfma16(af[i], bfr[2], acc[i][2]);
+        }
+      }
+    });
+  };
+  if constexpr (FUSED) phase(a.x_bf, a.Wih, a.Kin, std::true_type{});
+  phase(a.hprev_bf, a.Whh, H, std::false_type{});
 
   u16* st = lds[0];     // [64 rows][32 units]
 #pragma unroll
@@ -323,9 +341,12 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
       const int rr = wm * 32 + i * 16 + lq * 4 + e;
       const int b = b0 + rr;
       const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
-      const float r = sigmoidf_(gi[i][e][0] + ghr);
-      const float z = sigmoidf_(gi[i][e][1] + ghz);
-      const float n = tanhf_(gi[i][e][2] + r * ghn);
+      float gir, giz, gin;
+      if constexpr (FUSED) { gir = bi[0]; giz = bi[1]; gin = accN[FUSED ? i : 0][e] + bi[2]; }
+      else { gir = gi[FUSED ? 0 : i][e][0]; giz = gi[FUSED ? 0 : i][e][1]; gin = gi[FUSED ? 0 : i][e][2]; }
+      const float r = sigmoidf_(gir + ghr);
+      const float z = sigmoidf_(giz + ghz);
+      const float n = tanhf_(gin + r * ghn);
       const float h = n + z * (hp[i][e] - n);
       const size_t o = (size_t)b * H + u;
       a.h_f[o] = h;
@@ -1279,6 +1300,7 @@ StepLdsVariants& step_lds_variants() {
     env("GK_STEP_NT", d.fwd_nt);
     env("GK_FWD_LDS8", d.fwd8);
     env("GK_FWD_LDS64", d.fwd64);
+    env("GK_FWD_LDS64_FUSED", d.fwd64_fused);
     env("GK_BWD_SK64", d.bwd_sk64);
     env("GK_BWD_SK_MIN_H", d.bwd_sk_min_h);
     env("GK_BWD_SK_NS", d.bwd_sk_ns);
@@ -1311,6 +1333,13 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   if (ns != 2 && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
     if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<3>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
+    return;
+  }
+  // fused input phase (layers >= 1 of batched generation) on 64-row tiles (GK_FWD_LDS64_FUSED=0
+  // reverts): reference model at 1024 names 55.8-56.1 -> 54.3-54.9 us per char
+  // (profiles/r2_generate_fwd64_fused_ab.txt)
+  if (ns != 2 && a.x_bf && v.fwd64_fused && a.Bp % 64 == 0 && a.Kin % 64 == 0) {
+    hipLaunchKernelGGL((gru_fwd_step_lds64_kernel<3, true>), dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     return;
   }
   if (ns != 2 && !a.x_bf && eight) {

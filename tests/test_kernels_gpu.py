@@ -254,6 +254,13 @@ def test_fwd_step_variants(step_variants, mode, H, Bp, var):
     test_fwd_step(step_variants, mode, H, Bp, 2)
 
 
+@pytest.mark.parametrize("H,Bp", [(1024, 256), (1024, 1024), (512, 128)])
+def test_fwd_step_fused_64row(step_variants, H, Bp):
+    """The 64-row forward tile with the fused input phase (layers >= 1 of batched generation)."""
+    step_variants.set_step_lds_variants(dict(fwd64_fused=1))
+    test_fwd_step(step_variants, "fused", H, Bp, 2)
+
+
 @pytest.mark.parametrize("var", [dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=4), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=4),
                                  dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=5), dict(bwd_sk64=0, bwd_sk_pf=0, bwd_sk_ns=5),
                                  dict(bwd_sk64=0, bwd_sk_pf=1, bwd_sk_ns=3), dict(bwd_sk64=1)])
