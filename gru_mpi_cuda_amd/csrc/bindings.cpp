@@ -230,7 +230,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("step_lds_variants", []() {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
-    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused;
+    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
     d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk64"] = v.bwd_sk64; d["bwd_sk_min_h"] = v.bwd_sk_min_h;
     return d;
   });
@@ -244,6 +244,7 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "fwd8") v.fwd8 = x;
       else if (k == "fwd64") v.fwd64 = x;
       else if (k == "fwd64_fused") v.fwd64_fused = x;
+      else if (k == "fwd64_all") v.fwd64_all = x;
       else if (k == "bwd_sk_ns") v.bwd_sk_ns = x;
       else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
       else if (k == "bwd_sk64") v.bwd_sk64 = x;

@@ -1301,6 +1301,7 @@ StepLdsVariants& step_lds_variants() {
     env("GK_FWD_LDS8", d.fwd8);
     env("GK_FWD_LDS64", d.fwd64);
     env("GK_FWD_LDS64_FUSED", d.fwd64_fused);
+    env("GK_FWD_LDS64_ALL", d.fwd64_all);
     env("GK_BWD_SK64", d.bwd_sk64);
     env("GK_BWD_SK_MIN_H", d.bwd_sk_min_h);
     env("GK_BWD_SK_NS", d.bwd_sk_ns);
@@ -1330,7 +1331,8 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
   if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : v.fwd_ns == 5 ? 5 : 4;
   const bool nt = v.fwd_nt != 0, eight = v.fwd8 != 0;
-  if (ns != 2 && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
+  const bool big_grid_ok = ns != 2 || v.fwd64_all;   // GK_FWD_LDS64_ALL=1: also where the 2-deep 128-row kernel runs
+  if (big_grid_ok && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
     if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<3>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     return;
@@ -1338,7 +1340,7 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   // fused input phase (layers >= 1 of batched generation) on 64-row tiles (GK_FWD_LDS64_FUSED=0
   // reverts): reference model at 1024 names 55.8-56.1 -> 54.3-54.9 us per char
   // (profiles/r2_generate_fwd64_fused_ab.txt)
-  if (ns != 2 && a.x_bf && v.fwd64_fused && a.Bp % 64 == 0 && a.Kin % 64 == 0) {
+  if (big_grid_ok && a.x_bf && v.fwd64_fused && a.Bp % 64 == 0 && a.Kin % 64 == 0) {
     hipLaunchKernelGGL((gru_fwd_step_lds64_kernel<3, true>), dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     return;
   }

@@ -76,6 +76,7 @@ struct StepLdsVariants {
                          // 1 = group 0 runs the whole epilogue, 0 = the 4-wave kernel
   int fwd64 = 1;         // 64-row forward tile, two workgroups per CU (1: 3-deep ring, 2: 4-deep)
   int fwd64_fused = 1;   // the 64-row tile also for the fused input phase (layers >= 1 of generation)
+  int fwd64_all = 0;     // the 64-row tile also on grids of >= 512 128-row tiles (2-deep 128-row kernel otherwise)
   int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
   int bwd_sk64 = 0;      // split-K backward on 64-row tiles, two workgroups per CU
