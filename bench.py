@@ -54,6 +54,11 @@ def main() -> int:
                          "max(0, N - W) extra, reported as extra_warmup_steps (a fresh box runs its first "
                          "~20 ms of steps below full clocks: W=5 measured 0.232-0.243 ms/step vs 0.221 after "
                          "100, profiles/r2_bench_warmup_probe.txt).  Same count on every rank.")
+    ap.add_argument("--graph-steps", type=int, default=4,
+                    help="hip engine on GPUs: G consecutive training steps captured into one graph launch "
+                         "(1..4; the same G full steps, one graph boundary instead of G: ~13 us each at "
+                         "the headline, docs/DESIGN.md §6); used when the warm-up and timed step counts "
+                         "are multiples of G, else 1.  Reported as graph_steps.")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -108,6 +113,7 @@ def main() -> int:
         if args.no_graph and hasattr(tr, "t"):
             tr.t.set_use_graph(False)
         step = lambda i: tr.step(*pool[i % len(pool)])  # noqa: E731
+        G = args.graph_steps if ctx.device.type == "cuda" and hasattr(tr, "steps") else 1
         final_loss = lambda: tr.loss()                  # noqa: E731
         plan = tr.t.plan() if hasattr(tr, "t") else "cpu"
     else:
@@ -121,11 +127,15 @@ def main() -> int:
         gdist.barrier()
 
     extra = max(0, args.min_warmup - args.warmup) if ctx.device.type == "cuda" else 0   # GPU clock ramp only
-    for i in range(args.warmup + extra):
+    if args.impl != "hip" or (args.warmup + extra) % G or args.steps % G:
+        G = 1
+    if G > 1:   # G steps per graph launch: the same steps, fewer graph boundaries
+        step = lambda i: tr.steps([pool[(i + j) % len(pool)] for j in range(G)])  # noqa: E731
+    for i in range(0, args.warmup + extra, G):
         step(i)
     sync()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(0, args.steps, G):
         step(args.warmup + extra + i)
     sync()
     el = time.perf_counter() - t0
@@ -142,6 +152,7 @@ def main() -> int:
                       f"char-tokens/sec (whole node) for GRU preset {args.preset}",
             "value": round(value, 1), "unit": "char-tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "extra_warmup_steps": extra,
+            "graph_steps": G,
             "ms_per_step": round(1000 * el / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic name sequences (seeded syllable generator), random-init weights",

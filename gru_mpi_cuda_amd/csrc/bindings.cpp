@@ -97,6 +97,16 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("comm"), py::arg("buckets"), py::arg("min_bucket_floats") = 2L << 20, py::keep_alive<1, 2>())
       .def("allreduce_log", &Trainer::allreduce_log)
       .def("step", [](Trainer& t, uintptr_t s) { t.step(S(s)); })
+      .def("set_graph_steps", &Trainer::set_graph_steps)
+      .def("graph_steps", &Trainer::graph_steps)
+      .def("set_batches", [](Trainer& t, py::array_t<int, py::array::c_style | py::array::forcecast> x,
+                             py::array_t<int, py::array::c_style | py::array::forcecast> y) {
+        if (x.ndim() != 3 || y.ndim() != 3 || x.shape(0) != y.shape(0) || x.shape(1) != y.shape(1) ||
+            x.shape(2) != y.shape(2))
+          throw std::runtime_error("set_batches: x and y must both be [G, B, T]");
+        t.set_batches(x.data(), y.data(), (int)x.shape(1), (int)x.shape(0));
+      })
+      .def("step_group", [](Trainer& t, uintptr_t s) { t.step_group(S(s)); })
       .def("forward_backward", [](Trainer& t, uintptr_t s) { t.forward_backward(S(s)); })
       .def("optimizer_step", [](Trainer& t, uintptr_t s) { t.optimizer_step(S(s)); })
       .def("read_loss", &Trainer::read_loss)

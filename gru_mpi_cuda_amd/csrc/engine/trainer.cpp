@@ -160,8 +160,9 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   events_.resize(64 + 8 * C_ * L);
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  HIP_CHECK(hipHostMalloc(&h_stage_, 2 * (2 * tok + 16) * sizeof(int)));
-  std::memset(h_stage_, 0, 2 * (2 * tok + 16) * sizeof(int));
+  constexpr int kSlots = 2 + 2 * kMaxGroup;   // per-step pair + two multi-step groups
+  HIP_CHECK(hipHostMalloc(&h_stage_, kSlots * (2 * tok + 16) * sizeof(int)));
+  std::memset(h_stage_, 0, kSlots * (2 * tok + 16) * sizeof(int));
   // The staging events only tell the host that the graph which read a pinned slot has finished;
   // the host never reads device results through them, so they skip the system-scope release
   // (an end-of-step L2 writeback to host-coherent memory between consecutive step graphs).
@@ -169,6 +170,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const unsigned stage_flags = hipEventDisableTiming |
                                ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
   for (auto& e : stage_done_) {
+    HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
+    HIP_CHECK(hipEventRecord(e, s0_));
+  }
+  for (auto& e : group_done_) {
     HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
     HIP_CHECK(hipEventRecord(e, s0_));
   }
@@ -183,9 +188,12 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
 Trainer::~Trainer() {
   for (auto& g : g_fb_) g.reset();
   for (auto& g : g_step_) g.reset();
+  for (auto& g : g_group_) g.reset();
   g_opt_.reset();
   for (auto& e : events_) (void)hipEventDestroy(e);
+  for (auto& g : g_group_) g.reset();
   for (auto& e : stage_done_) if (e) (void)hipEventDestroy(e);
+  for (auto& e : group_done_) if (e) (void)hipEventDestroy(e);
   wd_.reset();   // the watchdog thread reads err_host_
   if (h_stage_) (void)hipHostFree(h_stage_);
   if (err_host_) (void)hipHostFree(err_host_);
@@ -209,6 +217,7 @@ void Trainer::set_carry(bool on) {
   carry_ = on;
   for (auto& g : g_fb_) g.reset();   // the copies and the kernels' h0 argument are captured
   for (auto& g : g_step_) g.reset();
+  for (auto& g : g_group_) g.reset();
 }
 
 // Every copy of h kept per step: fp32 and bf16 row-major [T+1][Bp][H], the transposed bf16
@@ -246,6 +255,7 @@ void Trainer::set_lr(float lr) {
   o_.lr = lr;
   g_opt_.reset();   // lr is a kernel argument frozen into the captured graphs
   for (auto& g : g_step_) g.reset();
+  for (auto& g : g_group_) g.reset();
 }
 
 void Trainer::refresh_weights(hipStream_t s) {
@@ -504,6 +514,8 @@ void Trainer::set_shard_optim(bool on) {
   }
   g_step_[0].reset();
   g_step_[1].reset();
+  g_group_[0].reset();
+  g_group_[1].reset();
 }
 
 void Trainer::record_sharded_opt(hipStream_t s) {
@@ -639,6 +651,8 @@ void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& bu
   dP_inplace_ = (long)d_.V * 3 * d_.H <= 3L * d_.H * d_.E;
   g_step_[0].reset();
   g_step_[1].reset();
+  g_group_[0].reset();
+  g_group_[1].reset();
 }
 
 long Trainer::group_end(int l) const {
@@ -703,25 +717,7 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
-      if (shard_opt_) {
-        // sharded optimiser: whole backward first (slab sums into the flat gradient), then
-        // reduce-scatter -> Adam on the owned slice -> all-gather -> bf16 refresh
-        deferred_.n = 0;
-        if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
-        record_sharded_opt(s0_);
-      } else if (dp_overlap()) {
-        // readiness-ordered collectives on the comm stream, overlapped with the rest of the
-        // backward; joined before the optimiser (the embedding-side tail runs after the join)
-        deferred_.n = 0;
-        record_fb_seq(s0_, /*dp=*/true);
-      } else {
-        deferred_.n = 0;
-        defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
-        if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
-        defer_slabs_ = false;
-        record_allreduce(s0_);
-      }
-      if (!shard_opt_) record_opt(s0_);
+      record_step_body();
     } catch (...) {
       defer_slabs_ = false;
       deferred_.n = 0;
@@ -736,6 +732,75 @@ void Trainer::step(hipStream_t s) {
   g.launch(s);
   HIP_CHECK(hipEventRecord(stage_done_[slot], s));
   if (wd_) wd_->watch(stage_done_[slot]);
+}
+
+void Trainer::set_graph_steps(int G) {
+  if (G < 1 || G > kMaxGroup) throw std::runtime_error("set_graph_steps: 1.." + std::to_string(kMaxGroup));
+  group_ = G;
+  g_group_[0].reset();
+  g_group_[1].reset();
+}
+
+void Trainer::set_batches(const int* x, const int* y, int B, int n) {
+  if (n != group_) throw std::runtime_error("set_batches: expected " + std::to_string(group_) + " batches");
+  if (B > Bp_ || B <= 0) throw std::runtime_error("set_batches: batch larger than the trainer was built for");
+  const int gp = (group_parity_ ^= 1);
+  HIP_CHECK(hipEventSynchronize(group_done_[gp]));   // the group graph that last read these slots is done
+  const size_t per = (size_t)B * d_.T;
+  for (int j = 0; j < n; ++j) fill_slot(group_slot(gp, j), x + j * per, y + j * per, B);
+}
+
+void Trainer::step_group(hipStream_t s) {
+  GK_TRACE("gk.train_step_group");
+  if (!use_graph_) throw std::runtime_error("step_group: needs graph mode");
+  const int gp = group_parity_;
+  Graph& g = g_group_[gp];
+  if (!g.ready()) {
+    GK_TRACE("gk.capture_group_graph");
+    g.begin(s0_);
+    try {
+      for (int j = 0; j < group_; ++j) {
+        stage_src_ = h_stage_ + (size_t)group_slot(gp, j) * slot_ints();
+        record_step_body();
+      }
+    } catch (...) {
+      defer_slabs_ = false;
+      deferred_.n = 0;
+      hipGraph_t broken = nullptr;
+      (void)hipStreamEndCapture(s0_, &broken);
+      if (broken) (void)hipGraphDestroy(broken);
+      (void)hipGetLastError();
+      throw;
+    }
+    g.end(s0_);
+  }
+  g.launch(s);
+  HIP_CHECK(hipEventRecord(group_done_[gp], s));
+  if (wd_) wd_->watch(group_done_[gp]);
+}
+
+void Trainer::record_step_body() {
+  if (shard_opt_) {
+    // sharded optimiser: whole backward first (slab sums into the flat gradient), then
+    // reduce-scatter -> Adam on the owned slice -> all-gather -> bf16 refresh
+    deferred_.n = 0;
+    if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+    record_sharded_opt(s0_);
+    return;
+  }
+  if (dp_overlap()) {
+    // readiness-ordered collectives on the comm stream, overlapped with the rest of the
+    // backward; joined before the optimiser (the embedding-side tail runs after the join)
+    deferred_.n = 0;
+    record_fb_seq(s0_, /*dp=*/true);
+  } else {
+    deferred_.n = 0;
+    defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
+    if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
+    defer_slabs_ = false;
+    record_allreduce(s0_);
+  }
+  record_opt(s0_);
 }
 
 float Trainer::read_loss() {

@@ -102,6 +102,11 @@ class Trainer {
   void fill_slot(int slot, const int* x, const int* y, int B);
   // single-graph step (prep + fwd/bwd + in-graph RCCL all-reduce + optimiser)
   Graph g_step_[2];
+  Graph g_group_[2];
+  hipEvent_t group_done_[2] = {nullptr, nullptr};
+  int group_ = 1, group_parity_ = 0;
+  int group_slot(int parity, int j) const { return 2 + parity * kMaxGroup + j; }
+  void record_step_body();       // one step's capture body (shared by step() and step_group())
   RcclComm* comm_ = nullptr;
   std::vector<std::pair<long, long>> buckets_;   // plain buckets (eager / chunked-overlap paths)
   void record_allreduce(hipStream_t s);
@@ -146,6 +151,15 @@ class Trainer {
   long shard_chunk() const { return shard_chunk_; }
   void gather_opt_state(hipStream_t s);
   void step(hipStream_t s);      // whole training step as one graph replay
+  // Multi-step graphs: G consecutive steps (G = 1..kMaxGroup) captured into ONE graph, each reading
+  // its own staging slot -- one graph boundary (~13 us at the headline) per G steps.  set_batches()
+  // stages G batches ([G][B][T] each), step_group() launches them; two slot groups alternate so the
+  // host fills one while the other runs.
+  static constexpr int kMaxGroup = 4;
+  void set_graph_steps(int G);
+  int graph_steps() const { return group_; }
+  void set_batches(const int* x, const int* y, int B, int n);
+  void step_group(hipStream_t s);
   // test hook: set the device step error word (fault injection)
   void inject_error(unsigned bits) { HIP_CHECK(hipMemcpy(err_, &bits, 4, hipMemcpyHostToDevice)); }
   // watchdog over the launched steps (call after set_comm): timeout_ms > 0 aborts a step that

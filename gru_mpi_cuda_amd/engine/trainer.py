@@ -139,6 +139,28 @@ class HipTrainer:
         self.allreduce_grads()
         self.t.optimizer_step(s)
 
+    def steps(self, batches) -> None:
+        """len(batches) whole steps as ONE graph launch (Trainer::set_graph_steps): the graph boundary
+        (~13 us at the headline) is paid once per group.  Each batch is an (x, y) pair of [B, T]."""
+        n = len(batches)
+        if n == 1 or not self._one_graph:
+            for x, y in batches:
+                self.step(x, y)
+            return
+        if self.t.graph_steps() != n:
+            self.t.set_graph_steps(n)
+        s = self._stream()
+        self.t.set_batches(np.stack([np.asarray(x) for x, _ in batches]), np.stack([np.asarray(y) for _, y in batches]))
+        self.check_watchdog()
+        try:
+            self.t.step_group(s)
+        except RuntimeError as e:   # e.g. a collective refusing capture: one graph per step, loudly
+            import sys
+            print(f"[gru_mpi_cuda_amd] multi-step graph unavailable ({e}); one graph per step", file=sys.stderr)
+            self.t.set_graph_steps(1)
+            for x, y in batches:
+                self.step(x, y)
+
     def loss(self) -> float:
         return self.t.read_loss()
 

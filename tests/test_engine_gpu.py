@@ -324,6 +324,26 @@ def test_sharded_optimizer_step_world1(layers, E, H, opt):
     assert abs(a.loss() - b.loss()) < 1e-4
 
 
+@pytest.mark.parametrize("G,layers,H", [(4, 1, 512), (2, 2, 256), (3, 1, 256)])
+def test_multi_step_graph_matches_single_steps(G, layers, H):
+    """G whole steps captured into one graph (Trainer::set_graph_steps / step_group), each reading its
+    own staging slot, equal G single-step launches bit for bit; two groups in a row exercise both
+    slot groups."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=256, hidden=H, layers=layers, batch=64, seq=8, seed=3)
+    stream = NameStream(cfg.batch, cfg.seq, seed=4)
+    batches = [stream.next() for _ in range(2 * G)]
+    a = HipTrainer(cfg, params=init_params(cfg))
+    b = HipTrainer(cfg, params=init_params(cfg))
+    a.steps(batches[:G])
+    a.steps(batches[G:])
+    for x, y in batches:
+        b.step(x, y)
+    assert a.t.graph_steps() == G
+    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+    assert a.loss() == b.loss()
+
+
 def test_set_batch_device_matches_host():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=48, seq=8, seed=3)
