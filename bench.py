@@ -57,8 +57,8 @@ def main() -> int:
     ap.add_argument("--graph-steps", type=int, default=4,
                     help="hip engine on GPUs: G consecutive training steps captured into one graph launch "
                          "(1..4; the same G full steps, one graph boundary instead of G: ~13 us each at "
-                         "the headline, docs/DESIGN.md §6); used when the warm-up and timed step counts "
-                         "are multiples of G, else 1.  Reported as graph_steps.")
+                         "the headline, docs/DESIGN.md §6); a remainder of K or W modulo G runs as "
+                         "single-step graphs.  Reported as graph_steps.")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -127,16 +127,24 @@ def main() -> int:
         gdist.barrier()
 
     extra = max(0, args.min_warmup - args.warmup) if ctx.device.type == "cuda" else 0   # GPU clock ramp only
-    if args.impl != "hip" or (args.warmup + extra) % G or args.steps % G:
+    if args.impl != "hip":
         G = 1
-    if G > 1:   # G steps per graph launch: the same steps, fewer graph boundaries
-        step = lambda i: tr.steps([pool[(i + j) % len(pool)] for j in range(G)])  # noqa: E731
-    for i in range(0, args.warmup + extra, G):
-        step(i)
+    single = step
+
+    def run(i0, n):
+        """n steps from pool index i0: whole groups of G steps per graph launch (the same steps, fewer
+        graph boundaries), the remainder n % G as single-step graphs"""
+        i = 0
+        while G > 1 and i + G <= n:
+            tr.steps([pool[(i0 + i + j) % len(pool)] for j in range(G)])
+            i += G
+        for k in range(i, n):
+            single(i0 + k)
+
+    run(0, args.warmup + extra)
     sync()
     t0 = time.perf_counter()
-    for i in range(0, args.steps, G):
-        step(args.warmup + extra + i)
+    run(args.warmup + extra, args.steps)
     sync()
     el = time.perf_counter() - t0
     if world > 1:
@@ -144,6 +152,9 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss = final_loss()
+    if G > 1 and hasattr(tr, "t"):
+        # what actually ran: steps() falls back to one graph per step (loudly) if a capture fails
+        G = tr.t.graph_steps()
     tokens = cfg.batch * cfg.seq * args.steps
     value = tokens / el
     if ctx.is_main:

@@ -49,17 +49,17 @@ def _cfg_from(args):
 def save_checkpoint(tr, path: str, fmt: str = "gen") -> None:
     """Weights (reference or generalised layout) + Adam state + step counter (rank 0 writes)."""
     import torch
-    from .models.params import from_flat
     from .utils import ckpt
+    # optimiser state first, on EVERY rank: with a sharded optimiser it is a collective (the moment
+    # slices other ranks own are all-gathered); only then do the non-writing ranks leave
+    if hasattr(tr, "t"):                    # HipTrainer
+        (m, v), step = tr.opt_state(), tr.t.get_step()
+    else:
+        m, v, step = tr.opt_state()
     if getattr(tr, "ctx", None) is not None and not tr.ctx.is_main:
         return
     cfg = tr.cfg
     params = tr.state_dict()
-    if hasattr(tr, "t"):                    # HipTrainer
-        (m, v), step = tr.opt_state(), tr.t.get_step()
-    else:
-        from .models.params import to_flat
-        m, v, step = to_flat(cfg, tr.opt.m), to_flat(cfg, tr.opt.v), tr.opt.step_n
     os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     ckpt.save(path, cfg, params, fmt=fmt,
               opt_state={"m": m, "v": v, "step": torch.tensor([step], dtype=torch.int64)})
@@ -104,7 +104,6 @@ def _read_checkpoint(tr, path: Optional[str]):
 def load_checkpoint(tr, path: Optional[str]) -> int:
     """Restore weights (+ optimiser state when present) into a trainer; returns the step.
     ``path`` is only read on rank 0 (may be None elsewhere)."""
-    from .models.params import from_flat
     params, st = _read_checkpoint(tr, path)
     if hasattr(tr, "t"):
         tr.load_state(params)
@@ -115,11 +114,7 @@ def load_checkpoint(tr, path: Optional[str]) -> int:
         for k in tr.params:
             tr.params[k].copy_(params[k])
         if st is not None:
-            for k, x in from_flat(tr.cfg, st["m"]).items():
-                tr.opt.m[k].copy_(x)
-            for k, x in from_flat(tr.cfg, st["v"]).items():
-                tr.opt.v[k].copy_(x)
-            tr.opt.step_n = int(st["step"][0])
+            tr.load_opt_state(st["m"], st["v"], int(st["step"][0]))
     return int(st["step"][0]) if st is not None else 0
 
 
@@ -133,9 +128,12 @@ def cmd_train(args) -> int:
     ctx = gdist.init(use_gpu=torch.cuda.is_available() and not args.cpu, verbose=True)
     cfg = _cfg_from(args)
     if cfg.lr_sched != "const" and cfg.total_steps <= 0:
-        # decay over this run (a resumed run restores the step counter, so pass --total-steps to
-        # keep one schedule across restarts)
-        cfg = cfg.replace(total_steps=args.steps)
+        if args.resume:
+            # the resumed run restores the step counter: a default of --steps would put the whole run
+            # past the end of the schedule (at lr_min, warm-up skipped)
+            raise SystemExit("--resume with --lr-sched cosine/linear needs --total-steps (the schedule's "
+                             "length across restarts)")
+        cfg = cfg.replace(total_steps=args.steps)   # decay over this run
     comm = make_comm(ctx) if ctx.device.type == "cuda" else None
     tr = make_trainer(cfg, ctx, comm=comm)
     start = load_checkpoint(tr, args.resume) if args.resume else 0

@@ -131,7 +131,9 @@ PYBIND11_MODULE(_C, m) {
       .def("inject_error", &Trainer::inject_error)
       .def("watchdog_status", &Trainer::watchdog_status)
       .def("watchdog_message", &Trainer::watchdog_message)
-      .def("buffer", &Trainer::buffer);
+      .def("buffer", &Trainer::buffer)
+      .def("tail_plan", &Trainer::tail_plan)
+      .def("set_tail_dbg", [](Trainer& t, uintptr_t p) { t.set_tail_dbg(reinterpret_cast<unsigned long long*>(p)); });
 
   py::class_<Generator>(m, "Generator")
       .def(py::init([](py::dict dims, uintptr_t params, std::map<std::string, long> offsets) {
@@ -152,7 +154,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_persist", &Generator::set_persist)
       .def("set_persist_max", &Generator::set_persist_max)
       .def("set_persist_dbg", [](Generator& g, uintptr_t p) { g.set_persist_dbg(reinterpret_cast<unsigned long long*>(p)); })
-      .def("uses_persist", &Generator::uses_persist);
+      .def("uses_persist", &Generator::uses_persist)
+      .def("inject_persist_error", &Generator::inject_persist_error);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)
   m.def("gemm_f32", [](py::dict d, uintptr_t s) {   // fp32 MFMA GEMM of the fp32 generation path

@@ -264,6 +264,10 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);
     HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
+    // the error word is per batch: a spin timeout of an earlier persistent launch (bit 32, which
+    // makes every later wait of that launch give up at once) must not leak into this one
+    HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
+    bool persist_done = false;
     if (uses_persist(n)) {   // one launch for the whole batch: no graph needed
       GenPersistArgs a;
       for (int l = 0; l < d_.L; ++l) {
@@ -274,7 +278,27 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
       a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab32_; a.rf = rf_; a.out = out_; a.probs = probe_;
       a.ws = pws_; a.sync = psync_; a.err = err_; a.dbg = persist_dbg_;
       a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
+      if (inject_) {
+        static const unsigned kBit = 32u;
+        HIP_CHECK(hipMemcpyAsync(err_, &kBit, 4, hipMemcpyHostToDevice, s));
+        inject_ = false;
+      }
       gen_persist_f32(a, s);
+      // small batch, latency-bound launch: check its error word now.  A spin timeout means the
+      // workgroups were not co-resident (something else held CUs): the batch's output is garbage,
+      // so say so, stop using the persistent path and regenerate the batch on the per-char graph.
+      unsigned e = 0;
+      HIP_CHECK(hipMemcpyAsync(&e, err_, 4, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+      persist_done = !(e & 32u);
+      if (!persist_done) {
+        std::fprintf(stderr, "[generator] persistent launch hit its spin limit (error word %u): "
+                             "disabling it, regenerating %d names on the per-char graph\n", e, n);
+        persist_ = false;
+        HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
+      }
+    }
+    if (persist_done) {
     } else if (use_graph_) {
       auto& g = graphs_[n];
       if (!g) {

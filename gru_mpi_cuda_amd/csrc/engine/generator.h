@@ -43,6 +43,9 @@ class Generator {
   void set_persist_dbg(unsigned long long* p) { persist_dbg_ = p; }   // diagnostic stamps (nullable)
   bool uses_persist(int n) const;
   unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
+  // fault injection (tests): the next persistent launch starts with its spin-timeout bit set, as if
+  // an earlier wait had given up -- generate() must notice and regenerate the batch
+  void inject_persist_error() { inject_ = true; }
 
  private:
   void record_steps(int n_active, hipStream_t s);
@@ -77,6 +80,7 @@ class Generator {
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
   bool persist_ = true;
+  bool inject_ = false;
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
   int persist_max_bf16_ = 24;   // ... in the bf16 mode (it runs exact fp32, faster up to ~24 names)
   unsigned long long* persist_dbg_ = nullptr;

@@ -88,6 +88,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
+  size_t o_tsync = R((size_t)tail_sync_words(V, 3 * H, E) * 4);
   // split-K slab: large enough for every weight-gradient product it serves
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
@@ -112,6 +113,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
+  tail_sync_ = arena_.get<unsigned>(o_tsync);   // zero-filled; the tail kernel leaves it zeroed
   slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
   slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
   for (int l = 0; l < L; ++l) {
@@ -583,7 +585,8 @@ void Trainer::record_opt(hipStream_t s) {
       if (!used) rest.job[rest.n++] = D;
     }
     if (rest.n) reduce_slabs_multi(rest, s);
-    adam_cast_multi(a, j, s);
+    if (tail_fused_) record_tail(a, j, s);
+    else adam_cast_multi(a, j, s);
   } else {
     if (deferred_.n) reduce_slabs_multi(deferred_, s);
     adam_step(a, s);
@@ -591,6 +594,54 @@ void Trainer::record_opt(hipStream_t s) {
   }
   deferred_.n = 0;
   HIP_LAUNCH_CHECK();
+}
+
+bool Trainer::tail_ok() const {
+  const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
+  if (comm_ || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
+      V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", true))
+    return false;
+  // the whole tail grid must be resident at once (tail.hip): count its blocks as tail_step does
+  const int H = d_.H, L = d_.L, se = tail_emb_splits();
+  long adam = 0;
+  for (int l = 0; l < L; ++l) {
+    adam += (long)(3 * H / 64) * (H / 64) + 2 * ((3 * H + 1023) / 1024);   // W_hh, b_ih, b_hh
+    if (l > 0) adam += (long)(3 * H / 64) * (H / 64);                      // W_ih (l > 0)
+  }
+  adam += (long)(V / 64) * (H / 64) + (V + 1023) / 1024;                   // W_fc, b_fc
+  const long items = (long)(V / 32) * (H3 / 64) + 1 + adam + (long)(H3 / 64) * (E / 64) +
+                     (long)(V / 64) * (E / 64) * se;
+  return se <= 8 && items <= tail_resident_slots();
+}
+
+// dEmb = dP · W_ih0 (K = 3H) K-split: the same slices as record_emb_tail's GEMMs (so the fused tail
+// and the phased step sum the same partials in the same order: bitwise-equal gradients)
+int Trainer::tail_emb_splits() const {
+  const int V = d_.V, H3 = 3 * d_.H;
+  if (H3 % V == 0 && H3 / V <= splits_ && V % 64 == 0) return H3 / V;
+  int se = splits_;
+  while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
+  return se;
+}
+
+// The fused step tail (tail.hip) in place of reduce_multi + the embedding-side GEMMs + adam_cast
+void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
+  const int V = d_.V, E = d_.E, H3 = 3 * d_.H, nrb = Bp_ / 32;
+  const long tok = (long)d_.T * Bp_;
+  TailArgs t;
+  t.dP_part = dP_part_; t.nslP = nrb; t.V = V; t.H3 = H3; t.dP_bf = dP_bf_; t.dPT_bf = dPT_bf_;
+  t.EmbT = EmbT; t.WihT = Ls_[0].WihT; t.E = E; t.slab_e = slab_e_; t.se = tail_emb_splits();
+  for (int k = 0; k < j.n; ++k) {
+    if (j.job[k].off == off_.at("weight_ih_l0")) t.jw = k;
+    if (j.job[k].off == off_.at("embedding")) t.je = k;
+  }
+  t.loss_part = loss_part_; t.nloss = (int)(tok / 32); t.loss = loss_;
+  t.sync = tail_sync_;
+  t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
+  t.dbg = tail_dbg_;
+  if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
+  tail_items_ = t.nItems;
+  tail_plan_ = {t.nP, 1, t.nA0, t.nW, t.nE};
 }
 
 void Trainer::forward_backward(hipStream_t s) {
@@ -720,6 +771,7 @@ void Trainer::step(hipStream_t s) {
       record_step_body();
     } catch (...) {
       defer_slabs_ = false;
+      tail_fused_ = false;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow
       (void)hipStreamEndCapture(s0_, &broken);
@@ -765,6 +817,7 @@ void Trainer::step_group(hipStream_t s) {
       }
     } catch (...) {
       defer_slabs_ = false;
+      tail_fused_ = false;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;
       (void)hipStreamEndCapture(s0_, &broken);
@@ -796,11 +849,13 @@ void Trainer::record_step_body() {
   } else {
     deferred_.n = 0;
     defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
+    tail_fused_ = tail_ok();
     if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     defer_slabs_ = false;
     record_allreduce(s0_);
   }
   record_opt(s0_);
+  tail_fused_ = false;
 }
 
 float Trainer::read_loss() {

@@ -67,10 +67,33 @@ class Trainer {
   // over the gradients fewer).  slab_job() routes a job to `j` or, when deferring, to deferred_.
   bool defer_slabs_ = false;
   SlabJobs deferred_;
+  // Fused step tail (tail.hip): the dP reduction, loss, embedding-side products and the whole
+  // Adam + bf16 refresh as one launch.  Set while recording a one-graph step that qualifies
+  // (tail_ok(): single GPU, no clipping, fused-dP persistent backward); record_fb_seq then leaves
+  // those pieces to record_opt.  GK_TAIL=0 turns it off.
+  bool tail_fused_ = false;
+  bool tail_ok() const;
+  unsigned* tail_sync_ = nullptr;
+  unsigned long long* tail_dbg_ = nullptr;   // set_tail_dbg(): per-item stamps (TailArgs::dbg)
+  int tail_items_ = 0;
+ public:
+  // item counts of the last recorded fused tail, in item order: dP tiles, loss, Adam dep 0, products,
+  // Adam dep 2, Adam dep 1 (tests, probes)
+  std::vector<int> tail_plan() const { return tail_plan_; }
+  // diagnostic: device buffer of >= 4 * items u64 for the fused tail's per-item stamps (0 = off)
+  void set_tail_dbg(unsigned long long* p) {
+    tail_dbg_ = p;
+    for (auto& g : g_step_) g.reset();
+    for (auto& g : g_group_) g.reset();
+  }
+ private:
+  std::vector<int> tail_plan_;
+  int tail_emb_splits() const;
   void slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst);
   void record_carry(hipStream_t s);     // HS[T] -> HS[0] of every layer and copy (carry_ only)
   bool carry_ = false;
   void record_opt(hipStream_t s0);
+  void record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
   void fwd_step(int l, int t, hipStream_t s);
   void bwd_step(int l, int t, hipStream_t s);
   hipEvent_t ev();

@@ -270,6 +270,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
+      if (l == 0 && tail_fused_) a.bump = step_;   // step counter + tail epoch, read by the fused tail
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       gru_bwd_seq(a, s);
@@ -286,7 +287,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
       if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
-      else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
+      else if (!tail_fused_) j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
+      // (fused tail: the dP tiles are the tail kernel's first items)
     }
     if (l == 0 && q.bwd) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
@@ -294,7 +296,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (dp ? l == L - 1 : l == 0)
       for (int k2 = 0; k2 < tail.n; ++k2)
         slab_job(j, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
-    if (l == 0) {   // + the loss partials and the optimiser step counter
+    if (l == 0 && !tail_fused_) {   // + the loss partials and the optimiser step counter
       j.add(loss_part_, (int)(tok / 32), 1, loss_);
       j.bump = step_;
     }
@@ -374,7 +376,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     record_emb_tail(s, dP_target());
     defer_slabs_ = false;
   }
-  else record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
+  else if (!tail_fused_) record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
   HIP_LAUNCH_CHECK();
 }
 

@@ -734,6 +734,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)(((lk >> 4) * 3 * 512 + lr * 16 + (lk & 15)) * 2);   // exchange lane offset
   zero_next_flags(a.zero_next, a.zero_words);
+  if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) { a.bump[0] += 1; a.bump[1] += 1; }   // read after this launch
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
   // next poll they would delay it (vmcnt retires in order), and they have a whole step to land

@@ -162,6 +162,7 @@ struct SeqBwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
+  int* bump = nullptr;             // [2]: optimiser step counter and fused-tail epoch, +1 each at launch (nullable)
   int T = 0, Bp = 0, H = 0;
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
@@ -393,6 +394,34 @@ struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
   void add(long off, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
     job[n++] = OptCastJob{off, R, C, d, dT, dF, dTF}; } };
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
+
+// ------------------------------------------------------------------ fused step tail (tail.hip)
+// Everything after the backward sequence kernel as ONE launch: the layer-0 table gradient dP (its
+// per-row-block partials -> bf16 dP and dP^T), the loss sum, Adam + bf16 refresh of every tensor,
+// and the embedding-side products dW_ih0 = dP^T Emb and dEmb = dP W_ih0, each output tile followed
+// directly by the Adam update of that tile.  One block per work item; the product items come last
+// in the grid and wait (bounded) on per-column-block counters of the dP tiles.
+struct TailArgs {
+  const float* dP_part = nullptr; int nslP = 0, V = 0, H3 = 0;   // [nslP][V][H3] -> dP_bf, dPT_bf
+  u16* dP_bf = nullptr; u16* dPT_bf = nullptr;
+  const u16* EmbT = nullptr;       // [E][V]   B operand of dW_ih0
+  const u16* WihT = nullptr;       // [E][H3]  B operand of dEmb
+  int E = 0;
+  float* slab_e = nullptr; int se = 1;   // dEmb K-split partials [se][V][E] (H3 / se % 64 == 0)
+  int jw = -1, je = -1;            // W_ih0 / embedding jobs of the OptCastJobs list (updated by the product items)
+  const float* loss_part = nullptr; int nloss = 0; float* loss = nullptr;
+  unsigned* sync = nullptr;        // tail_sync_words(): monotonic counters, zero before the first launch
+  const unsigned* epoch = nullptr; // launches so far incl. this one (bumped before the launch: SeqBwdArgs::bump)
+  unsigned long long* dbg = nullptr;   // diagnostic (nullable): [nItems][4] = start, wait done, end, wg | xcc << 16
+  int nP = 0, nA0 = 0, nW = 0, nE = 0, nItems = 0;   // filled by tail_step()
+};
+// counters: dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of Emb^T / W_ih^T per
+// E-tile (E/64) and per (E-tile, K-slice) (8 E/64), one 64-B line each
+inline long tail_sync_words(int V, int H3, int E) { return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64)) * 16; }
+// false: the grid cannot hold the waiting product items beside the others (the caller takes the
+// phased tail); true: launched
+bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s);
+int tail_resident_slots();   // workgroups of the tail kernel the device holds at once (0: query failed)
 void fill_f32(float* p, long n, float v, hipStream_t s);
 // placement census: out[b] = HW_REG_XCC_ID of the CU that ran block b
 void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);

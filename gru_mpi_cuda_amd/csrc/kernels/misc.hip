@@ -5,6 +5,7 @@
 #include <stdexcept>
 #include "kernels.h"
 #include "common.h"
+#include "optim_dev.h"
 
 namespace gk {
 
@@ -89,23 +90,6 @@ void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
 // One launch for many independent jobs (the tail of a training step is otherwise a chain of
 // tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
 // prefix sum over their block counts.
-// acc = sum over `splits` slabs (stride n floats) of the float4 at src + o, slab order 0,1,2,...
-// (deterministic), with the loads of 8 slabs in flight at once instead of one dependent
-// round trip per slab
-DEV float4 sum_slabs4(const float* __restrict__ src, long n, int splits, size_t o) {
-  float4 acc = *reinterpret_cast<const float4*>(src + o);
-  for (int s0 = 1; s0 < splits; s0 += 8) {
-    float4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (s0 + k < splits) v[k] = *reinterpret_cast<const float4*>(src + (size_t)(s0 + k) * n + o);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (s0 + k < splits) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
-  }
-  return acc;
-}
-
 __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
   __shared__ u16 tile[16][72];   // 144-B rows: the transposed reads (one column, 8 rows) spread over banks
   int b = blockIdx.x, k = 0;
@@ -235,24 +219,6 @@ void cast_multi(CastJobs& j, hipStream_t s) {
   hipLaunchKernelGGL(cast_multi_kernel, dim3(tot), dim3(256), 0, s, j);
 }
 
-// true when the step must not be applied (see OptimArgs::err); uniform over the block
-DEV bool step_failed(const OptimArgs& a) {
-  if (!a.err) return false;
-  const unsigned e = *a.err;
-  if (a.err_host && blockIdx.x == 0 && threadIdx.x == 0) *a.err_host = e;
-  return e != 0u;
-}
-
-// learning rate of update t (1-based): warm-up, then the decay of OptimArgs::sched
-DEV float sched_lr(const OptimArgs& a, int t) {
-  float lr = a.lr;
-  if (a.warmup > 0 && t <= a.warmup) return lr * (float)t / (float)a.warmup;
-  if (a.sched == 0 || a.total <= a.warmup) return lr;
-  const float p = fminf(1.f, (float)(t - a.warmup) / (float)(a.total - a.warmup));
-  const float f = a.sched == 1 ? 0.5f * (1.f + cosf(3.14159265358979f * p)) : 1.f - p;
-  return a.lr_min + (lr - a.lr_min) * f;
-}
-
 __global__ void adam_kernel(OptimArgs a) {
   if (step_failed(a)) return;
   const int t = *a.step;
@@ -291,157 +257,12 @@ void adam_step(const OptimArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks(a.n / 4, 256, 2048)), dim3(256), 0, s, a);
 }
 
-// Adam/SGD update of 4 consecutive elements (same math as adam_kernel)
-struct AdamCoef { float sc, ib1, ib2, lr; };
-DEV AdamCoef adam_coef(const OptimArgs& a) {
-  const int t = *a.step;
-  return AdamCoef{a.gscale ? *a.gscale : 1.f, 1.f / (1.f - powf(a.b1, (float)t)), 1.f / (1.f - powf(a.b2, (float)t)),
-                  sched_lr(a, t)};
-}
-// gradient float4 i (flat index) of job J: from the gradient buffer, or summed from J's slabs
-// (same order as sum_slabs4 in reduce_multi) and written back to the gradient buffer
-DEV float4 job_grad4(const OptimArgs& a, const OptCastJob& J, long i) {
-  if (!J.gsl) return reinterpret_cast<const float4*>(a.g)[i];
-  const long n = J.R ? (long)J.R * J.C : (long)J.C;
-  const float4 g = sum_slabs4(J.gsl, n, J.nsl, (size_t)(i * 4 - J.off));
-  reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
-  return g;
-}
-DEV float4 adam4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, long i /*float4 index*/) {
-  float4 p = reinterpret_cast<float4*>(a.p)[i];
-  const float4 g4 = job_grad4(a, J, i);
-  float pv[4] = {p.x, p.y, p.z, p.w};
-  const float gv[4] = {g4.x * k.sc, g4.y * k.sc, g4.z * k.sc, g4.w * k.sc};
-  if (a.sgd) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pv[e] -= k.lr * (gv[e] + a.wd * pv[e]);
-  } else {
-    const float4 m = reinterpret_cast<float4*>(a.m)[i];
-    const float4 v = reinterpret_cast<float4*>(a.v)[i];
-    float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      mv[e] = a.b1 * mv[e] + (1.f - a.b1) * gv[e];
-      vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
-      float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
-      if (a.wd != 0.f) u += a.wd * pv[e];
-      pv[e] -= k.lr * u;
-    }
-    reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
-    reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-  }
-  p = make_float4(pv[0], pv[1], pv[2], pv[3]);
-  reinterpret_cast<float4*>(a.p)[i] = p;
-  return p;
-}
-
-// adam4 on 4 float4s at element offsets off + q*stride (q = 0..3): every load issued before any
-// update, so one memory round trip instead of four
-DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, long off, long stride,
-                 float4 (&out)[4]) {
-  float4 p[4], g[4], m[4], v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const long i = (off + q * stride) >> 2;
-    p[q] = reinterpret_cast<const float4*>(a.p)[i];
-    g[q] = job_grad4(a, J, i);
-    if (!a.sgd) { m[q] = reinterpret_cast<const float4*>(a.m)[i]; v[q] = reinterpret_cast<const float4*>(a.v)[i]; }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const long i = (off + q * stride) >> 2;
-    float pv[4] = {p[q].x, p[q].y, p[q].z, p[q].w};
-    const float gv[4] = {g[q].x * k.sc, g[q].y * k.sc, g[q].z * k.sc, g[q].w * k.sc};
-    if (a.sgd) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pv[e] -= k.lr * (gv[e] + a.wd * pv[e]);
-    } else {
-      float mv[4] = {m[q].x, m[q].y, m[q].z, m[q].w}, vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        mv[e] = a.b1 * mv[e] + (1.f - a.b1) * gv[e];
-        vv[e] = a.b2 * vv[e] + (1.f - a.b2) * gv[e] * gv[e];
-        float u = (mv[e] * k.ib1) / (sqrtf(vv[e] * k.ib2) + a.eps);
-        if (a.wd != 0.f) u += a.wd * pv[e];
-        pv[e] -= k.lr * u;
-      }
-      reinterpret_cast<float4*>(a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
-      reinterpret_cast<float4*>(a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    }
-    out[q] = make_float4(pv[0], pv[1], pv[2], pv[3]);
-    reinterpret_cast<float4*>(a.p)[i] = out[q];
-  }
-}
-
-// Matrix job: one 64x64 tile per block; thread (ty = tid/16, tx = tid%16) updates rows ty+16q,
-// columns 4tx..4tx+3 with float4 traffic, writes the row-major bf16 copy as 8-B stores, and the
-// transpose leaves through an LDS tile as 16-B stores (8 consecutive rows of one column).
 __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs j) {
-  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)    // [row][col] bf16, padded
+  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
-  const OptCastJob& J = j.job[k];
-  const int t = b - j.blk_start[k];
   if (step_failed(a)) return;
-  const AdamCoef co = adam_coef(a);
-  if (J.R == 0) {   // flat job: 1024 elements per block
-    const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
-    if ((long)t * 1024 + threadIdx.x * 4 < J.C) adam4(a, J, co, i4);
-    return;
-  }
-  const int tiles_c = J.C / 64;
-  const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  float4 upd[4];
-  adam4x4(a, J, co, J.off + (long)(r0 + ty) * J.C + c0 + 4 * tx, 16L * J.C, upd);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = r0 + ty + 16 * q, c = c0 + 4 * tx;
-    const float4 p = upd[q];
-    const u16 h0 = f2bf(p.x), h1 = f2bf(p.y), h2 = f2bf(p.z), h3 = f2bf(p.w);
-    if (J.dst) {
-      uint2 w;
-      w.x = (unsigned)h0 | ((unsigned)h1 << 16);
-      w.y = (unsigned)h2 | ((unsigned)h3 << 16);
-      *reinterpret_cast<uint2*>(J.dst + (size_t)r * J.C + c) = w;
-    }
-    if (!J.dstT && !J.dstF && !J.dstTF) continue;
-    uint2 w2;
-    w2.x = (unsigned)h0 | ((unsigned)h1 << 16);
-    w2.y = (unsigned)h2 | ((unsigned)h3 << 16);
-    *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w2;
-  }
-  if (!J.dstT && !J.dstF && !J.dstTF) return;
-  __syncthreads();
-  if (J.dstT) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int piece = threadIdx.x + 256 * q;          // 64 columns x 8 row segments
-      const int col = piece >> 3, seg = piece & 7;
-      u16 v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
-      *reinterpret_cast<uint4*>(J.dstT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
-    }
-  }
-  // FT copies (fragment-tiled, kernels.h ft_offset): 512 16-B pieces per 64 x 64 tile
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int pc = threadIdx.x + 256 * q;
-    const int fl = pc & 63, fr = (pc >> 6) & 3, fk = pc >> 8;   // lane, 16-row tile, 32-k step
-    const int rr = fr * 16 + (fl & 15), kk = fk * 32 + 8 * (fl >> 4);
-    u16 v[8];
-    if (J.dstF) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[rr][kk + e];
-      *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = *reinterpret_cast<const uint4*>(v);
-    }
-    if (J.dstTF) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[kk + e][rr];
-      *reinterpret_cast<uint4*>(J.dstTF + ft_offset(c0 + rr, r0 + kk, J.R)) = *reinterpret_cast<const uint4*>(v);
-    }
-  }
+  adam_cast_unit<false, false>(a, j.job[k], b - j.blk_start[k], adam_coef(a), tile);
 }
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   int tot = 0;

@@ -288,6 +288,38 @@ class CpuTrainer:
     def grad_dict(self) -> Dict[str, torch.Tensor]:
         return {k: v.detach().clone() for k, v in self.gviews.items()}
 
+    def opt_state(self):
+        """(m, v, step): Adam moments as flat fp32 tensors in the flat layout.  COLLECTIVE when the
+        optimiser is sharded -- every rank all-gathers the owned slices (the tail past world*c is
+        identical everywhere), so all ranks must call it, not only the one that writes."""
+        if self.shard is None:
+            return to_flat(self.cfg, self.opt.m), to_flat(self.cfg, self.opt.v), self.opt.step_n
+        import torch.distributed as dist
+        c, sl = self.shard
+        W, n = self.ctx.world, self.layout.total
+        out = []
+        for mom in (self.opt.m, self.opt.v):
+            flat = torch.zeros(n, dtype=self.flat_p.dtype)
+            if c:
+                parts = list(flat[:W * c].view(W, c).unbind(0))
+                dist.all_gather(parts, mom["own"].contiguous())
+            flat[sl["tail"]] = mom["tail"]
+            out.append(flat)
+        return out[0], out[1], self.opt.step_n
+
+    def load_opt_state(self, m: torch.Tensor, v: torch.Tensor, step: int) -> None:
+        """Inverse of opt_state(): full flat moments in; a sharded rank keeps its own slices."""
+        if self.shard is None:
+            for dst, src in ((self.opt.m, m), (self.opt.v, v)):
+                for k, x in from_flat(self.cfg, src.float()).items():
+                    dst[k].copy_(x)
+        else:
+            _, sl = self.shard
+            for dst, src in ((self.opt.m, m), (self.opt.v, v)):
+                for k, s in sl.items():
+                    dst[k].copy_(src[s])
+        self.opt.step_n = int(step)
+
 
 def make_trainer(cfg: GRUConfig, ctx: DistCtx, comm=None, params=None):
     if ctx.device.type == "cuda":

@@ -5,7 +5,7 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 if "--all" in sys.argv:   # whole trace (e.g. generation, no optimiser marker)
     seg = rows
 else:
-    marks = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"]]
+    marks = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"] or "tail_kernel" in r["Kernel_Name"]]
     a, b = marks[-2], marks[-1]
     seg = rows[a + 1:b + 1]
 t0 = int(seg[0]["Start_Timestamp"]); t1 = int(seg[-1]["End_Timestamp"])

@@ -206,6 +206,29 @@ def test_generator_persistent_fp32(L, E, H, N):
         assert same_b >= 0.95 and same_r >= 0.95, (same_b, same_r)
 
 
+def test_generator_persistent_spin_timeout_recovers():
+    """Fault injection: a persistent launch whose spin-timeout bit is set gives up its
+    waits and writes garbage; generate() must see the bit, regenerate the batch on the per-char
+    graph (same names as a generator with the persistent path off) and leave a clean error word,
+    and a later call must not inherit the bit."""
+    from gru_mpi_cuda_amd.engine.generator import HipGenerator
+    from gru_mpi_cuda_amd.utils.data import random_floats
+    cfg = GRUConfig(vocab=256, embed=128, hidden=512, layers=1, max_len=10, sos=0, eos=0, seed=4)
+    params = init_params(cfg)
+    rf = random_floats(17, cfg.max_len, seed=9)
+    ref_gen = HipGenerator(cfg, params, precision="fp32")
+    ref_gen.g.set_persist(False)
+    want = ref_gen.generate(rf)
+    gen = HipGenerator(cfg, params, precision="fp32")
+    assert gen.g.uses_persist(17)
+    gen.g.inject_persist_error()
+    got = gen.generate(rf)
+    assert (got == want).all()
+    assert not gen.g.uses_persist(17)        # the persistent path is off after a timeout
+    assert gen.g.read_error() == 0
+    assert (gen.generate(rf) == want).all()
+
+
 def test_generator_bf16_mode_small_batch_runs_persistent_fp32():
     """bf16 mode up to 24 names takes the persistent launch, which is exact fp32 and faster there:
     same names as the fp32 mode; above it stays on the bf16 per-char graph."""
