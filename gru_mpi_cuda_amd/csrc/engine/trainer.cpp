@@ -9,6 +9,12 @@ namespace gk {
 
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+static bool env_on(const char* name, bool dflt) {
+  const char* v = std::getenv(name);
+  return v && v[0] ? v[0] != '0' : dflt;
+}
+
+
 Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, float* m, float* v, long nflat,
                  const std::map<std::string, long>& offsets)
     : d_(d), o_(o), params_(params), grads_(grads), m_(m), v_(v), nflat_(nflat), off_(offsets) {
@@ -209,10 +215,6 @@ hipEvent_t Trainer::ev() {
   return events_[ev_next_++];
 }
 
-static bool env_on(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  return v && v[0] ? v[0] != '0' : dflt;
-}
 
 void Trainer::set_carry(bool on) {
   if (on == carry_) return;
@@ -601,17 +603,10 @@ bool Trainer::tail_ok() const {
   if (comm_ || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
       V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", true))
     return false;
-  // the whole tail grid must be resident at once (tail.hip): count its blocks as tail_step does
-  const int H = d_.H, L = d_.L, se = tail_emb_splits();
-  long adam = 0;
-  for (int l = 0; l < L; ++l) {
-    adam += (long)(3 * H / 64) * (H / 64) + 2 * ((3 * H + 1023) / 1024);   // W_hh, b_ih, b_hh
-    if (l > 0) adam += (long)(3 * H / 64) * (H / 64);                      // W_ih (l > 0)
-  }
-  adam += (long)(V / 64) * (H / 64) + (V + 1023) / 1024;                   // W_fc, b_fc
-  const long items = (long)(V / 32) * (H3 / 64) + 1 + adam + (long)(H3 / 64) * (E / 64) +
-                     (long)(V / 64) * (E / 64) * se;
-  return se <= 8 && items <= tail_resident_slots();
+  // tail.hip's conditions: 256-deep K-slices, fewer waiting product blocks than resident slots
+  const int se = tail_emb_splits();
+  const long waiting = (long)(H3 / 64) * (E / 64) + (long)(V / 64) * (E / 64) * se;
+  return se <= 8 && (H3 / se) % 256 == 0 && V % 256 == 0 && waiting < tail_resident_slots();
 }
 
 // dEmb = dP · W_ih0 (K = 3H) K-split: the same slices as record_emb_tail's GEMMs (so the fused tail
@@ -639,6 +634,7 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   t.sync = tail_sync_;
   t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
   t.dbg = tail_dbg_;
+  t.adam_after_dp = env_on("GK_TAIL_ADAM_WAIT", false) ? 1 : 0;
   if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
   tail_items_ = t.nItems;
   tail_plan_ = {t.nP, 1, t.nA0, t.nW, t.nE};

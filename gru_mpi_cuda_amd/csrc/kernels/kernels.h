@@ -413,6 +413,7 @@ struct TailArgs {
   unsigned* sync = nullptr;        // tail_sync_words(): monotonic counters, zero before the first launch
   const unsigned* epoch = nullptr; // launches so far incl. this one (bumped before the launch: SeqBwdArgs::bump)
   unsigned long long* dbg = nullptr;   // diagnostic (nullable): [nItems][4] = start, wait done, end, wg | xcc << 16
+  int adam_after_dp = 0;           // Adam blocks start once a dP column block is complete (the dP chain first)
   int nP = 0, nA0 = 0, nW = 0, nE = 0, nItems = 0;   // filled by tail_step()
 };
 // counters: dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of Emb^T / W_ih^T per

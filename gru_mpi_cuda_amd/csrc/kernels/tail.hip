@@ -20,9 +20,9 @@
 //   the tile's slices to arrive (its atomic add returns the epoch's last count) sums the slabs in
 //   fixed order and runs the Adam + refresh of that tile of Emb, after the dW_ih0 blocks that read
 //   the same Emb^T rows have signalled.  Every product block signals its reads before it waits.
-// * Waits are bounded by wall clock (error bit 8).  Only the product blocks wait, on blocks that
-//   never wait before signalling, and the whole grid is resident at once (checked on the host):
-//   the launch drains whatever the dispatch order.
+// * Waits are bounded by wall clock (error bit 8).  Only the product blocks wait, on points other
+//   blocks reach without waiting first, and there are fewer product blocks than resident slots
+//   (checked on the host): the launch drains whatever the dispatch order.
 // * Counters are monotonic per epoch (the fused-tail launch count, bumped together with the step
 //   counter by the backward kernel before this launch): a column block is complete at
 //   (V / 32) * epoch arrivals, a dEmb tile's last slice sees se * epoch - 1.  Nothing is reset.
@@ -107,43 +107,52 @@ DEV void tail_dp_tile(const TailArgs& t, int id, u16 (*tile)[68]) {
   }
 }
 
-// ---- one 64 x 64 tile of an NT product over K-slice [k0, k0 + kl): 4 waves as 2 x 2 of 32 x 32,
-// register-direct MFMA 16x16x32 bf16 (k-steps in increasing order, like gemm_small), A read with
-// sc1 loads (written in this launch), two k-steps per batch, double-buffered
-DEV void tail_mma(const u16* A, int lda, const u16* B, int ldb, long a_bytes, int row0, int col0, int k0, int kl,
-                  f32x4 (&acc)[2][2]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
-  const int lr = lane & 15, lk = 8 * (lane >> 4);
-  const size_t ra = (size_t)(row0 + wm * 32 + lr), rbb = (size_t)(col0 + wn * 32 + lr);
+// ---- one 64 x 64 tile of an NT product over a K-slice of 8 k-steps (256): 4 waves as 2 x 2 of
+// 32 x 32, register-direct MFMA 16x16x32 bf16, k-steps in increasing order (the MFMA sequence of
+// gemm_small).  Every operand load of the slice is in flight at once: B (written by an earlier
+// launch) is issued by tail_loadB BEFORE the block waits for A (written in this launch, sc1 loads),
+// so only A's latency follows the wait -- one round trip instead of one per k-step pair.
+struct TailFrags { bf16x8 a[8][2], b[8][2]; };
+DEV void tail_loadB(const u16* B, int ldb, int col0, int k0, TailFrags& f) {
+  const int lane = threadIdx.x & 63, wn = (threadIdx.x >> 6) & 1;
+  const u16* p = B + (size_t)(col0 + wn * 32 + (lane & 15)) * ldb + k0 + 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) f.b[ks][c] = ld8(p + (size_t)16 * c * ldb + ks * 32);
+}
+DEV void tail_loadA_sc1(const u16* A, int lda, long a_bytes, int row0, int k0, TailFrags& f) {
+  const int lane = threadIdx.x & 63, wm = (threadIdx.x >> 6) >> 1;
   const brsrc_t rA = brsrc(A, (unsigned)a_bytes);
-  auto ldA = [&](int r, int ks) { return bld8_sc1(rA, (unsigned)(((ra + 16 * r) * lda + k0 + ks * 32 + lk) * 2)); };
-  auto ldB = [&](int c, int ks) { return ld8(B + (rbb + 16 * c) * ldb + k0 + ks * 32 + lk); };
+  const unsigned base = (unsigned)(((size_t)(row0 + wm * 32 + (lane & 15)) * lda + k0 + 8 * (lane >> 4)) * 2);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) f.a[ks][r] = bld8_sc1(rA, base + (unsigned)((16 * r * lda + ks * 32) * 2));
+}
+DEV void tail_mma(const TailFrags& f, f32x4 (&acc)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(f.a[ks][i], f.b[ks][j], acc[i][j]);
+}
+// the whole product tile: K-slices of 256 in order, each slice's B loads issued before `wait`
+// (called once, before the first slice's A loads)
+template <class Wait>
+DEV void tail_product(const u16* A, int lda, long a_bytes, const u16* B, int ldb, int row0, int col0, int k0, int kl,
+                      f32x4 (&acc)[2][2], Wait&& wait) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a0[2][2], b0[2][2], a1[2][2], b1[2][2];   // [k-step of the batch][fragment]
-  auto load = [&](bf16x8 (&a)[2][2], bf16x8 (&b)[2][2], int ks) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int f = 0; f < 2; ++f) { a[kk][f] = ldA(f, ks + kk); b[kk][f] = ldB(f, ks + kk); }
-  };
-  auto mma = [&](const bf16x8 (&a)[2][2], const bf16x8 (&b)[2][2]) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(a[kk][i], b[kk][j], acc[i][j]);
-  };
-  const int nks = kl / 32;   // even (K-slices are multiples of 64)
-  load(a0, b0, 0);
-  for (int ks = 0; ks < nks; ks += 4) {
-    if (ks + 2 < nks) load(a1, b1, ks + 2);
-    mma(a0, b0);
-    if (ks + 4 < nks) load(a0, b0, ks + 4);
-    if (ks + 2 < nks) mma(a1, b1);
+  TailFrags f;
+  for (int kc = 0; kc < kl; kc += 256) {
+    tail_loadB(B, ldb, col0, k0 + kc, f);
+    if (kc == 0) wait();
+    tail_loadA_sc1(A, lda, a_bytes, row0, k0 + kc, f);
+    tail_mma(f, acc);
   }
 }
 // row / column within the 64 x 64 tile of this lane's acc[i][j][e]
@@ -183,16 +192,21 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
     }
   } else if (it < eW) {    // Adam + bf16 refresh (every tensor but W_ih0 / Emb: blk_start skips them)
     const int b = it - eA0;
+    if (t.adam_after_dp) {   // let the dP tiles have the memory system first (spread over the column counters)
+      tail_wait(tail_ctr(t.sync, b % (t.H3 / 64)), colTarget, err);
+      __syncthreads();
+    }
     int k = 0;
     while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
     if (!failed) adam_cast_unit<false, false>(a, j.job[k], b - j.blk_start[k], co, tile);
   } else if (it < eE) {    // dW_ih0 tile (tm, tn) = dP[:, tm]^T · Emb[:, tn] (K = V), then its Adam
     const int id = it - eW, tm = id / ntE, tn = id % ntE;
-    tail_wait(tail_ctr(t.sync, tm), colTarget, err);
-    if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
     f32x4 acc[2][2];
-    tail_mma(t.dPT_bf, t.V, t.EmbT, t.V, (long)t.V * t.H3 * 2, tm * 64, tn * 64, 0, t.V, acc);
+    tail_product(t.dPT_bf, t.V, (long)t.V * t.H3 * 2, t.EmbT, t.V, tm * 64, tn * 64, 0, t.V, acc, [&] {
+      tail_wait(tail_ctr(t.sync, tm), colTarget, err);
+      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();
+    });
     tail_reads_done(rdW + 16 * tn);
     // this tile's refresh rewrites W_ih^T rows tn*64.., columns tm*64..: K-slice tm*64 / kl of the
     // dEmb blocks of E-tile tn, all V/64 of them, must have read it
@@ -208,11 +222,12 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
   } else {                 // dEmb tile (vm, tn) over K-slice ks; the tile's last slice runs its Adam
     const int id = it - eE, ks = id % t.se, tl = id / t.se, vm = tl / ntE, tn = tl % ntE;
     const int kl = t.H3 / t.se;
-    for (int c = ks * kl / 64; c < (ks + 1) * kl / 64; ++c) tail_wait(tail_ctr(t.sync, c), colTarget, err);
-    if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
     f32x4 acc[2][2];
-    tail_mma(t.dP_bf, t.H3, t.WihT, t.H3, (long)t.V * t.H3 * 2, vm * 64, tn * 64, ks * kl, kl, acc);
+    tail_product(t.dP_bf, t.H3, (long)t.V * t.H3 * 2, t.WihT, t.H3, vm * 64, tn * 64, ks * kl, kl, acc, [&] {
+      for (int c = ks * kl / 64; c < (ks + 1) * kl / 64; ++c) tail_wait(tail_ctr(t.sync, c), colTarget, err);
+      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      __syncthreads();
+    });
     tail_reads_done(rdE + 16 * (tn * 8 + ks));
     const long n = (long)t.V * t.E;
     const brsrc_t rS = brsrc(t.slab_e, (unsigned)(t.se * n * 4));
@@ -288,8 +303,10 @@ bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s) {
   t.nItems = t.nP + 1 + t.nA0 + t.nW + t.nE;
   const int occ = tail_occ();
   const int cap = tail_resident_slots();
-  // every block resident at once: a waiting block never holds the slot of one it waits for
-  if (cap <= 0 || t.nItems > cap || t.se > 8) return false;
+  // A product block waits only for points that other blocks reach without waiting first (dP tiles;
+  // product blocks signal their reads before they wait).  With fewer product blocks than resident
+  // slots, a block they wait for always gets a slot: the launch drains whatever the dispatch order.
+  if (cap <= 0 || t.nW + t.nE >= cap || t.se > 8 || (t.H3 / t.se) % 256 || t.V % 256) return false;
   if (t.dbg && t.nItems > 65536) t.dbg = nullptr;
   if (occ == 4) hipLaunchKernelGGL(tail_kernel<4>, dim3(t.nItems), dim3(256), 0, s, a, j, t);
   else hipLaunchKernelGGL(tail_kernel<3>, dim3(t.nItems), dim3(256), 0, s, a, j, t);
