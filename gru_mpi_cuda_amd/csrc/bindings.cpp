@@ -236,6 +236,7 @@ PYBIND11_MODULE(_C, m) {
     HIP_LAUNCH_CHECK();
   });
   m.def("spin_delay", [](int us, uintptr_t s) { spin_delay(us, S(s)); HIP_LAUNCH_CHECK(); });
+  m.def("block_cus", [](int nblocks, int us, uintptr_t s) { block_cus(nblocks, us, S(s)); });
   m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
@@ -398,6 +399,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("allreduce_sum_f32", [](RcclComm& c, uintptr_t p, long n, uintptr_t s) {
         c.allreduce_sum_f32(Pp<float>(p), n, S(s));
+      })
+      .def("allreduce_max_u32", [](RcclComm& c, uintptr_t p, long n, uintptr_t s) {
+        c.allreduce_max_u32(Pp<unsigned>(p), n, S(s));
       })
       .def("broadcast_f32", [](RcclComm& c, uintptr_t p, long n, int root, uintptr_t s) {
         c.broadcast_f32(Pp<float>(p), n, root, S(s));

@@ -49,6 +49,15 @@ void RcclComm::allreduce_avg_f32(float* p, long n, hipStream_t s) {
 void RcclComm::allreduce_sum_f32(float* p, long n, hipStream_t s) {
   RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclSum, C(live()), s));
 }
+void RcclComm::allreduce_max_u32(unsigned* p, long n, hipStream_t s) {
+  RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclUint32, ncclMax, C(live()), s));
+}
+void RcclComm::allreduce_avg_f32_err(float* p, long n, unsigned* err, hipStream_t s) {
+  RCCL_CHECK(ncclGroupStart());
+  if (n > 0) RCCL_CHECK(ncclAllReduce(p, p, (size_t)n, ncclFloat32, ncclAvg, C(live()), s));
+  RCCL_CHECK(ncclAllReduce(err, err, 1, ncclUint32, ncclMax, C(live()), s));
+  RCCL_CHECK(ncclGroupEnd());
+}
 void RcclComm::broadcast_f32(float* p, long n, int root, hipStream_t s) {
   RCCL_CHECK(ncclBroadcast(p, p, (size_t)n, ncclFloat32, root, C(live()), s));
 }

@@ -20,6 +20,10 @@ class RcclComm {
   ~RcclComm();
   void allreduce_avg_f32(float* p, long n, hipStream_t s);
   void allreduce_sum_f32(float* p, long n, hipStream_t s);
+  void allreduce_max_u32(unsigned* p, long n, hipStream_t s);
+  // the step's last gradient collective grouped (one launch) with a max-reduction of the step error
+  // word: every rank then sees a spin timeout of ANY rank and skips the update together
+  void allreduce_avg_f32_err(float* p, long n, unsigned* err, hipStream_t s);
   void broadcast_f32(float* p, long n, int root, hipStream_t s);
   void allgather_u8(const unsigned char* send, unsigned char* recv, long n, hipStream_t s);
   // sharded optimiser (ZeRO-1 style): recv[n] = mean over ranks of send[rank*n .. rank*n+n)

@@ -94,7 +94,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
-  size_t o_tsync = R((size_t)tail_sync_words(V, 3 * H, E) * 4);
+  size_t o_tsync = R((size_t)tail_sync_words(V, 3 * H, E, H) * 4);
   // split-K slab: large enough for every weight-gradient product it serves
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
@@ -529,8 +529,10 @@ void Trainer::record_sharded_opt(hipStream_t s) {
   // in-place reduce-scatter: the owned slice's mean lands at grads_ + r*c, where Adam reads it
   if (c > 0) comm_->reduce_scatter_avg_f32(grads_, grads_ + (long)r * c, c, s);
   if (tail > 0) {
-    comm_->allreduce_avg_f32(grads_ + (long)W * c, tail, s);
+    comm_->allreduce_avg_f32_err(grads_ + (long)W * c, tail, err_, s);
     ar_log_.push_back({(long)W * c, tail});
+  } else {
+    comm_->allreduce_max_u32(err_, 1, s);   // every rank skips a step that failed anywhere
   }
   // the fused optimiser launch's flat path (same update code as the replicated step), no casts:
   // the bf16 copies are refreshed from the gathered masters below
@@ -629,6 +631,13 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   for (int k = 0; k < j.n; ++k) {
     if (j.job[k].off == off_.at("weight_ih_l0")) t.jw = k;
     if (j.job[k].off == off_.at("embedding")) t.je = k;
+    if (j.job[k].off == off_.at("fc.weight")) t.jf = k;
+    if (j.job[k].off == off_.at("fc.bias")) t.jb = k;
+  }
+  if (tail_nfc_) {   // dW_fc / db_fc (record_fb_seq left them to the tail)
+    const int L = d_.L, T = d_.T, B = Bp_;
+    t.dlT = dlT_; t.ldl = (int)tok; t.HTop = Ls_[L - 1].HT + B; t.ldh = (T + 1) * B;
+    t.slab_fc = slab_fc2_; t.rs_fc = rs_fc2_; t.nfc = tail_nfc_; t.tok = (int)tok; t.H = d_.H;
   }
   t.loss_part = loss_part_; t.nloss = (int)(tok / 32); t.loss = loss_;
   t.sync = tail_sync_;
@@ -637,7 +646,7 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   t.adam_after_dp = env_on("GK_TAIL_ADAM_WAIT", false) ? 1 : 0;
   if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
   tail_items_ = t.nItems;
-  tail_plan_ = {t.nP, 1, t.nA0, t.nW, t.nE};
+  tail_plan_ = {t.nF, t.nP, 1, t.nA0, t.nW, t.nE};
 }
 
 void Trainer::forward_backward(hipStream_t s) {
@@ -708,22 +717,27 @@ long Trainer::group_end(int l) const {
   return off_.at("weight_ih_l0") + (dP_inplace_ ? (long)d_.V * 3 * d_.H : 0L);
 }
 
-void Trainer::ar_flush(hipStream_t s, bool force) {
+bool Trainer::ar_flush(hipStream_t s, bool force, bool with_err) {
   const long n = ar_ready_ - ar_launched_;
-  if (n <= 0 || (!force && n < min_bucket_)) return;
+  if (n <= 0 || (!force && n < min_bucket_)) return false;
+  auto reduce = [&](hipStream_t st) {
+    if (with_err) comm_->allreduce_avg_f32_err(grads_ + ar_launched_, n, err_, st);
+    else comm_->allreduce_avg_f32(grads_ + ar_launched_, n, st);
+  };
   if (!env_on("GK_AR_FORK", true)) {   // A/B switch: the collective in line on the step stream
-    comm_->allreduce_avg_f32(grads_ + ar_launched_, n, s);
+    reduce(s);
     ar_log_.push_back({ar_launched_, n});
     ar_launched_ = ar_ready_;
-    return;
+    return true;
   }
   hipEvent_t e = ev();
   HIP_CHECK(hipEventRecord(e, s));          // fork: everything recorded on s so far
   HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
-  comm_->allreduce_avg_f32(grads_ + ar_launched_, n, sc_);
+  reduce(sc_);
   ar_log_.push_back({ar_launched_, n});
   ar_launched_ = ar_ready_;
   ar_busy_ = true;
+  return true;
 }
 
 void Trainer::ar_join(hipStream_t s) {
@@ -735,9 +749,15 @@ void Trainer::ar_join(hipStream_t s) {
 }
 
 void Trainer::record_allreduce(hipStream_t s) {
-  // plain bucketed mean all-reduce of the whole flat fp32 gradient after the backward
+  // plain bucketed mean all-reduce of the whole flat fp32 gradient after the backward; the last
+  // bucket carries the error word (max over ranks) so every rank skips a failed step together
   if (!comm_) return;
-  for (const auto& b : buckets_) comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
+  for (size_t i = 0; i < buckets_.size(); ++i) {
+    const auto& b = buckets_[i];
+    if (i + 1 == buckets_.size()) comm_->allreduce_avg_f32_err(grads_ + b.first, b.second, err_, s);
+    else comm_->allreduce_avg_f32(grads_ + b.first, b.second, s);
+  }
+  if (buckets_.empty()) comm_->allreduce_max_u32(err_, 1, s);
 }
 
 void Trainer::enable_watchdog(int timeout_ms) {
@@ -891,6 +911,7 @@ uintptr_t Trainer::buffer(const std::string& n) const {
   if (n == "loss") return u(loss_);
   if (n == "dl") return u(dl_);
   if (n == "step") return u(step_);
+  if (n == "err") return u(err_);
   if (n.rfind("HSf", 0) == 0) return u(Ls_.at(std::stoi(n.substr(3))).HSf);
   if (n.rfind("dy", 0) == 0) return u(Ls_.at(std::stoi(n.substr(2))).dy);
   throw std::runtime_error("unknown buffer " + n);

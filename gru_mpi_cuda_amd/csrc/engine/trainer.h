@@ -72,6 +72,7 @@ class Trainer {
   // (tail_ok(): single GPU, no clipping, fused-dP persistent backward); record_fb_seq then leaves
   // those pieces to record_opt.  GK_TAIL=0 turns it off.
   bool tail_fused_ = false;
+  int tail_nfc_ = 0;             // dW_fc K-slices computed inside the fused tail (0: before the backward)
   bool tail_ok() const;
   unsigned* tail_sync_ = nullptr;
   unsigned long long* tail_dbg_ = nullptr;   // set_tail_dbg(): per-item stamps (TailArgs::dbg)
@@ -146,7 +147,8 @@ class Trainer {
   // joins the comm stream before launching the next one.
   bool dp_overlap() const { return comm_ != nullptr && !overlap_; }
   long group_end(int l) const;       // end of layer l's readiness group (l == L: the FC group)
-  void ar_flush(hipStream_t s, bool force);
+  // returns true when a collective was recorded; with_err: it also max-reduces the error word
+  bool ar_flush(hipStream_t s, bool force, bool with_err = false);
   void ar_join(hipStream_t s);
   float* dP_target() { return dP_inplace_ ? G("weight_ih_l0") : dP_; }
   hipStream_t sc_ = nullptr;

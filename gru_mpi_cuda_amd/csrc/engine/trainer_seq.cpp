@@ -249,9 +249,14 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ws.splits = (int)(tok / kslice); ws.algo = 3;
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
     }
-    gemm_nt(w, s);
-    tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
-    tail.add(rs_fc2_, sp, V, G("fc.bias"));
+    // fused tail: the same K-slices as blocks of the tail launch (their last slice per tile runs that
+    // tile's Adam), so no launch here and no slab jobs
+    tail_nfc_ = (tail_fused_ && w.algo == 3 && (tok / sp) % 256 == 0 && env_flag("GK_TAIL_FC", true)) ? sp : 0;
+    if (!tail_nfc_) {
+      gemm_nt(w, s);
+      tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
+      tail.add(rs_fc2_, sp, V, G("fc.bias"));
+    }
   }
   // ------------------------------------------------------------------ backward (BPTT)
   for (int l = L - 1; l >= 0; --l) {
@@ -319,27 +324,37 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       }
       if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
         ar_ready_ = group_end(0);
+        // The step's LAST collective carries the error word along (max over ranks, same launch):
+        // a persistent kernel that gave up on ANY rank makes every rank skip the update.
         if (!ar_busy_) {
           // nothing left to overlap with: the last collectives go on the step stream itself (a
           // fork + join around them only adds graph edges -- measured: a forked branch in the
           // step graph slowed the kernels beside it)
-          if (ar_ready_ > ar_launched_) {
-            comm_->allreduce_avg_f32(grads_ + ar_launched_, ar_ready_ - ar_launched_, s);
-            ar_log_.push_back({ar_launched_, ar_ready_ - ar_launched_});
+          const long n = ar_ready_ - ar_launched_;
+          if (n > 0) {
+            if (dP_inplace_) comm_->allreduce_avg_f32_err(grads_ + ar_launched_, n, err_, s);
+            else comm_->allreduce_avg_f32(grads_ + ar_launched_, n, s);
+            ar_log_.push_back({ar_launched_, n});
             ar_launched_ = ar_ready_;
           }
           if (!dP_inplace_) {
-            comm_->allreduce_avg_f32(dP_, (long)V * H3, s);
+            comm_->allreduce_avg_f32_err(dP_, (long)V * H3, err_, s);
             ar_log_.push_back({-1, (long)V * H3});
+          } else if (n <= 0) {
+            comm_->allreduce_max_u32(err_, 1, s);
           }
         } else {
-          ar_flush(s, true);
-          if (!dP_inplace_) {
+          const bool sent = ar_flush(s, true, /*with_err=*/dP_inplace_);
+          if (!dP_inplace_ || !sent) {
             hipEvent_t e = ev();
             HIP_CHECK(hipEventRecord(e, s));
             HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
-            comm_->allreduce_avg_f32(dP_, (long)V * H3, sc_);
-            ar_log_.push_back({-1, (long)V * H3});
+            if (!dP_inplace_) {
+              comm_->allreduce_avg_f32_err(dP_, (long)V * H3, err_, sc_);
+              ar_log_.push_back({-1, (long)V * H3});
+            } else {
+              comm_->allreduce_max_u32(err_, 1, sc_);
+            }
           }
           ar_join(s);
         }

@@ -45,7 +45,22 @@ DEV bf16x8 ld8_sc1s(rsrc_t r, unsigned voff, int soff) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-static constexpr unsigned kSpinLimit = 1u << 21;   // x s_sleep(2): ~0.3 s, >> any real wait
+// Every cross-workgroup wait is bounded by WALL CLOCK, not by a poll count: workgroups that start
+// late because something else holds their CUs (an RCCL kernel of a data-parallel step waiting for a
+// slow peer, another process's kernel) delay the wait without tripping it.  5 s of the 100 MHz
+// s_memrealtime counter, checked every 64 polls; past it the wait sets the error word and gives up
+// (the step's update is skipped on every rank and the watchdog reports it).
+static constexpr unsigned long long kSpinTicks = 500000000ull;
+struct SpinBudget {
+  unsigned long long t0 = 0;
+  unsigned n = 0;
+  DEV bool expired() {
+    if ((n++ & 63u) != 0u) return false;
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    if (!t0) { t0 = now; return false; }
+    return now - t0 > kSpinTicks;
+  }
+};
 
 // Per-producer epoch flags: producer p of a row block owns flags[p * kFlagStride] (its own 64-B
 // line, no read-modify-write contention); after its payload drained it stores the epoch with a
@@ -58,14 +73,14 @@ static constexpr int kFlagStride = 16;   // uints (64 B)
 DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* err) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    unsigned spins = 0;
+    SpinBudget spin;
     for (;;) {
       bool ok = true;
       if (lane < nprod) ok = __hip_atomic_load(flags + lane * kFlagStride, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT) >= epoch;
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
+      if (spin.expired()) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -79,14 +94,14 @@ DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* 
 // H/16 producers.  The acquire-at-wavefront fence only pins the following sc1 loads below
 // the poll (no instruction is emitted).
 DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch, unsigned* err) {
-  unsigned spins = 0;
+  SpinBudget spin;
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT) >= epoch;
     if (__all(ok)) break;
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > kSpinLimit) {
+    if (spin.expired()) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -102,7 +117,8 @@ template <int NK, class LoadK>
 DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned epoch, unsigned* err,
                         LoadK&& loadk) {
   constexpr unsigned all = (1u << NK) - 1u;
-  unsigned loaded = 0, spins = 0;
+  unsigned loaded = 0;
+  SpinBudget spin;
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
@@ -117,7 +133,7 @@ DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned e
       }
     if (loaded == all) break;
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > kSpinLimit) {
+    if (spin.expired()) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk)
@@ -138,7 +154,8 @@ DEV void wave_wait_load2(const unsigned* fa, const unsigned* fb, int prod0, unsi
   const bool active = (lane & 31) < 2 * NK;
   const unsigned* f = (lane < 32 ? fa : fb) + (size_t)(prod0 + (lane & 31)) * kFlagStride;
   const unsigned ep = lane < 32 ? ea : eb;
-  unsigned da = 0, db = 0, spins = 0;
+  unsigned da = 0, db = 0;
+  SpinBudget spin;
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ep;
@@ -157,7 +174,7 @@ DEV void wave_wait_load2(const unsigned* fa, const unsigned* fb, int prod0, unsi
     }
     if (da == all && db == all) break;
     __builtin_amdgcn_s_sleep(1);
-    if (++spins > kSpinLimit) {
+    if (spin.expired()) {
       if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int kk = 0; kk < NK; ++kk) {   // garbage, flagged: keep the grid draining
@@ -220,12 +237,13 @@ DEV bool row_block_local(unsigned* flags /* the row block's producer lines */, i
     __hip_atomic_store(flags + ut * kFlagStride + 1, id + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    unsigned v = id + 1u, spins = 0;
+    unsigned v = id + 1u;
+    SpinBudget spin;
     for (;;) {
       if (lane < nunit) v = __hip_atomic_load(flags + lane * kFlagStride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__all(v != 0u)) break;
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kSpinLimit) {
+      if (spin.expired()) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

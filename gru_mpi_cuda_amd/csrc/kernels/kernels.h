@@ -414,11 +414,21 @@ struct TailArgs {
   const unsigned* epoch = nullptr; // launches so far incl. this one (bumped before the launch: SeqBwdArgs::bump)
   unsigned long long* dbg = nullptr;   // diagnostic (nullable): [nItems][4] = start, wait done, end, wg | xcc << 16
   int adam_after_dp = 0;           // Adam blocks start once a dP column block is complete (the dP chain first)
-  int nP = 0, nA0 = 0, nW = 0, nE = 0, nItems = 0;   // filled by tail_step()
+  // dW_fc = dl^T · H_top and db_fc = row sums of dl^T over nfc K-slices of tokens (0: not in the
+  // tail; the W_fc / b_fc jobs then take their gradient as before).  Slice s goes to slab s of
+  // slab_fc / rs_fc; a tile's LAST slice sums the slabs and runs the Adam of that W_fc tile (and of
+  // its 64 b_fc elements for the first column tile).  Nothing waits for these blocks.
+  const u16* dlT = nullptr; int ldl = 0;    // [V][ldl] bf16 dlogits^T
+  const u16* HTop = nullptr; int ldh = 0;   // [H][ldh] bf16 top-layer h^T (token columns)
+  float* slab_fc = nullptr; float* rs_fc = nullptr;   // [nfc][V][H], [nfc][V]
+  int nfc = 0, tok = 0, H = 0, jf = -1, jb = -1;
+  int nF = 0, nP = 0, nA0 = 0, nW = 0, nE = 0, nItems = 0;   // filled by tail_step()
 };
-// counters: dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of Emb^T / W_ih^T per
-// E-tile (E/64) and per (E-tile, K-slice) (8 E/64), one 64-B line each
-inline long tail_sync_words(int V, int H3, int E) { return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64)) * 16; }
+// counters (one 64-B line each): dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of
+// Emb^T per E-tile (E/64) and of W_ih^T per (E-tile, K-slice) (8 E/64), dW_fc tiles ((V/64)(H/64))
+inline long tail_sync_words(int V, int H3, int E, int H) {
+  return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64) + (V / 64) * (H / 64)) * 16;
+}
 // false: the grid cannot hold the waiting product items beside the others (the caller takes the
 // phased tail); true: launched
 bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s);
@@ -428,6 +438,8 @@ void fill_f32(float* p, long n, float v, hipStream_t s);
 void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)
 void spin_delay(int us, hipStream_t s);
+// fault injection: nblocks blocks each holding a whole CU's LDS for `us` microseconds (capped at 5 s)
+void block_cus(int nblocks, int us, hipStream_t s);
 
 // Batch preparation on device: in = [hdr 16 ints: B, float-bits of 1/#valid][x Bmax*T][y Bmax*T]
 // batch-major int32 (may be pinned host memory, read zero-copy); out ids/labels time-major [T][Bp]

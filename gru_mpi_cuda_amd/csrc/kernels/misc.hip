@@ -355,6 +355,25 @@ void spin_delay(int us, hipStream_t s) {
   hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, (unsigned long long)capped * 100ull);
 }
 
+// CU blocker (fault injection): one 64-thread block per CU holding the CU's whole LDS for `ticks`
+// of the 100 MHz clock, so no workgroup that needs LDS can start there meanwhile -- a stand-in for
+// an RCCL kernel that holds CUs while it waits for a slow peer.  The loop always ends.
+__global__ void block_cu_kernel(unsigned long long ticks) {
+  extern __shared__ unsigned char lds_block[];
+  if (threadIdx.x == 0) lds_block[0] = 1;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+void block_cus(int nblocks, int us, hipStream_t s) {
+  const long capped = us < 0 ? 0 : (us > 5000000 ? 5000000 : us);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)block_cu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(block_cu_kernel, dim3(nblocks), dim3(64), 160 * 1024, s, (unsigned long long)capped * 100ull);
+}
+
 // Placement census (diagnostic): out[b] = XCC id of the CU that ran block b (HW_REG_XCC_ID).
 __global__ void xcc_census_kernel(unsigned* out) {
   unsigned id;

@@ -9,8 +9,12 @@
 // Only the embedding side depends on the dP chain; the bulk of the Adam bytes (W_hh, W_fc, the
 // biases) does not.  Here every piece is a block of one grid:
 //
-//   blocks  [dP tiles] [loss] [Adam: every tensor but W_ih0 / Emb] [dW_ih0 tiles] [dEmb K-slices]
-//                                                                   wait: their dP column blocks
+//   blocks  [dW_fc K-slices] [dP tiles] [loss] [Adam: the other tensors] [dW_ih0 tiles] [dEmb K-slices]
+//                                                                          wait: their dP column blocks
+//
+// * A dW_fc block computes one 64 x 64 tile of dW_fc = dl^T H (+ the b_fc row sums) over one token
+//   slice into a partial slab; the tile's last slice to arrive sums the slabs and runs the Adam of
+//   that W_fc tile (and b_fc).  These replace the separate dW_fc launch before the backward.
 //
 // * A dW_ih0 block computes one 64 x 64 output tile (K = V, unsplit) and then runs the Adam +
 //   refresh of exactly that tile of W_ih0 from the gradient it holds in LDS (no hand-off) -- once
@@ -140,9 +144,10 @@ DEV void tail_mma(const TailFrags& f, f32x4 (&acc)[2][2]) {
 }
 // the whole product tile: K-slices of 256 in order, each slice's B loads issued before `wait`
 // (called once, before the first slice's A loads)
+// rs (do_rs): this lane's partial row sums of its two A fragments, in the order of gemm_small's
 template <class Wait>
 DEV void tail_product(const u16* A, int lda, long a_bytes, const u16* B, int ldb, int row0, int col0, int k0, int kl,
-                      f32x4 (&acc)[2][2], Wait&& wait) {
+                      f32x4 (&acc)[2][2], Wait&& wait, float* rs = nullptr) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -153,6 +158,13 @@ DEV void tail_product(const u16* A, int lda, long a_bytes, const u16* B, int ldb
     if (kc == 0) wait();
     tail_loadA_sc1(A, lda, a_bytes, row0, k0 + kc, f);
     tail_mma(f, acc);
+    if (rs)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rs[i] += (float)f.a[ks][i][e];
   }
 }
 // row / column within the 64 x 64 tile of this lane's acc[i][j][e]
@@ -163,6 +175,7 @@ template <int MINW>   // minimum waves per SIMD (= resident 256-thread workgroup
 __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJobs j, TailArgs t) {
   __shared__ __attribute__((aligned(16))) u16 tile[64][68];
   __shared__ __attribute__((aligned(16))) float gt[64][68];   // a product tile's fp32 gradient
+  __shared__ __attribute__((aligned(16))) float gb[64];       // b_fc gradients of a dW_fc row tile
   __shared__ unsigned s_prev;
   const int it = blockIdx.x;
   if (t.dbg && threadIdx.x == 0) {
@@ -177,12 +190,74 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
   const unsigned ep = *t.epoch;
   const int ntE = t.E / 64;
   const unsigned colTarget = (unsigned)(t.V / 32) * ep;
-  const int eA0 = t.nP + 1, eW = eA0 + t.nA0, eE = eW + t.nW;
+  const int eP = t.nF, eL = eP + t.nP, eA0 = eL + 1, eW = eA0 + t.nA0, eE = eW + t.nW;
   unsigned* rdW = tail_ctr(t.sync, t.H3 / 64 + (t.V / 64) * ntE);   // [E/64]: dW_ih0 blocks done reading Emb^T
   unsigned* rdE = rdW + 16 * ntE;                                     // [E/64][8]: dEmb blocks done reading W_ih^T
-  if (it < t.nP) {
-    tail_dp_tile(t, it, tile);
-    (void)tail_arrive(tail_ctr(t.sync, it % (t.H3 / 64)), &s_prev);   // its column block
+  unsigned* cFc = rdE + 16 * 8 * ntE;                                 // [V/64][H/64]: dW_fc slices arrived
+  if (it < eP) {           // dW_fc tile (tm, tn) over token slice sp; the tile's last slice runs its Adam
+    const int ntH = t.H / 64, ntV = t.V / 64;
+    const int tn = it % ntH, tm = (it / ntH) % ntV, sp = it / (ntH * ntV);
+    const int kl = t.tok / t.nfc;
+    const bool do_rs = tn == 0 && ((threadIdx.x >> 6) & 1) == 0;
+    float rs[2] = {0.f, 0.f};
+    f32x4 acc[2][2];
+    tail_product(t.dlT, t.ldl, (long)t.V * t.ldl * 2, t.HTop, t.ldh, tm * 64, tn * 64, sp * kl, kl, acc, [] {},
+                 do_rs ? rs : nullptr);
+    const long n = (long)t.V * t.H;
+    const brsrc_t rS = brsrc(t.slab_fc, (unsigned)(t.nfc * n * 4));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const size_t o = (size_t)sp * n + (size_t)(tm * 64 + acc_row(i, e)) * t.H + tn * 64 + acc_col(jj);
+          bst1_sc1(rS, (unsigned)(o * 4), acc[i][jj][e]);
+        }
+    if (do_rs) {   // as gemm_small: lane partials over lane >> 4, then lanes 0..15 hold the 16 rows
+      const int lane = threadIdx.x & 63;
+      const brsrc_t rR = brsrc(t.rs_fc, (unsigned)(t.nfc * t.V * 4));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        float v = rs[i];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16)
+          bst1_sc1(rR, (unsigned)(((size_t)sp * t.V + tm * 64 + ((threadIdx.x >> 6) >> 1) * 32 + i * 16 + lane) * 4), v);
+      }
+    }
+    const unsigned prev = tail_arrive(cFc + 16 * (tm * ntH + tn), &s_prev);
+    if (prev == (unsigned)t.nfc * ep - 1u) {   // last slice of this tile: every slab is published
+      const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const size_t o = (size_t)(tm * 64 + ty + 16 * q) * t.H + tn * 64 + 4 * tx;
+        *reinterpret_cast<float4*>(&gt[ty + 16 * q][4 * tx]) = sum_slabs4<true>(t.slab_fc, n, t.nfc, o);
+      }
+      if (tn == 0 && threadIdx.x < 16)   // this row tile's 64 b_fc gradients (row 0 of the tile holds them)
+        *reinterpret_cast<float4*>(&gb[4 * threadIdx.x]) =
+            sum_slabs4<true>(t.rs_fc, t.V, t.nfc, (size_t)tm * 64 + 4 * threadIdx.x);
+      __syncthreads();
+      if (!failed) {
+        adam_cast_unit<false, false>(a, j.job[t.jf], tm * ntH + tn, co, tile, gt);
+        if (tn == 0 && threadIdx.x < 16) {   // b_fc elements tm*64 .. +63: one float4 per thread
+          const OptCastJob& J = j.job[t.jb];
+          const long i4 = (J.off >> 2) + tm * 16 + threadIdx.x;
+          float4 p = reinterpret_cast<float4*>(a.p)[i4];
+          const float4 g = *reinterpret_cast<const float4*>(&gb[4 * threadIdx.x]);
+          float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m;
+          if (!a.sgd) { m = reinterpret_cast<float4*>(a.m)[i4]; v = reinterpret_cast<float4*>(a.v)[i4]; }
+          adam_update4(a, co, p, g, m, v);
+          if (!a.sgd) { reinterpret_cast<float4*>(a.m)[i4] = m; reinterpret_cast<float4*>(a.v)[i4] = v; }
+          reinterpret_cast<float4*>(a.p)[i4] = p;
+          reinterpret_cast<float4*>(const_cast<float*>(a.g))[i4] = g;
+        }
+      }
+    }
+  } else if (it < eL) {
+    const int id = it - eP;
+    tail_dp_tile(t, id, tile);
+    (void)tail_arrive(tail_ctr(t.sync, id % (t.H3 / 64)), &s_prev);   // its column block
   } else if (it < eA0) {   // loss = sum of the per-block partials, fixed order (one wave)
     if (threadIdx.x < 64) {
       float acc = 0.f;
@@ -287,20 +362,28 @@ bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s) {
   const OptCastJob &W = j.job[t.jw], &Em = j.job[t.je];
   if (W.R != t.H3 || W.C != t.E || Em.R != t.V || Em.C != t.E)
     throw std::runtime_error("tail_step: W_ih0 / embedding jobs do not match the products");
+  if (t.nfc) {
+    if (!t.dlT || !t.HTop || !t.slab_fc || !t.rs_fc || t.tok % t.nfc || (t.tok / t.nfc) % 256 || t.H % 64 ||
+        t.jf < 0 || t.jb < 0 || t.jf >= j.n || t.jb >= j.n || j.job[t.jf].R != t.V || j.job[t.jf].C != t.H ||
+        j.job[t.jb].R != 0 || j.job[t.jb].C != t.V || t.ldl % 8 || t.ldh % 8)
+      throw std::runtime_error("tail_step: inconsistent dW_fc arguments");
+  }
   int tot = 0;
   for (int k = 0; k < j.n; ++k) {
     const OptCastJob& J = j.job[k];
     if (J.R && (J.R % 64 || J.C % 64)) throw std::runtime_error("tail_step: matrix job needs R, C % 64 == 0");
     if (!J.R && J.C % 4) throw std::runtime_error("tail_step: flat job needs C % 4 == 0");
     j.blk_start[k] = tot;
-    if (k != t.jw && k != t.je) tot += J.R == 0 ? (J.C + 1023) / 1024 : (J.R / 64) * (J.C / 64);
+    const bool in_products = k == t.jw || k == t.je || (t.nfc && (k == t.jf || k == t.jb));
+    if (!in_products) tot += J.R == 0 ? (J.C + 1023) / 1024 : (J.R / 64) * (J.C / 64);
   }
   j.blk_start[j.n] = tot;
+  t.nF = t.nfc ? (t.V / 64) * (t.H / 64) * t.nfc : 0;
   t.nP = (t.V / 32) * (t.H3 / 64);
   t.nA0 = tot;
   t.nW = (t.H3 / 64) * (t.E / 64);
   t.nE = (t.V / 64) * (t.E / 64) * t.se;
-  t.nItems = t.nP + 1 + t.nA0 + t.nW + t.nE;
+  t.nItems = t.nF + t.nP + 1 + t.nA0 + t.nW + t.nE;
   const int occ = tail_occ();
   const int cap = tail_resident_slots();
   // A product block waits only for points that other blocks reach without waiting first (dP tiles;

@@ -113,6 +113,8 @@ class HipTrainer:
         base = self.grads.data_ptr()
         for a, b in self.buckets:
             self.comm.allreduce_avg_f32(base + 4 * a, b - a, s)
+        # the step error word, max over ranks: a step that failed anywhere is skipped everywhere
+        self.comm.allreduce_max_u32(self.t.buffer("err"), 1, s)
 
     def optimizer_step(self) -> None:
         self.t.optimizer_step(self._stream())
@@ -245,6 +247,7 @@ class CpuTrainer:
         self.buckets = _bucket_list(cfg, self.layout.total)
         self._loss = float("nan")
         self._state = None            # carried hidden state (cfg.carry_hidden)
+        self._err = 0                 # step error word (inject_error), max-reduced over ranks
 
     def reset_state(self) -> None:
         self._state = None
@@ -260,10 +263,24 @@ class CpuTrainer:
             self.gviews[k].copy_(g)
         self._loss = float(loss)
 
+    def inject_error(self, bits: int = 1) -> None:
+        """Fault injection twin of Trainer::inject_error: this rank's step error word (sticky)."""
+        self._err |= int(bits)
+
+    def error_word(self) -> int:
+        return self._err
+
     def allreduce_grads(self) -> None:
         allreduce_mean_buckets(self.flat_g, self.buckets, self.ctx.world)
+        if self.ctx.world > 1:   # max over ranks, like the device word in the last collective
+            import torch.distributed as dist
+            e = torch.tensor([self._err], dtype=torch.int64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            self._err = int(e.item())
 
     def optimizer_step(self) -> None:
+        if self._err:   # a step that failed on any rank is skipped on every rank
+            return
         if self.shard is None:
             self.opt.step(self.params, self.gviews)
             return

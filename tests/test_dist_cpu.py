@@ -249,3 +249,51 @@ def test_sharded_optimizer_checkpoint_resume(tmp_path):
         b = torch.load(tmp_path / f"shard_resume_r{r}.pt", weights_only=True)
         for k in a:
             assert torch.equal(a[k], b[k]), (r, k)
+
+
+def _err_worker(rank, world, port, outdir, inject):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=16, hidden=16, layers=1, batch=12, seq=5, lr=1e-2)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1))
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    per = cfg.batch // world
+    for i in range(3):
+        x, y = ds.next()
+        if inject and i == 1 and rank == world - 1:
+            tr.inject_error(1)        # e.g. a persistent kernel's spin limit on the last rank only
+        tr.step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+        if i == 0:
+            after1 = tr.state_dict()
+    torch.save({"p": tr.state_dict(), "after1": after1, "err": tr.error_word()},
+               os.path.join(outdir, f"err{int(inject)}_r{rank}.pt"))
+    gdist.shutdown()
+
+
+def test_error_word_is_global_across_ranks(tmp_path):
+    """the step error word rides the last gradient collective as a max over
+    ranks, so an error raised on ONE rank skips the update on EVERY rank (the replicas never
+    diverge).  gloo twin of the device path (RcclComm::allreduce_avg_f32_err)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    for inject in (False, True):
+        port = _free_port()
+        procs = [ctx.Process(target=_err_worker, args=(r, world, port, str(tmp_path), inject)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(120)
+            assert p.exitcode == 0
+    for r in range(world):
+        ok = torch.load(tmp_path / f"err0_r{r}.pt", weights_only=True)
+        bad = torch.load(tmp_path / f"err1_r{r}.pt", weights_only=True)
+        assert ok["err"] == 0 and bad["err"] == 1
+        for k in bad["p"]:
+            # the failed step and every later one left the weights at their step-1 values, on every rank
+            assert torch.equal(bad["p"][k], bad["after1"][k]), (r, k)
+            assert not torch.equal(ok["p"][k], ok["after1"][k]) or k.startswith("bias"), (r, k)
+        ref = torch.load(tmp_path / "err1_r0.pt", weights_only=True)
+        for k in bad["p"]:
+            assert torch.equal(bad["p"][k], ref["p"][k])
