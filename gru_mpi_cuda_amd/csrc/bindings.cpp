@@ -155,7 +155,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_persist_max", &Generator::set_persist_max)
       .def("set_persist_dbg", [](Generator& g, uintptr_t p) { g.set_persist_dbg(reinterpret_cast<unsigned long long*>(p)); })
       .def("uses_persist", &Generator::uses_persist)
-      .def("inject_persist_error", &Generator::inject_persist_error);
+      .def("inject_persist_error", &Generator::inject_persist_error)
+      .def("dump_graph", &Generator::dump_graph);
 
   // ---------------------------------------------------------------- raw kernels (tests, bench)
   m.def("gemm_f32", [](py::dict d, uintptr_t s) {   // fp32 MFMA GEMM of the fp32 generation path
@@ -236,6 +237,8 @@ PYBIND11_MODULE(_C, m) {
     HIP_LAUNCH_CHECK();
   });
   m.def("spin_delay", [](int us, uintptr_t s) { spin_delay(us, S(s)); HIP_LAUNCH_CHECK(); });
+  m.def("graph_node_probe_detail", &graph_node_probe_detail);
+  m.def("graph_node_probe", &graph_node_probe);
   m.def("block_cus", [](int nblocks, int us, uintptr_t s) { block_cus(nblocks, us, S(s)); });
   m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });

@@ -121,6 +121,39 @@ void Generator::refresh_weights(hipStream_t s) {
 // made replays disagree (scripts/repro_gen_fp32.py with SYNC_FIRST=1: error word 16, replays not
 // identical); a kernel node is ordered like every other node of the chain.
 void Generator::reset_batch(int Bp, bool bf16, hipStream_t s) {
+  // diagnostic: 1 = round 2's memset-node reset, 2 = the same behind a no-op kernel node (probes only)
+  static const int memset_nodes = [] {
+    const char* e = std::getenv("GK_GEN_MEMSET_RESET");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (memset_nodes >= 3) {   // 3/4/5: the kernel reset, then ONE redundant memset group (same values):
+    // it can change results only by running late, after the kernels that follow it have started
+    GenResetArgs r;
+    r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
+    r.hb_cols = split3() ? 3 * d_.H : d_.H;
+    for (int l = 0; l < d_.L; ++l) { r.hf[l] = hf_[2 * l]; r.hb[l] = (bf16 || split3()) ? hb_[2 * l] : nullptr; }
+    r.ids = ids_; r.alive = alive_; r.out = out_;
+    gen_reset(r, s);
+    if (memset_nodes == 3)
+      for (int l = 0; l < d_.L; ++l) HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * d_.H * 4, s));
+    if (memset_nodes == 4) {
+      HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
+      HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
+    }
+    if (memset_nodes == 5) HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (d_.max_len + 1), s));
+    return;
+  }
+  if (memset_nodes) {
+    if (memset_nodes == 2) block_cus(1, 0, s);   // the graph's root node is then a kernel
+    for (int l = 0; l < d_.L; ++l) {
+      HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * d_.H * 4, s));
+      if (bf16 || split3()) HIP_CHECK(hipMemsetAsync(hb_[2 * l], 0, (size_t)Bp * (split3() ? 3 : 1) * d_.H * 2, s));
+    }
+    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
+    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
+    HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (d_.max_len + 1), s));
+    return;
+  }
   GenResetArgs r;
   r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
   r.hb_cols = split3() ? 3 * d_.H : d_.H;

@@ -46,6 +46,13 @@ class Generator {
   // fault injection (tests): the next persistent launch starts with its spin-timeout bit set, as if
   // an earlier wait had given up -- generate() must notice and regenerate the batch
   void inject_persist_error() { inject_ = true; }
+  // diagnostic: DOT dump of the per-char graph captured for batches of n names (false: none yet)
+  bool dump_graph(int n, const std::string& path) const {
+    auto it = graphs_.find(n);
+    if (it == graphs_.end() || !it->second) return false;
+    it->second->dot(path.c_str());
+    return true;
+  }
 
  private:
   void record_steps(int n_active, hipStream_t s);

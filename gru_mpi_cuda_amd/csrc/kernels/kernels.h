@@ -6,6 +6,7 @@
 // (all three gate GEMMs + sigmoid/tanh/Hadamard epilogue), one fused FC+softmax(+xent or
 // +sampling) launch, and MFMA GEMMs for the hoisted / weight-gradient products.
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -438,6 +439,11 @@ void fill_f32(float* p, long n, float v, hipStream_t s);
 void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)
 void spin_delay(int us, hipStream_t s);
+// graph-replay probe: a memset (mode 0), memcpy (1), 2-D memcpy (2), 32-bit pattern memset (3), five
+// memset nodes in a row (4) or an odd-sized byte memset (5) captured before a checking kernel on one stream, replayed `reps` times (host sync every `sync_every` replays, 0 = never);
+// returns how many words the kernel found not yet written by the node, summed over the replays
+long graph_node_probe(long words, int reps, int sync_every, int mode);
+std::vector<long> graph_node_probe_detail();
 // fault injection: nblocks blocks each holding a whole CU's LDS for `us` microseconds (capped at 5 s)
 void block_cus(int nblocks, int us, hipStream_t s);
 

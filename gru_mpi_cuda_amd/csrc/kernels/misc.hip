@@ -3,9 +3,11 @@
 // reductions.  All vectorised 16 B per lane (cdna_hip_programming.md Guideline 13) and free
 // of float atomics, so a training step is bitwise reproducible run to run.
 #include <stdexcept>
+#include <vector>
 #include "kernels.h"
 #include "common.h"
 #include "optim_dev.h"
+#include "../runtime/runtime.h"
 
 namespace gk {
 
@@ -372,6 +374,108 @@ void block_cus(int nblocks, int us, hipStream_t s) {
     attr = true;
   }
   hipLaunchKernelGGL(block_cu_kernel, dim3(nblocks), dim3(64), 160 * 1024, s, (unsigned long long)capped * 100ull);
+}
+
+// ---- graph-replay probe: is a memset / memcpy node captured on a stream ordered
+// before the kernel captured after it on the same stream, on every replay, with and without host
+// syncs between replays?  The kernel counts words that are not the node's value (a node that ran
+// late or not at all), then overwrites every word with a pattern so a skipped node shows up on the
+// next replay.  Returns the total count over all replays (0 = ordered every time).
+__global__ void graph_probe_kernel(unsigned* buf, long n, unsigned want, unsigned pattern, unsigned* bad, long lo, long hi) {
+  unsigned cnt = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (i >= lo && i < hi) cnt += buf[i] != want;   // words the node covers completely
+    buf[i] = pattern;
+  }
+  cnt = (unsigned)wave_sum((float)cnt);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(bad, cnt);
+}
+static std::vector<long> g_probe_detail;   // stale words seen per kernel of the chain (last probe)
+std::vector<long> graph_node_probe_detail() { return g_probe_detail; }
+long graph_node_probe(long words, int reps, int sync_every, int mode) {
+  // modes 8 / 9: modes 6 / 7 with the replays (and the copies around them) on the NULL stream --
+  // the stream torch's current stream is by default, which the generator launches its graphs on
+  const bool null_launch = mode >= 8;
+  const bool copy_node = mode == 10;   // 10: mode 9 with a memcpy node in place of the memset
+  if (mode == 10) mode = 7;
+  else if (null_launch) mode -= 2;
+  unsigned *buf = nullptr, *src = nullptr, *bad = nullptr;
+  HIP_CHECK(hipMalloc(&buf, words * 4));
+  HIP_CHECK(hipMalloc(&src, words * 4));
+  HIP_CHECK(hipMalloc(&bad, 72 * 4));
+  HIP_CHECK(hipMemset(src, 0x5A, words * 4));
+  HIP_CHECK(hipMemset(bad, 0, 72 * 4));
+  HIP_CHECK(hipMemset(buf, 0xFF, words * 4));
+  hipStream_t s;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const unsigned want = copy_node ? 0x5A5A5A5Au : mode == 0 || mode >= 4 ? 0u : (mode == 3 ? 0x12345678u : 0x5A5A5A5Au);
+  long lo = 0, hi = words;
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  if (mode == 0) HIP_CHECK(hipMemsetAsync(buf, 0, words * 4, s));                                   // memset node
+  else if (mode == 1) HIP_CHECK(hipMemcpyAsync(buf, src, words * 4, hipMemcpyDeviceToDevice, s));   // memcpy node
+  else if (mode == 2) {
+    HIP_CHECK(hipMemcpy2DAsync(buf, 256, src, 256, 256, words * 4 / 256, hipMemcpyDeviceToDevice, s));
+    hi = words / 64 * 64;   // whole 256-B rows only
+  }
+  else if (mode == 3)   // 32-bit pattern memset node (the generator's ids / alive reset of round 2)
+    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(buf), 0x12345678, words, s));
+  else if (mode == 4)   // five back-to-back memset nodes over consecutive fifths (round 2's reset chain)
+    for (int q = 0; q < 5; ++q) {
+      const long a = words * q / 5, b = words * (q + 1) / 5;
+      HIP_CHECK(hipMemsetAsync(buf + a, 0, (b - a) * 4, s));
+    }
+  else if (copy_node)
+    HIP_CHECK(hipMemcpyAsync(buf, src, words * 4, hipMemcpyDeviceToDevice, s));
+  else if (mode == 6 || mode == 7)   // memset node first; each replay's result is copied OUT after the launch
+    HIP_CHECK(hipMemsetAsync(buf, 0, words * 4, s));
+  else {                // a byte memset of odd size and offset (round 2's output-row reset: Bp x (MAX_LEN+1) bytes)
+    HIP_CHECK(hipMemsetAsync(reinterpret_cast<unsigned char*>(buf) + 1, 0, words * 4 - 6, s));
+    lo = 1; hi = words - 2;
+  }
+  hipLaunchKernelGGL(graph_probe_kernel, dim3(256), dim3(256), 0, s, buf, words, want, 0xDEADBEEFu, bad, lo, hi);
+  // mode 7 mirrors the generator's graph size: 70 more kernel nodes after the check (each leaves
+  // the pattern in place), and outside the graph a copy-in + a memset before every replay
+  if (mode == 7)
+    for (int k = 0; k < 70; ++k)
+      hipLaunchKernelGGL(graph_probe_kernel, dim3(64), dim3(256), 0, s, buf, words, 0xDEADBEEFu, 0xDEADBEEFu, bad + 1 + k, lo, hi);
+  HIP_CHECK(hipStreamEndCapture(s, &g));
+  HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  // mode 6 mirrors Generator::generate(): after each replay the stream copies the result out
+  // (hipMemcpyAsync D2D); the NEXT replay's leading memset node must not overtake that copy
+  unsigned* outs = nullptr;
+  if (mode >= 6) HIP_CHECK(hipMalloc(&outs, (size_t)reps * words * 4));
+  hipStream_t ls = null_launch ? nullptr : s;
+  for (int r = 0; r < reps; ++r) {
+    if (mode == 7) {
+      HIP_CHECK(hipMemcpyAsync(src + words / 2, src, words / 2 * 4, hipMemcpyDeviceToDevice, ls));
+      HIP_CHECK(hipMemsetAsync(src, 0x5A, 16, ls));
+    }
+    HIP_CHECK(hipGraphLaunch(ge, ls));
+    if (mode >= 6) HIP_CHECK(hipMemcpyAsync(outs + (size_t)r * words, buf, words * 4, hipMemcpyDeviceToDevice, ls));
+    if (sync_every > 0 && (r + 1) % sync_every == 0) HIP_CHECK(hipStreamSynchronize(ls));
+  }
+  HIP_CHECK(hipStreamSynchronize(ls));
+  HIP_CHECK(hipStreamSynchronize(s));
+  unsigned hb[72];
+  HIP_CHECK(hipMemcpy(hb, bad, 72 * 4, hipMemcpyDeviceToHost));
+  unsigned h = 0;
+  g_probe_detail.assign(72, 0);
+  for (int k = 0; k < 72; ++k) { h += hb[k]; g_probe_detail[k] = hb[k]; }
+  long copies_bad = 0;
+  if (mode >= 6) {   // every copy must hold the kernel's pattern
+    std::vector<unsigned> host((size_t)reps * words);
+    HIP_CHECK(hipMemcpy(host.data(), outs, host.size() * 4, hipMemcpyDeviceToHost));
+    for (unsigned v : host) copies_bad += v != 0xDEADBEEFu;
+    (void)hipFree(outs);
+  }
+  (void)hipGraphExecDestroy(ge);
+  (void)hipGraphDestroy(g);
+  (void)hipStreamDestroy(s);
+  (void)hipFree(buf); (void)hipFree(src); (void)hipFree(bad);
+  // low 32 bits: words the checking kernels saw stale; high bits: copied-out words without the pattern
+  return (long)h + (copies_bad << 32);
 }
 
 // Placement census (diagnostic): out[b] = XCC id of the CU that ran block b (HW_REG_XCC_ID).

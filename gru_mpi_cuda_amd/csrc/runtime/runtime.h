@@ -76,6 +76,8 @@ class Graph {
     HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
   }
   void launch(hipStream_t s) { HIP_CHECK(hipGraphLaunch(exec_, s)); }
+  // diagnostic: the captured graph as Graphviz DOT (nodes, their kinds and dependency edges)
+  void dot(const char* path) const { if (graph_) HIP_CHECK(hipGraphDebugDotPrint(graph_, path, 0)); }
 
  private:
   hipGraph_t graph_ = nullptr;

@@ -641,3 +641,53 @@ def test_trainer_lr_schedule_matches_cpu():
         upd[name] = {k: v - params[k] for k, v in tr.state_dict().items()}
     for k in upd["const"]:
         assert rel(upd["warm"][k] * 4, upd["const"][k]) < 1e-3, k
+
+
+_NULL_STREAM_MEMSET = pytest.mark.xfail(
+    reason="ROCm runtime: a memset node at the head of a graph replayed on the NULL stream after a copy-in "
+           "+ memset, with a host sync every >=3 replays, is not complete before the next kernel "
+           "(docs/DESIGN.md 'Graph replay and memset nodes'); the framework keeps memset nodes out of "
+           "replayed graphs", strict=False)
+
+
+@pytest.mark.parametrize("mode", [m if m != 9 else pytest.param(9, marks=_NULL_STREAM_MEMSET) for m in range(11)])
+@pytest.mark.parametrize("sync_every", [0, 1, 3])
+def test_graph_nodes_ordered_on_replay(mode, sync_every):
+    """VERDICT r2 item 5, minimal repro of the round-2 generator fault (garbage char ids after memset
+    nodes were replayed behind a host sync): a memset (0), memcpy (1), 2-D memcpy (2), 32-bit pattern
+    memset (3), five memset nodes in a row (4), an odd-sized byte memset (5), a memset with the
+    result copied out after every replay (6), the same with a 71-kernel chain and a copy-in + memset
+    before every replay (7), 6 / 7 launched on the NULL stream (8, 9) and 9 with a memcpy node in
+    place of the memset (10) captured on the stream
+    before a checking kernel must have completed before that kernel on EVERY replay,
+    with host syncs between replays (1, 3) or none (0).  The kernel overwrites the buffer after
+    checking, so a node that ran late or not at all is counted."""
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    assert C.graph_node_probe(1 << 20, 40, sync_every, mode) == 0
+
+
+@pytest.mark.parametrize("synced", [True, False])
+@pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 256, 64)])
+def test_carry_graph_replay_matches_eager(layers, H, B, synced):
+    """the carry-mode step graph holds the h carry copies (HS[T] -> HS[0] of every
+    h copy, Trainer::record_carry).  Replayed with a host sync between steps (tr.loss()) or back to
+    back (the case where a memset node in the generator graph ran out of order, docs/DESIGN.md
+    "Graph replay and memset nodes") it must give bitwise the same weights as the same steps run
+    eagerly (no graphs)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=8, carry_hidden=True)
+    params = init_params(cfg)
+    ds = NameStream(B, cfg.seq, seed=6)
+    batches = [ds.next() for _ in range(5)]
+    g = HipTrainer(cfg, params=params)
+    e = HipTrainer(cfg, params=params, use_graph=False)
+    for x, y in batches:
+        g.step(x, y)
+        e.step(x, y)
+        if synced:
+            lg, le = g.loss(), e.loss()          # host syncs between replays
+            assert lg == le
+    torch.cuda.synchronize()
+    assert torch.equal(g.params, e.params)
+    assert g.t.read_error() == 0
