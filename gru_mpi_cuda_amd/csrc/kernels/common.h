@@ -101,4 +101,13 @@ DEV void prep_batch_body(const PrepJob& j, int blk, int nblk) {
   if (blk == 0 && threadIdx.x == 0) j.inv_count[0] = __int_as_float(j.in[1]);
 }
 
+// Workgroup barrier WITHOUT the release fence __syncthreads() carries (that fence is an
+// s_waitcnt vmcnt(0), which drains every global load in flight, prefetches included): own LDS
+// operations retired, then s_barrier.  For LDS hand-offs between the waves of a workgroup only.
+DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 }  // namespace gk

@@ -32,14 +32,7 @@ template <int PER, int A> DEV void wait_ahead(int ahead) {
   if (ahead >= A) { vm_wait<A * PER>(); return; }
   if constexpr (A > 0) wait_ahead<PER, A - 1>(ahead);
 }
-// Workgroup barrier WITHOUT the release fence __syncthreads() carries (that fence is an
-// s_waitcnt vmcnt(0), which would drain the whole prefetch ring): own LDS reads retired, then
-// s_barrier.  LDS-DMA completion is covered by the explicit vm_wait before it.
-DEV void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
+// lds_barrier (common.h): LDS-DMA completion is covered by the explicit vm_wait before it.
 // NS-deep LDS ring: NS-1 k-tiles in flight.  One barrier per k-tile: it publishes tile kt and
 // proves every wave is done with the slot tile kt+NS-1 is about to overwrite.
 template <int NS, int PER, class Stage, class Compute>

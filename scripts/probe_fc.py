@@ -46,12 +46,16 @@ p = torch.softmax(logits, -1)
 p[torch.arange(M), y.long()] -= 1
 ref_dy = (p / M).bfloat16().float() @ W.float()
 err = (dy - ref_dy).abs().max().item()
-dbg = torch.zeros(16, device=dev, dtype=torch.int64)
+dbg = torch.zeros(32, device=dev, dtype=torch.int64)
 d["dbg"] = dbg.data_ptr()
 C.fc_xent(d, s)
 torch.cuda.synchronize()
 st = dbg.cpu().numpy().astype(np.float64)
+waves = st[16:24]
+st = st[:16]
 n = int((st > 0).sum())
+if waves.min() > 0:   # per-wave "logits done" relative to wave 0's stamp at the start
+    print(json.dumps({"logits_done_us_per_wave": [round((x - st[0]) * 0.01, 2) for x in waves]}))
 phases = [round((st[i + 1] - st[i]) * 0.01, 2) for i in range(n - 1)]   # 100 MHz -> us
 print(json.dumps({"phases_us_wg0": phases}))
 print(json.dumps({"M": M, "H": H, "V": V, "us": round(float(np.median(times[5:])), 2),

@@ -89,7 +89,7 @@ def test_dp_training_equals_single_rank(tmp_path, world):
     ctx = mp.get_context("spawn")
     for w in (1, world):
         port = _free_port()
-        procs = [ctx.Process(target=_train_worker, args=(r, w, port, str(tmp_path), 3)) for r in range(w)]
+        procs = [ctx.Process(target=_train_worker, args=(r, w, port, str(tmp_path), 5)) for r in range(w)]
         for p in procs:
             p.start()
         for p in procs:
