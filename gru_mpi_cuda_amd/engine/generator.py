@@ -34,17 +34,19 @@ _MODE = {"bf16": 0, "fp32": 1, "bf16x3": 2}   # GenDims::fp32
 
 
 class HipGenerator:
-    """precision "fp32" (default): fp32-faithful -- fp32 MFMA GEMMs on the fp32 master weights,
-    IEEE gates and softmax, the reference's arithmetic (namegensf.cu:233-242, 294-333);
-    "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies);
-    "bf16x3": the fp32 path with its products as bf16 MFMA GEMMs over split operands
-    (x = hi + lo, hi*hi + hi*lo + lo*hi in fp32: ~2^-16 relative error per product instead of fp32's
-    2^-24, at the bf16 MFMA rate x 1/3).  Batches of <= 32 names run the exact fp32 persistent
-    kernel in both fp32 modes."""
+    """precision "bf16x3" (default): the fp32-faithful path (IEEE gates and softmax, the reference's
+    arithmetic, namegensf.cu:233-242, 294-333) with its products as bf16 MFMA GEMMs over split
+    operands (x = hi + lo, hi*hi + hi*lo + lo*hi in fp32: ~2^-16 relative error per product, at the
+    bf16 MFMA rate x 1/3).  It names exactly what the fp64 oracle names as often as "fp32" does
+    (100 % over 3 seeds x 2 reference-shaped presets, profiles/r3_gen_default_decision.jsonl) at
+    1.9x its speed at 4096 names;
+    "fp32": fp32 MFMA GEMMs on the fp32 master weights;
+    "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies).
+    Small batches run the exact fp32 persistent kernel in both fp32 modes."""
 
     def __init__(self, cfg: GRUConfig, params: Dict[str, torch.Tensor], max_batch: int = 4096,
                  device: Optional[torch.device] = None, flat: Optional[torch.Tensor] = None,
-                 precision: str = "fp32"):
+                 precision: str = "bf16x3"):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         self.precision = precision
@@ -100,10 +102,10 @@ _S: Optional[_State] = None
 
 
 def namegen_initialize(N: int, rng_seed: int, parameter_fname: str, cfg: Optional[GRUConfig] = None,
-                       fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "fp32") -> None:
+                       fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "bf16x3") -> None:
     """namegensf.cu:359-618.  ``rng_seed`` is accepted and unused, as in the reference.
-    ``precision``: "fp32" (faithful, default), "bf16" (fast mode) or "bf16x3" (split-bf16 products)
-    on the GPU path; the CPU path is the fp32 oracle."""
+    ``precision``: "bf16x3" (split-bf16 products, default), "fp32" or "bf16" (fast mode) on the GPU
+    path (see HipGenerator); the CPU path is the fp32 oracle."""
     global _S
     from ..parallel import dist as gdist
     from ..utils import ckpt
