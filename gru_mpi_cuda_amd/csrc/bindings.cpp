@@ -237,6 +237,10 @@ PYBIND11_MODULE(_C, m) {
     HIP_LAUNCH_CHECK();
   });
   m.def("spin_delay", [](int us, uintptr_t s) { spin_delay(us, S(s)); HIP_LAUNCH_CHECK(); });
+  // tests: copy an internal device buffer (Trainer::buffer) into a caller tensor
+  m.def("copy_d2d", [](uintptr_t dst, uintptr_t src, size_t bytes) {
+    HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes, hipMemcpyDeviceToDevice));
+  });
   m.def("graph_node_probe_detail", &graph_node_probe_detail);
   m.def("graph_node_probe", &graph_node_probe);
   m.def("block_cus", [](int nblocks, int us, uintptr_t s) { block_cus(nblocks, us, S(s)); });

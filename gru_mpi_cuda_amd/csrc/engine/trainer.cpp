@@ -275,6 +275,24 @@ void Trainer::refresh_weights(hipStream_t s) {
   j.add(P("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
   cast_multi(j, s);
   HIP_LAUNCH_CHECK();
+  p_valid_ = false;   // the master weights may have been rewritten: the next P comes from a GEMM
+}
+
+// The layer-0 table alone, with the prologue's GEMM kernel (gemm_small: the k-sequence the fused
+// tail's P items reproduce, so the table is bitwise the same whichever computed it)
+void Trainer::record_p_gemm(hipStream_t s) {
+  GemmArgs g;
+  g.A = Emb; g.lda = d_.E; g.B = Ls_[0].Wih; g.ldb = d_.E; g.C = Ptab_; g.ldc = 3 * d_.H;
+  g.bias = P("bias_ih_l0"); g.M = d_.V; g.N = 3 * d_.H; g.K = d_.E;
+  if (gemm_small_kblocks(g) > 0) gemm_small(g, s);
+  else gemm_nt(g, s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::ensure_p(hipStream_t s) {
+  if (p_valid_) return;
+  record_p_gemm(s);
+  p_valid_ = true;
 }
 
 void Trainer::set_batch(const int* x, const int* y, int B, hipStream_t s) {
@@ -602,7 +620,9 @@ void Trainer::record_opt(hipStream_t s) {
 
 bool Trainer::tail_ok() const {
   const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
-  if (comm_ || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
+  // data-parallel: the readiness-ordered path (dp_overlap) runs it after the last collective, on the
+  // all-reduced dP (one slab); the plain-bucket and sharded paths do not
+  if ((comm_ && !dp_overlap()) || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
       V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", true))
     return false;
   // tail.hip's conditions: 256-deep K-slices, fewer waiting product blocks than resident slots
@@ -627,6 +647,9 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   const long tok = (long)d_.T * Bp_;
   TailArgs t;
   t.dP_part = dP_part_; t.nslP = nrb; t.V = V; t.H3 = H3; t.dP_bf = dP_bf_; t.dPT_bf = dPT_bf_;
+  if (comm_) {   // data-parallel: the all-reduced dP (reduced from the partials before the collective)
+    t.dP_part = dP_target(); t.nslP = 1; t.dP_alias = dP_inplace_ ? 1 : 0;
+  }
   t.EmbT = EmbT; t.WihT = Ls_[0].WihT; t.E = E; t.slab_e = slab_e_; t.se = tail_emb_splits();
   for (int k = 0; k < j.n; ++k) {
     if (j.job[k].off == off_.at("weight_ih_l0")) t.jw = k;
@@ -639,6 +662,13 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
     t.dlT = dlT_; t.ldl = (int)tok; t.HTop = Ls_[L - 1].HT + B; t.ldh = (T + 1) * B;
     t.slab_fc = slab_fc2_; t.rs_fc = rs_fc2_; t.nfc = tail_nfc_; t.tok = (int)tok; t.H = d_.H;
   }
+  if (tail_p_) {   // the next step's P table
+    t.P = Ptab_; t.EmbR = Emb; t.WihR = Ls_[0].Wih; t.bih = P("bias_ih_l0");
+    for (int k = 0; k < j.n; ++k)
+      if (j.job[k].off == off_.at("bias_ih_l0")) t.jbi = k;
+  }
+  if (tail_batch_ && next_stage_src_)   // the next step's batch, when this graph holds that step
+    t.prep = PrepJob{next_stage_src_, Bp_, d_.T, Bp_, ids_, labels_, inv_count_};
   t.loss_part = loss_part_; t.nloss = (int)(tok / 32); t.loss = loss_;
   t.sync = tail_sync_;
   t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
@@ -646,7 +676,7 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   t.adam_after_dp = env_on("GK_TAIL_ADAM_WAIT", false) ? 1 : 0;
   if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
   tail_items_ = t.nItems;
-  tail_plan_ = {t.nF, t.nP, 1, t.nA0, t.nW, t.nE};
+  tail_plan_ = {t.nB, t.nF, t.nP, 1, t.nA0, t.nW, t.nE, t.nPt};
 }
 
 void Trainer::forward_backward(hipStream_t s) {
@@ -674,6 +704,7 @@ void Trainer::forward_backward(hipStream_t s) {
 
 void Trainer::optimizer_step(hipStream_t s) {
   GK_TRACE("gk.optimizer_step");
+  p_valid_ = false;   // the phased path recomputes P in every step's prologue
   if (!use_graph_) { record_opt(s); return; }
   if (!g_opt_.ready()) {
     g_opt_.begin(s0_);
@@ -784,10 +815,14 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
+      next_stage_src_ = nullptr;
+      batch_from_prev_tail_ = false;
       record_step_body();
+      g_step_p_[slot] = body_tail_p_;
     } catch (...) {
       defer_slabs_ = false;
-      tail_fused_ = false;
+      tail_fused_ = tail_p_ = tail_batch_ = false;
+      p_in_prologue_ = batch_in_prologue_ = true;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow
       (void)hipStreamEndCapture(s0_, &broken);
@@ -797,7 +832,9 @@ void Trainer::step(hipStream_t s) {
     }
     g.end(s0_);
   }
+  if (g_step_p_[slot]) ensure_p(s);
   g.launch(s);
+  p_valid_ = g_step_p_[slot];
   HIP_CHECK(hipEventRecord(stage_done_[slot], s));
   if (wd_) wd_->watch(stage_done_[slot]);
 }
@@ -827,13 +864,19 @@ void Trainer::step_group(hipStream_t s) {
     GK_TRACE("gk.capture_group_graph");
     g.begin(s0_);
     try {
+      batch_from_prev_tail_ = false;
       for (int j = 0; j < group_; ++j) {
         stage_src_ = h_stage_ + (size_t)group_slot(gp, j) * slot_ints();
+        next_stage_src_ = j + 1 < group_ ? h_stage_ + (size_t)group_slot(gp, j + 1) * slot_ints() : nullptr;
         record_step_body();
       }
+      next_stage_src_ = nullptr;
+      g_group_p_[gp] = body_tail_p_;
     } catch (...) {
+      next_stage_src_ = nullptr;
       defer_slabs_ = false;
-      tail_fused_ = false;
+      tail_fused_ = tail_p_ = tail_batch_ = false;
+      p_in_prologue_ = batch_in_prologue_ = true;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;
       (void)hipStreamEndCapture(s0_, &broken);
@@ -843,7 +886,9 @@ void Trainer::step_group(hipStream_t s) {
     }
     g.end(s0_);
   }
+  if (g_group_p_[gp]) ensure_p(s);
   g.launch(s);
+  p_valid_ = g_group_p_[gp];
   HIP_CHECK(hipEventRecord(group_done_[gp], s));
   if (wd_) wd_->watch(group_done_[gp]);
 }
@@ -859,19 +904,36 @@ void Trainer::record_step_body() {
   }
   if (dp_overlap()) {
     // readiness-ordered collectives on the comm stream, overlapped with the rest of the
-    // backward; joined before the optimiser (the embedding-side tail runs after the join)
+    // backward; joined before the optimiser (the embedding-side tail runs after the join, as
+    // the fused step tail when it qualifies)
     deferred_.n = 0;
+    tail_fused_ = tail_ok();
     record_fb_seq(s0_, /*dp=*/true);
   } else {
     deferred_.n = 0;
     defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
     tail_fused_ = tail_ok();
+    // GK_TAIL_P=1: the next step's P in the tail.  Measured slower at the headline (its items can
+    // only start once the last Emb tile is refreshed: tail 40.8 -> 51.1 us, step 0.215 -> 0.224 ms,
+    // profiles/r3_tail_p_ab.jsonl), so off by default.
+    tail_p_ = tail_fused_ && d_.E % 256 == 0 && env_on("GK_TAIL_P", false);
+    // GK_TAIL_BATCH=1: the next step's batch preparation in the tail (multi-step graphs): measured
+    // neutral (0.2186-0.2273 vs 0.219 ms), off by default
+    tail_batch_ = tail_fused_ && env_on("GK_TAIL_BATCH", false);
+    // with tail_p_ every step of this configuration leaves the next P behind: this one's came from
+    // the previous tail (or ensure_p() before the launch); its batch inside a multi-step graph
+    p_in_prologue_ = !tail_p_;
+    batch_in_prologue_ = !(tail_batch_ && batch_from_prev_tail_);
     if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     defer_slabs_ = false;
     record_allreduce(s0_);
   }
   record_opt(s0_);
+  body_tail_p_ = tail_p_;
+  batch_from_prev_tail_ = tail_batch_ && next_stage_src_ != nullptr;
   tail_fused_ = false;
+  tail_p_ = tail_batch_ = false;
+  p_in_prologue_ = batch_in_prologue_ = true;
 }
 
 float Trainer::read_loss() {

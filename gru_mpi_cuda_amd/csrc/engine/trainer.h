@@ -73,6 +73,19 @@ class Trainer {
   // those pieces to record_opt.  GK_TAIL=0 turns it off.
   bool tail_fused_ = false;
   int tail_nfc_ = 0;             // dW_fc K-slices computed inside the fused tail (0: before the backward)
+  // The next step's layer-0 table (and, inside a multi-step graph, its batch preparation) in the
+  // fused tail (GK_TAIL_P=0: off).  A step recorded with tail_p_ takes P from the previous step's
+  // tail instead of its prologue GEMM; p_valid_ says whether Ptab_ matches the current weights
+  // (false after refresh_weights() or a step without it), and a launch that relies on it runs
+  // ensure_p() first.
+  bool tail_p_ = false, tail_batch_ = false;
+  bool p_in_prologue_ = true, batch_in_prologue_ = true, batch_from_prev_tail_ = false;
+  const int* next_stage_src_ = nullptr;   // staging slot of the next step in the same graph (or null)
+  bool p_valid_ = false;
+  bool body_tail_p_ = false;              // the last recorded step body computed the next P in its tail
+  bool g_step_p_[2] = {false, false}, g_group_p_[2] = {false, false};
+  void ensure_p(hipStream_t s);           // P = Emb·W_ih0^T + b_ih0 now, if it is stale
+  void record_p_gemm(hipStream_t s);
   bool tail_ok() const;
   unsigned* tail_sync_ = nullptr;
   unsigned long long* tail_dbg_ = nullptr;   // set_tail_dbg(): per-item stamps (TailArgs::dbg)

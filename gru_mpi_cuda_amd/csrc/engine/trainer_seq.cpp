@@ -133,13 +133,18 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
-  {   // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched
-      // together with the batch preparation (independent work, one graph node)
+  if (p_in_prologue_ && batch_in_prologue_) {
+    // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
+    // with the batch preparation (independent work, one graph node)
     GemmArgs g;
     g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
     g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
     gemm_with_prep(g, PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_}, s);
-  }
+  } else if (p_in_prologue_) {   // the batch came from the previous step's fused tail
+    record_p_gemm(s);
+  } else if (batch_in_prologue_) {   // P came from the previous step's fused tail
+    prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
+  }   // else the previous step's tail prepared both
   if (carry_) record_carry(s);
   // ------------------------------------------------------------------ forward
   auto fwd_args = [&](int l) {
@@ -251,11 +256,31 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     // fused tail: the same K-slices as blocks of the tail launch (their last slice per tile runs that
     // tile's Adam), so no launch here and no slab jobs
-    tail_nfc_ = (tail_fused_ && w.algo == 3 && (tok / sp) % 256 == 0 && env_flag("GK_TAIL_FC", true)) ? sp : 0;
+    // (data-parallel: dW_fc is all-reduced with the other gradients, so it stays a GEMM here)
+    tail_nfc_ = (tail_fused_ && !dp && w.algo == 3 && (tok / sp) % 256 == 0 && env_flag("GK_TAIL_FC", true)) ? sp : 0;
     if (!tail_nfc_) {
       gemm_nt(w, s);
       tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
       tail.add(rs_fc2_, sp, V, G("fc.bias"));
+    }
+    // data-parallel: the FC group [W_fc, b_fc] is final here, before the whole backward sweep.  Its
+    // collective goes out now on the comm stream and stays open across the top layer's persistent
+    // backward kernel, whatever the bucket size: a collective that spans the
+    // longest kernel of the step costs nothing on the critical path.  (The sequence kernels bound
+    // their waits by wall clock, so an RCCL kernel holding CUs only delays them.)  GK_AR_FC_EARLY=0:
+    // the group rides with the top layer's.
+    //
+    // Off by default: ROCm's graph executor ran the forked collective BEFORE the backward kernel, not
+    // beside it, with 6-10 us of fork / join gaps (--rccl-self trace: 0.2292 -> 0.2517 ms per step,
+    // profiles/r3_rccl_self_fc_early.txt).
+    if (dp && ar_span() && seq_[L - 1].bwd && env_flag("GK_AR_FC_EARLY", false) && tail.n) {
+      SlabJobs fcj;
+      for (int k2 = 0; k2 < tail.n; ++k2)
+        slab_job(fcj, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
+      if (fcj.n) reduce_slabs_multi(fcj, s);
+      tail.n = 0;
+      ar_ready_ = group_end(L);
+      ar_flush(s, /*force=*/true);
     }
   }
   // ------------------------------------------------------------------ backward (BPTT)
@@ -324,39 +349,25 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       }
       if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
         ar_ready_ = group_end(0);
-        // The step's LAST collective carries the error word along (max over ranks, same launch):
-        // a persistent kernel that gave up on ANY rank makes every rank skip the update.
-        if (!ar_busy_) {
-          // nothing left to overlap with: the last collectives go on the step stream itself (a
-          // fork + join around them only adds graph edges -- measured: a forked branch in the
-          // step graph slowed the kernels beside it)
-          const long n = ar_ready_ - ar_launched_;
-          if (n > 0) {
-            if (dP_inplace_) comm_->allreduce_avg_f32_err(grads_ + ar_launched_, n, err_, s);
-            else comm_->allreduce_avg_f32(grads_ + ar_launched_, n, s);
-            ar_log_.push_back({ar_launched_, n});
-            ar_launched_ = ar_ready_;
-          }
-          if (!dP_inplace_) {
-            comm_->allreduce_avg_f32_err(dP_, (long)V * H3, err_, s);
-            ar_log_.push_back({-1, (long)V * H3});
-          } else if (n <= 0) {
-            comm_->allreduce_max_u32(err_, 1, s);
-          }
-        } else {
-          const bool sent = ar_flush(s, true, /*with_err=*/dP_inplace_);
-          if (!dP_inplace_ || !sent) {
-            hipEvent_t e = ev();
-            HIP_CHECK(hipEventRecord(e, s));
-            HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
-            if (!dP_inplace_) {
-              comm_->allreduce_avg_f32_err(dP_, (long)V * H3, err_, sc_);
-              ar_log_.push_back({-1, (long)V * H3});
-            } else {
-              comm_->allreduce_max_u32(err_, 1, sc_);
-            }
-          }
-          ar_join(s);
+        // collectives still open across the backward (the early FC group, upper layers' groups)
+        // end here; nothing is left to overlap with, so the last collectives go on the step
+        // stream itself (a fork + join around them only adds graph edges -- measured: a forked
+        // branch in the step graph slowed the kernels beside it).  The step's LAST collective
+        // carries the error word along (max over ranks, same launch): a persistent kernel that
+        // gave up on ANY rank makes every rank skip the update.
+        ar_join(s);
+        const long n = ar_ready_ - ar_launched_;
+        if (n > 0) {
+          if (dP_inplace_) comm_->allreduce_avg_f32_err(grads_ + ar_launched_, n, err_, s);
+          else comm_->allreduce_avg_f32(grads_ + ar_launched_, n, s);
+          ar_log_.push_back({ar_launched_, n});
+          ar_launched_ = ar_ready_;
+        }
+        if (!dP_inplace_) {
+          comm_->allreduce_avg_f32_err(dP_, (long)V * H3, err_, s);
+          ar_log_.push_back({-1, (long)V * H3});
+        } else if (n <= 0) {
+          comm_->allreduce_max_u32(err_, 1, s);
         }
       }
     } else {
@@ -384,13 +395,13 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients
-  if (dp) {
+  if (dp && !tail_fused_) {
     // from the averaged dP; its dEmb slabs are already global (after the collective), so like the
     // single-GPU step they are summed inside the Adam launch (one reduce launch fewer)
     defer_slabs_ = o_.clip <= 0.f && env_flag("GK_DEFER_SLABS", true);
     record_emb_tail(s, dP_target());
     defer_slabs_ = false;
-  }
+  }   // (fused tail: the dP tiles read the averaged dP, see Trainer::record_tail)
   else if (!tail_fused_) record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
   HIP_LAUNCH_CHECK();
 }

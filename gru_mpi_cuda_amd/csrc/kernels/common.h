@@ -86,17 +86,19 @@ DEV float wave_sum(float v) {
 
 
 // Batch preparation body (see prep_batch in kernels.h): block `blk` of `nblk` 256-thread blocks.
+// The staging slot is pinned HOST memory (one round trip ~1.5-2 us): the batch size and the x / y
+// words are loaded together (rows up to Bmax >= Bp are always inside the slot) and selected after,
+// so a block pays one round trip, not two dependent ones.
 DEV void prep_batch_body(const PrepJob& j, int blk, int nblk) {
-  const int B = j.in[0];
   const int* x = j.in + 16;
   const int* y = x + (size_t)j.Bmax * j.T;
   const int n = j.T * j.Bp;
+  const int B = j.in[0];
   for (int i = blk * 256 + (int)threadIdx.x; i < n; i += nblk * 256) {
     const int b = i / j.T, t = i - b * j.T;       // read in batch-major order (coalesced)
-    int xi = 0, yi = -1;
-    if (b < B) { xi = x[i]; yi = y[i]; }
-    j.ids[(size_t)t * j.Bp + b] = xi;
-    j.labels[(size_t)t * j.Bp + b] = yi;
+    const int xr = x[i], yr = y[i];
+    j.ids[(size_t)t * j.Bp + b] = b < B ? xr : 0;
+    j.labels[(size_t)t * j.Bp + b] = b < B ? yr : -1;
   }
   if (blk == 0 && threadIdx.x == 0) j.inv_count[0] = __int_as_float(j.in[1]);
 }

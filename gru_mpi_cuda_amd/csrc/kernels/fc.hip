@@ -329,6 +329,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
     }
   lds_barrier();   // not __syncthreads: its vmcnt(0) would wait for the W_fc^T prefetch
+  STAMP();
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -342,6 +343,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       if (lr == 0) red[NW * 32 + w * 32 + row] = e;
     }
   lds_barrier();   // not __syncthreads: its vmcnt(0) would wait for the W_fc^T prefetch
+  STAMP();
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll

@@ -402,8 +402,12 @@ void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 // and the embedding-side products dW_ih0 = dP^T Emb and dEmb = dP W_ih0, each output tile followed
 // directly by the Adam update of that tile.  One block per work item; the product items come last
 // in the grid and wait (bounded) on per-column-block counters of the dP tiles.
+struct PrepJob { const int* in; int Bmax, T, Bp; int* ids; int* labels; float* inv_count; };
 struct TailArgs {
   const float* dP_part = nullptr; int nslP = 0, V = 0, H3 = 0;   // [nslP][V][H3] -> dP_bf, dPT_bf
+  // dP_part aliases the W_ih0 gradient slot (data-parallel: the all-reduced dP lives there): the
+  // W_ih0 tiles then keep their gradient to themselves (no write-back over dP still being read)
+  int dP_alias = 0;
   u16* dP_bf = nullptr; u16* dPT_bf = nullptr;
   const u16* EmbT = nullptr;       // [E][V]   B operand of dW_ih0
   const u16* WihT = nullptr;       // [E][H3]  B operand of dEmb
@@ -423,12 +427,24 @@ struct TailArgs {
   const u16* HTop = nullptr; int ldh = 0;   // [H][ldh] bf16 top-layer h^T (token columns)
   float* slab_fc = nullptr; float* rs_fc = nullptr;   // [nfc][V][H], [nfc][V]
   int nfc = 0, tok = 0, H = 0, jf = -1, jb = -1;
-  int nF = 0, nP = 0, nA0 = 0, nW = 0, nE = 0, nItems = 0;   // filled by tail_step()
+  // The NEXT step's layer-0 table P = Emb·W_ih0^T + b_ih0 from the weights this launch refreshes
+  // (null: the next step's prologue computes it).  One 64 x 64 tile per item, after the Emb rows,
+  // the W_ih0 rows and b_ih0 it reads are refreshed (their refresh stores are write-through then).
+  float* P = nullptr;
+  const u16* EmbR = nullptr;       // [V][E] bf16 row-major copies (the refreshed ones)
+  const u16* WihR = nullptr;       // [H3][E]
+  const float* bih = nullptr;      // [H3] fp32 master of b_ih0
+  int jbi = -1;                    // its job in the OptCastJobs list
+  // The NEXT step's batch preparation (prep.in null: its prologue does it): zero-copy reads of its
+  // pinned staging slot on blocks that wait for nothing, ahead of everything else in the grid.
+  PrepJob prep{nullptr, 0, 0, 0, nullptr, nullptr, nullptr};
+  int nF = 0, nP = 0, nA0 = 0, nW = 0, nE = 0, nPt = 0, nB = 0, nItems = 0;   // filled by tail_step()
 };
 // counters (one 64-B line each): dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of
-// Emb^T per E-tile (E/64) and of W_ih^T per (E-tile, K-slice) (8 E/64), dW_fc tiles ((V/64)(H/64))
+// Emb^T per E-tile (E/64) and of W_ih^T per (E-tile, K-slice) (8 E/64), dW_fc tiles ((V/64)(H/64)),
+// refreshed Emb row blocks (V/64), refreshed W_ih0 row blocks (H3/64), refreshed b_ih0 (1)
 inline long tail_sync_words(int V, int H3, int E, int H) {
-  return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64) + (V / 64) * (H / 64)) * 16;
+  return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64) + (V / 64) * (H / 64) + V / 64 + H3 / 64 + 1) * 16;
 }
 // false: the grid cannot hold the waiting product items beside the others (the caller takes the
 // phased tail); true: launched
@@ -451,7 +467,6 @@ void block_cus(int nblocks, int us, hipStream_t s);
 // batch-major int32 (may be pinned host memory, read zero-copy); out ids/labels time-major [T][Bp]
 // (pad rows: id 0, label -1) and inv_count.
 void prep_batch(const int* in, int Bmax, int T, int Bp, int* ids, int* labels, float* inv_count, hipStream_t s);
-struct PrepJob { const int* in; int Bmax, T, Bp; int* ids; int* labels; float* inv_count; };
 inline int prep_batch_blocks(int T, int Bp) {
   const int n = (T * Bp + 255) / 256;
   return n < 64 ? n : 64;

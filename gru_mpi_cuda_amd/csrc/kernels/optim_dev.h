@@ -24,6 +24,9 @@ DEV float4 bld4_sc1(brsrc_t r, unsigned off) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
   return __builtin_bit_cast(float4, v);
 }
+DEV float bld1_sc1(brsrc_t r, unsigned off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
 DEV bf16x8 bld8_sc1(brsrc_t r, unsigned off) {
   const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
   return __builtin_bit_cast(bf16x8, v);
@@ -169,10 +172,11 @@ DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
 // DSC1: the row-major bf16 copy (matrix) or the fp32 master (flat) leaves with write-through
 // stores (read again later in the same launch).  Uniform over the block (J is).
 // gtile (nullable): the tile's fp32 gradient already in LDS ([64][68], this tile's 64 x 64 block);
-// it is also written to the gradient buffer (observable), and J.gsl is ignored
+// it is also written to the gradient buffer (observable) unless store_g is false (the buffer
+// holds something still being read, e.g. the all-reduced dP in the W_ih0 slot), and J.gsl is ignored
 template <bool GSC1, bool DSC1>
 DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const AdamCoef& co, u16 (*tile)[68],
-                        const float (*gtile)[68] = nullptr) {
+                        const float (*gtile)[68] = nullptr, bool store_g = true) {
   if (J.R == 0) {   // flat job: 1024 elements per block
     const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
     if ((long)t * 1024 + threadIdx.x * 4 < J.C) {
@@ -197,7 +201,7 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
   if (gtile) {
     adam4x4_g(a, co, J.off + (long)(r0 + ty) * J.C + c0 + 4 * tx, 16L * J.C, upd, [&](int q, long i) {
       const float4 g = *reinterpret_cast<const float4*>(&gtile[ty + 16 * q][4 * tx]);
-      reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
+      if (store_g) reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
       return g;
     });
   } else {

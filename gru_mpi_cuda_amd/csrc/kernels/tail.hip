@@ -134,6 +134,16 @@ DEV void tail_loadA_sc1(const u16* A, int lda, long a_bytes, int row0, int k0, T
 #pragma unroll
     for (int r = 0; r < 2; ++r) f.a[ks][r] = bld8_sc1(rA, base + (unsigned)((16 * r * lda + ks * 32) * 2));
 }
+// both operands written in this launch (the next step's P table): sc1 loads of rows row0 + wsel*32..
+DEV void tail_load_sc1(const u16* A, int lda, long a_bytes, int row0, int k0, int wsel, bf16x8 (&fr)[8][2]) {
+  const int lane = threadIdx.x & 63;
+  const brsrc_t rA = brsrc(A, (unsigned)a_bytes);
+  const unsigned base = (unsigned)(((size_t)(row0 + wsel * 32 + (lane & 15)) * lda + k0 + 8 * (lane >> 4)) * 2);
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) fr[ks][r] = bld8_sc1(rA, base + (unsigned)((16 * r * lda + ks * 32) * 2));
+}
 DEV void tail_mma(const TailFrags& f, f32x4 (&acc)[2][2]) {
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks)
@@ -177,23 +187,32 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
   __shared__ __attribute__((aligned(16))) float gt[64][68];   // a product tile's fp32 gradient
   __shared__ __attribute__((aligned(16))) float gb[64];       // b_fc gradients of a dW_fc row tile
   __shared__ unsigned s_prev;
-  const int it = blockIdx.x;
+  const int gi = blockIdx.x;   // grid index (stamps); item index below it (after the batch-prep blocks)
   if (t.dbg && threadIdx.x == 0) {
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    t.dbg[(size_t)it * 4 + 0] = __builtin_amdgcn_s_memrealtime();
-    t.dbg[(size_t)it * 4 + 3] = (unsigned long long)it | ((unsigned long long)xcc << 16);
+    t.dbg[(size_t)gi * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+    t.dbg[(size_t)gi * 4 + 3] = (unsigned long long)gi | ((unsigned long long)xcc << 16);
   }
+  if (gi < t.nB) {   // the next step's batch preparation (its slot's pinned host reads), waits for nothing
+    prep_batch_body(t.prep, gi, t.nB);
+    if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)gi * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+    return;
+  }
+  const int it = gi - t.nB;
   const bool failed = step_failed(a);         // a persistent kernel of this step gave up: no update
   const AdamCoef co = adam_coef(a);           // the step counter was bumped before this launch
   unsigned* err = const_cast<unsigned*>(a.err);
   const unsigned ep = *t.epoch;
   const int ntE = t.E / 64;
   const unsigned colTarget = (unsigned)(t.V / 32) * ep;
-  const int eP = t.nF, eL = eP + t.nP, eA0 = eL + 1, eW = eA0 + t.nA0, eE = eW + t.nW;
+  const int eP = t.nF, eL = eP + t.nP, eA0 = eL + 1, eW = eA0 + t.nA0, eE = eW + t.nW, eQ = eE + t.nE;
   unsigned* rdW = tail_ctr(t.sync, t.H3 / 64 + (t.V / 64) * ntE);   // [E/64]: dW_ih0 blocks done reading Emb^T
   unsigned* rdE = rdW + 16 * ntE;                                     // [E/64][8]: dEmb blocks done reading W_ih^T
   unsigned* cFc = rdE + 16 * 8 * ntE;                                 // [V/64][H/64]: dW_fc slices arrived
+  unsigned* cEmb = cFc + 16 * (t.V / 64) * (t.H / 64);                // [V/64]: Emb row block tiles refreshed
+  unsigned* cWih = cEmb + 16 * (t.V / 64);                            // [H3/64]: W_ih0 row block tiles refreshed
+  unsigned* cBi = cWih + 16 * (t.H3 / 64);                            // b_ih0 blocks refreshed
   if (it < eP) {           // dW_fc tile (tm, tn) over token slice sp; the tile's last slice runs its Adam
     const int ntH = t.H / 64, ntV = t.V / 64;
     const int tn = it % ntH, tm = (it / ntH) % ntV, sp = it / (ntH * ntV);
@@ -273,13 +292,18 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
     }
     int k = 0;
     while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
-    if (!failed) adam_cast_unit<false, false>(a, j.job[k], b - j.blk_start[k], co, tile);
+    if (t.P && k == t.jbi) {   // b_ih0: read by the P items of this launch
+      if (!failed) adam_cast_unit<false, true>(a, j.job[k], b - j.blk_start[k], co, tile);
+      (void)tail_arrive(cBi, &s_prev);
+    } else if (!failed) {
+      adam_cast_unit<false, false>(a, j.job[k], b - j.blk_start[k], co, tile);
+    }
   } else if (it < eE) {    // dW_ih0 tile (tm, tn) = dP[:, tm]^T · Emb[:, tn] (K = V), then its Adam
     const int id = it - eW, tm = id / ntE, tn = id % ntE;
     f32x4 acc[2][2];
     tail_product(t.dPT_bf, t.V, (long)t.V * t.H3 * 2, t.EmbT, t.V, tm * 64, tn * 64, 0, t.V, acc, [&] {
       tail_wait(tail_ctr(t.sync, tm), colTarget, err);
-      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)gi * 4 + 1] = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
     });
     tail_reads_done(rdW + 16 * tn);
@@ -293,14 +317,19 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
 #pragma unroll
         for (int e = 0; e < 4; ++e) gt[acc_row(i, e)][acc_col(jj)] = acc[i][jj][e];
     __syncthreads();
-    if (!failed) adam_cast_unit<false, false>(a, j.job[t.jw], tm * ntE + tn, co, tile, gt);
-  } else {                 // dEmb tile (vm, tn) over K-slice ks; the tile's last slice runs its Adam
+    if (t.P) {   // the refreshed rows feed the P items: write-through row-major copy, then count the tile
+      if (!failed) adam_cast_unit<false, true>(a, j.job[t.jw], tm * ntE + tn, co, tile, gt, !t.dP_alias);
+      (void)tail_arrive(cWih + 16 * tm, &s_prev);
+    } else if (!failed) {
+      adam_cast_unit<false, false>(a, j.job[t.jw], tm * ntE + tn, co, tile, gt, !t.dP_alias);
+    }
+  } else if (it < eQ) {    // dEmb tile (vm, tn) over K-slice ks; the tile's last slice runs its Adam
     const int id = it - eE, ks = id % t.se, tl = id / t.se, vm = tl / ntE, tn = tl % ntE;
     const int kl = t.H3 / t.se;
     f32x4 acc[2][2];
     tail_product(t.dP_bf, t.H3, (long)t.V * t.H3 * 2, t.WihT, t.H3, vm * 64, tn * 64, ks * kl, kl, acc, [&] {
       for (int c = ks * kl / 64; c < (ks + 1) * kl / 64; ++c) tail_wait(tail_ctr(t.sync, c), colTarget, err);
-      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)gi * 4 + 1] = __builtin_amdgcn_s_memrealtime();
       __syncthreads();
     });
     tail_reads_done(rdE + 16 * (tn * 8 + ks));
@@ -327,10 +356,45 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
         *reinterpret_cast<float4*>(&gt[ty + 16 * q][4 * tx]) = sum_slabs4<true>(t.slab_e, n, t.se, o);
       }
       __syncthreads();
-      if (!failed) adam_cast_unit<false, false>(a, j.job[t.je], vm * ntE + tn, co, tile, gt);
+      if (t.P) {
+        if (!failed) adam_cast_unit<false, true>(a, j.job[t.je], vm * ntE + tn, co, tile, gt);
+        (void)tail_arrive(cEmb + 16 * vm, &s_prev);
+      } else if (!failed) {
+        adam_cast_unit<false, false>(a, j.job[t.je], vm * ntE + tn, co, tile, gt);
+      }
+    }
+  } else {                 // the next step's P tile (tv, tn) = Emb[tv] · W_ih0[tn]^T + b_ih0[tn] (K = E)
+    const int id = it - eQ, tv = id / (t.H3 / 64), tn = id % (t.H3 / 64);
+    const int nbi = (t.H3 + 1023) / 1024;   // blocks of the flat b_ih0 job
+    tail_wait(cEmb + 16 * tv, (unsigned)ntE * ep, err);
+    tail_wait(cWih + 16 * tn, (unsigned)ntE * ep, err);
+    tail_wait(cBi, (unsigned)nbi * ep, err);
+    if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)gi * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    const int wm = (threadIdx.x >> 6) >> 1, wn = (threadIdx.x >> 6) & 1;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    TailFrags f;
+    for (int kc = 0; kc < t.E; kc += 256) {   // the k-step sequence of the prologue's P GEMM (gemm_small)
+      tail_load_sc1(t.EmbR, t.E, (long)t.V * t.E * 2, tv * 64, kc, wm, f.a);
+      tail_load_sc1(t.WihR, t.E, (long)t.H3 * t.E * 2, tn * 64, kc, wn, f.b);
+      tail_mma(f, acc);
+    }
+    const brsrc_t rb = brsrc(t.bih, (unsigned)(t.H3 * 4));
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int c = tn * 64 + acc_col(jj);
+      const float bias = bld1_sc1(rb, (unsigned)(c * 4));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t.P[(size_t)(tv * 64 + acc_row(i, e)) * t.H3 + c] = acc[i][jj][e] + bias;
     }
   }
-  if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)it * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+  if (t.dbg && threadIdx.x == 0) t.dbg[(size_t)gi * 4 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
 static int tail_occ() {   // GK_TAIL_OCC: 3 (default) or 4 resident workgroups per CU
@@ -383,13 +447,24 @@ bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s) {
   t.nA0 = tot;
   t.nW = (t.H3 / 64) * (t.E / 64);
   t.nE = (t.V / 64) * (t.E / 64) * t.se;
-  t.nItems = t.nF + t.nP + 1 + t.nA0 + t.nW + t.nE;
+  if (t.P) {
+    if (!t.EmbR || !t.WihR || !t.bih || t.E % 256 || t.jbi < 0 || t.jbi >= j.n || j.job[t.jbi].R != 0 ||
+        j.job[t.jbi].C != t.H3 || t.jbi == t.jw || t.jbi == t.je)
+      throw std::runtime_error("tail_step: inconsistent P-table arguments");
+    t.nPt = (t.V / 64) * (t.H3 / 64);
+  } else {
+    t.nPt = 0;
+  }
+  t.nB = t.prep.in ? prep_batch_blocks(t.prep.T, t.prep.Bp) : 0;
+  t.nItems = t.nB + t.nF + t.nP + 1 + t.nA0 + t.nW + t.nE + t.nPt;
   const int occ = tail_occ();
   const int cap = tail_resident_slots();
   // A product block waits only for points that other blocks reach without waiting first (dP tiles;
   // product blocks signal their reads before they wait).  With fewer product blocks than resident
   // slots, a block they wait for always gets a slot: the launch drains whatever the dispatch order.
-  if (cap <= 0 || t.nW + t.nE >= cap || t.se > 8 || (t.H3 / t.se) % 256 || t.V % 256) return false;
+  // The P items wait for product blocks (which wait only for dP tiles): still a bounded chain, and
+  // all waiting blocks together stay below the resident slots.
+  if (cap <= 0 || t.nW + t.nE + t.nPt >= cap || t.se > 8 || (t.H3 / t.se) % 256 || t.V % 256) return false;
   if (t.dbg && t.nItems > 65536) t.dbg = nullptr;
   if (occ == 4) hipLaunchKernelGGL(tail_kernel<4>, dim3(t.nItems), dim3(256), 0, s, a, j, t);
   else hipLaunchKernelGGL(tail_kernel<3>, dim3(t.nItems), dim3(256), 0, s, a, j, t);

@@ -19,7 +19,7 @@ for _ in range(steps):
     tr.step(*ds.next())
 torch.cuda.synchronize()
 plan = tr.t.tail_plan()
-names = ["dWfc", "dP", "loss", "adam", "dWih0", "dEmb"]
+names = ["prep", "dWfc", "dP", "loss", "adam", "dWih0", "dEmb", "P"]
 n = sum(plan)
 d = dbg[: 4 * n].view(n, 4).cpu().numpy().astype(np.int64)
 t0 = d[:, 0].min()

@@ -287,17 +287,21 @@ def test_generator_fp32_probs_match_fp64(precision, persist, atol, rtol):
     torch.testing.assert_close(probs[:N].cpu().double(), want, atol=atol, rtol=rtol)
 
 
-@pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll", [(1, 256, 256, 8.0, 1), (2, 128, 256, 0.25, 3),
-                                                         (1, 512, 512, 1.0, 1), (2, 512, 256, 0.25, 2),
-                                                         (2, 512, 256, 64.0, 1)])
-def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
+@pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll,fc_early", [
+    (1, 256, 256, 8.0, 1, "0"), (2, 128, 256, 0.25, 3, "0"), (1, 512, 512, 1.0, 1, "0"),
+    (2, 512, 256, 0.25, 2, "0"), (2, 512, 256, 64.0, 1, "0"),
+    (1, 512, 512, 8.0, 2, "1"), (2, 512, 256, 0.25, 3, "1")])
+def test_single_graph_step_with_rccl_world1(monkeypatch, layers, E, H, bucket_mb, n_coll, fc_early):
     """The whole step as one graph with captured RCCL all-reduces (1-rank communicator) on the
     comm stream: must equal the no-comm step bit for bit (mean over one rank is the identity).
     With a communicator the step all-reduces dP instead of dEmb / dW_ih0 (in the W_ih0 slot when
-    V <= E, else as its own collective) and derives those two after the join; small buckets
-    make the top layer's group go out while layer 0 is still in its backward."""
+    V <= E, else as its own collective) and derives those two after the join (the fused step tail
+    on the averaged dP where it qualifies); small buckets make the top layer's group go out while
+    layer 0 is still in its backward.  fc_early (GK_AR_FC_EARLY=1, off by default): the FC group
+    goes out before the backward sweep, whatever the bucket size."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
+    monkeypatch.setenv("GK_AR_FC_EARLY", fc_early)
     C = load_ext()
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=64, seq=8, seed=3, bucket_mb=bucket_mb)
     x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
@@ -365,6 +369,48 @@ def test_multi_step_graph_matches_single_steps(G, layers, H):
     assert a.t.graph_steps() == G
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
     assert a.loss() == b.loss()
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_tail_p_table_tracks_the_weights(monkeypatch, G):
+    """The fused tail leaves the NEXT step's layer-0 table P = Emb·W_ih0^T + b_ih0 behind (and,
+    inside a multi-step graph, its batch).  After steps P matches the refreshed weights; after an
+    external rewrite of the weights (load_state -> refresh_weights) the next launch recomputes it
+    first: bit for bit the same as a trainer with the same history that computes P in every
+    step's prologue (GK_TAIL_P=0, read when a step graph is recorded).  (GK_TAIL_P is off by
+    default: measured slower at the headline.)"""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    monkeypatch.setenv("GK_TAIL_P", "1")
+    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=7)
+    stream = NameStream(cfg.batch, cfg.seq, seed=8)
+    batches = [stream.next() for _ in range(G + 1)]
+
+    def run(tr):
+        if G > 1:
+            tr.steps(batches[:G])
+        else:
+            tr.step(*batches[0])
+    a = HipTrainer(cfg, params=init_params(cfg))
+    run(a)
+    torch.cuda.synchronize()
+    assert a.t.tail_plan()[-1] > 0, a.t.tail_plan()    # the tail computed the next P
+    sd = a.state_dict()
+    got = torch.empty(cfg.vocab, 3 * cfg.hidden, dtype=torch.float32, device="cuda")
+    load_ext().copy_d2d(got.data_ptr(), a.t.buffer("P"), got.numel() * 4)
+    want = sd["embedding"].bfloat16().float() @ sd["weight_ih_l0"].bfloat16().float().T + sd["bias_ih_l0"]
+    torch.testing.assert_close(got.cpu(), want, atol=1e-4, rtol=1e-4)
+    new = {k: v * 0.9 for k, v in sd.items()}
+    a.load_state(new)
+    a.step(*batches[G])
+    monkeypatch.setenv("GK_TAIL_P", "0")
+    c = HipTrainer(cfg, params=init_params(cfg))
+    run(c)
+    c.load_state(new)
+    c.step(*batches[G])
+    torch.cuda.synchronize()
+    assert c.t.tail_plan()[-1] == 0, c.t.tail_plan()
+    assert torch.equal(a.params, c.params)
 
 
 def test_set_batch_device_matches_host():
