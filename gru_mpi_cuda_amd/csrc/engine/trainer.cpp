@@ -32,7 +32,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   struct Pend { size_t off; };
   std::vector<size_t> lo;
   auto R = [&](size_t bytes) { return arena_.reserve(bytes); };
-  size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4);
+  size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4 * kPSlabsMax);
   size_t o_lp = R(tok / 32 * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
   size_t o_sP = R((size_t)C_ * V * 3 * H * 4), o_dP = R((size_t)V * 3 * H * 4);
   size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
@@ -674,6 +674,7 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
   t.dbg = tail_dbg_;
   t.adam_after_dp = env_on("GK_TAIL_ADAM_WAIT", false) ? 1 : 0;
+  t.fc_after_dp = env_on("GK_TAIL_FC_WAIT", false) ? 1 : 0;
   if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
   tail_items_ = t.nItems;
   tail_plan_ = {t.nB, t.nF, t.nP, 1, t.nA0, t.nW, t.nE, t.nPt};

@@ -79,6 +79,13 @@ class Trainer {
   // (false after refresh_weights() or a step without it), and a launch that relies on it runs
   // ensure_p() first.
   bool tail_p_ = false, tail_batch_ = false;
+  // The prologue's P table as split-K slabs summed by the persistent forward's gather (GK_P_SLABS=4;
+  // default 1 = one table with the bias): 4x the workgroups, each fetching a quarter of Emb / W_ih0.
+  // Measured much slower at the headline (0.2458-0.2489 vs 0.2176-0.2180 ms/step): the gather's 12
+  // scattered loads per step instead of 3 sit in the recurrence's in-order vmcnt window.
+  static constexpr int kPSlabsMax = 4;
+  int p_slabs_ = 1;               // of the step being recorded
+  int p_slabs_for_record() const;
   bool p_in_prologue_ = true, batch_in_prologue_ = true, batch_from_prev_tail_ = false;
   const int* next_stage_src_ = nullptr;   // staging slot of the next step in the same graph (or null)
   bool p_valid_ = false;

@@ -25,6 +25,24 @@ static bool ar_span() {
   return on;
 }
 
+// Split-K slabs of the prologue's P table: only where the persistent forward reads it (its gather
+// sums the slabs) and the small GEMM takes the K-slices
+int Trainer::p_slabs_for_record() const {
+  if (!persist_fwd_) return 1;
+  const char* e = std::getenv("GK_P_SLABS");
+  int n = e ? std::atoi(e) : 1;
+  if (n < 1) n = 1;
+  if (n > kPSlabsMax) n = kPSlabsMax;
+  while (n > 1) {
+    GemmArgs g;
+    g.A = Emb; g.lda = d_.E; g.B = Ls_[0].Wih; g.ldb = d_.E; g.C = Ptab_; g.ldc = 3 * d_.H;
+    g.M = d_.V; g.N = 3 * d_.H; g.K = d_.E; g.splits = n;
+    if (d_.E % n == 0 && gemm_small_kblocks(g) > 0) break;
+    n >>= 1;
+  }
+  return n;
+}
+
 // Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
 // split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
 // 128 x 128 split-K path only.  GK_WGRAD_GEMM overrides the default.
@@ -133,14 +151,18 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
+  p_slabs_ = p_in_prologue_ ? p_slabs_for_record() : 1;
   if (p_in_prologue_ && batch_in_prologue_) {
     // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
-    // with the batch preparation (independent work, one graph node)
+    // with the batch preparation (independent work, one graph node); as p_slabs_ split-K partial
+    // tables (no bias: the persistent forward's gather sums them and adds b_ih0) where that applies
     GemmArgs g;
     g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
     g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
+    if (p_slabs_ > 1) { g.splits = p_slabs_; g.bias = nullptr; }
     gemm_with_prep(g, PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_}, s);
   } else if (p_in_prologue_) {   // the batch came from the previous step's fused tail
+    p_slabs_ = 1;                  // (one table with the bias)
     record_p_gemm(s);
   } else if (batch_in_prologue_) {   // P came from the previous step's fused tail
     prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
@@ -154,7 +176,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
     a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
-    if (l == 0) { a.P = Ptab_; a.ids = ids_; } else { a.Gi = y.Gi; }
+    if (l == 0) {
+      a.P = Ptab_; a.ids = ids_;
+      if (p_slabs_ > 1) { a.p_slabs = p_slabs_; a.p_slab = (long)V * H3; a.bih = P("bias_ih_l0"); }
+    } else {
+      a.Gi = y.Gi;
+    }
     a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
     if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
     a.T = T; a.Bp = B; a.H = H;

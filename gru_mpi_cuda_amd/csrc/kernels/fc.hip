@@ -199,42 +199,33 @@ constexpr int kX2Pad = 8;   // bf16 of padding per staged X row
 }
 
 // fragments from the FT layout (kernels.h ft_offset): one whole 1-KB block per load instruction
-// k-steps are visited from a per-workgroup rotation (rot, any value < H/32): the
-// 32 CUs of an XCD stream the same 256-KB weight matrix at the same moment, and in lock-step order
-// they would all hit the same L2 channel at once
 template <int NKC>
-DEV void fc2_load_w(bf16x8 (&b)[NKC][2], const u16* Wf, int H, int v0, int ks, int lane, int rot) {
-  const int nks = H / 32;
+DEV void fc2_load_w(bf16x8 (&b)[NKC][2], const u16* Wf, int H, int v0, int ks, int lane) {
 #pragma unroll
-  for (int kk = 0; kk < NKC; ++kk) {
-    const int k = (ks + kk + rot) & (nks - 1);
+  for (int kk = 0; kk < NKC; ++kk)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) b[kk][c] = ld8(Wf + ((size_t)((v0 / 16 + c) * nks + k) * 64 + lane) * 8);
-  }
+    for (int c = 0; c < 2; ++c) b[kk][c] = ld8(Wf + ((size_t)((v0 / 16 + c) * (H / 32) + ks + kk) * 64 + lane) * 8);
 }
 template <int NKC>
-DEV void fc2_mma(f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], const u16* xs, int ldx, int ks, int lane, int rot,
-                 int nks) {
+DEV void fc2_mma(f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], const u16* xs, int ldx, int ks, int lane) {
   const int lr = lane & 15, lk = 8 * (lane >> 4);
 #pragma unroll
   for (int kk = 0; kk < NKC; ++kk) {
-    const int k = (ks + kk + rot) & (nks - 1);
     bf16x8 af[2];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(xs + (r * 16 + lr) * ldx + k * 32 + lk);
+    for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(xs + (r * 16 + lr) * ldx + (ks + kk) * 32 + lk);
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int c = 0; c < 2; ++c) acc[r][c] = mfma16(af[r], b[kk][c], acc[r][c]);
   }
 }
-// W_fc^T fragments of one 64-column dH pass: [8 k-steps of V=256][4 column tiles], k-step kk
-// holding V block (kk + rot) % 8 (rotated per workgroup like fc2_load_w)
-DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WTf, int n0, int lane, int rot) {
+// W_fc^T fragments of one 64-column dH pass: [8 k-steps of V=256][4 column tiles]
+DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WTf, int n0, int lane) {
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WTf + ((size_t)((n0 / 16 + c) * 8 + ((kk + rot) & 7)) * 64 + lane) * 8);
+    for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WTf + ((size_t)((n0 / 16 + c) * 8 + kk) * 64 + lane) * 8);
 }
 
 // DH = false (the persistent backward path): no dH here -- the backward sequence kernel computes
@@ -279,9 +270,8 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
     xv[e] = *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
   }
   const int ylab = tid < FROWS ? a.labels[m0 + tid] : 0;
-  const int rot = (int)(blockIdx.x >> 3) & (nks - 1), rot8 = rot & 7;   // consecutive blocks: other XCDs
-  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane, rot);
-  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane, rot);
+  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane);
+  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane);
 #pragma unroll
   for (int e = 0; e < nxp; ++e) {
     const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
@@ -296,22 +286,20 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   f32x4 acc[2][2];
   zero_acc(acc);
   for (int ks = 0; ks < nks; ks += 2 * NKC) {
-    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane, rot, nks);
-    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane, rot);
+    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane);
+    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane);
     if (ks + NKC < nks) {
-      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane, rot, nks);
-      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane, rot);
+      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane);
+      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane);
     }
   }
   // the first dH pass's W_fc^T fragments go out now, under the softmax reductions (not earlier:
   // the scheduler barrier keeps them from overlapping the W_fc slab's registers)
   __builtin_amdgcn_sched_barrier(0);
   STAMP();
-  if (a.dbg && blockIdx.x == 0 && lane == 0) a.dbg[16 + w] = __builtin_amdgcn_s_memrealtime();   // per-wave logits done
   const int per = H / NW;                 // dH columns of this wave (a multiple of 64)
   bf16x8 bt[8][4];
-  static constexpr bool kWtEarly = false;   // experiment: W_fc^T prefetch under the softmax or after it
-  if constexpr (DH && kWtEarly) fc2_load_wt(bt, a.WTf, w * per, lane, rot8);
+  if constexpr (DH) fc2_load_wt(bt, a.WTf, w * per, lane);
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -328,8 +316,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       const float m = max16(fmaxf(acc[r][0][i], acc[r][1][i]));
       if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
     }
-  lds_barrier();   // not __syncthreads: its vmcnt(0) would wait for the W_fc^T prefetch
-  STAMP();
+  __syncthreads();
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -342,8 +329,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       const float e = sum16(__expf(acc[r][0][i] - m) + __expf(acc[r][1][i] - m));
       if (lr == 0) red[NW * 32 + w * 32 + row] = e;
     }
-  lds_barrier();   // not __syncthreads: its vmcnt(0) would wait for the W_fc^T prefetch
-  STAMP();
+  __syncthreads();
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -367,9 +353,8 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
         dlr[row * LDR + col] = db;
       }
     }
-  lds_barrier();   // not __syncthreads: its vmcnt(0) would wait for the W_fc^T prefetch
+  __syncthreads();
   STAMP();
-  if constexpr (DH && !kWtEarly) fc2_load_wt(bt, a.WTf, w * per, lane, rot8);
   // per-row nll (one thread per row; the statistics are still in LDS)
   if (tid < FROWS) {
     const int row = tid, y = ys[row];
@@ -394,14 +379,14 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   }
   // ---- dH = dl · W_fc: 32 rows x this wave's columns, 64 per pass, K = V = 256
   if constexpr (DH) for (int n0 = w * per; n0 < (w + 1) * per; n0 += 64) {
-    if (n0 != w * per) fc2_load_wt(bt, a.WTf, n0, lane, rot8);
+    if (n0 != w * per) fc2_load_wt(bt, a.WTf, n0, lane);
     f32x4 dacc[2][4];
     zero_acc(dacc);
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       bf16x8 af[2];
 #pragma unroll
-      for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(dlr + (r * 16 + lr) * LDR + ((kk + rot8) & 7) * 32 + 8 * lq);
+      for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(dlr + (r * 16 + lr) * LDR + kk * 32 + 8 * lq);
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -513,9 +498,8 @@ __global__ void __launch_bounds__(512, 1) fc_sample_v256_kernel(FcSampleArgs a) 
     const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
     xv[e] = *reinterpret_cast<const uint4*>(a.X + (size_t)(m0 + row) * H + c8 * 8);
   }
-  const int rot = (int)(blockIdx.x >> 3) & (nks - 1), rot8 = rot & 7;   // consecutive blocks: other XCDs
-  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane, rot);
-  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane, rot);
+  fc2_load_w<NKC>(b0, a.Wf, H, v0, 0, lane);
+  if (nks > NKC) fc2_load_w<NKC>(b1, a.Wf, H, v0, NKC, lane);
 #pragma unroll
   for (int e = 0; e < nxp; ++e) {
     const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
@@ -525,11 +509,11 @@ __global__ void __launch_bounds__(512, 1) fc_sample_v256_kernel(FcSampleArgs a) 
   f32x4 acc[2][2];
   zero_acc(acc);
   for (int ks = 0; ks < nks; ks += 2 * NKC) {
-    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane, rot, nks);
-    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane, rot);
+    fc2_mma<NKC>(acc, b0, xs, ldx, ks, lane);
+    if (ks + 2 * NKC < nks) fc2_load_w<NKC>(b0, a.Wf, H, v0, ks + 2 * NKC, lane);
     if (ks + NKC < nks) {
-      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane, rot, nks);
-      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane, rot);
+      fc2_mma<NKC>(acc, b1, xs, ldx, ks + NKC, lane);
+      if (ks + 3 * NKC < nks) fc2_load_w<NKC>(b1, a.Wf, H, v0, ks + 3 * NKC, lane);
     }
   }
 #pragma unroll

@@ -19,6 +19,7 @@
 //     XCD's resident workgroups share A and B panels in its L2.
 // Measured (scripts/bench_gemm.py, random operands, profiles/r2_gemm256.jsonl): 4096^3 1172 TF,
 // 8192^3 1287 TF (hipBLASLt on the same box 1190 / 1441); the 128^2 kernel 906 / 893.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include "kernels.h"
@@ -176,6 +177,141 @@ __global__ void __launch_bounds__(512, 1) gemm256_kernel(GemmArgs a, int ntn, in
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same 256 x 256 x 64 pipeline on v_mfma_f32_32x32x16_bf16: a wave's
+// 128 x 64 output is 4 x 2 accumulators of 32 x 32 (f32x16, 128 VGPRs as before), a 64-deep k-tile
+// four 16-deep k-steps of 8 MFMAs, each MFMA twice the FLOPs per operand VGPR read of 16x16x32.
+// Operand lane map (cdna_hip_programming.md): lane l holds row / column l & 31, k = 8 (l >> 5) + j,
+// i.e. 16-B chunk 2 ks + (l >> 5) of the LDS row -- the same XOR swizzle keeps the ds_read_b128
+// conflict-free (16 lanes = 16 rows, pairs of rows on the two bank halves, 8 distinct slots).
+// Accumulator: col = l & 31, row = (q & 3) + 8 (q >> 2) + 4 (l >> 5) for register q.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool BIAS, bool ACC, bool RS>
+__global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][2][128 * 64];
+  const int id = xcd_remap256(blockIdx.x, gridDim.x);
+  constexpr int kGroupM = 4;
+  const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
+  const int per_group = kGroupM * ntn, first_m = (pid / per_group) * kGroupM;
+  const int gm = min(ntm - first_m, kGroupM);
+  const int tm = first_m + (pid % per_group) % gm, tn = (pid % per_group) / gm;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int row0 = tm * kBM, col0 = tn * kBN;
+  const int kbeg = sp * kper, nk = kper / kBK;
+
+  const int srow = lane >> 3, sslot = lane & 7;
+  const u16* src[2][2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (2 * w + q) * 8 + srow;
+      const int c = sslot ^ ((r >> 1) & 7);
+      src[0][h][q] = a.A + (size_t)(row0 + h * 128 + r) * a.lda + kbeg + c * 8;
+      src[1][h][q] = a.B + (size_t)(col0 + h * 128 + r) * a.ldb + kbeg + c * 8;
+    }
+  auto stage = [&](int buf, int kt) {
+#pragma unroll
+    for (int op = 0; op < 2; ++op)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          __builtin_amdgcn_global_load_lds(src[op][h][q] + kt * kBK, (lds256_t*)(&lds[buf][op][h][(2 * w + q) * 8 * 64]),
+                                           16, 0, 0);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int bh = wc >> 1, bo = (wc & 1) * 64;
+  auto rdA = [&](int buf, int i, int ks) {
+    const int r = i * 32 + l32, c = ks * 2 + lh;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][0][wr][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  auto rdB = [&](int buf, int j, int ks) {
+    const int r = bo + j * 32 + l32, c = ks * 2 + lh;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][1][bh][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  bf16x8 fa[2][4], fb[2][2];   // register double buffer over k-steps
+  const bool do_rs = RS && tn == 0 && wc == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+#define GK_RD(set, buf, ks) { for (int i = 0; i < 4; ++i) fa[set][i] = rdA(buf, i, ks); \
+                              for (int j = 0; j < 2; ++j) fb[set][j] = rdB(buf, j, ks); }
+#define GK_MMA(set) { for (int i = 0; i < 4; ++i) for (int j = 0; j < 2; ++j) \
+    acc[i][j] = mfma32(fa[set][i], fb[set][j], acc[i][j]); \
+    if (do_rs) for (int i = 0; i < 4; ++i) rs[i] = add_sum8(fa[set][i], rs[i]); }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    GK_RD(0, cur, 0);
+    GK_RD(1, cur, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(0);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_RD(0, cur, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(1);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_RD(1, cur, 3);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(0);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#undef GK_RD
+#undef GK_MMA
+
+  if (do_rs) {   // lanes l and l + 32 hold the two k-halves of row l & 31
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = rs[i] + __shfl_xor(rs[i], 32, 64);
+      if (lane < 32) a.rowsumA[(size_t)sp * a.M + row0 + wr * 128 + i * 32 + lane] = v;
+    }
+  }
+  float* C = a.C + (size_t)sp * a.M * a.ldc;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = col0 + wc * 64 + j * 32 + l32;
+    const float bb = BIAS ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = row0 + wr * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * lh;
+        float* dst = C + (size_t)row * a.ldc + col;
+        const float v = acc[i][j][q] + bb;
+        if (ACC) *dst += v; else *dst = v;
+      }
+  }
+}
+
+// Which form (GK_GEMM256_MFMA=16 / 32 forces one; read per launch so tests and benches switch it
+// in-process).  Default: 32x32x16 only for short K-slices (<= 256), where it measured faster --
+// h2048 dH 65536 x 2048 x 256: 438 vs 360 TF -- and 16x16x32 elsewhere (sq8192 1284 vs 1203 TF,
+// h2048 dW_hh 4-way split 1139 vs 1073 TF; profiles/r3_gemm256_m32.jsonl)
+static int gemm256_mfma(int kper) {
+  const char* e = std::getenv("GK_GEMM256_MFMA");
+  if (e && e[0]) return std::atoi(e);
+  return kper <= 256 ? 32 : 16;
+}
+
 bool gemm256_ok(const GemmArgs& a) {
   if (a.onehot_ids || !a.A) return false;
   if (a.M % kBM || a.N % kBN || a.splits < 1 || a.K % a.splits) return false;
@@ -190,7 +326,12 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   if (!gemm256_ok(a)) throw std::runtime_error("gemm256: unsupported shape");
   const int ntn = a.N / kBN, ntm = a.M / kBM, kper = a.K / a.splits;
   const dim3 grid(ntn * ntm * a.splits), block(512);
-#define GK_L(B_, A_, R_) hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper)
+  const bool m32 = gemm256_mfma(kper) == 32;
+#define GK_L(B_, A_, R_)                                                                                   \
+  do {                                                                                                     \
+    if (m32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);    \
+    else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);           \
+  } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate
     if (a.bias || a.accumulate) throw std::runtime_error("gemm256: row sums only without bias / accumulate");
     GK_L(false, false, true);

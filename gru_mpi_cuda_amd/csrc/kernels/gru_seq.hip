@@ -310,11 +310,22 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order).
   // The char id it needs is loaded one step earlier still, so the gather never waits on an id load.
   int idn = a.ids ? a.ids[b] : 0;   // id of the step whose row load_gi gathers next
+  float bi[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it
+  if (a.ids && a.p_slabs > 1)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
   auto load_gi = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
     const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    if (a.ids && a.p_slabs > 1) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[g] += bi[g];
+      for (int q = 1; q < a.p_slabs; ++q)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * a.p_slab + g * H + j];
+    }
     if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};
@@ -529,11 +540,22 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
   // lo's input projection for step t, gathered one iteration ahead (off the critical path), from
   // a char id loaded one iteration before that (the gather never waits on an id load)
   int idn = L0.ids ? L0.ids[b] : 0;
+  float bi0[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it
+  if (L0.ids && L0.p_slabs > 1)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bi0[g] = L0.bih[g * H + j];
   auto load_gi0 = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
     const float* src = L0.ids ? L0.P + (size_t)idn * 3 * H : L0.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    if (L0.ids && L0.p_slabs > 1) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[g] += bi0[g];
+      for (int q = 1; q < L0.p_slabs; ++q)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * L0.p_slab + g * H + j];
+    }
     if (L0.ids && t + 1 < T) idn = L0.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};

@@ -109,6 +109,10 @@ struct SeqFwdArgs {
   float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
   const u16* Whh = nullptr; const float* bhh = nullptr;
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
+  // P as p_slabs K-slice partial tables p_slab floats apart, b_ih0 not included (p_slabs > 1: the
+  // gather sums them and adds bih) -- a split-K table GEMM of 4x the workgroups, each fetching a
+  // quarter of the operands
+  int p_slabs = 1; long p_slab = 0; const float* bih = nullptr;
   const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
   const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
   unsigned* cnt = nullptr;         // [Bp/32][H/16][16] epoch flags, zero at launch
@@ -419,6 +423,7 @@ struct TailArgs {
   const unsigned* epoch = nullptr; // launches so far incl. this one (bumped before the launch: SeqBwdArgs::bump)
   unsigned long long* dbg = nullptr;   // diagnostic (nullable): [nItems][4] = start, wait done, end, wg | xcc << 16
   int adam_after_dp = 0;           // Adam blocks start once a dP column block is complete (the dP chain first)
+  int fc_after_dp = 0;             // dW_fc blocks likewise (they are off the critical path)
   // dW_fc = dl^T · H_top and db_fc = row sums of dl^T over nfc K-slices of tokens (0: not in the
   // tail; the W_fc / b_fc jobs then take their gradient as before).  Slice s goes to slab s of
   // slab_fc / rs_fc; a tile's LAST slice sums the slabs and runs the Adam of that W_fc tile (and of

@@ -220,8 +220,12 @@ __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJob
     const bool do_rs = tn == 0 && ((threadIdx.x >> 6) & 1) == 0;
     float rs[2] = {0.f, 0.f};
     f32x4 acc[2][2];
-    tail_product(t.dlT, t.ldl, (long)t.V * t.ldl * 2, t.HTop, t.ldh, tm * 64, tn * 64, sp * kl, kl, acc, [] {},
-                 do_rs ? rs : nullptr);
+    tail_product(t.dlT, t.ldl, (long)t.V * t.ldl * 2, t.HTop, t.ldh, tm * 64, tn * 64, sp * kl, kl, acc, [&] {
+      if (t.fc_after_dp) {   // let the dP chain have the memory system first
+        tail_wait(tail_ctr(t.sync, it % (t.H3 / 64)), colTarget, err);
+        __syncthreads();
+      }
+    }, do_rs ? rs : nullptr);
     const long n = (long)t.V * t.H;
     const brsrc_t rS = brsrc(t.slab_fc, (unsigned)(t.nfc * n * 4));
 #pragma unroll
@@ -464,7 +468,8 @@ bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s) {
   // slots, a block they wait for always gets a slot: the launch drains whatever the dispatch order.
   // The P items wait for product blocks (which wait only for dP tiles): still a bounded chain, and
   // all waiting blocks together stay below the resident slots.
-  if (cap <= 0 || t.nW + t.nE + t.nPt >= cap || t.se > 8 || (t.H3 / t.se) % 256 || t.V % 256) return false;
+  const int waiting = t.nW + t.nE + t.nPt + (t.fc_after_dp ? t.nF : 0) + (t.adam_after_dp ? t.nA0 : 0);
+  if (cap <= 0 || waiting >= cap || t.se > 8 || (t.H3 / t.se) % 256 || t.V % 256) return false;
   if (t.dbg && t.nItems > 65536) t.dbg = nullptr;
   if (occ == 4) hipLaunchKernelGGL(tail_kernel<4>, dim3(t.nItems), dim3(256), 0, s, a, j, t);
   else hipLaunchKernelGGL(tail_kernel<3>, dim3(t.nItems), dim3(256), 0, s, a, j, t);

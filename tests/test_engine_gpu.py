@@ -377,8 +377,8 @@ def test_tail_p_table_tracks_the_weights(monkeypatch, G):
     inside a multi-step graph, its batch).  After steps P matches the refreshed weights; after an
     external rewrite of the weights (load_state -> refresh_weights) the next launch recomputes it
     first: bit for bit the same as a trainer with the same history that computes P in every
-    step's prologue (GK_TAIL_P=0, read when a step graph is recorded).  (GK_TAIL_P is off by
-    default: measured slower at the headline.)"""
+    step's prologue as one table (GK_TAIL_P=0, GK_P_SLABS=1; read when a step graph is recorded).
+    (GK_TAIL_P is off by default: measured slower at the headline.)"""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     monkeypatch.setenv("GK_TAIL_P", "1")
@@ -404,6 +404,7 @@ def test_tail_p_table_tracks_the_weights(monkeypatch, G):
     a.load_state(new)
     a.step(*batches[G])
     monkeypatch.setenv("GK_TAIL_P", "0")
+    monkeypatch.setenv("GK_P_SLABS", "1")   # one table with the bias, as the tail and ensure_p() write it
     c = HipTrainer(cfg, params=init_params(cfg))
     run(c)
     c.load_state(new)
