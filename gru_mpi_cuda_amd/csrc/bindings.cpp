@@ -247,6 +247,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
+  m.def("fwd_seq_pl_supported", &gru_fwd_seq_pl_supported);
   m.def("bwd_step_sk_splits", &gru_bwd_step_sk_splits);
   m.def("step_lds_variants", []() {
     const StepLdsVariants& v = step_lds_variants();
@@ -311,7 +312,15 @@ PYBIND11_MODULE(_C, m) {
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
-    if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
+    // table-free layer 0: Emb, Wih0, bih, V, E (+ the staging slot prep_in with labels / inv_count)
+    a.Emb = GP(const u16, d, "Emb"); a.Wih0 = GP(const u16, d, "Wih0"); a.bih = GP(const float, d, "bih");
+    a.V = get<int>(d, "V", 0); a.E = get<int>(d, "E", 0);
+    if (GP(const int, d, "prep_in")) {
+      a.prep = PrepJob{GP(const int, d, "prep_in"), get<int>(d, "Bmax", a.Bp), a.T, a.Bp, const_cast<int*>(a.ids),
+                       GP(int, d, "labels"), GP(float, d, "inv_count")};
+    }
+    if (a.Emb ? !gru_fwd_seq_pl_supported(a.H, a.Bp, a.V, a.E, a.T) : !gru_fwd_seq_supported(a.H, a.Bp))
+      throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });

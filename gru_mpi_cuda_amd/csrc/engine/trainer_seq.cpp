@@ -151,8 +151,16 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
-  p_slabs_ = p_in_prologue_ ? p_slabs_for_record() : 1;
-  if (p_in_prologue_ && batch_in_prologue_) {
+  // table-free layer 0 (GK_FWD_PL=1, off by default): the persistent forward computes the P-table
+  // columns it gathers from and transposes the batch itself -- no prologue kernel (gru_seq.hip, PL).
+  // Measured slower: every workgroup streams all of Emb (256 x 304 KB of L2 reads) and redoes 8x the
+  // table's MFMAs, 10-17 us before its first step against the 7 us prologue kernel
+  // (forward 60 -> 90 us, step 0.216 -> 0.240 ms, profiles/r3s5_fwd_pl_ab.jsonl)
+  const bool fwd_pl = fwd_pl_ok();
+  p_slabs_ = (p_in_prologue_ && !fwd_pl) ? p_slabs_for_record() : 1;
+  if (fwd_pl) {
+    // (nothing before the forward launch)
+  } else if (p_in_prologue_ && batch_in_prologue_) {
     // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
     // with the batch preparation (independent work, one graph node); as p_slabs_ split-K partial
     // tables (no bias: the persistent forward's gather sums them and adds b_ih0) where that applies
@@ -176,7 +184,10 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
     a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
-    if (l == 0) {
+    if (l == 0 && fwd_pl) {
+      a.Emb = Emb; a.Wih0 = Ls_[0].Wih; a.bih = P("bias_ih_l0"); a.V = V; a.E = E; a.ids = ids_;
+      if (batch_in_prologue_) a.prep = PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_};
+    } else if (l == 0) {
       a.P = Ptab_; a.ids = ids_;
       if (p_slabs_ > 1) { a.p_slabs = p_slabs_; a.p_slab = (long)V * H3; a.bih = P("bias_ih_l0"); }
     } else {
@@ -479,8 +490,17 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   HIP_LAUNCH_CHECK();
 }
 
+// layer 0 through the table-free persistent forward (no prologue P GEMM / batch kernel): read when a
+// step is recorded
+bool Trainer::fwd_pl_ok() const {
+  if (!persist_fwd_ || !p_in_prologue_ || (fwd_wave_ && d_.L >= 2)) return false;
+  if (!env_flag("GK_FWD_PL", false)) return false;
+  return gru_fwd_seq_pl_supported(d_.H, Bp_, d_.V, d_.E, d_.T);
+}
+
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") + (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
+  if (fwd_pl_ok()) p += "+pl";
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

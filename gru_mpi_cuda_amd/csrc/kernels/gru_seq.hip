@@ -265,9 +265,27 @@ DEV void signal_flag_local(unsigned* flag, unsigned epoch) {
 // RS = 2: waves 0-3 own row tile 0, waves 4-7 row tile 1, each over a K/4 slice (NKW = H/128):
 //         the same MFMAs and exchange loads per wave, half the LDS partial traffic (4 partials of
 //         3 gates per output instead of 8, read by the epilogue thread of the same row tile).
-template <int NKW, int RS>
+//
+// PL = true (SeqFwdArgs::Emb, layer 0 without a P table): the launch also does what the step's
+// prologue kernel did.  Each workgroup
+//   * computes the 48 columns of P = Emb · W_ih0^T + b_ih0 it gathers from (3 gates x its 16 units,
+//     all V rows) into LDS: the W_ih0 slice staged once (XOR-swizzled 16-B pieces), wave w takes row
+//     tiles w and w + 8 of Emb straight into registers, 16x16x32 MFMAs over k-steps of 32 in
+//     increasing order + the bias after -- gemm_small's sequence, so bitwise the prologue's table;
+//   * transposes its share of the batch (rows 32 rb + ut + k H/16) from the pinned staging slot into
+//     ids / labels (agent-scope stores), its round trip issued after the product's operand loads so
+//     the product's waits do not include it (vmcnt retires in order);
+//   * then joins its row block's start-up exchange (row_block_local), which now also publishes those
+//     ids: the step loop's id loads follow it (plain loads when the row block shares one L2, agent-scope
+//     loads otherwise).
+// The per-step gather then reads the table from LDS.  Measured slower than the prologue's table
+// (off by default, GK_FWD_PL=1): the 8 row blocks of a unit tile redo the same columns, so the chip
+// streams 78 MB of Emb / W_ih0 through L2 and runs 8x the table's MFMAs -- 10-17 us before the
+// first step, against the 7 us prologue kernel (profiles/r3s5_fwd_pl_ab.jsonl).
+template <int NKW, int RS, bool PL>
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][6][256];
+  __shared__ __attribute__((aligned(16))) float Pl[PL ? 256 : 1][PL ? 48 : 1];   // [V][gate * 16 + unit]
   // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
   // u16 writes -- rows 4 apart within a wave -- land in distinct banks (unpadded: 2-way / 4-way)
   __shared__ __attribute__((aligned(16))) u16 stg[32][24];
@@ -283,10 +301,13 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const unsigned nunit = (unsigned)(H / 16);
 
   bf16x8 bw[NKW][3];   // this wave's K-slice of W_h{r,z,n} for the 16 units, resident all sequence
+  auto load_bw = [&]() {
 #pragma unroll
-  for (int kk = 0; kk < NKW; ++kk)
+    for (int kk = 0; kk < NKW; ++kk)
 #pragma unroll
-    for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
+      for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
+  };
+  if constexpr (!PL) load_bw();   // (PL: after the table product, which needs the registers)
 
   // this thread's epilogue item (row, unit) -- one per thread with 512 threads
   const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
@@ -303,19 +324,134 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
   const rsrc_t rSn = make_rsrc(a.sn, a.sn ? sv_bytes : 0u), rSg = make_rsrc(a.sghn, a.sghn ? sv_bytes : 0u);
   const unsigned sv_lane = (unsigned)((b * H + j) * 4);
+  stamp(a.dbg, T + 1, 0);   // prologue stamps in the (unused) step slot T + 1
   zero_next_flags(a.zero_next, a.zero_words);
-  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
+  if constexpr (PL) {
+    const int E = a.E, V = a.V, npe = E >> 3;          // 16-B pieces per row
+    // W_ih0 slice [48][E]: row rr = gate rr/16, unit j0 + rr%16; piece p at (p ^ (rr & 7)) (B-fragment
+    // reads 2-way instead of 16-way bank conflicts).  Aliases the partials: unused until the loop.
+    u16* Ws = reinterpret_cast<u16*>(&part[0][0][0]);
+    uint4 wv[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int q = tid + e * 512;
+      if (q < 48 * npe) {
+        const int rr = q / npe, p = q - rr * npe;
+        wv[e] = *reinterpret_cast<const uint4*>(a.Wih0 + (size_t)((rr >> 4) * H + j0 + (rr & 15)) * E + p * 8);
+      }
+    }
+    const int nrt = V >> 7;   // Emb row tiles of this wave: w and w + 8
+    bf16x8 ae[2][16];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        if (r < nrt && ks < (E >> 5)) ae[r][ks] = ld8(a.Emb + (size_t)((w + 8 * r) * 16 + lr) * E + ks * 32 + lk);
+    __builtin_amdgcn_sched_barrier(0);
+    // this workgroup's batch share (pinned host memory, one round trip), issued after the operands
+    const PrepJob& pj = a.prep;
+    const int nr = (32 - ut + (int)nunit - 1) / (int)nunit;   // rows ut + k * nunit < 32
+    int xr[2] = {0, 0}, yr[2] = {0, 0}, bn = 0;
+    if (pj.in) {
+      const int* xs = pj.in + 16;
+      const int* ys = xs + (size_t)pj.Bmax * T;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int q = tid + e * 512;
+        if (q < nr * T) {
+          const int k = q / T, tt = q - k * T;
+          const size_t i = (size_t)(b0 + ut + k * (int)nunit) * T + tt;
+          xr[e] = xs[i];
+          yr[e] = ys[i];
+        }
+      }
+      bn = pj.in[0];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      const int q = tid + e * 512;
+      if (q < 48 * npe) {
+        const int rr = q / npe, p = q - rr * npe;
+        *reinterpret_cast<uint4*>(Ws + (size_t)rr * E + ((p ^ (rr & 7)) << 3)) = wv[e];
+      }
+    }
+    __syncthreads();
+    stamp(a.dbg, T + 1, 1);
+    f32x4 pacc[2][3];
+    zero_acc(pacc);
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (ks < (E >> 5)) {
+        bf16x8 bq[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          const int rr = g * 16 + lr, p = ks * 4 + (lk >> 3);
+          bq[g] = *reinterpret_cast<const bf16x8*>(Ws + (size_t)rr * E + ((p ^ (rr & 7)) << 3));
+        }
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          if (r < nrt)
+#pragma unroll
+            for (int g = 0; g < 3; ++g) pacc[r][g] = mfma16(ae[r][ks], bq[g], pacc[r][g]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      const float bb = a.bih[g * H + j0 + lr];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        if (r < nrt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) Pl[(w + 8 * r) * 16 + (lane >> 4) * 4 + i][g * 16 + lr] = pacc[r][g][i] + bb;
+    }
+    stamp(a.dbg, T + 1, 2);
+    if (pj.in) {   // the batch share, stored write-through; drained before the start-up exchange below
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int q = tid + e * 512;
+        if (q < nr * T) {
+          const int k = q / T, tt = q - k * T, bb = b0 + ut + k * (int)nunit;
+          const bool ok = bb < bn;
+          __hip_atomic_store(pj.ids + (size_t)tt * Bp + bb, ok ? xr[e] : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(pj.labels + (size_t)tt * Bp + bb, ok ? yr[e] : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (blockIdx.x == 0 && tid == 0) pj.inv_count[0] = __int_as_float(pj.in[1]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();   // every wave's stores drained (and Ws read) before the exchange's first store
+    stamp(a.dbg, T + 1, 3);
+    load_bw();
+  }
+  // PL: the exchange runs whatever allow_local says (it also publishes the batch share)
+  const bool rbl = (PL || a.allow_local) && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
+  const bool loc = a.allow_local && rbl;
+  stamp(a.dbg, T + 1, 4);
 
   // the input projection of step t, gathered one step ahead, after the publish (its latency off
   // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order).
   // The char id it needs is loaded one step earlier still, so the gather never waits on an id load.
-  int idn = a.ids ? a.ids[b] : 0;   // id of the step whose row load_gi gathers next
+  // (PL: ids written in this launch -- agent-scope loads unless the row block shares one L2)
+  auto load_id = [&](size_t o) -> int {
+    if constexpr (PL) {
+      if (!loc) return __hip_atomic_load(a.ids + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return a.ids[o];
+  };
+  int idn = a.ids ? load_id(b) : 0;   // id of the step whose row load_gi gathers next
   float bi[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it
   if (a.ids && a.p_slabs > 1)
 #pragma unroll
     for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
   auto load_gi = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
+    if constexpr (PL) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[g] = Pl[idn][g * 16 + col];
+      if (t + 1 < T) idn = load_id((size_t)(t + 1) * Bp + b);
+      return;
+    }
     const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
@@ -326,7 +462,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
 #pragma unroll
         for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * a.p_slab + g * H + j];
     }
-    if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
+    if (a.ids && t + 1 < T) idn = load_id((size_t)(t + 1) * Bp + b);
   };
   float gin[3] = {0.f, 0.f, 0.f};
   load_gi(0, gin);
@@ -1038,7 +1174,19 @@ bool gru_fwd_seq_supported(int H, int Bp) {
   if (Bp % 32) return false;
   const int rs = fwd_rs(H);
   int cap = -1;
-#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS>);
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, false>);
+  FWD_VARIANTS(X)
+#undef X
+  return cap >= (H / 16) * (Bp / 32);
+}
+
+bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T) {
+  if (Bp % 32 || H % 16 || (V != 128 && V != 256) || E % 64 || E < 64 || E > 512 || T < 1) return false;
+  const int nunit = H / 16, nr = (32 + nunit - 1) / nunit;
+  if (T * nr > 1024) return false;
+  const int rs = fwd_rs(H);
+  int cap = -1;
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, true>);
   FWD_VARIANTS(X)
 #undef X
   return cap >= (H / 16) * (Bp / 32);
@@ -1049,10 +1197,16 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
-#define X(HH, NK, RS)                                                        \
-  if (a.H == HH && rs == RS) {                                              \
-    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS>), grid, block, 0, s, a); \
-    return;                                                                  \
+  const bool pl = a.Emb != nullptr;
+  if (pl && (!a.Wih0 || !a.bih || !a.ids || a.P || a.Gi || !gru_fwd_seq_pl_supported(a.H, a.Bp, a.V, a.E, a.T) ||
+             (a.prep.in && (a.prep.ids != a.ids || !a.prep.labels || !a.prep.inv_count || a.prep.T != a.T ||
+                            a.prep.Bp != a.Bp || a.prep.Bmax < a.Bp))))
+    throw std::runtime_error("gru_fwd_seq: inconsistent table-free layer-0 arguments");
+#define X(HH, NK, RS)                                                                    \
+  if (a.H == HH && rs == RS) {                                                          \
+    if (pl) hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, true>), grid, block, 0, s, a); \
+    else hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, false>), grid, block, 0, s, a);   \
+    return;                                                                              \
   }
   FWD_VARIANTS(X)
 #undef X

@@ -94,6 +94,9 @@ void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s);
 // ------------------------------------------------------------------ persistent sequence kernels
 // One launch per layer runs all T steps (gru_seq.hip).  Requires 512-thread co-residency of
 // (H/16) x (Bp/32) workgroups; callers check *_supported() and fall back to per-step kernels.
+// Batch preparation: a pinned staging slot (in[0] = rows, in[1] = 1/valid labels as float bits,
+// x [Bmax][T] at in + 16, y after it) transposed into ids / labels [T][Bp] (rows >= in[0]: id 0, label -1)
+struct PrepJob { const int* in = nullptr; int Bmax = 0, T = 0, Bp = 0; int* ids = nullptr; int* labels = nullptr; float* inv_count = nullptr; };
 struct SeqFwdArgs {
   u16* HSb = nullptr;              // [T+1][Bp][H] bf16; HS[0] = h_init, step t writes HS[t+1]
   // exchange copy of h_{t+1}, tiled per producer: [T][Bp/32][H/16][32 rows][16] bf16 -- every
@@ -114,6 +117,15 @@ struct SeqFwdArgs {
   // quarter of the operands
   int p_slabs = 1; long p_slab = 0; const float* bih = nullptr;
   const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
+  // layer 0 WITHOUT a P table (Emb != nullptr; gru_fwd_seq_pl_supported): every workgroup computes
+  // the 48 columns of P = Emb · W_ih0^T + b_ih0 it gathers from (its 16 units x 3 gates, all V rows)
+  // into LDS at launch -- the k-sequence of gemm_small, so bitwise the prologue table -- and
+  // transposes its share of the batch (prep, rows 32 rb + ut (mod H/16)) from the pinned staging slot
+  // into ids / labels before its row block's start-up exchange.  No prologue kernel in the step.
+  const u16* Emb = nullptr;        // [V][E] bf16
+  const u16* Wih0 = nullptr;       // [3H][E] bf16 (bias in bih)
+  int V = 0, E = 0;
+  PrepJob prep;                    // prep.in == nullptr: ids already hold the batch
   const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
   unsigned* cnt = nullptr;         // [Bp/32][H/16][16] epoch flags, zero at launch
   unsigned* zero_next = nullptr;   // flag block of the NEXT sequence kernel, zeroed here (nullable)
@@ -126,6 +138,9 @@ struct SeqFwdArgs {
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
 inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 16; }
 bool gru_fwd_seq_supported(int H, int Bp);
+// the table-free layer-0 variant (SeqFwdArgs::Emb): V in {128, 256}, E % 64 == 0, E <= 512, and a
+// row block's batch share fits one pass (T * ceil(32 / (H/16)) <= 1024)
+bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
@@ -406,7 +421,6 @@ void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 // and the embedding-side products dW_ih0 = dP^T Emb and dEmb = dP W_ih0, each output tile followed
 // directly by the Adam update of that tile.  One block per work item; the product items come last
 // in the grid and wait (bounded) on per-column-block counters of the dP tiles.
-struct PrepJob { const int* in; int Bmax, T, Bp; int* ids; int* labels; float* inv_count; };
 struct TailArgs {
   const float* dP_part = nullptr; int nslP = 0, V = 0, H3 = 0;   // [nslP][V][H3] -> dP_bf, dPT_bf
   // dP_part aliases the W_ih0 gradient slot (data-parallel: the all-reduced dP lives there): the

@@ -738,3 +738,31 @@ def test_carry_graph_replay_matches_eager(layers, H, B, synced):
     torch.cuda.synchronize()
     assert torch.equal(g.params, e.params)
     assert g.t.read_error() == 0
+
+
+@pytest.mark.parametrize("G,batch,H", [(1, 64, 512), (4, 80, 512), (3, 64, 256)])
+def test_table_free_forward_matches_prologue_table(monkeypatch, G, batch, H):
+    """Layer 0 through the table-free persistent forward (GK_FWD_PL=1, opt-in: the launch computes its
+    P-table columns and transposes the batch, no prologue kernel) trains bit for bit like the
+    prologue's table + batch kernel (GK_FWD_PL=0, the default), single steps and multi-step graphs,
+    with padded batch rows (80 of 96)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=1, batch=batch, seq=8, seed=9)
+    stream = NameStream(cfg.batch, cfg.seq, seed=10)
+    batches = [stream.next() for _ in range(2 * G)]
+    runs = []
+    for pl in ("1", "0"):
+        monkeypatch.setenv("GK_FWD_PL", pl)
+        tr = HipTrainer(cfg, params=init_params(cfg))
+        assert ("+pl" in tr.t.plan()) == (pl == "1"), tr.t.plan()
+        if G > 1:
+            tr.steps(batches[:G])
+            tr.steps(batches[G:])
+        else:
+            for x, y in batches:
+                tr.step(x, y)
+        torch.cuda.synchronize()
+        runs.append(tr)
+    a, b = runs
+    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+    assert a.loss() == b.loss()
