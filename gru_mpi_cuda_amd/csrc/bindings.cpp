@@ -324,6 +324,26 @@ PYBIND11_MODULE(_C, m) {
     gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
+  m.def("fwd_seq_fc", [](py::dict d, py::dict fd, uintptr_t s) {   // diagnostics / tests: the FC-pipeline forward
+    SeqFwdArgs a;
+    a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+    a.HF = GP(u16, d, "HF"); a.xch = GP(u16, d, "xch");
+    a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
+    a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
+    a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
+    a.h0 = GP(const float, d, "h0"); a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
+    a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+    a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    FwdFcArgs f;
+    f.Wfc = GP(const u16, fd, "Wfc"); f.WfcT = GP(const u16, fd, "WfcT"); f.bfc = GP(const float, fd, "bfc");
+    f.labels = GP(const int, fd, "labels"); f.inv_count = GP(const float, fd, "inv_count");
+    f.xdl = GP(u16, fd, "xdl"); f.xdlT = GP(u16, fd, "xdlT"); f.xst = GP(float, fd, "xst"); f.dy = GP(float, fd, "dy");
+    f.dW_part = GP(float, fd, "dW_part"); f.db_part = GP(float, fd, "db_part"); f.loss_part = GP(float, fd, "loss_part");
+    f.V = get<int>(fd, "V", 256);
+    gru_fwd_seq_fc(a, f, S(s));
+    HIP_LAUNCH_CHECK();
+  });
+  m.def("fwd_seq_fc_supported", &gru_fwd_seq_fc_supported);
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
     a.dy = GP(const float, d, "dy");

@@ -33,7 +33,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   std::vector<size_t> lo;
   auto R = [&](size_t bytes) { return arena_.reserve(bytes); };
   size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4 * kPSlabsMax);
-  size_t o_lp = R(tok / 32 * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
+  size_t o_lp = R(std::max(tok / 32, (size_t)(H / 16) * (B / 32)) * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
   size_t o_sP = R((size_t)C_ * V * 3 * H * 4), o_dP = R((size_t)V * 3 * H * 4);
   size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
   size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
@@ -43,6 +43,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   fc_split_ = !fc_xent_fused_ok(V, H, (int)tok) && tok % 128 == 0 && V % 128 == 0 && V <= 512 && H % 64 == 0 &&
               H >= 128;
   size_t o_lg = fc_split_ ? R(tok * V * 4) : 0;
+  // row statistics exchange of the forward's FC pipeline (gru_fwd_seq_fc; its dl tiles live in dl_ / dlT_)
+  size_t o_xst = (V == 256 && H <= 512 && B % 32 == 0) ? R((size_t)T * (B / 32) * 16 * 256) : 0;
   struct LO { size_t HSf, sr, sz, sn, sghn, dy, Gi, c0, c1, HSb, HT, g0, g1, dghT, dgiT, dgi, Whh, WhhT, Wih, WihT, shh, rhh, sih, rih; };
   std::vector<LO> los(L);
   for (int l = 0; l < L; ++l) {
@@ -134,6 +136,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
 
   ids_ = arena_.get<int>(o_ids); labels_ = arena_.get<int>(o_lab); inv_count_ = arena_.get<float>(o_inv);
   Ptab_ = arena_.get<float>(o_P); loss_part_ = arena_.get<float>(o_lp); loss_ = arena_.get<float>(o_loss);
+  xst_ = o_xst ? arena_.get<float>(o_xst) : nullptr;
   slab_fc_ = arena_.get<float>(o_sfc); rs_fc_ = arena_.get<float>(o_rfc); slab_P_ = arena_.get<float>(o_sP);
   dP_ = arena_.get<float>(o_dP); norm_parts_ = arena_.get<float>(o_np); gscale_ = arena_.get<float>(o_gs);
   step_ = arena_.get<int>(o_step);
@@ -669,7 +672,7 @@ void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
   }
   if (tail_batch_ && next_stage_src_)   // the next step's batch, when this graph holds that step
     t.prep = PrepJob{next_stage_src_, Bp_, d_.T, Bp_, ids_, labels_, inv_count_};
-  t.loss_part = loss_part_; t.nloss = (int)(tok / 32); t.loss = loss_;
+  t.loss_part = loss_part_; t.nloss = nloss_; t.loss = loss_;
   t.sync = tail_sync_;
   t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
   t.dbg = tail_dbg_;

@@ -252,6 +252,9 @@ class Trainer {
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
+  float* xst_ = nullptr;         // forward FC pipeline: row statistics exchange
+  int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks or forward workgroups)
+  bool fwd_fc_ok() const;
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }

@@ -157,6 +157,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // table's MFMAs, 10-17 us before its first step against the 7 us prologue kernel
   // (forward 60 -> 90 us, step 0.216 -> 0.240 ms, profiles/r3s5_fwd_pl_ab.jsonl)
   const bool fwd_pl = fwd_pl_ok();
+  const bool fwd_fc = !fwd_pl && fwd_fc_ok();
+  nloss_ = fwd_fc ? (H / 16) * (B / 32) : (int)(tok / 32);
   p_slabs_ = (p_in_prologue_ && !fwd_pl) ? p_slabs_for_record() : 1;
   if (fwd_pl) {
     // (nothing before the forward launch)
@@ -221,6 +223,13 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       w2.Wih = Ls_[l + 1].Wih; w2.bih = P("bias_ih_l" + std::to_string(l + 1));
       gru_fwd_seq2(w2, s);
       ++l;
+    } else if (persist_fwd_ && l == L - 1 && fwd_fc) {
+      // the top layer with the FC / softmax-xent / dH pipeline inside the launch
+      FwdFcArgs f;
+      f.Wfc = Wfc; f.WfcT = WfcT; f.bfc = P("fc.bias"); f.labels = labels_; f.inv_count = inv_count_;
+      f.xdl = dl_; f.xdlT = dlT_; f.xst = xst_; f.dy = Ls_[l].dy;
+      f.dW_part = slab_fc2_; f.db_part = rs_fc2_; f.loss_part = loss_part_; f.V = V;
+      gru_fwd_seq_fc(fwd_args(l), f, s);
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
     } else {
@@ -235,8 +244,23 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // Off by default: fc_xent 16.3 -> 11.4 us but the backward kernel +7..10 us at h512 (its step
   // 2.6 -> 2.8 us, every phase a little longer; profiles/r2_bwd_dh_ab.jsonl).  GK_BWD_DH=1 turns it on.
   static const bool bwd_dh_env = env_flag("GK_BWD_DH", false);
-  const bool bwd_dh = bwd_dh_env && seq_[L - 1].bwd && V == 256 && fc_xent_fused_ok(V, H, (int)tok);
-  {
+  const bool bwd_dh = !fwd_fc && bwd_dh_env && seq_[L - 1].bwd && V == 256 && fc_xent_fused_ok(V, H, (int)tok);
+  if (fwd_fc) {
+    // logits, loss, dl and dH came out of the forward launch; dW_fc / db_fc as one partial per row
+    // block, summed with the other slabs
+    tail_nfc_ = 0;
+    tail.add(slab_fc2_, nrb, (long)V * H, G("fc.weight"));
+    tail.add(rs_fc2_, nrb, V, G("fc.bias"));
+    if (dp && ar_span() && seq_[L - 1].bwd && env_flag("GK_AR_FC_EARLY", false) && tail.n) {
+      SlabJobs fcj;
+      for (int k2 = 0; k2 < tail.n; ++k2)
+        slab_job(fcj, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
+      if (fcj.n) reduce_slabs_multi(fcj, s);
+      tail.n = 0;
+      ar_ready_ = group_end(L);
+      ar_flush(s, /*force=*/true);
+    }
+  } else {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
     f.labels = labels_; f.inv_count = inv_count_;
@@ -365,7 +389,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       for (int k2 = 0; k2 < tail.n; ++k2)
         slab_job(j, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
     if (l == 0 && !tail_fused_) {   // + the loss partials and the optimiser step counter
-      j.add(loss_part_, (int)(tok / 32), 1, loss_);
+      j.add(loss_part_, nloss_, 1, loss_);
       j.bump = step_;
     }
     if (j.n) reduce_slabs_multi(j, s);
@@ -498,9 +522,21 @@ bool Trainer::fwd_pl_ok() const {
   return gru_fwd_seq_pl_supported(d_.H, Bp_, d_.V, d_.E, d_.T);
 }
 
+// the top layer's forward carries the FC pipeline (GK_FWD_FC=1, opt-in): one layer, H = 512, V = 256.
+// Measured: the tail loses its dW_fc items (42.8 -> 29.9 us) and fc_xent goes away (15.5 us), but the
+// pipeline's dl row-block loads (+32 KB per workgroup per step on top of the 32 KB h exchange) slow the
+// latency-bound recurrence from 1.84 to 3.6-3.7 us per step (forward 69 -> 132 us): 0.217 -> 0.261
+// ms/step (profiles/r3s5_fwd_fc_ab.jsonl)
+bool Trainer::fwd_fc_ok() const {
+  if (!persist_fwd_ || d_.L != 1 || !xst_ || !seq_[0].bwd) return false;
+  if (!env_flag("GK_FWD_FC", false)) return false;
+  return gru_fwd_seq_fc_supported(d_.H, Bp_, d_.V);
+}
+
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") + (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   if (fwd_pl_ok()) p += "+pl";
+  else if (fwd_fc_ok()) p += "+fc";
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

@@ -573,6 +573,345 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   }
 }
 
+// ==================================================================== forward + FC / softmax-xent / dH
+// The top layer's output h(t) feeds logits = h W_fc^T + b_fc, a softmax cross-entropy and dH =
+// dl W_fc (and dW_fc = dl^T h).  As a kernel of its own (fc_xent, 15.5 us at the headline) every
+// 32-row block streams all of W_fc twice, and the tail's dW_fc product re-reads dl and h (64 MB);
+// here the same work rides along the recurrence on operands the persistent workgroups already hold,
+// as a pipeline that runs five steps behind it:
+//   step t     S1: the 16 workgroups ut < 16 of a row block own logits columns 16 ut .. +15; their
+//                  waves multiply the h(t-1) K-slice fragments they loaded for the gates by a resident
+//                  W_fc slice (K-partials to LDS, double-buffered);
+//              after the publish (the slack before the next poll): the logits, each row's local max
+//                  and sum-exp over the 16 columns (DPP);
+//   step t+1   those statistics go out with the h tile (same drain, same flag);
+//   step t+2   the 16 producers' statistics of each row arrive with the exchange fragments (LDS-DMA);
+//              after the publish: dl = (softmax - onehot) / count, the loss and db_fc per thread;
+//   step t+3   the bf16 dl tile (row-major and transposed) goes out with the h tile;
+//   step t+4   every workgroup loads the dl row block as MFMA fragments (V k-steps assigned to the waves
+//              that already poll those producers): dH = dl W_fc for its 16 units (K-partials in LDS,
+//              stored fp32 for the backward) and, after the publish, dW_fc[:, its units] += dl^T h
+//              from a ring of its transposed h tiles -- per row block partials, summed by the
+//              optimiser's slab sums.
+// Five drain iterations after the last step finish it (flags advance in each).  No fc_xent launch,
+// no dW_fc product in the tail.  H = 512 (RS = 2: waves 0-3 row tile 0, 4-7 row tile 1), V = 256.
+template <int NKW>
+__global__ void __launch_bounds__(512, 1) gru_fwd_seq_fc_kernel(SeqFwdArgs a, FwdFcArgs f) {
+  constexpr int NKV = NKW / 2;   // V k-steps (32 logits each) per dH wave
+  constexpr int V = 256;
+  constexpr int DEP = 5;         // pipeline depth: dH of step t - 5 at step t
+  __shared__ __attribute__((aligned(16))) float part[8][6][256];   // gates r,z,n | - | dH row tile 0, 1
+  __shared__ __attribute__((aligned(16))) float lgp[2][8][256];    // logits K-partials (step parity)
+  __shared__ __attribute__((aligned(16))) u16 stg[32][24];
+  __shared__ __attribute__((aligned(16))) u16 stgT[8][16][40];     // ring of h(t)^T: dW_fc's B operand at t + 5
+  __shared__ __attribute__((aligned(16))) float stl[2][16][64];    // producers' (max, sum-exp) per row
+  __shared__ __attribute__((aligned(16))) float sst[2][64];        // this workgroup's, to publish
+  __shared__ __attribute__((aligned(16))) u16 sdl[2][32][24];      // dl tile row-major, to publish
+  __shared__ __attribute__((aligned(16))) u16 sdlT[2][16][40];     // dl tile transposed, to publish
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int H = a.H, Bp = a.Bp, T = a.T;
+  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
+  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
+  const int lr = lane & 15, lk = 8 * (lane >> 4);
+  const int rt = w >> 2;                       // this wave's row tile
+  const int k0 = (w & 3) * NKW * 32;           // and K-slice
+  const unsigned nunit = (unsigned)(H / 16);
+  const bool fcw = ut < 16;                    // owns logits columns 16 ut .. +15
+  // dH k-steps of this wave: kvb .. kvb + NKV - 1 (producers 2 kv, 2 kv + 1 are among the ones it polls)
+  const int kvb = (k0 >> 5) + rt * NKV;
+  const bool s4w = kvb < 8;
+
+  bf16x8 bw[NKW][3];
+#pragma unroll
+  for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
+  // the FC operands stay resident lane-linear in LDS (each lane re-reads only its own 16-B slots:
+  // conflict-free, no barrier) -- in VGPRs they pushed the register file into spills
+  __shared__ __attribute__((aligned(16))) bf16x8 wfL[NKW][512];   // W_fc rows 16 ut + lr, this wave's K-slice
+  __shared__ __attribute__((aligned(16))) bf16x8 wfTL[NKV][512];  // W_fc^T rows j0 + lr, this wave's V k-steps
+#pragma unroll
+  for (int kk = 0; kk < NKW; ++kk) wfL[kk][tid] = fcw ? ld8(f.Wfc + (size_t)(16 * ut + lr) * H + k0 + kk * 32 + lk) : zero8();
+#pragma unroll
+  for (int q = 0; q < NKV; ++q) wfTL[q][tid] = s4w ? ld8(f.WfcT + (size_t)(j0 + lr) * V + (kvb + q) * 32 + lk) : zero8();
+
+  const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
+  const int row = rb * 16 + (ln >> 4) * 4 + reg, col = ln & 15;
+  const int b = b0 + row, j = j0 + col;
+  float bh[3];
+#pragma unroll
+  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + j];
+  const float bfc = fcw ? f.bfc[16 * ut + col] : 0.f;
+  const float inv = f.inv_count[0];
+  float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
+  const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+  const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
+  const unsigned fcb = (unsigned)((size_t)T * nrb * 16 * 1024);   // bytes of xdl / xdlT
+  const rsrc_t rD = make_rsrc(f.xdl, fcb), rDT = make_rsrc(f.xdlT, fcb);
+  const rsrc_t rS = make_rsrc(f.xst, (unsigned)((size_t)T * nrb * 16 * 256));
+  const unsigned sv_bytes = (unsigned)((size_t)T * Bp * H * 4);
+  const rsrc_t rHSf = make_rsrc(a.HSf, sv_bytes + (unsigned)(Bp * H * 4));
+  const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
+  const rsrc_t rSn = make_rsrc(a.sn, a.sn ? sv_bytes : 0u), rSg = make_rsrc(a.sghn, a.sghn ? sv_bytes : 0u);
+  const rsrc_t rDy = make_rsrc(f.dy, sv_bytes);
+  const unsigned sv_lane = (unsigned)((b * H + j) * 4);
+  zero_next_flags(a.zero_next, a.zero_words);
+  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
+
+  int idn = a.ids ? a.ids[b] : 0;
+  float bi[3] = {0.f, 0.f, 0.f};
+  if (a.ids && a.p_slabs > 1)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
+  auto load_gi = [&](int t, float (&gi)[3]) {
+    if (t >= T) return;
+    const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
+    if (a.ids && a.p_slabs > 1) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) gi[g] += bi[g];
+      for (int q = 1; q < a.p_slabs; ++q)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * a.p_slab + g * H + j];
+    }
+    if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
+  };
+  float gin[3] = {0.f, 0.f, 0.f};
+  load_gi(0, gin);
+  float lg0 = 0.f, lg1 = 0.f;        // logits of the last two S1 sums (lg1 = the one S3 uses)
+  float nll = 0.f, dbs = 0.f;        // loss and db_fc accumulators
+  int ylab = -1;                     // label of the step S3 handles next
+  f32x4 accF[NKV][2];                // dW_fc tiles (v tile 2 kv + pp) x (16 units)
+  zero_acc(accF);
+  for (int t = 0; t < T + DEP; ++t) {
+    stamp(a.dbg, t, 0);
+    const bool rec = t < T;                                  // the recurrence
+    const bool s1 = fcw && t >= 1 && t <= T;                 // logits of h(t-1)
+    const bool st3 = fcw && t >= 3 && t <= T + 2;            // statistics of step t-3 arrive; dl(t-3)
+    const bool s4 = t >= DEP;                                // dH (+ dW_fc) of step t-5
+    const int par = t & 1;
+    const float gi[3] = {gin[0], gin[1], gin[2]};
+    f32x4 acc[3], accL, accD[2];
+    accL = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[0] = acc[1] = acc[2] = accL;
+    accD[0] = accD[1] = accL;
+    bf16x8 af[NKW];
+    bf16x8 dlf[NKV][2], dltf[NKV][2];
+    if (t > 0) {
+      const size_t slot = ((size_t)(t - 1) * nrb + rbk) * nunit;
+      const size_t sd = ((size_t)(s4 ? t - DEP : 0) * nrb + rbk) * 16;   // dl of step t-5
+      const size_t ss = ((size_t)(t >= 3 ? t - 3 : 0) * nrb + rbk) * 16;  // statistics of step t-3
+      wave_wait_load<NKW>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
+                          (unsigned)t, a.err, [&](int kk) {
+        const int u = k0 + kk * 32 + lk;
+        if (t <= T) {
+          const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
+          af[kk] = ld8_sc1(rX, tb + (unsigned)(rt * 16 * 16 * 2));
+        }
+        const int p0 = k0 / 16 + 2 * kk;   // the two producers of this k-step
+        // their row statistics straight into LDS (lanes 0-31, 16 B each; no registers)
+        if (w < 4 && p0 < 16 && st3 && lane < 32)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void*)(&stl[par][p0][0]), 16,
+                                                   (unsigned)(lane * 16), (int)((ss + p0) * 256), 0, 16);
+        const int q = kk & (NKV - 1);   // compile-time slot (kk is unrolled); this wave's k-steps: kk / NKV == rt
+        if (s4 && s4w && kk / NKV == rt) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+            dlf[q][r] = ld8_sc1(rD, (unsigned)(((sd + u / 16) * 32 + r * 16 + lr) * 16 + (u & 15)) * 2);
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+            dltf[q][pp] = ld8_sc1(rDT, (unsigned)(((sd + p0 + pp) * 16 + lr) * 32 + lk) * 2);
+        }
+      });
+    } else if (a.h0) {
+      const unsigned base = (unsigned)((((size_t)b0 + rt * 16 + lr) * H + k0 + lk) * 2);
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk) af[kk] = ld8_sc1(rH, base + (unsigned)(kk * 64));
+    }
+    stamp(a.dbg, t, 1);
+    if (rec && (t > 0 || a.h0)) {
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) acc[g] = mfma16(af[kk], bw[kk][g], acc[g]);
+    }
+    if (s4 && s4w) {
+#pragma unroll
+      for (int q = 0; q < NKV; ++q)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) accD[r] = mfma16(dlf[q][r], wfTL[q][tid], accD[r]);
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[w][g][i * 64 + lane] = acc[g][i];
+    if (s4 && s4w)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[w][4 + r][i * 64 + lane] = accD[r][i];
+    if (s1) {   // logits K-partials: consumed after the publish
+#pragma unroll
+      for (int kk = 0; kk < NKW; ++kk) accL = mfma16(af[kk], wfL[kk][tid], accL);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lgp[par][w][i * 64 + lane] = accL[i];
+    }
+    if (w < 4 && st3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the statistics' LDS-DMA landed
+    __syncthreads();
+    stamp(a.dbg, t, 2);
+    float h = 0.f, r = 0.f, z = 0.f, n = 0.f, ghn = 0.f;
+    if (rec) {
+      float gh[3];
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) sum += part[rb * 4 + ww][g][reg * 64 + ln];
+        gh[g] = sum + bh[g];
+      }
+      r = sigmoidf_(gi[0] + gh[0]);
+      z = sigmoidf_(gi[1] + gh[1]);
+      n = tanhf_(gi[2] + r * gh[2]);
+      ghn = gh[2];
+      h = n + z * (hp - n);
+      hp = h;
+      const u16 hb = f2bf(h);
+      stg[row][col] = hb;
+      stgT[t & 7][col][row] = hb;
+    }
+    float dh = 0.f;   // dH of step t-5 for this thread's (row, unit); stored after the publish
+    if (s4) {
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww)
+        if ((((ww & 3) * NKW) + (ww >> 2) * NKV) < 8) dh += part[ww][4 + rb][reg * 64 + ln];
+    }
+    __syncthreads();
+    stamp(a.dbg, t, 3);
+    if (w == 0 && t <= T + DEP - 2) {
+      // publish: h tile (t < T), the row statistics of step t-2 and the dl tiles of step t-4 (both
+      // computed after the previous publish), one drain, one signal
+      const bool pst = fcw && t >= 2 && t <= T + 1, pdl = fcw && t >= 4 && t <= T + 3;
+      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (rec) v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
+      const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
+      const unsigned so = (unsigned)((((size_t)(t - 2) * nrb + rbk) * 16 + ut) * 64 + lane * 4) * 4;
+      const unsigned dofs = (unsigned)((((size_t)(t - 4) * nrb + rbk) * 16 + ut) * 512 + lane * 8) * 2;
+      const int pq = par ^ 1;
+      if (loc) {
+        if (rec) st16_plain(rX, xo, v);
+        if (pst && lane < 16) st16_plain(rS, so, *reinterpret_cast<const u32x4*>(&sst[pq][lane * 4]));
+        if (pdl) {
+          st16_plain(rD, dofs, *reinterpret_cast<const u32x4*>(&sdl[pq][lane >> 1][(lane & 1) * 8]));
+          st16_plain(rDT, dofs, *reinterpret_cast<const u32x4*>(&sdlT[pq][lane >> 2][(lane & 3) * 8]));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_flag_local(fl, (unsigned)(t + 1));
+      } else {
+        if (rec) st16_sc1(rX, xo, v);
+        if (pst && lane < 16) st16_sc1(rS, so, *reinterpret_cast<const u32x4*>(&sst[pq][lane * 4]));
+        if (pdl) {
+          st16_sc1(rD, dofs, *reinterpret_cast<const u32x4*>(&sdl[pq][lane >> 1][(lane & 1) * 8]));
+          st16_sc1(rDT, dofs, *reinterpret_cast<const u32x4*>(&sdlT[pq][lane >> 2][(lane & 3) * 8]));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_flag(fl, (unsigned)(t + 1));
+      }
+      stamp(a.dbg, t, 4);
+      if (rec)
+        *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
+      stamp(a.dbg, t, 5);
+    } else if (w == 1 && a.HT && rec) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[t & 7][lane >> 2][(lane & 3) * 8]);
+      *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
+    } else if (w == 2 && a.HF && rec) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[t & 7][lane & 15][8 * (lane >> 4)]);
+      *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
+    }
+    // ---- after the publish (the slack before the next poll)
+    if (rec) {
+      load_gi(t + 1, gin);
+      const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
+      if (a.sr) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ghn), rSg, sv_lane, sstep, 0);
+      }
+    }
+    if (s4) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dh), rDy, sv_lane,
+                                            __builtin_amdgcn_readfirstlane((t - DEP) * Bp * H * 4), 0);
+      if (s4w) {   // dW_fc[:, units] += dl(t-5)^T h(t-5) (B: the transposed h tile of step t-5, in the ring)
+        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&stgT[(t - DEP) & 7][lr][lk]);
+#pragma unroll
+        for (int q = 0; q < NKV; ++q)
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) accF[q][pp] = mfma16(dltf[q][pp], hb, accF[q][pp]);
+      }
+    }
+    if (fcw) {
+      if (st3) {   // dl of step t-3 from its logit (lg1) and the 16 producers' statistics of the row:
+                   // the row's 16 threads take one producer each and combine over DPP
+        const float mp = stl[par][col][row * 2], sp = stl[par][col][row * 2 + 1];
+        const float M = max16(mp);
+        const float S = sum16(sp * __expf(mp - M));
+        const int v = 16 * ut + col;
+        const float scale = ylab >= 0 ? inv : 0.f;
+        const float d = (__expf(lg1 - M) * __builtin_amdgcn_rcpf(S) - (v == ylab ? 1.f : 0.f)) * scale;
+        if (v == ylab) nll += (__logf(S) + M - lg1) * scale;
+        dbs += d;
+        const u16 db = f2bf(d);
+        sdl[par][row][col] = db;
+        sdlT[par][col][row] = db;
+      }
+      float lg = 0.f;
+      if (s1) {   // logits of h(t-1): this row's 16 columns, their max and sum-exp (DPP over the row's lanes)
+        lg = bfc;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) lg += lgp[par][rb * 4 + ww][reg * 64 + ln];
+        const float m = max16(lg);
+        const float se = sum16(__expf(lg - m));
+        if (col == 0) { sst[par][row * 2] = m; sst[par][row * 2 + 1] = se; }
+      }
+      lg1 = lg0;
+      lg0 = lg;
+      // the label S3 needs at the next step (step t-2's), one step ahead
+      if (t + 1 >= 3 && t + 1 <= T + 2) ylab = f.labels[(size_t)(t - 2) * Bp + b];
+    }
+    stamp(a.dbg, t, 6);
+  }
+  // ---- per-row-block partials: dW_fc (dH waves), db_fc and the loss (logits workgroups)
+  if (s4w) {
+    float* W = f.dW_part + (size_t)rbk * V * H;
+#pragma unroll
+    for (int q = 0; q < NKV; ++q)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          W[(size_t)(16 * (2 * (kvb + q) + pp) + (lane >> 4) * 4 + i) * H + j0 + lr] = accF[q][pp][i];
+  }
+  float* red = &part[0][0][0];   // [16 cols][33] db sums | [512] loss
+  __syncthreads();
+  red[col * 33 + row] = dbs;
+  red[1024 + tid] = nll;
+  __syncthreads();
+  if (fcw && tid < 16) {
+    float s = 0.f;
+    for (int rr = 0; rr < 32; ++rr) s += red[tid * 33 + rr];
+    f.db_part[(size_t)rbk * V + 16 * ut + tid] = s;
+  }
+  if (tid < 64) {
+    float s = 0.f;
+    for (int q = tid; q < 512; q += 64) s += red[1024 + q];
+    s = wave_sum(s);
+    if (tid == 0) f.loss_part[blockIdx.x] = s;
+  }
+}
+
 // ==================================================================== two-layer wavefront forward
 // Layer hi at step t depends on layer lo only through h_lo(t) (/root/reference/namegensf.cu:773-854:
 // layer 1's input is layer 0's output for the same char), so one launch runs lo's step s and hi's
@@ -1211,6 +1550,22 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
   FWD_VARIANTS(X)
 #undef X
   throw std::runtime_error("gru_fwd_seq: no kernel variant for this shape");
+}
+
+bool gru_fwd_seq_fc_supported(int H, int Bp, int V) {
+  if (Bp % 32 || V != 256 || H != 512 || fwd_rs(H) != 2) return false;
+  const int cap = resident_blocks(gru_fwd_seq_fc_kernel<4>);
+  return cap >= (H / 16) * (Bp / 32);
+}
+
+void gru_fwd_seq_fc(const SeqFwdArgs& a, const FwdFcArgs& f, hipStream_t s) {
+  if (!gru_fwd_seq_fc_supported(a.H, a.Bp, f.V) || a.Emb || !f.Wfc || !f.WfcT || !f.bfc || !f.labels ||
+      !f.inv_count || !f.xdl || !f.xdlT || !f.xst || !f.dy || !f.dW_part || !f.db_part || !f.loss_part)
+    throw std::runtime_error("gru_fwd_seq_fc: unsupported shape or incomplete arguments");
+  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31) || (size_t)a.T * (a.Bp / 32) * 16 * 1024 >= (1ull << 31))
+    throw std::runtime_error("gru_fwd_seq_fc: buffers exceed the 2 GB buffer-offset range");
+  dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
+  hipLaunchKernelGGL((gru_fwd_seq_fc_kernel<4>), grid, block, 0, s, a, f);
 }
 
 #define FWD2_VARIANTS(X) X(256, 1) X(512, 2) X(1024, 4)

@@ -142,6 +142,27 @@ bool gru_fwd_seq_supported(int H, int Bp);
 // row block's batch share fits one pass (T * ceil(32 / (H/16)) <= 1024)
 bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
+// Top layer's forward with the FC / softmax-xent / dH pipeline inside the persistent launch
+// (gru_seq.hip, gru_fwd_seq_fc_kernel): replaces fc_xent and the dW_fc product.  V = 256,
+// H in {256, 512} (the row-split forward), Bp % 32 == 0.
+struct FwdFcArgs {
+  const u16* Wfc = nullptr;        // [V][H] bf16
+  const u16* WfcT = nullptr;       // [H][V] bf16
+  const float* bfc = nullptr;      // [V]
+  const int* labels = nullptr;     // [T][Bp] (-1: no loss)
+  const float* inv_count = nullptr;
+  u16* xdl = nullptr;              // dl exchange [T][Bp/32][16][32][16] bf16
+  u16* xdlT = nullptr;             // [T][Bp/32][16][16][32] bf16
+  float* xst = nullptr;            // row statistics [T][Bp/32][16][32][2]
+  float* dy = nullptr;             // [T][Bp][H] fp32: dL/dh of every step (the backward's input)
+  float* dW_part = nullptr;        // [Bp/32][V][H] dW_fc per row block
+  float* db_part = nullptr;        // [Bp/32][V]   db_fc per row block
+  float* loss_part = nullptr;      // [grid] loss partials
+  int V = 0;
+};
+bool gru_fwd_seq_fc_supported(int H, int Bp, int V);
+inline long fwd_fc_xbytes(int T, int Bp) { return (long)T * (Bp / 32) * 16 * (1024 + 1024 + 256); }
+void gru_fwd_seq_fc(const SeqFwdArgs& a, const FwdFcArgs& f, hipStream_t s);
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
 // `lo` at step s and layer `hi` at step s-1 in iteration s = 0..T.  hi's input projection

@@ -766,3 +766,45 @@ def test_table_free_forward_matches_prologue_table(monkeypatch, G, batch, H):
     a, b = runs
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
     assert a.loss() == b.loss()
+
+
+@pytest.mark.parametrize("H,B,padded", [(512, 256, False), (512, 64, False), (512, 40, True), (512, 96, True)])
+def test_forward_fc_pipeline_matches_fc_kernel(monkeypatch, H, B, padded):
+    """The top layer's forward with the FC / softmax-xent / dH pipeline inside the persistent launch
+    (GK_FWD_FC=1, opt-in; one layer at H = 512, V = 256) against the separate fc_xent kernel + dW_fc
+    product (GK_FWD_FC=0, the default): loss and every gradient agree to bf16 rounding of dl (the
+    softmax statistics are reduced in a different order), three Adam steps to 1e-2 (Adam turns
+    near-zero gradients into full-size steps); and against the fp64 oracle."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=1, batch=B, seq=8, seed=13)
+    params = init_params(cfg)
+    if padded:
+        batches = [make_padded_batch(synthetic_names(B, seed=s, max_len=10), cfg.seq) for s in (4, 5, 6)]
+    else:
+        st = NameStream(B, cfg.seq, seed=4)
+        batches = [st.next() for _ in range(3)]
+    res = {}
+    for fc in ("1", "0"):
+        monkeypatch.setenv("GK_FWD_FC", fc)
+        tr = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
+        assert ("+fc" in tr.t.plan()) == (fc == "1"), tr.t.plan()
+        tr.forward_backward(*batches[0])
+        loss, g = tr.loss(), {k: v.clone() for k, v in tr.grad_dict().items()}
+        tr2 = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
+        for x, y in batches:
+            tr2.step(x, y)
+        torch.cuda.synchronize()
+        res[fc] = (loss, g, tr2.state_dict(), tr2.loss())
+    (la, ga, sa, l2a), (lb, gb, sb, l2b) = res["1"], res["0"]
+    assert abs(la - lb) < 1e-4 * abs(lb), (la, lb)
+    for k in gb:
+        assert rel(ga[k], gb[k]) < 5e-3, f"{k}: {rel(ga[k], gb[k]):.2e}"
+    for k in sb:
+        assert rel(sa[k], sb[k]) < 1e-2, f"{k}: {rel(sa[k], sb[k]):.2e}"
+    assert abs(l2a - l2b) < 1e-3 * abs(l2b)
+    p64 = {k: v.double() for k, v in params.items()}
+    x, y = batches[0]
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(la - float(ref_loss)) < 1e-2 * float(ref_loss)
+    for k in ref_g:
+        assert rel(ga[k], ref_g[k]) < 0.04, k
