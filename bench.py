@@ -54,11 +54,12 @@ def main() -> int:
                          "max(0, N - W) extra, reported as extra_warmup_steps (a fresh box runs its first "
                          "~20 ms of steps below full clocks: W=5 measured 0.232-0.243 ms/step vs 0.221 after "
                          "100, profiles/r2_bench_warmup_probe.txt).  Same count on every rank.")
-    ap.add_argument("--graph-steps", type=int, default=4,
+    ap.add_argument("--graph-steps", type=int, default=0,
                     help="hip engine on GPUs: G consecutive training steps captured into one graph launch "
-                         "(1..4; the same G full steps, one graph boundary instead of G: ~13 us each at "
+                         "(1..16; the same G full steps, one graph boundary instead of G: ~13 us each at "
                          "the headline, docs/DESIGN.md §6); a remainder of K or W modulo G runs as "
-                         "single-step graphs.  Reported as graph_steps.")
+                         "single-step graphs.  0 (default): the largest G <= 16 that divides K.  Reported "
+                         "as graph_steps.")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -113,7 +114,8 @@ def main() -> int:
         if args.no_graph and hasattr(tr, "t"):
             tr.t.set_use_graph(False)
         step = lambda i: tr.step(*pool[i % len(pool)])  # noqa: E731
-        G = args.graph_steps if ctx.device.type == "cuda" and hasattr(tr, "steps") else 1
+        G = args.graph_steps or max(g for g in range(1, 17) if args.steps % g == 0)
+        G = G if ctx.device.type == "cuda" and hasattr(tr, "steps") else 1
         final_loss = lambda: tr.loss()                  # noqa: E731
         plan = tr.t.plan() if hasattr(tr, "t") else "cpu"
     else:
