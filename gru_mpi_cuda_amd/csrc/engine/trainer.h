@@ -87,6 +87,7 @@ class Trainer {
   int p_slabs_ = 1;               // of the step being recorded
   int p_slabs_for_record() const;
   bool fwd_pl_ok() const;
+  bool fwd_xp_ok() const;
   bool p_in_prologue_ = true, batch_in_prologue_ = true, batch_from_prev_tail_ = false;
   const int* next_stage_src_ = nullptr;   // staging slot of the next step in the same graph (or null)
   bool p_valid_ = false;

@@ -158,10 +158,14 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // (forward 60 -> 90 us, step 0.216 -> 0.240 ms, profiles/r3s5_fwd_pl_ab.jsonl)
   const bool fwd_pl = fwd_pl_ok();
   const bool fwd_fc = !fwd_pl && fwd_fc_ok();
+  const bool fwd_xp = !fwd_pl && !fwd_fc && fwd_xp_ok();
   nloss_ = fwd_fc ? (H / 16) * (B / 32) : (int)(tok / 32);
-  p_slabs_ = (p_in_prologue_ && !fwd_pl) ? p_slabs_for_record() : 1;
+  p_slabs_ = (p_in_prologue_ && !fwd_pl && !fwd_xp) ? p_slabs_for_record() : 1;
   if (fwd_pl) {
     // (nothing before the forward launch)
+  } else if (fwd_xp) {
+    // layer 0's input projection runs inside the forward launch: the prologue is the batch alone
+    if (batch_in_prologue_) prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
   } else if (p_in_prologue_ && batch_in_prologue_) {
     // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
     // with the batch preparation (independent work, one graph node); as p_slabs_ split-K partial
@@ -186,7 +190,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
     a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
-    if (l == 0 && fwd_pl) {
+    if (l == 0 && fwd_xp) {
+      a.xp = 1; a.Emb = Emb; a.Wih0 = Ls_[0].Wih; a.bih = P("bias_ih_l0"); a.E = E; a.V = V; a.ids = ids_;
+    } else if (l == 0 && fwd_pl) {
       a.Emb = Emb; a.Wih0 = Ls_[0].Wih; a.bih = P("bias_ih_l0"); a.V = V; a.E = E; a.ids = ids_;
       if (batch_in_prologue_) a.prep = PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_};
     } else if (l == 0) {
@@ -522,6 +528,18 @@ bool Trainer::fwd_pl_ok() const {
   return gru_fwd_seq_pl_supported(d_.H, Bp_, d_.V, d_.E, d_.T);
 }
 
+// layer 0's input projection inside the persistent forward (GK_FWD_XP=1, opt-in): one forward launch
+// for layer 0, the row-split H = 512 kernel, E = H.  Measured slower: the per-step Emb rows (32 KB per
+// workgroup) and 12 MFMAs per wave in the post-publish slack are not hidden by the flag propagation
+// (forward 60.6 -> 88.4 us); the prologue it removes is mostly the batch's pinned-memory read
+// (prep_batch alone 5.2-5.6 us), so the step goes 0.214-0.220 -> 0.240-0.242 ms
+// (profiles/r3s5_fwd_xp_ab.jsonl)
+bool Trainer::fwd_xp_ok() const {
+  if (!persist_fwd_ || !p_in_prologue_ || (fwd_wave_ && d_.L >= 2)) return false;
+  if (!env_flag("GK_FWD_XP", false)) return false;
+  return gru_fwd_seq_xp_supported(d_.H, Bp_, d_.E);
+}
+
 // the top layer's forward carries the FC pipeline (GK_FWD_FC=1, opt-in): one layer, H = 512, V = 256.
 // Measured: the tail loses its dW_fc items (42.8 -> 29.9 us) and fc_xent goes away (15.5 us), but the
 // pipeline's dl row-block loads (+32 KB per workgroup per step on top of the 32 KB h exchange) slow the
@@ -537,6 +555,7 @@ std::string Trainer::plan() const {
   std::string p = std::string("fwd=") + (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   if (fwd_pl_ok()) p += "+pl";
   else if (fwd_fc_ok()) p += "+fc";
+  else if (fwd_xp_ok()) p += "+xp";
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

@@ -282,8 +282,16 @@ DEV void signal_flag_local(unsigned* flag, unsigned epoch) {
 // (off by default, GK_FWD_PL=1): the 8 row blocks of a unit tile redo the same columns, so the chip
 // streams 78 MB of Emb / W_ih0 through L2 and runs 8x the table's MFMAs -- 10-17 us before the
 // first step, against the 7 us prologue kernel (profiles/r3s5_fwd_pl_ab.jsonl).
-template <int NKW, int RS, bool PL>
+//
+// XP = true (SeqFwdArgs::xp, layer 0, RS = 2, E = H): no P table either, and no per-WG table --
+// the input projection of step t+1 (the 32 rows' Emb rows x this workgroup's W_ih0 slice, the same
+// K-split over the waves as the recurrent product) runs in the slack after step t's publish, into the
+// free partial sets 3-5; its Emb rows were loaded one step earlier still, and their ids one step
+// before that.  The step's prologue kernel is left with the batch preparation only.  Measured slower
+// (opt-in, GK_FWD_XP=1): the slack work is not hidden, +0.87 us per step (profiles/r3s5_fwd_xp_ab.jsonl).
+template <int NKW, int RS, bool PL, bool XP = false>
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
+  static_assert(!XP || (RS == 2 && !PL), "XP: row-split forward, table-free mode excluded");
   __shared__ __attribute__((aligned(16))) float part[8][6][256];
   __shared__ __attribute__((aligned(16))) float Pl[PL ? 256 : 1][PL ? 48 : 1];   // [V][gate * 16 + unit]
   // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
@@ -440,12 +448,43 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     return a.ids[o];
   };
   int idn = a.ids ? load_id(b) : 0;   // id of the step whose row load_gi gathers next
-  float bi[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it
-  if (a.ids && a.p_slabs > 1)
+  float bi[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it (or XP)
+  if (a.ids && (a.p_slabs > 1 || XP))
 #pragma unroll
     for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
+  // XP: W_ih0 K-slice (B operand), the Emb fragments of the next input product and their row's id
+  bf16x8 wi[XP ? NKW : 1][3], en[XP ? NKW : 1];
+  int idA = 0;
+  const int bA = b0 + rt * 16 + lr;   // the A-operand row of this lane
+  auto load_emb = [&](int id) {
+#pragma unroll
+    for (int kk = 0; kk < NKW; ++kk) en[kk] = ld8(a.Emb + (size_t)id * H + k0 + kk * 32 + lk);
+  };
+  auto input_product = [&]() {   // the Emb fragments in en x W_ih0 -> partial sets 3..5
+    f32x4 ai[3];
+    ai[0] = ai[1] = ai[2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) ai[g] = mfma16(en[kk], wi[kk][g], ai[g]);
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[w][3 + g][i * 64 + lane] = ai[g][i];
+  };
+  if constexpr (XP) {
+#pragma unroll
+    for (int kk = 0; kk < NKW; ++kk)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) wi[kk][g] = ld8(a.Wih0 + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
+    load_emb(a.ids[bA]);
+    input_product();                                  // step 0's, read by its epilogue
+    if (T > 1) load_emb(a.ids[(size_t)Bp + bA]);      // step 1's rows
+    if (T > 2) idA = a.ids[(size_t)2 * Bp + bA];      // step 2's id
+  }
   auto load_gi = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
+    if constexpr (XP) return;
     if constexpr (PL) {
 #pragma unroll
       for (int g = 0; g < 3; ++g) gi[g] = Pl[idn][g * 16 + col];
@@ -521,9 +560,19 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       }
       gh[g] = s + bh[g];
     }
-    const float r = sigmoidf_(gi[0] + gh[0]);
-    const float z = sigmoidf_(gi[1] + gh[1]);
-    const float n = tanhf_(gi[2] + r * gh[2]);
+    float gx[3] = {gi[0], gi[1], gi[2]};
+    if constexpr (XP) {   // this step's input projection from the partials written after the last publish
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float s = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) s += part[rb * 4 + ww][3 + g][reg * 64 + ln];
+        gx[g] = s + bi[g];
+      }
+    }
+    const float r = sigmoidf_(gx[0] + gh[0]);
+    const float z = sigmoidf_(gx[1] + gh[1]);
+    const float n = tanhf_(gx[2] + r * gh[2]);
     const float h = n + z * (hp - n);
     hp = h;
     const u16 hb = f2bf(h);
@@ -561,6 +610,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     // scalar offset -- with 64-bit VGPR address math the compiler reused the in-flight gather's
     // destination as a temporary and waited for it (+0.3 us per step at H = 512).
     load_gi(t + 1, gin);
+    if constexpr (XP) {   // step t+1's input product (rows loaded last step), then step t+2's rows
+      if (t + 1 < T) input_product();
+      if (t + 2 < T) load_emb(idA);
+      if (t + 3 < T) idA = a.ids[(size_t)(t + 3) * Bp + bA];
+    }
     const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
     if (a.sr) {
@@ -1519,6 +1573,11 @@ bool gru_fwd_seq_supported(int H, int Bp) {
   return cap >= (H / 16) * (Bp / 32);
 }
 
+bool gru_fwd_seq_xp_supported(int H, int Bp, int E) {
+  if (Bp % 32 || E != H || H != 512 || fwd_rs(H) != 2) return false;
+  return resident_blocks(gru_fwd_seq_kernel<4, 2, false, true>) >= (H / 16) * (Bp / 32);
+}
+
 bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T) {
   if (Bp % 32 || H % 16 || (V != 128 && V != 256) || E % 64 || E < 64 || E > 512 || T < 1) return false;
   const int nunit = H / 16, nr = (32 + nunit - 1) / nunit;
@@ -1536,6 +1595,12 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
+  if (a.xp) {
+    if (!a.Emb || !a.Wih0 || !a.bih || !a.ids || a.P || a.Gi || a.E != a.H || !gru_fwd_seq_xp_supported(a.H, a.Bp, a.E))
+      throw std::runtime_error("gru_fwd_seq: inconsistent in-kernel input projection arguments");
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<4, 2, false, true>), grid, block, 0, s, a);
+    return;
+  }
   const bool pl = a.Emb != nullptr;
   if (pl && (!a.Wih0 || !a.bih || !a.ids || a.P || a.Gi || !gru_fwd_seq_pl_supported(a.H, a.Bp, a.V, a.E, a.T) ||
              (a.prep.in && (a.prep.ids != a.ids || !a.prep.labels || !a.prep.inv_count || a.prep.T != a.T ||

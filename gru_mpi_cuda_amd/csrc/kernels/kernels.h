@@ -126,6 +126,9 @@ struct SeqFwdArgs {
   const u16* Wih0 = nullptr;       // [3H][E] bf16 (bias in bih)
   int V = 0, E = 0;
   PrepJob prep;                    // prep.in == nullptr: ids already hold the batch
+  // xp = 1 (gru_fwd_seq_xp_supported): layer 0's input projection inside the launch, one step
+  // ahead in the post-publish slack (Emb, Wih0, bih as above; ids from the prologue's batch prep)
+  int xp = 0;
   const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
   unsigned* cnt = nullptr;         // [Bp/32][H/16][16] epoch flags, zero at launch
   unsigned* zero_next = nullptr;   // flag block of the NEXT sequence kernel, zeroed here (nullable)
@@ -141,6 +144,7 @@ bool gru_fwd_seq_supported(int H, int Bp);
 // the table-free layer-0 variant (SeqFwdArgs::Emb): V in {128, 256}, E % 64 == 0, E <= 512, and a
 // row block's batch share fits one pass (T * ceil(32 / (H/16)) <= 1024)
 bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T);
+bool gru_fwd_seq_xp_supported(int H, int Bp, int E);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 // Top layer's forward with the FC / softmax-xent / dH pipeline inside the persistent launch
 // (gru_seq.hip, gru_fwd_seq_fc_kernel): replaces fc_xent and the dW_fc product.  V = 256,

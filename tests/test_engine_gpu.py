@@ -382,6 +382,7 @@ def test_tail_p_table_tracks_the_weights(monkeypatch, G):
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     monkeypatch.setenv("GK_TAIL_P", "1")
+    monkeypatch.setenv("GK_FWD_XP", "0")   # both trainers gather from a P table
     cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=7)
     stream = NameStream(cfg.batch, cfg.seq, seed=8)
     batches = [stream.next() for _ in range(G + 1)]
@@ -751,6 +752,7 @@ def test_table_free_forward_matches_prologue_table(monkeypatch, G, batch, H):
     stream = NameStream(cfg.batch, cfg.seq, seed=10)
     batches = [stream.next() for _ in range(2 * G)]
     runs = []
+    monkeypatch.setenv("GK_FWD_XP", "0")   # the prologue-table path this variant is bitwise equal to
     for pl in ("1", "0"):
         monkeypatch.setenv("GK_FWD_PL", pl)
         tr = HipTrainer(cfg, params=init_params(cfg))
@@ -802,6 +804,48 @@ def test_forward_fc_pipeline_matches_fc_kernel(monkeypatch, H, B, padded):
     for k in sb:
         assert rel(sa[k], sb[k]) < 1e-2, f"{k}: {rel(sa[k], sb[k]):.2e}"
     assert abs(l2a - l2b) < 1e-3 * abs(l2b)
+    p64 = {k: v.double() for k, v in params.items()}
+    x, y = batches[0]
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(la - float(ref_loss)) < 1e-2 * float(ref_loss)
+    for k in ref_g:
+        assert rel(ga[k], ref_g[k]) < 0.04, k
+
+
+@pytest.mark.parametrize("B,padded,G", [(256, False, 1), (96, True, 1), (64, False, 4)])
+def test_forward_input_projection_in_kernel(monkeypatch, B, padded, G):
+    """Layer 0's input projection inside the persistent forward (GK_FWD_XP=1, opt-in, H = E = 512:
+    Emb rows x W_ih0 in the post-publish slack, one step ahead, no P table) against the
+    prologue's P table (GK_FWD_XP=0): loss and gradients agree to fp32 summation order, a few Adam
+    steps (single and multi-step graphs) to Adam's sign sensitivity; and the fp64 oracle."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=512, hidden=512, layers=1, batch=B, seq=8, seed=21)
+    params = init_params(cfg)
+    if padded:
+        batches = [make_padded_batch(synthetic_names(B, seed=s, max_len=10), cfg.seq) for s in range(G + 1)]
+    else:
+        st = NameStream(B, cfg.seq, seed=22)
+        batches = [st.next() for _ in range(G + 1)]
+    res = {}
+    for xp in ("1", "0"):
+        monkeypatch.setenv("GK_FWD_XP", xp)
+        tr = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
+        assert ("+xp" in tr.t.plan()) == (xp == "1"), tr.t.plan()
+        tr.forward_backward(*batches[0])
+        loss, g = tr.loss(), {k: v.clone() for k, v in tr.grad_dict().items()}
+        tr2 = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
+        if G > 1:
+            tr2.steps(batches[1:G + 1])
+        else:
+            tr2.step(*batches[1])
+        torch.cuda.synchronize()
+        res[xp] = (loss, g, tr2.state_dict())
+    (la, ga, sa), (lb, gb, sb) = res["1"], res["0"]
+    assert abs(la - lb) < 1e-4 * abs(lb), (la, lb)
+    for k in gb:
+        assert rel(ga[k], gb[k]) < 5e-3, f"{k}: {rel(ga[k], gb[k]):.2e}"
+    for k in sb:
+        assert rel(sa[k], sb[k]) < 1e-2, f"{k}: {rel(sa[k], sb[k]):.2e}"
     p64 = {k: v.double() for k, v in params.items()}
     x, y = batches[0]
     ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
