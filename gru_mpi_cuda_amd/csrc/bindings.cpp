@@ -311,6 +311,7 @@ PYBIND11_MODULE(_C, m) {
     a.h0 = GP(const float, d, "h0");
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+    a.saves_in_drain = get<int>(d, "saves_in_drain", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     // table-free layer 0: Emb, Wih0, bih, V, E (+ the staging slot prep_in with labels / inv_count)
     a.Emb = GP(const u16, d, "Emb"); a.Wih0 = GP(const u16, d, "Wih0"); a.bih = GP(const float, d, "bih");
@@ -360,6 +361,7 @@ PYBIND11_MODULE(_C, m) {
     a.dP_part = GP(float, d, "dP_part"); a.V = get<int>(d, "V", 0);
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
     a.allow_local = get<int>(d, "allow_local", 1);
+    a.fused_in_drain = get<int>(d, "fused_in_drain", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     // "unchecked": skip the co-residency query and go straight to the dispatch table (tests its
     // unmatched-variant error without launching anything)

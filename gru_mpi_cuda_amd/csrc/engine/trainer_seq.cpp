@@ -19,6 +19,13 @@ static bool env_flag(const char* name, bool dflt) {
   return v && v[0] ? v[0] != '0' : dflt;
 }
 
+// persistent kernels: the publishing wave overlapping its own follow-up work with its exchange drain --
+// backward fused weight-gradient MFMAs (GK_BWD_FUSED_IN_DRAIN=1), forward saves (GK_FWD_SAVES_IN_DRAIN=1).
+// Both measured slower (the signal waits for the extra work: bwd 0.2195-0.2219 -> 0.2218-0.2233 ms/step,
+// forward 60.6 -> 62.5 us; profiles/r3s5_drain_overlap_ab.jsonl): off.  Read at record time.
+static bool bwd_fused_in_drain() { return env_flag("GK_BWD_FUSED_IN_DRAIN", false); }
+static bool fwd_saves_in_drain() { return env_flag("GK_FWD_SAVES_IN_DRAIN", false); }
+
 // data-parallel: a layer group's collective stays open across the next persistent backward kernel
 static bool ar_span() {
   static const bool on = env_flag("GK_AR_SPAN", true);
@@ -202,6 +209,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.Gi = y.Gi;
     }
     a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
+    a.saves_in_drain = fwd_saves_in_drain() ? 1 : 0;
     if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
     a.T = T; a.Bp = B; a.H = H;
     if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
@@ -367,6 +375,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
+      a.fused_in_drain = bwd_fused_in_drain() ? 1 : 0;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       if (l == 0 && tail_fused_) a.bump = step_;   // step counter + tail epoch, read by the fused tail
       a.T = T; a.Bp = B; a.H = H;

@@ -580,9 +580,22 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     stgT[col][row] = hb;
     __syncthreads();
     stamp(a.dbg, t, 3);
+    const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
+    auto saves = [&]() {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
+      if (a.sr) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
+      }
+    };
+    const bool sid = a.saves_in_drain != 0;
     if (w == 0) {
       // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
-      // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
+      // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.  (saves_in_drain:
+      // this wave's saves go out first and drain with the tile instead of after the signal)
+      if (sid) saves();
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
       const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
       unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
@@ -615,14 +628,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       if (t + 2 < T) load_emb(idA);
       if (t + 3 < T) idA = a.ids[(size_t)(t + 3) * Bp + bA];
     }
-    const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
-    if (a.sr) {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
-    }
+    if (!(w == 0 && sid)) saves();
     stamp(a.dbg, t, 6);
   }
 }
@@ -1435,6 +1441,40 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     }
     __syncthreads();
     stamp(a.dbg, s, 3);
+    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS), off the exchange: the
+    // publishing wave runs them while its exchange stores drain (fused_in_drain), the others right
+    // after the barrier.  (Deferred into the next step's exchange-load window they delayed its
+    // recurrent MFMAs: 0.2199 -> 0.2291 ms, profiles/r2_rejected_ab.jsonl)
+    auto fused_mma = [&]() {
+      if constexpr (NTW > 0 || NTP > 0) {
+        bf16x8 ga[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) ga[g] = *reinterpret_cast<const bf16x8*>(&sgT[g][lr][lk]);
+        if constexpr (NTW > 0) {
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) accW[g][nt] = mfma16(ga[g], hB[nt], accW[g][nt]);
+        }
+        if constexpr (NTP > 0) {
+          ga[2] = *reinterpret_cast<const bf16x8*>(&sgT[3][lr][lk]);   // dGi: n gate without r
+          int idv[8];
+          const int4 i0 = *reinterpret_cast<const int4*>(&idsL[lk]), i1 = *reinterpret_cast<const int4*>(&idsL[lk + 4]);
+          idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
+          idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
+#pragma unroll
+          for (int nt = 0; nt < NTP; ++nt) {
+            const int v = (w * NTP + nt) * 16 + lr;
+            bf16x8 oh;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) oh[e] = (__bf16)(idv[e] == v ? 1.0f : 0.0f);
+#pragma unroll
+            for (int g = 0; g < 3; ++g) accP[g][nt] = mfma16(ga[g], oh, accP[g][nt]);
+          }
+        }
+      }
+    };
+    const bool fid = a.fused_in_drain != 0;
     if (w == 0) {
       // publish the dGh_t tile as 3 gate blocks of [32 rows][16 units] (1 KB each, whole lines of its
       // own): a consumer's 16-row fragment of one gate is then 512 contiguous bytes per producer
@@ -1446,13 +1486,15 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
         if (loc) st16_plain(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
         else st16_sc1(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
-      if (lane == 0) {
-        if (loc) signal_flag_local(fl, (unsigned)(s + 1));
-        else signal_flag(fl, (unsigned)(s + 1));
-      }
-      stamp(a.dbg, s, 4);
+      if (!fid) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+        if (lane == 0) {
+          if (loc) signal_flag_local(fl, (unsigned)(s + 1));
+          else signal_flag(fl, (unsigned)(s + 1));
+        }
+        stamp(a.dbg, s, 4);
+      }   // (fid: the drain and the signal follow this wave's fused MFMAs below)
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate
       const int g = w - 1;          // 0..3 : dGh r, z, n and dGi n
@@ -1468,36 +1510,16 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
     }
     stamp(a.dbg, s, 5);
-    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS).  Here, between the publish
-    // and the next poll, they are hidden by the flag propagation; deferred into the next step's
-    // exchange-load window they delayed its recurrent MFMAs (0.2199 -> 0.2291 ms,
-    // profiles/r2_rejected_ab.jsonl)
-    if constexpr (NTW > 0 || NTP > 0) {
-      bf16x8 ga[3];
-#pragma unroll
-      for (int g = 0; g < 3; ++g) ga[g] = *reinterpret_cast<const bf16x8*>(&sgT[g][lr][lk]);
-      if constexpr (NTW > 0) {
-#pragma unroll
-        for (int g = 0; g < 3; ++g)
-#pragma unroll
-          for (int nt = 0; nt < NTW; ++nt) accW[g][nt] = mfma16(ga[g], hB[nt], accW[g][nt]);
+    fused_mma();
+    if (w == 0 && fid) {   // the exchange stores drained under the MFMAs: now the signal
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      if (lane == 0) {
+        if (loc) signal_flag_local(fl, (unsigned)(s + 1));
+        else signal_flag(fl, (unsigned)(s + 1));
       }
-      if constexpr (NTP > 0) {
-        ga[2] = *reinterpret_cast<const bf16x8*>(&sgT[3][lr][lk]);   // dGi: n gate without r
-        int idv[8];
-        const int4 i0 = *reinterpret_cast<const int4*>(&idsL[lk]), i1 = *reinterpret_cast<const int4*>(&idsL[lk + 4]);
-        idv[0] = i0.x; idv[1] = i0.y; idv[2] = i0.z; idv[3] = i0.w;
-        idv[4] = i1.x; idv[5] = i1.y; idv[6] = i1.z; idv[7] = i1.w;
-#pragma unroll
-        for (int nt = 0; nt < NTP; ++nt) {
-          const int v = (w * NTP + nt) * 16 + lr;
-          bf16x8 oh;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) oh[e] = (__bf16)(idv[e] == v ? 1.0f : 0.0f);
-#pragma unroll
-          for (int g = 0; g < 3; ++g) accP[g][nt] = mfma16(ga[g], oh, accP[g][nt]);
-        }
-      }
+      stamp(a.dbg, s, 4);
     }
     if constexpr (fdl) {   // dl image of step t - NB into the buffer this step just consumed
       if (t >= NB) load_dl(t - NB);

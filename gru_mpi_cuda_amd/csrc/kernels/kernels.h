@@ -136,6 +136,9 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
+  // 1: the publishing wave issues its saves for the backward before its exchange store (one drain for
+  // both) instead of after the signal (GK_FWD_SAVES_IN_DRAIN=1; measured slower, off)
+  int saves_in_drain = 0;
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -207,6 +210,9 @@ struct SeqBwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
+  // 1: the publishing wave runs its fused dW_hh / dP MFMAs while its exchange stores drain (before the
+  // signal) instead of after it (GK_BWD_FUSED_IN_DRAIN=1; measured slower, off)
+  int fused_in_drain = 0;
   int* bump = nullptr;             // [2]: optimiser step counter and fused-tail epoch, +1 each at launch (nullable)
   int T = 0, Bp = 0, H = 0;
 };
