@@ -621,12 +621,17 @@ void Trainer::record_opt(hipStream_t s) {
   HIP_LAUNCH_CHECK();
 }
 
+// The fused step tail (tail.hip) is opt-in (GK_TAIL=1) since round 3's last measurements: on the
+// current tree the phased tail (reduce_multi + gemm_small_group + adam_cast, dW_fc before the
+// backward) runs the headline 3.2 us faster in the driver's form (6 alternating pairs, 0.2245 vs
+// 0.2213 ms) and 2.5 us at K = 300 (profiles/r3s5_tail_fused_vs_phased_ab.jsonl): one grid of 1029
+// items contends for memory bandwidth (§6.3) where three back-to-back launches each get it whole.
 bool Trainer::tail_ok() const {
   const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
   // data-parallel: the readiness-ordered path (dp_overlap) runs it after the last collective, on the
   // all-reduced dP (one slab); the plain-bucket and sharded paths do not
   if ((comm_ && !dp_overlap()) || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
-      V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", true))
+      V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", false))
     return false;
   // tail.hip's conditions: 256-deep K-slices, fewer waiting product blocks than resident slots
   const int se = tail_emb_splits();

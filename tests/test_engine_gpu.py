@@ -381,6 +381,7 @@ def test_tail_p_table_tracks_the_weights(monkeypatch, G):
     (GK_TAIL_P is off by default: measured slower at the headline.)"""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
+    monkeypatch.setenv("GK_TAIL", "1")     # the fused step tail (opt-in) is what computes the next P
     monkeypatch.setenv("GK_TAIL_P", "1")
     monkeypatch.setenv("GK_FWD_XP", "0")   # both trainers gather from a P table
     cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=7)
@@ -571,12 +572,15 @@ def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
     assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
 
 
+@pytest.mark.parametrize("tail", ["0", "1"])
 @pytest.mark.parametrize("layers,H,B,opt", [(1, 512, 256, "adam"), (2, 256, 64, "adam"), (1, 256, 64, "sgd")])
-def test_one_graph_step_equals_phased_step(layers, H, B, opt):
+def test_one_graph_step_equals_phased_step(monkeypatch, layers, H, B, opt, tail):
     """The one-graph step hands optimiser-only slab reductions (dW_hh / bias / dW_fc / dEmb
-    partials) to the fused Adam launch; the phased path (forward_backward, then optimizer_step)
-    reduces them first.  Same partials, same summation order: bitwise-equal weights and grads."""
+    partials) to the fused Adam launch -- or, GK_TAIL=1, to the fused step tail (tail.hip); the
+    phased path (forward_backward, then optimizer_step) reduces them first.  Same partials, same
+    summation order: bitwise-equal weights and grads."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    monkeypatch.setenv("GK_TAIL", tail)
     cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=12, optimizer=opt)
     params = init_params(cfg)
     ds = NameStream(B, cfg.seq, seed=2)
@@ -852,3 +856,25 @@ def test_forward_input_projection_in_kernel(monkeypatch, B, padded, G):
     assert abs(la - float(ref_loss)) < 1e-2 * float(ref_loss)
     for k in ref_g:
         assert rel(ga[k], ref_g[k]) < 0.04, k
+
+
+@pytest.mark.parametrize("G", [10])
+def test_multi_step_graph_with_rccl_world1(G):
+    """The data-parallel step (in-graph RCCL collectives, here on a 1-rank communicator) captured G
+    steps per graph launch -- the bench's default for the driver's K = 20 -- equals G single-step
+    launches of the same structure bit for bit, and keeps its multi-step graph."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    cfg = GRUConfig(vocab=256, embed=512, hidden=512, layers=1, batch=64, seq=8, seed=5)
+    stream = NameStream(cfg.batch, cfg.seq, seed=6)
+    batches = [stream.next() for _ in range(G)]
+    a = HipTrainer(cfg, params=init_params(cfg), comm=C.RcclComm(C.RcclComm.unique_id(), 0, 1))
+    b = HipTrainer(cfg, params=init_params(cfg), comm=C.RcclComm(C.RcclComm.unique_id(), 0, 1))
+    a.steps(batches)
+    for x, y in batches:
+        b.step(x, y)
+    torch.cuda.synchronize()
+    assert a.t.graph_steps() == G
+    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
+    assert a.loss() == b.loss()
