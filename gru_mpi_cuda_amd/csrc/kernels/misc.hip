@@ -260,7 +260,7 @@ void adam_step(const OptimArgs& a, hipStream_t s) {
 }
 
 __global__ void __launch_bounds__(256) adam_cast_kernel(OptimArgs a, OptCastJobs j) {
-  __shared__ u16 tile[64][68];   // 136-B rows: 8-row-apart reads of one column hit distinct banks (2-way max)
+  __shared__ __attribute__((aligned(16))) u16 tile[64][kAdamTileP];   // optim_dev.h: conflict-free column reads
   int b = blockIdx.x, k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
   if (step_failed(a)) return;

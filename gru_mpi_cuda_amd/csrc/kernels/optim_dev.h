@@ -174,8 +174,12 @@ DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
 // gtile (nullable): the tile's fp32 gradient already in LDS ([64][68], this tile's 64 x 64 block);
 // it is also written to the gradient buffer (observable) unless store_g is false (the buffer
 // holds something still being read, e.g. the all-reduced dP in the W_ih0 slot), and J.gsl is ignored
+// bf16 staging tile pitch: 66 u16 = 33 dwords (odd), so the column reads of the transposed copies --
+// 8 lanes 8 rows apart, 8 columns -- land in distinct banks (68: 2-way); rows are then only 4-B
+// aligned, so the tile is written and read in 4-B pieces
+constexpr int kAdamTileP = 66;
 template <bool GSC1, bool DSC1>
-DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const AdamCoef& co, u16 (*tile)[68],
+DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const AdamCoef& co, u16 (*tile)[kAdamTileP],
                         const float (*gtile)[68] = nullptr, bool store_g = true) {
   if (J.R == 0) {   // flat job: 1024 elements per block
     const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
@@ -221,7 +225,9 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
       else *reinterpret_cast<uint2*>(J.dst + (size_t)r * J.C + c) = w;
     }
     if (!J.dstT && !J.dstF && !J.dstTF) continue;
-    *reinterpret_cast<uint2*>(&tile[ty + 16 * q][4 * tx]) = w;
+    unsigned* tw = reinterpret_cast<unsigned*>(&tile[ty + 16 * q][4 * tx]);
+    tw[0] = w.x;
+    tw[1] = w.y;
   }
   if (!J.dstT && !J.dstF && !J.dstTF) return;
   __syncthreads();
@@ -243,10 +249,10 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
     const int fl = pc & 63, fr = (pc >> 6) & 3, fk = pc >> 8;   // lane, 16-row tile, 32-k step
     const int rr = fr * 16 + (fl & 15), kk = fk * 32 + 8 * (fl >> 4);
     u16 v[8];
-    if (J.dstF) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[rr][kk + e];
-      *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = *reinterpret_cast<const uint4*>(v);
+    if (J.dstF) {   // 8 consecutive u16 of one row: four 4-B reads
+      const unsigned* tr = reinterpret_cast<const unsigned*>(&tile[rr][kk]);
+      const uint4 v4 = make_uint4(tr[0], tr[1], tr[2], tr[3]);
+      *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = v4;
     }
     if (J.dstTF) {
 #pragma unroll

@@ -82,7 +82,7 @@ DEV void tail_reads_done(unsigned* c) {
 
 // ---- dP tile: 32 rows x 64 columns of the [V][H3] table gradient, summed over the row-block
 // partials in fixed order (as reduce_multi), stored bf16 row-major and, through LDS, transposed
-DEV void tail_dp_tile(const TailArgs& t, int id, u16 (*tile)[68]) {
+DEV void tail_dp_tile(const TailArgs& t, int id, u16 (*tile)[kAdamTileP]) {
   const int tiles_c = t.H3 / 64;
   const int r0 = (id / tiles_c) * 32, c0 = (id % tiles_c) * 64;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -99,7 +99,9 @@ DEV void tail_dp_tile(const TailArgs& t, int id, u16 (*tile)[68]) {
     w.x = (unsigned)f2bf(acc[q].x) | ((unsigned)f2bf(acc[q].y) << 16);
     w.y = (unsigned)f2bf(acc[q].z) | ((unsigned)f2bf(acc[q].w) << 16);
     bst8_sc1(rb, (unsigned)(((size_t)r * t.H3 + c0 + 4 * tx) * 2), w);
-    *reinterpret_cast<u32x2_t*>(&tile[ty + 16 * q][4 * tx]) = w;
+    unsigned* tw = reinterpret_cast<unsigned*>(&tile[ty + 16 * q][4 * tx]);
+    tw[0] = w.x;
+    tw[1] = w.y;
   }
   __syncthreads();
   {   // 64 columns x 4 pieces of 8 rows: dP^T[c0 + col][r0 + 8 seg ..]
@@ -183,7 +185,7 @@ DEV int acc_col(int j) { return ((threadIdx.x >> 6) & 1) * 32 + j * 16 + (thread
 
 template <int MINW>   // minimum waves per SIMD (= resident 256-thread workgroups per CU)
 __global__ void __launch_bounds__(256, MINW) tail_kernel(OptimArgs a, OptCastJobs j, TailArgs t) {
-  __shared__ __attribute__((aligned(16))) u16 tile[64][68];
+  __shared__ __attribute__((aligned(16))) u16 tile[64][kAdamTileP];
   __shared__ __attribute__((aligned(16))) float gt[64][68];   // a product tile's fp32 gradient
   __shared__ __attribute__((aligned(16))) float gb[64];       // b_fc gradients of a dW_fc row tile
   __shared__ unsigned s_prev;
