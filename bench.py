@@ -29,6 +29,27 @@ import numpy as np
 METRIC = "char-tokens/sec (whole node) for GRU hidden=512 at 1/2/4/8 MI355X"
 
 
+def _launch_plan(K: int):
+    """(G, lead) for K timed steps: `lead` single-step graph launches, then groups of G steps (G <= 16
+    dividing K - lead).  Cost model from the headline's measurements: the first launch after the
+    timed region's synchronize is the only one whose host work the GPU does not hide -- ~20 us for a
+    single step, ~5 us per step + 40 us for a group (staging G batches, launching ~8G nodes,
+    profiles/r3s5_host_group_launch.txt) -- and every graph boundary costs ~12.8 us
+    (docs/DESIGN.md §6).  K = 20: 2 singles + 2 groups of 9; K = 300: 1 single + 23 groups of 13."""
+    best = None
+    for lead in range(0, min(8, K - 1) + 1):
+        rest = K - lead
+        for G in range(1, 17):
+            if rest % G:
+                continue
+            launches = lead + rest // G
+            first = 20.0 if lead else 5.0 * G + 40.0
+            cost = first + 12.8 * (launches - 1)
+            if best is None or cost < best[0] - 1e-9:
+                best = (cost, G, lead)
+    return best[1], best[2]
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -58,8 +79,10 @@ def main() -> int:
                     help="hip engine on GPUs: G consecutive training steps captured into one graph launch "
                          "(1..16; the same G full steps, one graph boundary instead of G: ~13 us each at "
                          "the headline, docs/DESIGN.md §6); a remainder of K or W modulo G runs as "
-                         "single-step graphs.  0 (default): the largest G <= 16 that divides K.  Reported "
-                         "as graph_steps.")
+                         "single-step graphs.  0 (default): a launch plan from the measured host / boundary "
+                         "costs (_launch_plan: a few single-step launches first, so the first launch after "
+                         "the timed region's synchronize is cheap, then groups).  Reported as graph_steps "
+                         "and lead_single_steps.")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -114,8 +137,9 @@ def main() -> int:
         if args.no_graph and hasattr(tr, "t"):
             tr.t.set_use_graph(False)
         step = lambda i: tr.step(*pool[i % len(pool)])  # noqa: E731
-        G = args.graph_steps or max(g for g in range(1, 17) if args.steps % g == 0)
-        G = G if ctx.device.type == "cuda" and hasattr(tr, "steps") else 1
+        G, lead = (args.graph_steps, 0) if args.graph_steps else _launch_plan(args.steps)
+        if not (ctx.device.type == "cuda" and hasattr(tr, "steps")):
+            G, lead = 1, 0
         final_loss = lambda: tr.loss()                  # noqa: E731
         plan = tr.t.plan() if hasattr(tr, "t") else "cpu"
     else:
@@ -134,9 +158,12 @@ def main() -> int:
     single = step
 
     def run(i0, n):
-        """n steps from pool index i0: whole groups of G steps per graph launch (the same steps, fewer
-        graph boundaries), the remainder n % G as single-step graphs"""
+        """n steps from pool index i0: `lead` single-step graphs, then whole groups of G steps per
+        graph launch (the same steps, fewer graph boundaries), the remainder as single-step graphs"""
         i = 0
+        for k in range(min(lead, n)):
+            single(i0 + k)
+            i += 1
         while G > 1 and i + G <= n:
             tr.steps([pool[(i0 + i + j) % len(pool)] for j in range(G)])
             i += G
@@ -165,7 +192,7 @@ def main() -> int:
                       f"char-tokens/sec (whole node) for GRU preset {args.preset}",
             "value": round(value, 1), "unit": "char-tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "extra_warmup_steps": extra,
-            "graph_steps": G,
+            "graph_steps": G, "lead_single_steps": lead,
             "ms_per_step": round(1000 * el / args.steps, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic name sequences (seeded syllable generator), random-init weights",
