@@ -30,7 +30,7 @@ METRIC = "char-tokens/sec (whole node) for GRU hidden=512 at 1/2/4/8 MI355X"
 
 
 def _launch_plan(K: int):
-    """(G, lead) for K timed steps: `lead` single-step graph launches, then groups of G steps (G <= 16
+    """(G, lead) for K timed steps: `lead` single-step graph launches, then groups of G steps (G <= 32
     dividing K - lead).  Cost model from the headline's measurements: the first launch after the
     timed region's synchronize is the only one whose host work the GPU does not hide -- ~20 us for a
     single step, ~5 us per step + 40 us for a group (staging G batches, launching ~8G nodes,
@@ -39,7 +39,7 @@ def _launch_plan(K: int):
     best = None
     for lead in range(0, min(8, K - 1) + 1):
         rest = K - lead
-        for G in range(1, 17):
+        for G in range(1, 33):
             if rest % G:
                 continue
             launches = lead + rest // G
@@ -77,7 +77,7 @@ def main() -> int:
                          "100, profiles/r2_bench_warmup_probe.txt).  Same count on every rank.")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="hip engine on GPUs: G consecutive training steps captured into one graph launch "
-                         "(1..16; the same G full steps, one graph boundary instead of G: ~13 us each at "
+                         "(1..32; the same G full steps, one graph boundary instead of G: ~13 us each at "
                          "the headline, docs/DESIGN.md §6); a remainder of K or W modulo G runs as "
                          "single-step graphs.  0 (default): a launch plan from the measured host / boundary "
                          "costs (_launch_plan: a few single-step launches first, so the first launch after "

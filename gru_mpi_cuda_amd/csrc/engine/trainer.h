@@ -202,7 +202,7 @@ class Trainer {
   // its own staging slot -- one graph boundary (~13 us at the headline) per G steps.  set_batches()
   // stages G batches ([G][B][T] each), step_group() launches them; two slot groups alternate so the
   // host fills one while the other runs.
-  static constexpr int kMaxGroup = 16;
+  static constexpr int kMaxGroup = 32;
   void set_graph_steps(int G);
   int graph_steps() const { return group_; }
   void set_batches(const int* x, const int* y, int B, int n);

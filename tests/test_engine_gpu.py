@@ -351,7 +351,7 @@ def test_sharded_optimizer_step_world1(layers, E, H, opt):
     assert abs(a.loss() - b.loss()) < 1e-4
 
 
-@pytest.mark.parametrize("G,layers,H", [(4, 1, 512), (2, 2, 256), (3, 1, 256), (10, 1, 512), (16, 1, 256)])
+@pytest.mark.parametrize("G,layers,H", [(4, 1, 512), (2, 2, 256), (3, 1, 256), (10, 1, 512), (16, 1, 256), (19, 1, 512)])
 def test_multi_step_graph_matches_single_steps(G, layers, H):
     """G whole steps captured into one graph (Trainer::set_graph_steps / step_group), each reading its
     own staging slot, equal G single-step launches bit for bit; two groups in a row exercise both
