@@ -858,10 +858,10 @@ def test_forward_input_projection_in_kernel(monkeypatch, B, padded, G):
         assert rel(ga[k], ref_g[k]) < 0.04, k
 
 
-@pytest.mark.parametrize("G", [10])
+@pytest.mark.parametrize("G", [10, 19])
 def test_multi_step_graph_with_rccl_world1(G):
     """The data-parallel step (in-graph RCCL collectives, here on a 1-rank communicator) captured G
-    steps per graph launch -- the bench's default for the driver's K = 20 -- equals G single-step
+    steps per graph launch -- the bench's plan for the driver's K = 20 is one single + 19 -- equals G single-step
     launches of the same structure bit for bit, and keeps its multi-step graph."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
