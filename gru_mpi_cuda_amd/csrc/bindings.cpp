@@ -131,9 +131,7 @@ PYBIND11_MODULE(_C, m) {
       .def("inject_error", &Trainer::inject_error)
       .def("watchdog_status", &Trainer::watchdog_status)
       .def("watchdog_message", &Trainer::watchdog_message)
-      .def("buffer", &Trainer::buffer)
-      .def("tail_plan", &Trainer::tail_plan)
-      .def("set_tail_dbg", [](Trainer& t, uintptr_t p) { t.set_tail_dbg(reinterpret_cast<unsigned long long*>(p)); });
+      .def("buffer", &Trainer::buffer);
 
   py::class_<Generator>(m, "Generator")
       .def(py::init([](py::dict dims, uintptr_t params, std::map<std::string, long> offsets) {
@@ -247,13 +245,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("xcc_census", [](uintptr_t out, int nblocks, int threads, uintptr_t s) {
     xcc_census(Pp<unsigned>(out), nblocks, threads, S(s)); HIP_LAUNCH_CHECK(); });
   m.def("fwd_seq_supported", &gru_fwd_seq_supported);
-  m.def("fwd_seq_pl_supported", &gru_fwd_seq_pl_supported);
   m.def("bwd_step_sk_splits", &gru_bwd_step_sk_splits);
   m.def("step_lds_variants", []() {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
-    d["fwd_ns"] = v.fwd_ns; d["fwd_nt"] = v.fwd_nt; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
-    d["bwd_sk_ns"] = v.bwd_sk_ns; d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk64"] = v.bwd_sk64; d["bwd_sk_min_h"] = v.bwd_sk_min_h;
+    d["fwd_ns"] = v.fwd_ns; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
+    d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk_min_h"] = v.bwd_sk_min_h;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -262,14 +259,11 @@ PYBIND11_MODULE(_C, m) {
       const std::string k = py::str(kv.first);
       const int x = kv.second.cast<int>();
       if (k == "fwd_ns") v.fwd_ns = x;
-      else if (k == "fwd_nt") v.fwd_nt = x;
       else if (k == "fwd8") v.fwd8 = x;
       else if (k == "fwd64") v.fwd64 = x;
       else if (k == "fwd64_fused") v.fwd64_fused = x;
       else if (k == "fwd64_all") v.fwd64_all = x;
-      else if (k == "bwd_sk_ns") v.bwd_sk_ns = x;
       else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
-      else if (k == "bwd_sk64") v.bwd_sk64 = x;
       else if (k == "bwd_sk_min_h") v.bwd_sk_min_h = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
@@ -311,45 +305,14 @@ PYBIND11_MODULE(_C, m) {
     a.h0 = GP(const float, d, "h0");
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
-    a.saves_in_drain = get<int>(d, "saves_in_drain", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
-    // table-free layer 0: Emb, Wih0, bih, V, E (+ the staging slot prep_in with labels / inv_count)
-    a.Emb = GP(const u16, d, "Emb"); a.Wih0 = GP(const u16, d, "Wih0"); a.bih = GP(const float, d, "bih");
-    a.V = get<int>(d, "V", 0); a.E = get<int>(d, "E", 0);
-    if (GP(const int, d, "prep_in")) {
-      a.prep = PrepJob{GP(const int, d, "prep_in"), get<int>(d, "Bmax", a.Bp), a.T, a.Bp, const_cast<int*>(a.ids),
-                       GP(int, d, "labels"), GP(float, d, "inv_count")};
-    }
-    if (a.Emb ? !gru_fwd_seq_pl_supported(a.H, a.Bp, a.V, a.E, a.T) : !gru_fwd_seq_supported(a.H, a.Bp))
-      throw std::runtime_error("fwd_seq: shape not supported");
+    if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
-  m.def("fwd_seq_fc", [](py::dict d, py::dict fd, uintptr_t s) {   // diagnostics / tests: the FC-pipeline forward
-    SeqFwdArgs a;
-    a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
-    a.HF = GP(u16, d, "HF"); a.xch = GP(u16, d, "xch");
-    a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
-    a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
-    a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
-    a.h0 = GP(const float, d, "h0"); a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
-    a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
-    a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
-    FwdFcArgs f;
-    f.Wfc = GP(const u16, fd, "Wfc"); f.WfcT = GP(const u16, fd, "WfcT"); f.bfc = GP(const float, fd, "bfc");
-    f.labels = GP(const int, fd, "labels"); f.inv_count = GP(const float, fd, "inv_count");
-    f.xdl = GP(u16, fd, "xdl"); f.xdlT = GP(u16, fd, "xdlT"); f.xst = GP(float, fd, "xst"); f.dy = GP(float, fd, "dy");
-    f.dW_part = GP(float, fd, "dW_part"); f.db_part = GP(float, fd, "db_part"); f.loss_part = GP(float, fd, "loss_part");
-    f.V = get<int>(fd, "V", 256);
-    gru_fwd_seq_fc(a, f, S(s));
-    HIP_LAUNCH_CHECK();
-  });
-  m.def("fwd_seq_fc_supported", &gru_fwd_seq_fc_supported);
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
     a.dy = GP(const float, d, "dy");
-    a.dl = GP(const u16, d, "dl"); a.WfcT = GP(const u16, d, "WfcT");
-    if (a.dl && get<int>(d, "V", 0) != 256) throw std::runtime_error("bwd_seq: in-kernel dH needs V = 256");
     a.sr = GP(const float, d, "sr"); a.sz = GP(const float, d, "sz"); a.sn = GP(const float, d, "sn");
     a.sghn = GP(const float, d, "sghn"); a.HSf = GP(const float, d, "HSf");
     a.HT = GP(const u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0); a.WhhT = GP(const u16, d, "WhhT");
@@ -361,7 +324,6 @@ PYBIND11_MODULE(_C, m) {
     a.dP_part = GP(float, d, "dP_part"); a.V = get<int>(d, "V", 0);
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
     a.allow_local = get<int>(d, "allow_local", 1);
-    a.fused_in_drain = get<int>(d, "fused_in_drain", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     // "unchecked": skip the co-residency query and go straight to the dispatch table (tests its
     // unmatched-variant error without launching anything)

@@ -60,7 +60,6 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);   // 0 auto, 1 reg, 2 LDS
   const char* gp = std::getenv("GK_GEN_PERSIST");
   if (gp && gp[0] == '0') persist_ = false;
-  if (const char* pm = std::getenv("GK_GEN_PERSIST_MAX")) persist_max_ = std::atoi(pm);
 }
 
 bool Generator::uses_persist(int n) const {
@@ -121,39 +120,7 @@ void Generator::refresh_weights(hipStream_t s) {
 // made replays disagree (scripts/repro_gen_fp32.py with SYNC_FIRST=1: error word 16, replays not
 // identical); a kernel node is ordered like every other node of the chain.
 void Generator::reset_batch(int Bp, bool bf16, hipStream_t s) {
-  // diagnostic: 1 = round 2's memset-node reset, 2 = the same behind a no-op kernel node (probes only)
-  static const int memset_nodes = [] {
-    const char* e = std::getenv("GK_GEN_MEMSET_RESET");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (memset_nodes >= 3) {   // 3/4/5: the kernel reset, then ONE redundant memset group (same values):
-    // it can change results only by running late, after the kernels that follow it have started
-    GenResetArgs r;
-    r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
-    r.hb_cols = split3() ? 3 * d_.H : d_.H;
-    for (int l = 0; l < d_.L; ++l) { r.hf[l] = hf_[2 * l]; r.hb[l] = (bf16 || split3()) ? hb_[2 * l] : nullptr; }
-    r.ids = ids_; r.alive = alive_; r.out = out_;
-    gen_reset(r, s);
-    if (memset_nodes == 3)
-      for (int l = 0; l < d_.L; ++l) HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * d_.H * 4, s));
-    if (memset_nodes == 4) {
-      HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
-      HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
-    }
-    if (memset_nodes == 5) HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (d_.max_len + 1), s));
-    return;
-  }
-  if (memset_nodes) {
-    if (memset_nodes == 2) block_cus(1, 0, s);   // the graph's root node is then a kernel
-    for (int l = 0; l < d_.L; ++l) {
-      HIP_CHECK(hipMemsetAsync(hf_[2 * l], 0, (size_t)Bp * d_.H * 4, s));
-      if (bf16 || split3()) HIP_CHECK(hipMemsetAsync(hb_[2 * l], 0, (size_t)Bp * (split3() ? 3 : 1) * d_.H * 2, s));
-    }
-    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ids_), d_.sos, Bp, s));
-    HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(alive_), 1, Bp, s));
-    HIP_CHECK(hipMemsetAsync(out_, 0, (size_t)Bp * (d_.max_len + 1), s));
-    return;
-  }
+  // (round 3's memset-node diagnostics, scripts/gpu_graph_fault3.sh, profiles/r3_graph_replay.md)
   GenResetArgs r;
   r.L = d_.L; r.Bp = Bp; r.H = d_.H; r.ML = d_.max_len; r.sos = d_.sos;
   r.hb_cols = split3() ? 3 * d_.H : d_.H;
@@ -243,8 +210,7 @@ int Generator::product_f32(const float* A32, const u16* A3, const float* W32, co
     g.bias = bias;   // split: the consumer adds the bias after the slab sum
     // the 256 x 256 kernel from 3/4 of a wave of its tiles (4096 names x 3H: 192 tiles), where the
     // 128 x 128 kernel's 1.5 rounds of 512 slots leave as much idle
-    static const bool big = [] { const char* e = std::getenv("GK_X3_GEMM256"); return !e || e[0] != '0'; }();
-    if (big && M % 256 == 0 && N % 256 == 0 && (M / 256) * (N / 256) >= 192) g.algo = 5;
+    if (M % 256 == 0 && N % 256 == 0 && (M / 256) * (N / 256) >= 192) g.algo = 5;
   } else {
     g.algo = 3;
   }
@@ -294,12 +260,12 @@ void Generator::record_steps_f32(int n, hipStream_t s) {
 void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t s) {
   GK_TRACE("gk.generate");
   const int ML = d_.max_len;
+  // the error word covers the whole call: every batch ORs its bits in, read_error() reports them all
+  // (a persistent launch's spin-limit bit 32 is taken out again below once its batch is regenerated)
+  HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);
     HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
-    // the error word is per batch: a spin timeout of an earlier persistent launch (bit 32, which
-    // makes every later wait of that launch give up at once) must not leak into this one
-    HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
     bool persist_done = false;
     if (uses_persist(n)) {   // one launch for the whole batch: no graph needed
       GenPersistArgs a;
@@ -328,7 +294,8 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
         std::fprintf(stderr, "[generator] persistent launch hit its spin limit (error word %u): "
                              "disabling it, regenerating %d names on the per-char graph\n", e, n);
         persist_ = false;
-        HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
+        const unsigned keep = e & ~32u;   // the other bits stay (earlier batches' errors)
+        HIP_CHECK(hipMemcpy(err_, &keep, 4, hipMemcpyHostToDevice));
       }
     }
     if (persist_done) {
@@ -352,7 +319,7 @@ unsigned Generator::read_error() {
   unsigned e[4] = {0, 0, 0, 0};
   HIP_CHECK(hipDeviceSynchronize());
   HIP_CHECK(hipMemcpy(e, err_, 16, hipMemcpyDeviceToHost));
-  if (e[0] && std::getenv("GK_GEN_DEBUG"))
+  if (e[0])
     std::fprintf(stderr, "[generator] error word %u: id %d (0x%08x) at row %u\n", e[0], (int)e[1], e[1], e[2]);
   return e[0];
 }

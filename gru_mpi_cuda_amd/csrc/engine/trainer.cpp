@@ -9,11 +9,6 @@ namespace gk {
 
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-static bool env_on(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  return v && v[0] ? v[0] != '0' : dflt;
-}
-
 
 Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, float* m, float* v, long nflat,
                  const std::map<std::string, long>& offsets)
@@ -32,8 +27,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   struct Pend { size_t off; };
   std::vector<size_t> lo;
   auto R = [&](size_t bytes) { return arena_.reserve(bytes); };
-  size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4 * kPSlabsMax);
-  size_t o_lp = R(std::max(tok / 32, (size_t)(H / 16) * (B / 32)) * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
+  size_t o_ids = R(tok * 4), o_lab = R(tok * 4), o_inv = R(16), o_P = R((size_t)V * 3 * H * 4);
+  size_t o_lp = R(tok / 32 * 4 + 16), o_loss = R(16), o_sfc = R((size_t)C_ * V * H * 4), o_rfc = R((size_t)C_ * V * 4);
   size_t o_sP = R((size_t)C_ * V * 3 * H * 4), o_dP = R((size_t)V * 3 * H * 4);
   size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
   size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
@@ -43,8 +38,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   fc_split_ = !fc_xent_fused_ok(V, H, (int)tok) && tok % 128 == 0 && V % 128 == 0 && V <= 512 && H % 64 == 0 &&
               H >= 128;
   size_t o_lg = fc_split_ ? R(tok * V * 4) : 0;
-  // row statistics exchange of the forward's FC pipeline (gru_fwd_seq_fc; its dl tiles live in dl_ / dlT_)
-  size_t o_xst = (V == 256 && H <= 512 && B % 32 == 0) ? R((size_t)T * (B / 32) * 16 * 256) : 0;
   struct LO { size_t HSf, sr, sz, sn, sghn, dy, Gi, c0, c1, HSb, HT, g0, g1, dghT, dgiT, dgi, Whh, WhhT, Wih, WihT, shh, rhh, sih, rih; };
   std::vector<LO> los(L);
   for (int l = 0; l < L; ++l) {
@@ -80,8 +73,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     // shapes where both one-hot dP call sites (whole sequence, and per time chunk in the overlapped
     // schedule) are LDS-kernel shapes with 128-aligned gate blocks (gemm_lds_ok with B2)
     const long tok = (long)d_.T * B, ctok = (long)Tc_ * B;
-    const char* ds = std::getenv("GK_DGIT_SHARE");
-    dgiT_share_ = !(ds && ds[0] == '0') && V % 128 == 0 && H % 128 == 0 && B % 8 == 0 && tok % 128 == 0 &&
+    dgiT_share_ = V % 128 == 0 && H % 128 == 0 && B % 8 == 0 && tok % 128 == 0 &&
                   ctok % 128 == 0;
   }
   seq_.resize(L);
@@ -96,7 +88,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
-  size_t o_tsync = R((size_t)tail_sync_words(V, 3 * H, E, H) * 4);
   // split-K slab: large enough for every weight-gradient product it serves
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
@@ -121,7 +112,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
-  tail_sync_ = arena_.get<unsigned>(o_tsync);   // zero-filled; the tail kernel leaves it zeroed
   slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
   slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
   for (int l = 0; l < L; ++l) {
@@ -136,7 +126,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
 
   ids_ = arena_.get<int>(o_ids); labels_ = arena_.get<int>(o_lab); inv_count_ = arena_.get<float>(o_inv);
   Ptab_ = arena_.get<float>(o_P); loss_part_ = arena_.get<float>(o_lp); loss_ = arena_.get<float>(o_loss);
-  xst_ = o_xst ? arena_.get<float>(o_xst) : nullptr;
   slab_fc_ = arena_.get<float>(o_sfc); rs_fc_ = arena_.get<float>(o_rfc); slab_P_ = arena_.get<float>(o_sP);
   dP_ = arena_.get<float>(o_dP); norm_parts_ = arena_.get<float>(o_np); gscale_ = arena_.get<float>(o_gs);
   step_ = arena_.get<int>(o_step);
@@ -177,9 +166,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   // The staging events only tell the host that the graph which read a pinned slot has finished;
   // the host never reads device results through them, so they skip the system-scope release
   // (an end-of-step L2 writeback to host-coherent memory between consecutive step graphs).
-  const char* sf = std::getenv("GK_STAGE_SYSTEM_FENCE");
-  const unsigned stage_flags = hipEventDisableTiming |
-                               ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+  const unsigned stage_flags = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
   for (auto& e : stage_done_) {
     HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
     HIP_CHECK(hipEventRecord(e, s0_));
@@ -278,24 +265,6 @@ void Trainer::refresh_weights(hipStream_t s) {
   j.add(P("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
   cast_multi(j, s);
   HIP_LAUNCH_CHECK();
-  p_valid_ = false;   // the master weights may have been rewritten: the next P comes from a GEMM
-}
-
-// The layer-0 table alone, with the prologue's GEMM kernel (gemm_small: the k-sequence the fused
-// tail's P items reproduce, so the table is bitwise the same whichever computed it)
-void Trainer::record_p_gemm(hipStream_t s) {
-  GemmArgs g;
-  g.A = Emb; g.lda = d_.E; g.B = Ls_[0].Wih; g.ldb = d_.E; g.C = Ptab_; g.ldc = 3 * d_.H;
-  g.bias = P("bias_ih_l0"); g.M = d_.V; g.N = 3 * d_.H; g.K = d_.E;
-  if (gemm_small_kblocks(g) > 0) gemm_small(g, s);
-  else gemm_nt(g, s);
-  HIP_LAUNCH_CHECK();
-}
-
-void Trainer::ensure_p(hipStream_t s) {
-  if (p_valid_) return;
-  record_p_gemm(s);
-  p_valid_ = true;
 }
 
 void Trainer::set_batch(const int* x, const int* y, int B, hipStream_t s) {
@@ -610,8 +579,7 @@ void Trainer::record_opt(hipStream_t s) {
       if (!used) rest.job[rest.n++] = D;
     }
     if (rest.n) reduce_slabs_multi(rest, s);
-    if (tail_fused_) record_tail(a, j, s);
-    else adam_cast_multi(a, j, s);
+    adam_cast_multi(a, j, s);
   } else {
     if (deferred_.n) reduce_slabs_multi(deferred_, s);
     adam_step(a, s);
@@ -619,73 +587,6 @@ void Trainer::record_opt(hipStream_t s) {
   }
   deferred_.n = 0;
   HIP_LAUNCH_CHECK();
-}
-
-// The fused step tail (tail.hip) is opt-in (GK_TAIL=1) since round 3's last measurements: on the
-// current tree the phased tail (reduce_multi + gemm_small_group + adam_cast, dW_fc before the
-// backward) runs the headline 3.2 us faster in the driver's form (6 alternating pairs, 0.2245 vs
-// 0.2213 ms) and 2.5 us at K = 300 (profiles/r3s5_tail_fused_vs_phased_ab.jsonl): one grid of 1029
-// items contends for memory bandwidth (§6.3) where three back-to-back launches each get it whole.
-bool Trainer::tail_ok() const {
-  const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
-  // data-parallel: the readiness-ordered path (dp_overlap) runs it after the last collective, on the
-  // all-reduced dP (one slab); the plain-bucket and sharded paths do not
-  if ((comm_ && !dp_overlap()) || shard_opt_ || o_.clip > 0.f || overlap_ || seq_.empty() || !seq_[0].fuse_p || !dP_part_ ||
-      V % 64 || E % 64 || d_.H % 64 || !env_on("GK_TAIL", false))
-    return false;
-  // tail.hip's conditions: 256-deep K-slices, fewer waiting product blocks than resident slots
-  const int se = tail_emb_splits();
-  const long waiting = (long)(H3 / 64) * (E / 64) + (long)(V / 64) * (E / 64) * se;
-  return se <= 8 && (H3 / se) % 256 == 0 && V % 256 == 0 && waiting < tail_resident_slots();
-}
-
-// dEmb = dP · W_ih0 (K = 3H) K-split: the same slices as record_emb_tail's GEMMs (so the fused tail
-// and the phased step sum the same partials in the same order: bitwise-equal gradients)
-int Trainer::tail_emb_splits() const {
-  const int V = d_.V, H3 = 3 * d_.H;
-  if (H3 % V == 0 && H3 / V <= splits_ && V % 64 == 0) return H3 / V;
-  int se = splits_;
-  while (se > 1 && (H3 % se || (H3 / se) % 64 || H3 / se < 128)) se >>= 1;
-  return se;
-}
-
-// The fused step tail (tail.hip) in place of reduce_multi + the embedding-side GEMMs + adam_cast
-void Trainer::record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s) {
-  const int V = d_.V, E = d_.E, H3 = 3 * d_.H, nrb = Bp_ / 32;
-  const long tok = (long)d_.T * Bp_;
-  TailArgs t;
-  t.dP_part = dP_part_; t.nslP = nrb; t.V = V; t.H3 = H3; t.dP_bf = dP_bf_; t.dPT_bf = dPT_bf_;
-  if (comm_) {   // data-parallel: the all-reduced dP (reduced from the partials before the collective)
-    t.dP_part = dP_target(); t.nslP = 1; t.dP_alias = dP_inplace_ ? 1 : 0;
-  }
-  t.EmbT = EmbT; t.WihT = Ls_[0].WihT; t.E = E; t.slab_e = slab_e_; t.se = tail_emb_splits();
-  for (int k = 0; k < j.n; ++k) {
-    if (j.job[k].off == off_.at("weight_ih_l0")) t.jw = k;
-    if (j.job[k].off == off_.at("embedding")) t.je = k;
-    if (j.job[k].off == off_.at("fc.weight")) t.jf = k;
-    if (j.job[k].off == off_.at("fc.bias")) t.jb = k;
-  }
-  if (tail_nfc_) {   // dW_fc / db_fc (record_fb_seq left them to the tail)
-    const int L = d_.L, T = d_.T, B = Bp_;
-    t.dlT = dlT_; t.ldl = (int)tok; t.HTop = Ls_[L - 1].HT + B; t.ldh = (T + 1) * B;
-    t.slab_fc = slab_fc2_; t.rs_fc = rs_fc2_; t.nfc = tail_nfc_; t.tok = (int)tok; t.H = d_.H;
-  }
-  if (tail_p_) {   // the next step's P table
-    t.P = Ptab_; t.EmbR = Emb; t.WihR = Ls_[0].Wih; t.bih = P("bias_ih_l0");
-    for (int k = 0; k < j.n; ++k)
-      if (j.job[k].off == off_.at("bias_ih_l0")) t.jbi = k;
-  }
-  if (tail_batch_ && next_stage_src_)   // the next step's batch, when this graph holds that step
-    t.prep = PrepJob{next_stage_src_, Bp_, d_.T, Bp_, ids_, labels_, inv_count_};
-  t.loss_part = loss_part_; t.nloss = nloss_; t.loss = loss_;
-  t.sync = tail_sync_;
-  t.epoch = reinterpret_cast<const unsigned*>(step_ + 1);   // bumped with the step by the backward kernel
-  t.dbg = tail_dbg_;
-  t.adam_after_dp = env_on("GK_TAIL_ADAM_WAIT", false) ? 1 : 0;
-  t.fc_after_dp = env_on("GK_TAIL_FC_WAIT", false) ? 1 : 0;
-  if (!tail_step(a, j, t, s)) throw std::runtime_error("fused tail: grid cannot hold its waiting blocks");
-  tail_items_ = t.nItems;
-  tail_plan_ = {t.nB, t.nF, t.nP, 1, t.nA0, t.nW, t.nE, t.nPt};
 }
 
 void Trainer::forward_backward(hipStream_t s) {
@@ -713,7 +614,6 @@ void Trainer::forward_backward(hipStream_t s) {
 
 void Trainer::optimizer_step(hipStream_t s) {
   GK_TRACE("gk.optimizer_step");
-  p_valid_ = false;   // the phased path recomputes P in every step's prologue
   if (!use_graph_) { record_opt(s); return; }
   if (!g_opt_.ready()) {
     g_opt_.begin(s0_);
@@ -764,12 +664,6 @@ bool Trainer::ar_flush(hipStream_t s, bool force, bool with_err) {
     if (with_err) comm_->allreduce_avg_f32_err(grads_ + ar_launched_, n, err_, st);
     else comm_->allreduce_avg_f32(grads_ + ar_launched_, n, st);
   };
-  if (!env_on("GK_AR_FORK", true)) {   // A/B switch: the collective in line on the step stream
-    reduce(s);
-    ar_log_.push_back({ar_launched_, n});
-    ar_launched_ = ar_ready_;
-    return true;
-  }
   hipEvent_t e = ev();
   HIP_CHECK(hipEventRecord(e, s));          // fork: everything recorded on s so far
   HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
@@ -824,14 +718,9 @@ void Trainer::step(hipStream_t s) {
     GK_TRACE("gk.capture_step_graph");
     g.begin(s0_);
     try {
-      next_stage_src_ = nullptr;
-      batch_from_prev_tail_ = false;
       record_step_body();
-      g_step_p_[slot] = body_tail_p_;
     } catch (...) {
       defer_slabs_ = false;
-      tail_fused_ = tail_p_ = tail_batch_ = false;
-      p_in_prologue_ = batch_in_prologue_ = true;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;          // leave the stream out of capture mode, then rethrow
       (void)hipStreamEndCapture(s0_, &broken);
@@ -841,9 +730,7 @@ void Trainer::step(hipStream_t s) {
     }
     g.end(s0_);
   }
-  if (g_step_p_[slot]) ensure_p(s);
   g.launch(s);
-  p_valid_ = g_step_p_[slot];
   HIP_CHECK(hipEventRecord(stage_done_[slot], s));
   if (wd_) wd_->watch(stage_done_[slot]);
 }
@@ -873,19 +760,12 @@ void Trainer::step_group(hipStream_t s) {
     GK_TRACE("gk.capture_group_graph");
     g.begin(s0_);
     try {
-      batch_from_prev_tail_ = false;
       for (int j = 0; j < group_; ++j) {
         stage_src_ = h_stage_ + (size_t)group_slot(gp, j) * slot_ints();
-        next_stage_src_ = j + 1 < group_ ? h_stage_ + (size_t)group_slot(gp, j + 1) * slot_ints() : nullptr;
         record_step_body();
       }
-      next_stage_src_ = nullptr;
-      g_group_p_[gp] = body_tail_p_;
     } catch (...) {
-      next_stage_src_ = nullptr;
       defer_slabs_ = false;
-      tail_fused_ = tail_p_ = tail_batch_ = false;
-      p_in_prologue_ = batch_in_prologue_ = true;
       deferred_.n = 0;
       hipGraph_t broken = nullptr;
       (void)hipStreamEndCapture(s0_, &broken);
@@ -895,9 +775,7 @@ void Trainer::step_group(hipStream_t s) {
     }
     g.end(s0_);
   }
-  if (g_group_p_[gp]) ensure_p(s);
   g.launch(s);
-  p_valid_ = g_group_p_[gp];
   HIP_CHECK(hipEventRecord(group_done_[gp], s));
   if (wd_) wd_->watch(group_done_[gp]);
 }
@@ -911,38 +789,18 @@ void Trainer::record_step_body() {
     record_sharded_opt(s0_);
     return;
   }
+  deferred_.n = 0;
   if (dp_overlap()) {
     // readiness-ordered collectives on the comm stream, overlapped with the rest of the
-    // backward; joined before the optimiser (the embedding-side tail runs after the join, as
-    // the fused step tail when it qualifies)
-    deferred_.n = 0;
-    tail_fused_ = tail_ok();
+    // backward; joined before the optimiser (the embedding-side tail runs after the join)
     record_fb_seq(s0_, /*dp=*/true);
   } else {
-    deferred_.n = 0;
-    defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f && env_on("GK_DEFER_SLABS", true);
-    tail_fused_ = tail_ok();
-    // GK_TAIL_P=1: the next step's P in the tail.  Measured slower at the headline (its items can
-    // only start once the last Emb tile is refreshed: tail 40.8 -> 51.1 us, step 0.215 -> 0.224 ms,
-    // profiles/r3_tail_p_ab.jsonl), so off by default.
-    tail_p_ = tail_fused_ && d_.E % 256 == 0 && env_on("GK_TAIL_P", false);
-    // GK_TAIL_BATCH=1: the next step's batch preparation in the tail (multi-step graphs): measured
-    // neutral (0.2186-0.2273 vs 0.219 ms), off by default
-    tail_batch_ = tail_fused_ && env_on("GK_TAIL_BATCH", false);
-    // with tail_p_ every step of this configuration leaves the next P behind: this one's came from
-    // the previous tail (or ensure_p() before the launch); its batch inside a multi-step graph
-    p_in_prologue_ = !tail_p_;
-    batch_in_prologue_ = !(tail_batch_ && batch_from_prev_tail_);
+    defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f;
     if (overlap_) record_fb(s0_); else record_fb_seq(s0_);
     defer_slabs_ = false;
     record_allreduce(s0_);
   }
   record_opt(s0_);
-  body_tail_p_ = tail_p_;
-  batch_from_prev_tail_ = tail_batch_ && next_stage_src_ != nullptr;
-  tail_fused_ = false;
-  tail_p_ = tail_batch_ = false;
-  p_in_prologue_ = batch_in_prologue_ = true;
 }
 
 float Trainer::read_loss() {

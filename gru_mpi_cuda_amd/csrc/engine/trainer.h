@@ -67,56 +67,10 @@ class Trainer {
   // over the gradients fewer).  slab_job() routes a job to `j` or, when deferring, to deferred_.
   bool defer_slabs_ = false;
   SlabJobs deferred_;
-  // Fused step tail (tail.hip): the dP reduction, loss, embedding-side products and the whole
-  // Adam + bf16 refresh as one launch.  Set while recording a one-graph step that qualifies
-  // (tail_ok(): single GPU, no clipping, fused-dP persistent backward); record_fb_seq then leaves
-  // those pieces to record_opt.  GK_TAIL=0 turns it off.
-  bool tail_fused_ = false;
-  int tail_nfc_ = 0;             // dW_fc K-slices computed inside the fused tail (0: before the backward)
-  // The next step's layer-0 table (and, inside a multi-step graph, its batch preparation) in the
-  // fused tail (GK_TAIL_P=0: off).  A step recorded with tail_p_ takes P from the previous step's
-  // tail instead of its prologue GEMM; p_valid_ says whether Ptab_ matches the current weights
-  // (false after refresh_weights() or a step without it), and a launch that relies on it runs
-  // ensure_p() first.
-  bool tail_p_ = false, tail_batch_ = false;
-  // The prologue's P table as split-K slabs summed by the persistent forward's gather (GK_P_SLABS=4;
-  // default 1 = one table with the bias): 4x the workgroups, each fetching a quarter of Emb / W_ih0.
-  // Measured much slower at the headline (0.2458-0.2489 vs 0.2176-0.2180 ms/step): the gather's 12
-  // scattered loads per step instead of 3 sit in the recurrence's in-order vmcnt window.
-  static constexpr int kPSlabsMax = 4;
-  int p_slabs_ = 1;               // of the step being recorded
-  int p_slabs_for_record() const;
-  bool fwd_pl_ok() const;
-  bool fwd_xp_ok() const;
-  bool p_in_prologue_ = true, batch_in_prologue_ = true, batch_from_prev_tail_ = false;
-  const int* next_stage_src_ = nullptr;   // staging slot of the next step in the same graph (or null)
-  bool p_valid_ = false;
-  bool body_tail_p_ = false;              // the last recorded step body computed the next P in its tail
-  bool g_step_p_[2] = {false, false}, g_group_p_[2] = {false, false};
-  void ensure_p(hipStream_t s);           // P = Emb·W_ih0^T + b_ih0 now, if it is stale
-  void record_p_gemm(hipStream_t s);
-  bool tail_ok() const;
-  unsigned* tail_sync_ = nullptr;
-  unsigned long long* tail_dbg_ = nullptr;   // set_tail_dbg(): per-item stamps (TailArgs::dbg)
-  int tail_items_ = 0;
- public:
-  // item counts of the last recorded fused tail, in item order: dP tiles, loss, Adam dep 0, products,
-  // Adam dep 2, Adam dep 1 (tests, probes)
-  std::vector<int> tail_plan() const { return tail_plan_; }
-  // diagnostic: device buffer of >= 4 * items u64 for the fused tail's per-item stamps (0 = off)
-  void set_tail_dbg(unsigned long long* p) {
-    tail_dbg_ = p;
-    for (auto& g : g_step_) g.reset();
-    for (auto& g : g_group_) g.reset();
-  }
- private:
-  std::vector<int> tail_plan_;
-  int tail_emb_splits() const;
   void slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst);
   void record_carry(hipStream_t s);     // HS[T] -> HS[0] of every layer and copy (carry_ only)
   bool carry_ = false;
   void record_opt(hipStream_t s0);
-  void record_tail(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
   void fwd_step(int l, int t, hipStream_t s);
   void bwd_step(int l, int t, hipStream_t s);
   hipEvent_t ev();
@@ -253,9 +207,7 @@ class Trainer {
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
-  float* xst_ = nullptr;         // forward FC pipeline: row statistics exchange
-  int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks or forward workgroups)
-  bool fwd_fc_ok() const;
+  int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks)
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }

@@ -14,41 +14,9 @@
 
 namespace gk {
 
-static bool env_flag(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  return v && v[0] ? v[0] != '0' : dflt;
-}
-
-// persistent kernels: the publishing wave overlapping its own follow-up work with its exchange drain --
-// backward fused weight-gradient MFMAs (GK_BWD_FUSED_IN_DRAIN=1), forward saves (GK_FWD_SAVES_IN_DRAIN=1).
-// Both measured slower (the signal waits for the extra work: bwd 0.2195-0.2219 -> 0.2218-0.2233 ms/step,
-// forward 60.6 -> 62.5 us; profiles/r3s5_drain_overlap_ab.jsonl): off.  Read at record time.
-static bool bwd_fused_in_drain() { return env_flag("GK_BWD_FUSED_IN_DRAIN", false); }
-static bool fwd_saves_in_drain() { return env_flag("GK_FWD_SAVES_IN_DRAIN", false); }
-
 // data-parallel: a layer group's collective stays open across the next persistent backward kernel
-static bool ar_span() {
-  static const bool on = env_flag("GK_AR_SPAN", true);
-  return on;
-}
-
-// Split-K slabs of the prologue's P table: only where the persistent forward reads it (its gather
-// sums the slabs) and the small GEMM takes the K-slices
-int Trainer::p_slabs_for_record() const {
-  if (!persist_fwd_) return 1;
-  const char* e = std::getenv("GK_P_SLABS");
-  int n = e ? std::atoi(e) : 1;
-  if (n < 1) n = 1;
-  if (n > kPSlabsMax) n = kPSlabsMax;
-  while (n > 1) {
-    GemmArgs g;
-    g.A = Emb; g.lda = d_.E; g.B = Ls_[0].Wih; g.ldb = d_.E; g.C = Ptab_; g.ldc = 3 * d_.H;
-    g.M = d_.V; g.N = 3 * d_.H; g.K = d_.E; g.splits = n;
-    if (d_.E % n == 0 && gemm_small_kblocks(g) > 0) break;
-    n >>= 1;
-  }
-  return n;
-}
+// (span mode; joining it before that kernel measured the same at one rank, docs/DESIGN.md §6.2)
+static bool ar_span() { return true; }
 
 // Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
 // split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
@@ -138,10 +106,7 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
 void Trainer::slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst) {
   // deep split-K slabs (the dW_fc GEMM's 32) stay with the reduce kernel: summed inside the Adam
   // launch they serialise 32 loads per element on its few tile blocks
-  static const int max_splits = [] {
-    const char* e = std::getenv("GK_DEFER_MAX_SPLITS");
-    return e ? std::atoi(e) : 8;
-  }();
+  constexpr int max_splits = 8;
   SlabJobs& t = (defer_slabs_ && splits <= max_splits) ? deferred_ : j;
   if (t.n >= 24) throw std::runtime_error("slab job list full");
   t.add(src, splits, n, dst);
@@ -158,36 +123,15 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
-  // table-free layer 0 (GK_FWD_PL=1, off by default): the persistent forward computes the P-table
-  // columns it gathers from and transposes the batch itself -- no prologue kernel (gru_seq.hip, PL).
-  // Measured slower: every workgroup streams all of Emb (256 x 304 KB of L2 reads) and redoes 8x the
-  // table's MFMAs, 10-17 us before its first step against the 7 us prologue kernel
-  // (forward 60 -> 90 us, step 0.216 -> 0.240 ms, profiles/r3s5_fwd_pl_ab.jsonl)
-  const bool fwd_pl = fwd_pl_ok();
-  const bool fwd_fc = !fwd_pl && fwd_fc_ok();
-  const bool fwd_xp = !fwd_pl && !fwd_fc && fwd_xp_ok();
-  nloss_ = fwd_fc ? (H / 16) * (B / 32) : (int)(tok / 32);
-  p_slabs_ = (p_in_prologue_ && !fwd_pl && !fwd_xp) ? p_slabs_for_record() : 1;
-  if (fwd_pl) {
-    // (nothing before the forward launch)
-  } else if (fwd_xp) {
-    // layer 0's input projection runs inside the forward launch: the prologue is the batch alone
-    if (batch_in_prologue_) prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
-  } else if (p_in_prologue_ && batch_in_prologue_) {
+  nloss_ = (int)(tok / 32);
+  {
     // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
-    // with the batch preparation (independent work, one graph node); as p_slabs_ split-K partial
-    // tables (no bias: the persistent forward's gather sums them and adds b_ih0) where that applies
+    // with the batch preparation (independent work, one graph node)
     GemmArgs g;
     g.A = Emb; g.lda = E; g.B = Ls_[0].Wih; g.ldb = E; g.C = Ptab_; g.ldc = H3;
     g.bias = P("bias_ih_l0"); g.M = V; g.N = H3; g.K = E;
-    if (p_slabs_ > 1) { g.splits = p_slabs_; g.bias = nullptr; }
     gemm_with_prep(g, PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_}, s);
-  } else if (p_in_prologue_) {   // the batch came from the previous step's fused tail
-    p_slabs_ = 1;                  // (one table with the bias)
-    record_p_gemm(s);
-  } else if (batch_in_prologue_) {   // P came from the previous step's fused tail
-    prep_batch(stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_, s);
-  }   // else the previous step's tail prepared both
+  }
   if (carry_) record_carry(s);
   // ------------------------------------------------------------------ forward
   auto fwd_args = [&](int l) {
@@ -197,19 +141,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
     a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
-    if (l == 0 && fwd_xp) {
-      a.xp = 1; a.Emb = Emb; a.Wih0 = Ls_[0].Wih; a.bih = P("bias_ih_l0"); a.E = E; a.V = V; a.ids = ids_;
-    } else if (l == 0 && fwd_pl) {
-      a.Emb = Emb; a.Wih0 = Ls_[0].Wih; a.bih = P("bias_ih_l0"); a.V = V; a.E = E; a.ids = ids_;
-      if (batch_in_prologue_) a.prep = PrepJob{stage_src_, Bp_, T, Bp_, ids_, labels_, inv_count_};
-    } else if (l == 0) {
-      a.P = Ptab_; a.ids = ids_;
-      if (p_slabs_ > 1) { a.p_slabs = p_slabs_; a.p_slab = (long)V * H3; a.bih = P("bias_ih_l0"); }
-    } else {
-      a.Gi = y.Gi;
-    }
+    if (l == 0) { a.P = Ptab_; a.ids = ids_; }
+    else a.Gi = y.Gi;
     a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
-    a.saves_in_drain = fwd_saves_in_drain() ? 1 : 0;
     if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
     a.T = T; a.Bp = B; a.H = H;
     if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
@@ -237,13 +171,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       w2.Wih = Ls_[l + 1].Wih; w2.bih = P("bias_ih_l" + std::to_string(l + 1));
       gru_fwd_seq2(w2, s);
       ++l;
-    } else if (persist_fwd_ && l == L - 1 && fwd_fc) {
-      // the top layer with the FC / softmax-xent / dH pipeline inside the launch
-      FwdFcArgs f;
-      f.Wfc = Wfc; f.WfcT = WfcT; f.bfc = P("fc.bias"); f.labels = labels_; f.inv_count = inv_count_;
-      f.xdl = dl_; f.xdlT = dlT_; f.xst = xst_; f.dy = Ls_[l].dy;
-      f.dW_part = slab_fc2_; f.db_part = rs_fc2_; f.loss_part = loss_part_; f.V = V;
-      gru_fwd_seq_fc(fwd_args(l), f, s);
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
     } else {
@@ -253,28 +180,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // ------------------------------------------------------------------ FC + loss + dH
   Layer& top = Ls_[L - 1];
   SlabJobs tail;   // reductions deferred to the last multi-tensor reduce (layer 0's)
-  // dH of the top layer inside its persistent backward kernel (dy = dl · W_fc on the MFMA pipe the
-  // recurrence leaves idle): fc_xent writes bf16 dl and skips the W_fc^T stream + fp32 dy store.
-  // Off by default: fc_xent 16.3 -> 11.4 us but the backward kernel +7..10 us at h512 (its step
-  // 2.6 -> 2.8 us, every phase a little longer; profiles/r2_bwd_dh_ab.jsonl).  GK_BWD_DH=1 turns it on.
-  static const bool bwd_dh_env = env_flag("GK_BWD_DH", false);
-  const bool bwd_dh = !fwd_fc && bwd_dh_env && seq_[L - 1].bwd && V == 256 && fc_xent_fused_ok(V, H, (int)tok);
-  if (fwd_fc) {
-    // logits, loss, dl and dH came out of the forward launch; dW_fc / db_fc as one partial per row
-    // block, summed with the other slabs
-    tail_nfc_ = 0;
-    tail.add(slab_fc2_, nrb, (long)V * H, G("fc.weight"));
-    tail.add(rs_fc2_, nrb, V, G("fc.bias"));
-    if (dp && ar_span() && seq_[L - 1].bwd && env_flag("GK_AR_FC_EARLY", false) && tail.n) {
-      SlabJobs fcj;
-      for (int k2 = 0; k2 < tail.n; ++k2)
-        slab_job(fcj, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
-      if (fcj.n) reduce_slabs_multi(fcj, s);
-      tail.n = 0;
-      ar_ready_ = group_end(L);
-      ar_flush(s, /*force=*/true);
-    }
-  } else {
+  {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
     f.labels = labels_; f.inv_count = inv_count_;
@@ -292,9 +198,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
       g.M = (int)tok; g.N = H; g.K = V;
       gemm_nt(g, s);
-    } else if (bwd_dh) {
-      f.dl = dl_; f.Wf = WfcF;
-      fc_xent(f, s);
     } else if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
       f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
@@ -319,45 +222,17 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     w.M = V; w.N = H; w.K = (int)tok; w.splits = sp;
     // one-shot small GEMM over 512-deep K-slices when that fits the slab budget: one memory
     // latency per workgroup and half the slabs of the 32-way 128 x 128 split
-    static const int kslice = [] {
-      const char* e = std::getenv("GK_FC_SMALL_K");
-      // 1024: 8 slabs, summed inside the Adam launch (0.2362 -> 0.2338 ms at h512,
-      // profiles/r1_fc_kslice_ab.jsonl; 512 measured equal to 128x128 split-K, r1_small_gemm_ab.jsonl)
-      return e ? std::atoi(e) : 1024;
-    }();
+    // 1024: 8 slabs, summed inside the Adam launch (0.2362 -> 0.2338 ms at h512,
+    // profiles/r1_fc_kslice_ab.jsonl; 512 measured equal to 128x128 split-K, r1_small_gemm_ab.jsonl)
+    constexpr int kslice = 1024;
     if (kslice > 0 && tok % kslice == 0 && tok / kslice <= kFcSplitsMax) {
       GemmArgs ws = w;
       ws.splits = (int)(tok / kslice); ws.algo = 3;
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
     }
-    // fused tail: the same K-slices as blocks of the tail launch (their last slice per tile runs that
-    // tile's Adam), so no launch here and no slab jobs
-    // (data-parallel: dW_fc is all-reduced with the other gradients, so it stays a GEMM here)
-    tail_nfc_ = (tail_fused_ && !dp && w.algo == 3 && (tok / sp) % 256 == 0 && env_flag("GK_TAIL_FC", true)) ? sp : 0;
-    if (!tail_nfc_) {
-      gemm_nt(w, s);
-      tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
-      tail.add(rs_fc2_, sp, V, G("fc.bias"));
-    }
-    // data-parallel: the FC group [W_fc, b_fc] is final here, before the whole backward sweep.  Its
-    // collective goes out now on the comm stream and stays open across the top layer's persistent
-    // backward kernel, whatever the bucket size: a collective that spans the
-    // longest kernel of the step costs nothing on the critical path.  (The sequence kernels bound
-    // their waits by wall clock, so an RCCL kernel holding CUs only delays them.)  GK_AR_FC_EARLY=0:
-    // the group rides with the top layer's.
-    //
-    // Off by default: ROCm's graph executor ran the forked collective BEFORE the backward kernel, not
-    // beside it, with 6-10 us of fork / join gaps (--rccl-self trace: 0.2292 -> 0.2517 ms per step,
-    // profiles/r3_rccl_self_fc_early.txt).
-    if (dp && ar_span() && seq_[L - 1].bwd && env_flag("GK_AR_FC_EARLY", false) && tail.n) {
-      SlabJobs fcj;
-      for (int k2 = 0; k2 < tail.n; ++k2)
-        slab_job(fcj, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
-      if (fcj.n) reduce_slabs_multi(fcj, s);
-      tail.n = 0;
-      ar_ready_ = group_end(L);
-      ar_flush(s, /*force=*/true);
-    }
+    gemm_nt(w, s);
+    tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
+    tail.add(rs_fc2_, sp, V, G("fc.bias"));
   }
   // ------------------------------------------------------------------ backward (BPTT)
   for (int l = L - 1; l >= 0; --l) {
@@ -366,8 +241,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     const std::string k = std::to_string(l);
     if (q.bwd) {
       SeqBwdArgs a;
-      a.dy = y.dy; a.sr = y.sr;
-      if (l == L - 1 && bwd_dh) { a.dy = nullptr; a.dl = dl_; a.WfcT = WfcT; } a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
       a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;
@@ -375,9 +249,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
-      a.fused_in_drain = bwd_fused_in_drain() ? 1 : 0;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
-      if (l == 0 && tail_fused_) a.bump = step_;   // step counter + tail epoch, read by the fused tail
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       gru_bwd_seq(a, s);
@@ -394,8 +266,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
       if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
-      else if (!tail_fused_) j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
-      // (fused tail: the dP tiles are the tail kernel's first items)
+      else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     }
     if (l == 0 && q.bwd) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
@@ -403,7 +274,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (dp ? l == L - 1 : l == 0)
       for (int k2 = 0; k2 < tail.n; ++k2)
         slab_job(j, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
-    if (l == 0 && !tail_fused_) {   // + the loss partials and the optimiser step counter
+    if (l == 0) {   // + the loss partials and the optimiser step counter
       j.add(loss_part_, nloss_, 1, loss_);
       j.bump = step_;
     }
@@ -426,8 +297,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       }
       if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
         ar_ready_ = group_end(0);
-        // collectives still open across the backward (the early FC group, upper layers' groups)
-        // end here; nothing is left to overlap with, so the last collectives go on the step
+        // collectives still open across the backward (upper layers' groups) end here; nothing is left to overlap with, so the last collectives go on the step
         // stream itself (a fork + join around them only adds graph edges -- measured: a forked
         // branch in the step graph slowed the kernels beside it).  The step's LAST collective
         // carries the error word along (max over ranks, same launch): a persistent kernel that
@@ -472,14 +342,15 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
   }
   // ------------------------------------------------------------------ embedding-side gradients
-  if (dp && !tail_fused_) {
+  if (dp) {
     // from the averaged dP; its dEmb slabs are already global (after the collective), so like the
     // single-GPU step they are summed inside the Adam launch (one reduce launch fewer)
-    defer_slabs_ = o_.clip <= 0.f && env_flag("GK_DEFER_SLABS", true);
+    defer_slabs_ = o_.clip <= 0.f;
     record_emb_tail(s, dP_target());
     defer_slabs_ = false;
-  }   // (fused tail: the dP tiles read the averaged dP, see Trainer::record_tail)
-  else if (!tail_fused_) record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
+  } else {
+    record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
+  }
   HIP_LAUNCH_CHECK();
 }
 
@@ -529,42 +400,8 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   HIP_LAUNCH_CHECK();
 }
 
-// layer 0 through the table-free persistent forward (no prologue P GEMM / batch kernel): read when a
-// step is recorded
-bool Trainer::fwd_pl_ok() const {
-  if (!persist_fwd_ || !p_in_prologue_ || (fwd_wave_ && d_.L >= 2)) return false;
-  if (!env_flag("GK_FWD_PL", false)) return false;
-  return gru_fwd_seq_pl_supported(d_.H, Bp_, d_.V, d_.E, d_.T);
-}
-
-// layer 0's input projection inside the persistent forward (GK_FWD_XP=1, opt-in): one forward launch
-// for layer 0, the row-split H = 512 kernel, E = H.  Measured slower: the per-step Emb rows (32 KB per
-// workgroup) and 12 MFMAs per wave in the post-publish slack are not hidden by the flag propagation
-// (forward 60.6 -> 88.4 us); the prologue it removes is mostly the batch's pinned-memory read
-// (prep_batch alone 5.2-5.6 us), so the step goes 0.214-0.220 -> 0.240-0.242 ms
-// (profiles/r3s5_fwd_xp_ab.jsonl)
-bool Trainer::fwd_xp_ok() const {
-  if (!persist_fwd_ || !p_in_prologue_ || (fwd_wave_ && d_.L >= 2)) return false;
-  if (!env_flag("GK_FWD_XP", false)) return false;
-  return gru_fwd_seq_xp_supported(d_.H, Bp_, d_.E);
-}
-
-// the top layer's forward carries the FC pipeline (GK_FWD_FC=1, opt-in): one layer, H = 512, V = 256.
-// Measured: the tail loses its dW_fc items (42.8 -> 29.9 us) and fc_xent goes away (15.5 us), but the
-// pipeline's dl row-block loads (+32 KB per workgroup per step on top of the 32 KB h exchange) slow the
-// latency-bound recurrence from 1.84 to 3.6-3.7 us per step (forward 69 -> 132 us): 0.217 -> 0.261
-// ms/step (profiles/r3s5_fwd_fc_ab.jsonl)
-bool Trainer::fwd_fc_ok() const {
-  if (!persist_fwd_ || d_.L != 1 || !xst_ || !seq_[0].bwd) return false;
-  if (!env_flag("GK_FWD_FC", false)) return false;
-  return gru_fwd_seq_fc_supported(d_.H, Bp_, d_.V);
-}
-
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") + (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
-  if (fwd_pl_ok()) p += "+pl";
-  else if (fwd_fc_ok()) p += "+fc";
-  else if (fwd_xp_ok()) p += "+xp";
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

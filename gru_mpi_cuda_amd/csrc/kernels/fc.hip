@@ -663,8 +663,7 @@ bool fc_xent_fused_ok(int V, int H, int M) { return V == 256 && (H == 512 || H =
 // the 8-wave V = 256 kernel: fused dH (dy + W_fc^T FT copy, no row-major dl), or dl only (no dy)
 static bool fc_xent_v256_ok(const FcXentArgs& a) {
   const bool dh = a.dy && a.WTf && !a.dl, dl_only = !a.dy && a.dl;
-  return a.V == 256 && a.Wf && (dh || dl_only) && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0 &&
-         !(std::getenv("GK_FC_V1") && std::getenv("GK_FC_V1")[0] == '1');
+  return a.V == 256 && a.Wf && (dh || dl_only) && (a.H == 512 || a.H == 1024) && a.M % FROWS == 0;
 }
 
 void fc_xent(const FcXentArgs& a, hipStream_t s) {

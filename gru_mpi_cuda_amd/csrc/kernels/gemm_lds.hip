@@ -43,7 +43,7 @@ DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u1
   // the shorter tile dimension is the fast block index, so the workgroups sharing the long
   // operand's panel are neighbours on one XCD and stream it through its L2 together (one-hot dP at
   // h2048, 2 x 48 tiles: B is the only operand in memory, and column-fast order read it once per
-  // row tile from HBM: 380 -> 341 us).  a.raster: 0 auto, 1 column-fast (GK_GEMM_RASTER=1)
+  // row tile from HBM: 380 -> 341 us).  a.raster: 0 auto, 1 column-fast (GemmArgs::raster)
   const bool mfast = OH ? a.raster != 1 : (a.raster == 0 && ntm < ntn);
   const int tn = mfast ? (id / ntm) % ntn : id % ntn;
   const int tm = mfast ? id % ntm : (id / ntn) % ntm;
@@ -263,12 +263,7 @@ void gemm_lds_group(const GemmArgs* jobs, int n, hipStream_t s) {
 }
 
 void gemm_lds(const GemmArgs& a0, hipStream_t s) {
-  static const int raster = [] {
-    const char* e = std::getenv("GK_GEMM_RASTER");
-    return e ? std::atoi(e) : 0;
-  }();
-  GemmArgs a = a0;
-  if (!a.raster) a.raster = raster;
+  const GemmArgs& a = a0;
   const int ntn = a.N / 128, ntm = a.M / 128, kper = a.K / a.splits;
   dim3 grid(ntn * ntm * a.splits), block(256);
   if (a.onehot_ids) {

@@ -159,8 +159,7 @@ void gemm_f32_nt(const GemmF32Args& g, hipStream_t s) {
   if (g.M % kT || g.N % kT || g.splits < 1 || g.K % g.splits || (g.K / g.splits) % kBK || g.lda % 4 || g.ldb % 4 ||
       (g.splits > 1 && g.slab < (long)g.M * g.ldc))
     throw std::runtime_error("gemm_f32_nt: needs M, N % 64 == 0, (K / splits) % 16 == 0 and 16-B aligned rows");
-  static const bool big_ok = [] { const char* e = std::getenv("GK_F32_GEMM128"); return !e || e[0] != '0'; }();
-  if (big_ok && g.splits == 1 && g.M % kT2 == 0 && g.N % kT2 == 0 && (g.M / kT2) * (g.N / kT2) >= 256) {
+  if (g.splits == 1 && g.M % kT2 == 0 && g.N % kT2 == 0 && (g.M / kT2) * (g.N / kT2) >= 256) {
     hipLaunchKernelGGL(gemm_f32_nt128_kernel, dim3(g.N / kT2, g.M / kT2), dim3(256), 0, s, g);
     return;
   }

@@ -265,35 +265,12 @@ DEV void signal_flag_local(unsigned* flag, unsigned epoch) {
 // RS = 2: waves 0-3 own row tile 0, waves 4-7 row tile 1, each over a K/4 slice (NKW = H/128):
 //         the same MFMAs and exchange loads per wave, half the LDS partial traffic (4 partials of
 //         3 gates per output instead of 8, read by the epilogue thread of the same row tile).
-//
-// PL = true (SeqFwdArgs::Emb, layer 0 without a P table): the launch also does what the step's
-// prologue kernel did.  Each workgroup
-//   * computes the 48 columns of P = Emb · W_ih0^T + b_ih0 it gathers from (3 gates x its 16 units,
-//     all V rows) into LDS: the W_ih0 slice staged once (XOR-swizzled 16-B pieces), wave w takes row
-//     tiles w and w + 8 of Emb straight into registers, 16x16x32 MFMAs over k-steps of 32 in
-//     increasing order + the bias after -- gemm_small's sequence, so bitwise the prologue's table;
-//   * transposes its share of the batch (rows 32 rb + ut + k H/16) from the pinned staging slot into
-//     ids / labels (agent-scope stores), its round trip issued after the product's operand loads so
-//     the product's waits do not include it (vmcnt retires in order);
-//   * then joins its row block's start-up exchange (row_block_local), which now also publishes those
-//     ids: the step loop's id loads follow it (plain loads when the row block shares one L2, agent-scope
-//     loads otherwise).
-// The per-step gather then reads the table from LDS.  Measured slower than the prologue's table
-// (off by default, GK_FWD_PL=1): the 8 row blocks of a unit tile redo the same columns, so the chip
-// streams 78 MB of Emb / W_ih0 through L2 and runs 8x the table's MFMAs -- 10-17 us before the
-// first step, against the 7 us prologue kernel (profiles/r3s5_fwd_pl_ab.jsonl).
-//
-// XP = true (SeqFwdArgs::xp, layer 0, RS = 2, E = H): no P table either, and no per-WG table --
-// the input projection of step t+1 (the 32 rows' Emb rows x this workgroup's W_ih0 slice, the same
-// K-split over the waves as the recurrent product) runs in the slack after step t's publish, into the
-// free partial sets 3-5; its Emb rows were loaded one step earlier still, and their ids one step
-// before that.  The step's prologue kernel is left with the batch preparation only.  Measured slower
-// (opt-in, GK_FWD_XP=1): the slack work is not hidden, +0.87 us per step (profiles/r3s5_fwd_xp_ab.jsonl).
-template <int NKW, int RS, bool PL, bool XP = false>
+// (Rejected and removed in round 4, history in docs/DESIGN.md §6.3: a table-free layer 0 computing
+// its P-table columns in every workgroup, layer 0's input projection in the post-publish slack, the
+// FC / softmax-xent pipeline inside the forward, and the saves issued inside the publish drain.)
+template <int NKW, int RS>
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
-  static_assert(!XP || (RS == 2 && !PL), "XP: row-split forward, table-free mode excluded");
   __shared__ __attribute__((aligned(16))) float part[8][6][256];
-  __shared__ __attribute__((aligned(16))) float Pl[PL ? 256 : 1][PL ? 48 : 1];   // [V][gate * 16 + unit]
   // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
   // u16 writes -- rows 4 apart within a wave -- land in distinct banks (unpadded: 2-way / 4-way)
   __shared__ __attribute__((aligned(16))) u16 stg[32][24];
@@ -309,13 +286,10 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const unsigned nunit = (unsigned)(H / 16);
 
   bf16x8 bw[NKW][3];   // this wave's K-slice of W_h{r,z,n} for the 16 units, resident all sequence
-  auto load_bw = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < NKW; ++kk)
+  for (int kk = 0; kk < NKW; ++kk)
 #pragma unroll
-      for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
-  };
-  if constexpr (!PL) load_bw();   // (PL: after the table product, which needs the registers)
+    for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
 
   // this thread's epilogue item (row, unit) -- one per thread with 512 threads
   const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
@@ -334,174 +308,19 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const unsigned sv_lane = (unsigned)((b * H + j) * 4);
   stamp(a.dbg, T + 1, 0);   // prologue stamps in the (unused) step slot T + 1
   zero_next_flags(a.zero_next, a.zero_words);
-  if constexpr (PL) {
-    const int E = a.E, V = a.V, npe = E >> 3;          // 16-B pieces per row
-    // W_ih0 slice [48][E]: row rr = gate rr/16, unit j0 + rr%16; piece p at (p ^ (rr & 7)) (B-fragment
-    // reads 2-way instead of 16-way bank conflicts).  Aliases the partials: unused until the loop.
-    u16* Ws = reinterpret_cast<u16*>(&part[0][0][0]);
-    uint4 wv[6];
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-      const int q = tid + e * 512;
-      if (q < 48 * npe) {
-        const int rr = q / npe, p = q - rr * npe;
-        wv[e] = *reinterpret_cast<const uint4*>(a.Wih0 + (size_t)((rr >> 4) * H + j0 + (rr & 15)) * E + p * 8);
-      }
-    }
-    const int nrt = V >> 7;   // Emb row tiles of this wave: w and w + 8
-    bf16x8 ae[2][16];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks)
-        if (r < nrt && ks < (E >> 5)) ae[r][ks] = ld8(a.Emb + (size_t)((w + 8 * r) * 16 + lr) * E + ks * 32 + lk);
-    __builtin_amdgcn_sched_barrier(0);
-    // this workgroup's batch share (pinned host memory, one round trip), issued after the operands
-    const PrepJob& pj = a.prep;
-    const int nr = (32 - ut + (int)nunit - 1) / (int)nunit;   // rows ut + k * nunit < 32
-    int xr[2] = {0, 0}, yr[2] = {0, 0}, bn = 0;
-    if (pj.in) {
-      const int* xs = pj.in + 16;
-      const int* ys = xs + (size_t)pj.Bmax * T;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int q = tid + e * 512;
-        if (q < nr * T) {
-          const int k = q / T, tt = q - k * T;
-          const size_t i = (size_t)(b0 + ut + k * (int)nunit) * T + tt;
-          xr[e] = xs[i];
-          yr[e] = ys[i];
-        }
-      }
-      bn = pj.in[0];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int e = 0; e < 6; ++e) {
-      const int q = tid + e * 512;
-      if (q < 48 * npe) {
-        const int rr = q / npe, p = q - rr * npe;
-        *reinterpret_cast<uint4*>(Ws + (size_t)rr * E + ((p ^ (rr & 7)) << 3)) = wv[e];
-      }
-    }
-    __syncthreads();
-    stamp(a.dbg, T + 1, 1);
-    f32x4 pacc[2][3];
-    zero_acc(pacc);
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      if (ks < (E >> 5)) {
-        bf16x8 bq[3];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int rr = g * 16 + lr, p = ks * 4 + (lk >> 3);
-          bq[g] = *reinterpret_cast<const bf16x8*>(Ws + (size_t)rr * E + ((p ^ (rr & 7)) << 3));
-        }
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-          if (r < nrt)
-#pragma unroll
-            for (int g = 0; g < 3; ++g) pacc[r][g] = mfma16(ae[r][ks], bq[g], pacc[r][g]);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-      const float bb = a.bih[g * H + j0 + lr];
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-        if (r < nrt)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) Pl[(w + 8 * r) * 16 + (lane >> 4) * 4 + i][g * 16 + lr] = pacc[r][g][i] + bb;
-    }
-    stamp(a.dbg, T + 1, 2);
-    if (pj.in) {   // the batch share, stored write-through; drained before the start-up exchange below
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int q = tid + e * 512;
-        if (q < nr * T) {
-          const int k = q / T, tt = q - k * T, bb = b0 + ut + k * (int)nunit;
-          const bool ok = bb < bn;
-          __hip_atomic_store(pj.ids + (size_t)tt * Bp + bb, ok ? xr[e] : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(pj.labels + (size_t)tt * Bp + bb, ok ? yr[e] : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      if (blockIdx.x == 0 && tid == 0) pj.inv_count[0] = __int_as_float(pj.in[1]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();   // every wave's stores drained (and Ws read) before the exchange's first store
-    stamp(a.dbg, T + 1, 3);
-    load_bw();
-  }
-  // PL: the exchange runs whatever allow_local says (it also publishes the batch share)
-  const bool rbl = (PL || a.allow_local) && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
-  const bool loc = a.allow_local && rbl;
+  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   stamp(a.dbg, T + 1, 4);
 
   // the input projection of step t, gathered one step ahead, after the publish (its latency off
   // the critical path; issued before wave 0's drain it would be part of it: vmcnt retires in order).
   // The char id it needs is loaded one step earlier still, so the gather never waits on an id load.
-  // (PL: ids written in this launch -- agent-scope loads unless the row block shares one L2)
-  auto load_id = [&](size_t o) -> int {
-    if constexpr (PL) {
-      if (!loc) return __hip_atomic_load(a.ids + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return a.ids[o];
-  };
-  int idn = a.ids ? load_id(b) : 0;   // id of the step whose row load_gi gathers next
-  float bi[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it (or XP)
-  if (a.ids && (a.p_slabs > 1 || XP))
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
-  // XP: W_ih0 K-slice (B operand), the Emb fragments of the next input product and their row's id
-  bf16x8 wi[XP ? NKW : 1][3], en[XP ? NKW : 1];
-  int idA = 0;
-  const int bA = b0 + rt * 16 + lr;   // the A-operand row of this lane
-  auto load_emb = [&](int id) {
-#pragma unroll
-    for (int kk = 0; kk < NKW; ++kk) en[kk] = ld8(a.Emb + (size_t)id * H + k0 + kk * 32 + lk);
-  };
-  auto input_product = [&]() {   // the Emb fragments in en x W_ih0 -> partial sets 3..5
-    f32x4 ai[3];
-    ai[0] = ai[1] = ai[2] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < NKW; ++kk)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) ai[g] = mfma16(en[kk], wi[kk][g], ai[g]);
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) part[w][3 + g][i * 64 + lane] = ai[g][i];
-  };
-  if constexpr (XP) {
-#pragma unroll
-    for (int kk = 0; kk < NKW; ++kk)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) wi[kk][g] = ld8(a.Wih0 + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
-    load_emb(a.ids[bA]);
-    input_product();                                  // step 0's, read by its epilogue
-    if (T > 1) load_emb(a.ids[(size_t)Bp + bA]);      // step 1's rows
-    if (T > 2) idA = a.ids[(size_t)2 * Bp + bA];      // step 2's id
-  }
+  int idn = a.ids ? a.ids[b] : 0;   // id of the step whose row load_gi gathers next
   auto load_gi = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
-    if constexpr (XP) return;
-    if constexpr (PL) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] = Pl[idn][g * 16 + col];
-      if (t + 1 < T) idn = load_id((size_t)(t + 1) * Bp + b);
-      return;
-    }
     const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
-    if (a.ids && a.p_slabs > 1) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] += bi[g];
-      for (int q = 1; q < a.p_slabs; ++q)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * a.p_slab + g * H + j];
-    }
-    if (a.ids && t + 1 < T) idn = load_id((size_t)(t + 1) * Bp + b);
+    if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};
   load_gi(0, gin);
@@ -560,19 +379,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       }
       gh[g] = s + bh[g];
     }
-    float gx[3] = {gi[0], gi[1], gi[2]};
-    if constexpr (XP) {   // this step's input projection from the partials written after the last publish
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        float s = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < 4; ++ww) s += part[rb * 4 + ww][3 + g][reg * 64 + ln];
-        gx[g] = s + bi[g];
-      }
-    }
-    const float r = sigmoidf_(gx[0] + gh[0]);
-    const float z = sigmoidf_(gx[1] + gh[1]);
-    const float n = tanhf_(gx[2] + r * gh[2]);
+    const float r = sigmoidf_(gi[0] + gh[0]);
+    const float z = sigmoidf_(gi[1] + gh[1]);
+    const float n = tanhf_(gi[2] + r * gh[2]);
     const float h = n + z * (hp - n);
     hp = h;
     const u16 hb = f2bf(h);
@@ -580,22 +389,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     stgT[col][row] = hb;
     __syncthreads();
     stamp(a.dbg, t, 3);
-    const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
-    auto saves = [&]() {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
-      if (a.sr) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
-      }
-    };
-    const bool sid = a.saves_in_drain != 0;
     if (w == 0) {
       // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
-      // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.  (saves_in_drain:
-      // this wave's saves go out first and drain with the tile instead of after the signal)
-      if (sid) saves();
+      // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
       const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
       unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
@@ -623,352 +419,15 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     // scalar offset -- with 64-bit VGPR address math the compiler reused the in-flight gather's
     // destination as a temporary and waited for it (+0.3 us per step at H = 512).
     load_gi(t + 1, gin);
-    if constexpr (XP) {   // step t+1's input product (rows loaded last step), then step t+2's rows
-      if (t + 1 < T) input_product();
-      if (t + 2 < T) load_emb(idA);
-      if (t + 3 < T) idA = a.ids[(size_t)(t + 3) * Bp + bA];
-    }
-    if (!(w == 0 && sid)) saves();
-    stamp(a.dbg, t, 6);
-  }
-}
-
-// ==================================================================== forward + FC / softmax-xent / dH
-// The top layer's output h(t) feeds logits = h W_fc^T + b_fc, a softmax cross-entropy and dH =
-// dl W_fc (and dW_fc = dl^T h).  As a kernel of its own (fc_xent, 15.5 us at the headline) every
-// 32-row block streams all of W_fc twice, and the tail's dW_fc product re-reads dl and h (64 MB);
-// here the same work rides along the recurrence on operands the persistent workgroups already hold,
-// as a pipeline that runs five steps behind it:
-//   step t     S1: the 16 workgroups ut < 16 of a row block own logits columns 16 ut .. +15; their
-//                  waves multiply the h(t-1) K-slice fragments they loaded for the gates by a resident
-//                  W_fc slice (K-partials to LDS, double-buffered);
-//              after the publish (the slack before the next poll): the logits, each row's local max
-//                  and sum-exp over the 16 columns (DPP);
-//   step t+1   those statistics go out with the h tile (same drain, same flag);
-//   step t+2   the 16 producers' statistics of each row arrive with the exchange fragments (LDS-DMA);
-//              after the publish: dl = (softmax - onehot) / count, the loss and db_fc per thread;
-//   step t+3   the bf16 dl tile (row-major and transposed) goes out with the h tile;
-//   step t+4   every workgroup loads the dl row block as MFMA fragments (V k-steps assigned to the waves
-//              that already poll those producers): dH = dl W_fc for its 16 units (K-partials in LDS,
-//              stored fp32 for the backward) and, after the publish, dW_fc[:, its units] += dl^T h
-//              from a ring of its transposed h tiles -- per row block partials, summed by the
-//              optimiser's slab sums.
-// Five drain iterations after the last step finish it (flags advance in each).  No fc_xent launch,
-// no dW_fc product in the tail.  H = 512 (RS = 2: waves 0-3 row tile 0, 4-7 row tile 1), V = 256.
-template <int NKW>
-__global__ void __launch_bounds__(512, 1) gru_fwd_seq_fc_kernel(SeqFwdArgs a, FwdFcArgs f) {
-  constexpr int NKV = NKW / 2;   // V k-steps (32 logits each) per dH wave
-  constexpr int V = 256;
-  constexpr int DEP = 5;         // pipeline depth: dH of step t - 5 at step t
-  __shared__ __attribute__((aligned(16))) float part[8][6][256];   // gates r,z,n | - | dH row tile 0, 1
-  __shared__ __attribute__((aligned(16))) float lgp[2][8][256];    // logits K-partials (step parity)
-  __shared__ __attribute__((aligned(16))) u16 stg[32][24];
-  __shared__ __attribute__((aligned(16))) u16 stgT[8][16][40];     // ring of h(t)^T: dW_fc's B operand at t + 5
-  __shared__ __attribute__((aligned(16))) float stl[2][16][64];    // producers' (max, sum-exp) per row
-  __shared__ __attribute__((aligned(16))) float sst[2][64];        // this workgroup's, to publish
-  __shared__ __attribute__((aligned(16))) u16 sdl[2][32][24];      // dl tile row-major, to publish
-  __shared__ __attribute__((aligned(16))) u16 sdlT[2][16][40];     // dl tile transposed, to publish
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int H = a.H, Bp = a.Bp, T = a.T;
-  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
-  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
-  const int lr = lane & 15, lk = 8 * (lane >> 4);
-  const int rt = w >> 2;                       // this wave's row tile
-  const int k0 = (w & 3) * NKW * 32;           // and K-slice
-  const unsigned nunit = (unsigned)(H / 16);
-  const bool fcw = ut < 16;                    // owns logits columns 16 ut .. +15
-  // dH k-steps of this wave: kvb .. kvb + NKV - 1 (producers 2 kv, 2 kv + 1 are among the ones it polls)
-  const int kvb = (k0 >> 5) + rt * NKV;
-  const bool s4w = kvb < 8;
-
-  bf16x8 bw[NKW][3];
-#pragma unroll
-  for (int kk = 0; kk < NKW; ++kk)
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bw[kk][g] = ld8(a.Whh + (size_t)(g * H + j0 + lr) * H + k0 + kk * 32 + lk);
-  // the FC operands stay resident lane-linear in LDS (each lane re-reads only its own 16-B slots:
-  // conflict-free, no barrier) -- in VGPRs they pushed the register file into spills
-  __shared__ __attribute__((aligned(16))) bf16x8 wfL[NKW][512];   // W_fc rows 16 ut + lr, this wave's K-slice
-  __shared__ __attribute__((aligned(16))) bf16x8 wfTL[NKV][512];  // W_fc^T rows j0 + lr, this wave's V k-steps
-#pragma unroll
-  for (int kk = 0; kk < NKW; ++kk) wfL[kk][tid] = fcw ? ld8(f.Wfc + (size_t)(16 * ut + lr) * H + k0 + kk * 32 + lk) : zero8();
-#pragma unroll
-  for (int q = 0; q < NKV; ++q) wfTL[q][tid] = s4w ? ld8(f.WfcT + (size_t)(j0 + lr) * V + (kvb + q) * 32 + lk) : zero8();
-
-  const int rb = tid >> 8, reg = (tid >> 6) & 3, ln = tid & 63;
-  const int row = rb * 16 + (ln >> 4) * 4 + reg, col = ln & 15;
-  const int b = b0 + row, j = j0 + col;
-  float bh[3];
-#pragma unroll
-  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + j];
-  const float bfc = fcw ? f.bfc[16 * ut + col] : 0.f;
-  const float inv = f.inv_count[0];
-  float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
-  const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
-  const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
-  const unsigned fcb = (unsigned)((size_t)T * nrb * 16 * 1024);   // bytes of xdl / xdlT
-  const rsrc_t rD = make_rsrc(f.xdl, fcb), rDT = make_rsrc(f.xdlT, fcb);
-  const rsrc_t rS = make_rsrc(f.xst, (unsigned)((size_t)T * nrb * 16 * 256));
-  const unsigned sv_bytes = (unsigned)((size_t)T * Bp * H * 4);
-  const rsrc_t rHSf = make_rsrc(a.HSf, sv_bytes + (unsigned)(Bp * H * 4));
-  const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
-  const rsrc_t rSn = make_rsrc(a.sn, a.sn ? sv_bytes : 0u), rSg = make_rsrc(a.sghn, a.sghn ? sv_bytes : 0u);
-  const rsrc_t rDy = make_rsrc(f.dy, sv_bytes);
-  const unsigned sv_lane = (unsigned)((b * H + j) * 4);
-  zero_next_flags(a.zero_next, a.zero_words);
-  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
-
-  int idn = a.ids ? a.ids[b] : 0;
-  float bi[3] = {0.f, 0.f, 0.f};
-  if (a.ids && a.p_slabs > 1)
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bi[g] = a.bih[g * H + j];
-  auto load_gi = [&](int t, float (&gi)[3]) {
-    if (t >= T) return;
-    const float* src = a.ids ? a.P + (size_t)idn * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
-#pragma unroll
-    for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
-    if (a.ids && a.p_slabs > 1) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] += bi[g];
-      for (int q = 1; q < a.p_slabs; ++q)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * a.p_slab + g * H + j];
-    }
-    if (a.ids && t + 1 < T) idn = a.ids[(size_t)(t + 1) * Bp + b];
-  };
-  float gin[3] = {0.f, 0.f, 0.f};
-  load_gi(0, gin);
-  float lg0 = 0.f, lg1 = 0.f;        // logits of the last two S1 sums (lg1 = the one S3 uses)
-  float nll = 0.f, dbs = 0.f;        // loss and db_fc accumulators
-  int ylab = -1;                     // label of the step S3 handles next
-  f32x4 accF[NKV][2];                // dW_fc tiles (v tile 2 kv + pp) x (16 units)
-  zero_acc(accF);
-  for (int t = 0; t < T + DEP; ++t) {
-    stamp(a.dbg, t, 0);
-    const bool rec = t < T;                                  // the recurrence
-    const bool s1 = fcw && t >= 1 && t <= T;                 // logits of h(t-1)
-    const bool st3 = fcw && t >= 3 && t <= T + 2;            // statistics of step t-3 arrive; dl(t-3)
-    const bool s4 = t >= DEP;                                // dH (+ dW_fc) of step t-5
-    const int par = t & 1;
-    const float gi[3] = {gin[0], gin[1], gin[2]};
-    f32x4 acc[3], accL, accD[2];
-    accL = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[0] = acc[1] = acc[2] = accL;
-    accD[0] = accD[1] = accL;
-    bf16x8 af[NKW];
-    bf16x8 dlf[NKV][2], dltf[NKV][2];
-    if (t > 0) {
-      const size_t slot = ((size_t)(t - 1) * nrb + rbk) * nunit;
-      const size_t sd = ((size_t)(s4 ? t - DEP : 0) * nrb + rbk) * 16;   // dl of step t-5
-      const size_t ss = ((size_t)(t >= 3 ? t - 3 : 0) * nrb + rbk) * 16;  // statistics of step t-3
-      wave_wait_load<NKW>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
-                          (unsigned)t, a.err, [&](int kk) {
-        const int u = k0 + kk * 32 + lk;
-        if (t <= T) {
-          const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
-          af[kk] = ld8_sc1(rX, tb + (unsigned)(rt * 16 * 16 * 2));
-        }
-        const int p0 = k0 / 16 + 2 * kk;   // the two producers of this k-step
-        // their row statistics straight into LDS (lanes 0-31, 16 B each; no registers)
-        if (w < 4 && p0 < 16 && st3 && lane < 32)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void*)(&stl[par][p0][0]), 16,
-                                                   (unsigned)(lane * 16), (int)((ss + p0) * 256), 0, 16);
-        const int q = kk & (NKV - 1);   // compile-time slot (kk is unrolled); this wave's k-steps: kk / NKV == rt
-        if (s4 && s4w && kk / NKV == rt) {
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-            dlf[q][r] = ld8_sc1(rD, (unsigned)(((sd + u / 16) * 32 + r * 16 + lr) * 16 + (u & 15)) * 2);
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp)
-            dltf[q][pp] = ld8_sc1(rDT, (unsigned)(((sd + p0 + pp) * 16 + lr) * 32 + lk) * 2);
-        }
-      });
-    } else if (a.h0) {
-      const unsigned base = (unsigned)((((size_t)b0 + rt * 16 + lr) * H + k0 + lk) * 2);
-#pragma unroll
-      for (int kk = 0; kk < NKW; ++kk) af[kk] = ld8_sc1(rH, base + (unsigned)(kk * 64));
-    }
-    stamp(a.dbg, t, 1);
-    if (rec && (t > 0 || a.h0)) {
-#pragma unroll
-      for (int kk = 0; kk < NKW; ++kk)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) acc[g] = mfma16(af[kk], bw[kk][g], acc[g]);
-    }
-    if (s4 && s4w) {
-#pragma unroll
-      for (int q = 0; q < NKV; ++q)
-#pragma unroll
-        for (int r = 0; r < 2; ++r) accD[r] = mfma16(dlf[q][r], wfTL[q][tid], accD[r]);
-    }
-#pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) part[w][g][i * 64 + lane] = acc[g][i];
-    if (s4 && s4w)
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) part[w][4 + r][i * 64 + lane] = accD[r][i];
-    if (s1) {   // logits K-partials: consumed after the publish
-#pragma unroll
-      for (int kk = 0; kk < NKW; ++kk) accL = mfma16(af[kk], wfL[kk][tid], accL);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) lgp[par][w][i * 64 + lane] = accL[i];
-    }
-    if (w < 4 && st3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the statistics' LDS-DMA landed
-    __syncthreads();
-    stamp(a.dbg, t, 2);
-    float h = 0.f, r = 0.f, z = 0.f, n = 0.f, ghn = 0.f;
-    if (rec) {
-      float gh[3];
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        float sum = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < 4; ++ww) sum += part[rb * 4 + ww][g][reg * 64 + ln];
-        gh[g] = sum + bh[g];
-      }
-      r = sigmoidf_(gi[0] + gh[0]);
-      z = sigmoidf_(gi[1] + gh[1]);
-      n = tanhf_(gi[2] + r * gh[2]);
-      ghn = gh[2];
-      h = n + z * (hp - n);
-      hp = h;
-      const u16 hb = f2bf(h);
-      stg[row][col] = hb;
-      stgT[t & 7][col][row] = hb;
-    }
-    float dh = 0.f;   // dH of step t-5 for this thread's (row, unit); stored after the publish
-    if (s4) {
-#pragma unroll
-      for (int ww = 0; ww < 8; ++ww)
-        if ((((ww & 3) * NKW) + (ww >> 2) * NKV) < 8) dh += part[ww][4 + rb][reg * 64 + ln];
-    }
-    __syncthreads();
-    stamp(a.dbg, t, 3);
-    if (w == 0 && t <= T + DEP - 2) {
-      // publish: h tile (t < T), the row statistics of step t-2 and the dl tiles of step t-4 (both
-      // computed after the previous publish), one drain, one signal
-      const bool pst = fcw && t >= 2 && t <= T + 1, pdl = fcw && t >= 4 && t <= T + 3;
-      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
-      u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (rec) v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
-      const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
-      const unsigned so = (unsigned)((((size_t)(t - 2) * nrb + rbk) * 16 + ut) * 64 + lane * 4) * 4;
-      const unsigned dofs = (unsigned)((((size_t)(t - 4) * nrb + rbk) * 16 + ut) * 512 + lane * 8) * 2;
-      const int pq = par ^ 1;
-      if (loc) {
-        if (rec) st16_plain(rX, xo, v);
-        if (pst && lane < 16) st16_plain(rS, so, *reinterpret_cast<const u32x4*>(&sst[pq][lane * 4]));
-        if (pdl) {
-          st16_plain(rD, dofs, *reinterpret_cast<const u32x4*>(&sdl[pq][lane >> 1][(lane & 1) * 8]));
-          st16_plain(rDT, dofs, *reinterpret_cast<const u32x4*>(&sdlT[pq][lane >> 2][(lane & 3) * 8]));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) signal_flag_local(fl, (unsigned)(t + 1));
-      } else {
-        if (rec) st16_sc1(rX, xo, v);
-        if (pst && lane < 16) st16_sc1(rS, so, *reinterpret_cast<const u32x4*>(&sst[pq][lane * 4]));
-        if (pdl) {
-          st16_sc1(rD, dofs, *reinterpret_cast<const u32x4*>(&sdl[pq][lane >> 1][(lane & 1) * 8]));
-          st16_sc1(rDT, dofs, *reinterpret_cast<const u32x4*>(&sdlT[pq][lane >> 2][(lane & 3) * 8]));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) signal_flag(fl, (unsigned)(t + 1));
-      }
-      stamp(a.dbg, t, 4);
-      if (rec)
-        *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
-      stamp(a.dbg, t, 5);
-    } else if (w == 1 && a.HT && rec) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[t & 7][lane >> 2][(lane & 3) * 8]);
-      *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
-    } else if (w == 2 && a.HF && rec) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[t & 7][lane & 15][8 * (lane >> 4)]);
-      *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
-    }
-    // ---- after the publish (the slack before the next poll)
-    if (rec) {
-      load_gi(t + 1, gin);
-      const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
-      if (a.sr) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ghn), rSg, sv_lane, sstep, 0);
-      }
-    }
-    if (s4) {
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dh), rDy, sv_lane,
-                                            __builtin_amdgcn_readfirstlane((t - DEP) * Bp * H * 4), 0);
-      if (s4w) {   // dW_fc[:, units] += dl(t-5)^T h(t-5) (B: the transposed h tile of step t-5, in the ring)
-        const bf16x8 hb = *reinterpret_cast<const bf16x8*>(&stgT[(t - DEP) & 7][lr][lk]);
-#pragma unroll
-        for (int q = 0; q < NKV; ++q)
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) accF[q][pp] = mfma16(dltf[q][pp], hb, accF[q][pp]);
-      }
-    }
-    if (fcw) {
-      if (st3) {   // dl of step t-3 from its logit (lg1) and the 16 producers' statistics of the row:
-                   // the row's 16 threads take one producer each and combine over DPP
-        const float mp = stl[par][col][row * 2], sp = stl[par][col][row * 2 + 1];
-        const float M = max16(mp);
-        const float S = sum16(sp * __expf(mp - M));
-        const int v = 16 * ut + col;
-        const float scale = ylab >= 0 ? inv : 0.f;
-        const float d = (__expf(lg1 - M) * __builtin_amdgcn_rcpf(S) - (v == ylab ? 1.f : 0.f)) * scale;
-        if (v == ylab) nll += (__logf(S) + M - lg1) * scale;
-        dbs += d;
-        const u16 db = f2bf(d);
-        sdl[par][row][col] = db;
-        sdlT[par][col][row] = db;
-      }
-      float lg = 0.f;
-      if (s1) {   // logits of h(t-1): this row's 16 columns, their max and sum-exp (DPP over the row's lanes)
-        lg = bfc;
-#pragma unroll
-        for (int ww = 0; ww < 4; ++ww) lg += lgp[par][rb * 4 + ww][reg * 64 + ln];
-        const float m = max16(lg);
-        const float se = sum16(__expf(lg - m));
-        if (col == 0) { sst[par][row * 2] = m; sst[par][row * 2 + 1] = se; }
-      }
-      lg1 = lg0;
-      lg0 = lg;
-      // the label S3 needs at the next step (step t-2's), one step ahead
-      if (t + 1 >= 3 && t + 1 <= T + 2) ylab = f.labels[(size_t)(t - 2) * Bp + b];
+    const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
+    if (a.sr) {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
     }
     stamp(a.dbg, t, 6);
-  }
-  // ---- per-row-block partials: dW_fc (dH waves), db_fc and the loss (logits workgroups)
-  if (s4w) {
-    float* W = f.dW_part + (size_t)rbk * V * H;
-#pragma unroll
-    for (int q = 0; q < NKV; ++q)
-#pragma unroll
-      for (int pp = 0; pp < 2; ++pp)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          W[(size_t)(16 * (2 * (kvb + q) + pp) + (lane >> 4) * 4 + i) * H + j0 + lr] = accF[q][pp][i];
-  }
-  float* red = &part[0][0][0];   // [16 cols][33] db sums | [512] loss
-  __syncthreads();
-  red[col * 33 + row] = dbs;
-  red[1024 + tid] = nll;
-  __syncthreads();
-  if (fcw && tid < 16) {
-    float s = 0.f;
-    for (int rr = 0; rr < 32; ++rr) s += red[tid * 33 + rr];
-    f.db_part[(size_t)rbk * V + 16 * ut + tid] = s;
-  }
-  if (tid < 64) {
-    float s = 0.f;
-    for (int q = tid; q < 512; q += 64) s += red[1024 + q];
-    s = wave_sum(s);
-    if (tid == 0) f.loss_part[blockIdx.x] = s;
   }
 }
 
@@ -1075,22 +534,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
   // lo's input projection for step t, gathered one iteration ahead (off the critical path), from
   // a char id loaded one iteration before that (the gather never waits on an id load)
   int idn = L0.ids ? L0.ids[b] : 0;
-  float bi0[3] = {0.f, 0.f, 0.f};   // b_ih0 when the table comes as split-K slabs without it
-  if (L0.ids && L0.p_slabs > 1)
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bi0[g] = L0.bih[g * H + j];
   auto load_gi0 = [&](int t, float (&gi)[3]) {
     if (t >= T) return;
     const float* src = L0.ids ? L0.P + (size_t)idn * 3 * H : L0.Gi + ((size_t)t * Bp + b) * 3 * H;
 #pragma unroll
     for (int g = 0; g < 3; ++g) gi[g] = src[g * H + j];
-    if (L0.ids && L0.p_slabs > 1) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) gi[g] += bi0[g];
-      for (int q = 1; q < L0.p_slabs; ++q)
-#pragma unroll
-        for (int g = 0; g < 3; ++g) gi[g] += src[(size_t)q * L0.p_slab + g * H + j];
-    }
     if (L0.ids && t + 1 < T) idn = L0.ids[(size_t)(t + 1) * Bp + b];
   };
   float gin[3] = {0.f, 0.f, 0.f};
@@ -1265,8 +713,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
 // NKW3: k-steps per wave of the dh GEMM (K = 3H split over 8 waves)
 // NTW : 16-col tiles per wave of the fused dW_hh accumulator (H / 128); 0 = not fused
 // NTP : 16-col tiles per wave of the fused dP accumulator (V / 128); 0 = not fused
-// DL   : top layer's dy = dl · W_fc computed here (SeqBwdArgs::dl) instead of read from a.dy
-template <int NKW3, int NTW, int NTP, bool DL>
+// (Rejected and removed in round 4: dy = dl · W_fc inside this kernel, and the fused weight-gradient
+// MFMAs inside the publish drain; docs/DESIGN.md §3.4, §6.3.)
+template <int NKW3, int NTW, int NTP>
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][2][256];      // 16 KB
   __shared__ __attribute__((aligned(16))) u16 srow[3][32][24];        // dGh tile, gate-major (exchange; 48-B rows)
@@ -1309,7 +758,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)(((lk >> 4) * 3 * 512 + lr * 16 + (lk & 15)) * 2);   // exchange lane offset
   zero_next_flags(a.zero_next, a.zero_words);
-  if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) { a.bump[0] += 1; a.bump[1] += 1; }   // read after this launch
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
   // next poll they would delay it (vmcnt retires in order), and they have a whole step to land
@@ -1319,37 +767,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   // unit column 0 and read back right before use (8 ids held in registers across the barriers and
   // the publish pushed the register file over the limit)
   __shared__ __attribute__((aligned(16))) int idsL[NTP > 0 ? 32 : 1];
-  // top layer with a.dl: this wave's K = 32 slice (logits 32w..32w+31) of dy = dl · W_fc for the
-  // 16 units, into the same accumulators as the recurrent dh GEMM (summed over the waves).  No
-  // registers held across steps (the fused variants' file is full): the W_fc^T fragment sits
-  // lane-linear in LDS like bwL, and the step's two dl fragments go global -> LDS directly
-  // (buffer_load ... lds, 16 B per lane; each wave reads back only what it loaded itself, so no
-  // barrier).  The copy for step t-NB is issued at the END of step t, after its last barrier: the
-  // compiler makes every barrier wait for outstanding LDS-DMA (issued with the saves it put a load
-  // latency on each step's critical path: +0.3 us/step, probe_seq_bwd.py), and the exchange poll's
-  // own vmcnt(0) waits for it too (vmcnt retires in order), so it must be a whole step old by then:
-  // two buffers (NB = 2; one at H = 1024, where LDS is full).
-  constexpr bool fdl = DL;
-  __shared__ __attribute__((aligned(16))) bf16x8 bfcL[DL ? 512 : 1];
-  constexpr int NB = NKW3 >= 12 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) bf16x8 dlL[DL ? NB : 1][2][DL ? 512 : 1];   // [buf][row tile][wave*64+lane]
-  if constexpr (fdl) bfcL[tid] = ld8(a.WfcT + (size_t)(j0 + lr) * 256 + w * 32 + lk);
-  // buffer addressing: one per-lane 32-bit offset, the step and row tile in the scalar offset
-  const rsrc_t rDL = make_rsrc(a.dl, fdl ? (unsigned)((size_t)T * Bp * 256 * 2) : 0u);
-  const unsigned dl_lane = (unsigned)((lr * 256 + w * 32 + lk) * 2);
-  auto load_dl = [&](int t) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rDL, (__attribute__((address_space(3))) void*)(&dlL[t % NB][r][w * 64]), 16,
-                                               dl_lane, (int)(((size_t)t * Bp + b0 + r * 16) * 512), 0, 0);
-  };
-  if constexpr (fdl) {
-    load_dl(T - 1);
-    if (NB > 1 && T > 1) load_dl(T - 2);
-  }
   auto load_saves = [&](int t) {
     const size_t o = ((size_t)t * Bp + b) * H + j;
-    sv[0] = fdl ? 0.f : a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
     sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
     if constexpr (NTP > 0) svid = a.ids[(size_t)t * Bp + b];   // this thread's row id (fused dP)
   };
@@ -1391,13 +811,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) acc[r] = mfma16(af[kk][r], bk, acc[r]);
       }
-    }
-    if constexpr (fdl) {
-      // after the exchange loads have been waited on this wait is free (the copy is older)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const bf16x8 bfc = bfcL[tid];
-#pragma unroll
-      for (int r = 0; r < 2; ++r) acc[r] = mfma16(dlL[t % NB][r][tid], bfc, acc[r]);
     }
     const int idc = svid;
     const float dy = sv[0], sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4], hprev = sv[5];
@@ -1441,9 +854,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     }
     __syncthreads();
     stamp(a.dbg, s, 3);
-    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS), off the exchange: the
-    // publishing wave runs them while its exchange stores drain (fused_in_drain), the others right
-    // after the barrier.  (Deferred into the next step's exchange-load window they delayed its
+    // fused weight-gradient MFMAs (A = this step's dG^T tile from LDS), off the exchange: every wave
+    // runs them after the publish / transposed copies.  (Deferred into the next step's exchange-load window they delayed its
     // recurrent MFMAs: 0.2199 -> 0.2291 ms, profiles/r2_rejected_ab.jsonl)
     auto fused_mma = [&]() {
       if constexpr (NTW > 0 || NTP > 0) {
@@ -1474,7 +886,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
         }
       }
     };
-    const bool fid = a.fused_in_drain != 0;
     if (w == 0) {
       // publish the dGh_t tile as 3 gate blocks of [32 rows][16 units] (1 KB each, whole lines of its
       // own): a consumer's 16-row fragment of one gate is then 512 contiguous bytes per producer
@@ -1486,15 +897,13 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
         if (loc) st16_plain(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
         else st16_sc1(rX, (unsigned)((tile + g * 512 + lane * 8) * 2), v);
       }
-      if (!fid) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
-        if (lane == 0) {
-          if (loc) signal_flag_local(fl, (unsigned)(s + 1));
-          else signal_flag(fl, (unsigned)(s + 1));
-        }
-        stamp(a.dbg, s, 4);
-      }   // (fid: the drain and the signal follow this wave's fused MFMAs below)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      if (lane == 0) {
+        if (loc) signal_flag_local(fl, (unsigned)(s + 1));
+        else signal_flag(fl, (unsigned)(s + 1));
+      }
+      stamp(a.dbg, s, 4);
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the (non-fused) weight-gradient GEMMs: 16 units x 32 rows per gate
       const int g = w - 1;          // 0..3 : dGh r, z, n and dGi n
@@ -1511,19 +920,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
     }
     stamp(a.dbg, s, 5);
     fused_mma();
-    if (w == 0 && fid) {   // the exchange stores drained under the MFMAs: now the signal
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
-      if (lane == 0) {
-        if (loc) signal_flag_local(fl, (unsigned)(s + 1));
-        else signal_flag(fl, (unsigned)(s + 1));
-      }
-      stamp(a.dbg, s, 4);
-    }
-    if constexpr (fdl) {   // dl image of step t - NB into the buffer this step just consumed
-      if (t >= NB) load_dl(t - NB);
-    }
     stamp(a.dbg, s, 6);
   }
 
@@ -1573,15 +969,8 @@ static int resident_blocks(K kernel, int block = 512) {
 
 // row-tile split: RS = 2 up to H = 512 (H=512 forward kernel 77.5 -> 72.5 us, per step 2.16 ->
 // 2.00 us); RS = 1 at H = 1024, where the K/4 slice's 16 producers per wave measured no better
-// (profiles/r1_fwd_row_split_ab.json).  GK_FWD_RS=1/2 forces one.
-static int fwd_rs(int H) {
-  static const int forced = [] {
-    const char* e = std::getenv("GK_FWD_RS");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced == 1 || forced == 2) return forced;
-  return H <= 512 ? 2 : 1;
-}
+// (profiles/r1_fwd_row_split_ab.json).
+static int fwd_rs(int H) { return H <= 512 ? 2 : 1; }
 
 #define FWD_VARIANTS(X) X(256, 1, 1) X(256, 2, 2) X(512, 2, 1) X(512, 4, 2) X(1024, 4, 1) X(1024, 8, 2)
 
@@ -1589,24 +978,7 @@ bool gru_fwd_seq_supported(int H, int Bp) {
   if (Bp % 32) return false;
   const int rs = fwd_rs(H);
   int cap = -1;
-#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, false>);
-  FWD_VARIANTS(X)
-#undef X
-  return cap >= (H / 16) * (Bp / 32);
-}
-
-bool gru_fwd_seq_xp_supported(int H, int Bp, int E) {
-  if (Bp % 32 || E != H || H != 512 || fwd_rs(H) != 2) return false;
-  return resident_blocks(gru_fwd_seq_kernel<4, 2, false, true>) >= (H / 16) * (Bp / 32);
-}
-
-bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T) {
-  if (Bp % 32 || H % 16 || (V != 128 && V != 256) || E % 64 || E < 64 || E > 512 || T < 1) return false;
-  const int nunit = H / 16, nr = (32 + nunit - 1) / nunit;
-  if (T * nr > 1024) return false;
-  const int rs = fwd_rs(H);
-  int cap = -1;
-#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, true>);
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS>);
   FWD_VARIANTS(X)
 #undef X
   return cap >= (H / 16) * (Bp / 32);
@@ -1617,42 +989,14 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
-  if (a.xp) {
-    if (!a.Emb || !a.Wih0 || !a.bih || !a.ids || a.P || a.Gi || a.E != a.H || !gru_fwd_seq_xp_supported(a.H, a.Bp, a.E))
-      throw std::runtime_error("gru_fwd_seq: inconsistent in-kernel input projection arguments");
-    hipLaunchKernelGGL((gru_fwd_seq_kernel<4, 2, false, true>), grid, block, 0, s, a);
-    return;
-  }
-  const bool pl = a.Emb != nullptr;
-  if (pl && (!a.Wih0 || !a.bih || !a.ids || a.P || a.Gi || !gru_fwd_seq_pl_supported(a.H, a.Bp, a.V, a.E, a.T) ||
-             (a.prep.in && (a.prep.ids != a.ids || !a.prep.labels || !a.prep.inv_count || a.prep.T != a.T ||
-                            a.prep.Bp != a.Bp || a.prep.Bmax < a.Bp))))
-    throw std::runtime_error("gru_fwd_seq: inconsistent table-free layer-0 arguments");
-#define X(HH, NK, RS)                                                                    \
-  if (a.H == HH && rs == RS) {                                                          \
-    if (pl) hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, true>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, false>), grid, block, 0, s, a);   \
-    return;                                                                              \
+#define X(HH, NK, RS)                                                          \
+  if (a.H == HH && rs == RS) {                                                \
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS>), grid, block, 0, s, a);   \
+    return;                                                                    \
   }
   FWD_VARIANTS(X)
 #undef X
   throw std::runtime_error("gru_fwd_seq: no kernel variant for this shape");
-}
-
-bool gru_fwd_seq_fc_supported(int H, int Bp, int V) {
-  if (Bp % 32 || V != 256 || H != 512 || fwd_rs(H) != 2) return false;
-  const int cap = resident_blocks(gru_fwd_seq_fc_kernel<4>);
-  return cap >= (H / 16) * (Bp / 32);
-}
-
-void gru_fwd_seq_fc(const SeqFwdArgs& a, const FwdFcArgs& f, hipStream_t s) {
-  if (!gru_fwd_seq_fc_supported(a.H, a.Bp, f.V) || a.Emb || !f.Wfc || !f.WfcT || !f.bfc || !f.labels ||
-      !f.inv_count || !f.xdl || !f.xdlT || !f.xst || !f.dy || !f.dW_part || !f.db_part || !f.loss_part)
-    throw std::runtime_error("gru_fwd_seq_fc: unsupported shape or incomplete arguments");
-  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31) || (size_t)a.T * (a.Bp / 32) * 16 * 1024 >= (1ull << 31))
-    throw std::runtime_error("gru_fwd_seq_fc: buffers exceed the 2 GB buffer-offset range");
-  dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
-  hipLaunchKernelGGL((gru_fwd_seq_fc_kernel<4>), grid, block, 0, s, a, f);
 }
 
 #define FWD2_VARIANTS(X) X(256, 1) X(512, 2) X(1024, 4)
@@ -1692,11 +1036,8 @@ void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s) {
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
   if (Bp % 32) return false;
   int cap = -1;
-  // both the dy-reading and the in-kernel-dH (DL) instantiation must fit (more LDS with DL)
-#define X(HH, NK, NW, NP)                                                                       \
-  if (H == HH && (NW > 0) == fuse_w && (NP > 0) == fuse_p)                                      \
-    cap = std::min(resident_blocks(gru_bwd_seq_kernel<NK, NW, NP, false>),                      \
-                   resident_blocks(gru_bwd_seq_kernel<NK, NW, NP, true>));
+#define X(HH, NK, NW, NP) \
+  if (H == HH && (NW > 0) == fuse_w && (NP > 0) == fuse_p) cap = resident_blocks(gru_bwd_seq_kernel<NK, NW, NP>);
   BWD_VARIANTS(X)
 #undef X
   return cap >= (H / 16) * (Bp / 32);
@@ -1705,12 +1046,10 @@ bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
-  if (a.dl && (!a.WfcT || a.dy)) throw std::runtime_error("gru_bwd_seq: in-kernel dH takes dl + W_fc^T and no dy");
-#define X(HH, NK, NW, NP)                                                                   \
-  if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                                     \
-    if (a.dl) hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP, true>), grid, block, 0, s, a); \
-    else hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP, false>), grid, block, 0, s, a);     \
-    return;                                                                                 \
+#define X(HH, NK, NW, NP)                                                              \
+  if (a.H == HH && (NW > 0) == fw && (NP > 0) == fp) {                                \
+    hipLaunchKernelGGL((gru_bwd_seq_kernel<NK, NW, NP>), grid, block, 0, s, a);       \
+    return;                                                                            \
   }
   BWD_VARIANTS(X)
 #undef X

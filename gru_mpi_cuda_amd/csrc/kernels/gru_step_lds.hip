@@ -60,11 +60,9 @@ constexpr int FNS = 4, BNS = 6;
 // NS: LDS ring depth.  4 (112 KiB, one workgroup per CU) when the grid is about one wave of
 // workgroups (training at H = 2048: 256 tiles); 2 (56 KiB, two per CU) for big-batch generation,
 // where several rounds of tiles per CU need the second workgroup to hide latency.
-// NT: saves (fp32 h, r, z, n, gh_n) with nontemporal stores (A/B switch GK_STEP_NT=1): they are
-// re-read only by the backward sweep, after T more steps of traffic.
-template <class T> DEV void save_st(T* p, T v, std::true_type) { __builtin_nontemporal_store(v, p); }
-template <class T> DEV void save_st(T* p, T v, std::false_type) { *p = v; }
-template <bool FUSED, int NS, bool NT = false>
+// (A 5-deep ring and nontemporal saves measured slower and were removed in round 4:
+// profiles/r2_h2048_skns3_ab.jsonl.)
+template <bool FUSED, int NS>
 __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(FwdStepArgs a) {
   __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
   const int H = a.H;
@@ -191,11 +189,10 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
       const float n = tanhf_(gin + r * ghn);
       const float h = n + z * (hp[i][e] - n);
       const size_t o = (size_t)b * H + u;
-      const std::integral_constant<bool, NT> nt{};
-      save_st(a.h_f + o, h, nt);
+      a.h_f[o] = h;
       const u16 hb = f2bf(h);
       a.h_bf[o] = hb;
-      if (a.sr) { save_st(a.sr + o, r, nt); save_st(a.sz + o, z, nt); save_st(a.sn + o, n, nt); save_st(a.sghn + o, ghn, nt); }
+      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
       st[rr * 32 + wn * 16 + lr] = hb;
     }
   if (a.hT) {
@@ -659,117 +656,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_step_big_kernel(FwdStepArgs a)
 }
 
 // ==================================================================== backward
-// tile 64 rows x 64 units; 4 waves 2 x 2 of 32 x 32 (2 x 2 MFMA tiles); K = 3H
-__global__ void __launch_bounds__(256, 1) gru_bwd_step_lds_kernel(BwdStepArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[BNS][(64 + 64) * 64];
-  const int H = a.H, H3 = 3 * a.H;
-  const int j0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int lr = lane & 15, lq = lane >> 4;
-  const int srow = lane >> 3, sslot = lane & 7;
-
-  // epilogue operands: element (i, jt, e) -> row b0 + wm*32 + i*16 + lq*4 + e, unit j0 + wn*32 + jt*16 + lr
-  float dy[2][2][4], cin[2][2][4], sr_[2][2][4], sz_[2][2][4], sn_[2][2][4], sg_[2][2][4], hpv[2][2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const size_t o = (size_t)(b0 + wm * 32 + i * 16 + lq * 4 + e) * H + j0 + wn * 32 + jt * 16 + lr;
-        dy[i][jt][e] = a.dy[o];
-        cin[i][jt][e] = a.carry_in ? a.carry_in[o] : 0.f;
-        sr_[i][jt][e] = a.r[o]; sz_[i][jt][e] = a.z[o]; sn_[i][jt][e] = a.n[o];
-        sg_[i][jt][e] = a.ghn[o]; hpv[i][jt][e] = a.hprev[o];
-      }
-
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (a.dgh_next) {
-    const u16* srcA[2];
-    const u16* srcB[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = (2 * w + q) * 8 + srow;
-      srcA[q] = a.dgh_next + (size_t)(b0 + r) * H3 + swz(r, sslot) * 8;
-      srcB[q] = a.WhhT + (size_t)(j0 + r) * H3 + swz(r, sslot) * 8;
-    }
-    auto stage = [&](int buf, int kt) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        __builtin_amdgcn_global_load_lds(srcA[q] + kt * 64, (lds_void_t*)(&lds[buf][(2 * w + q) * 8 * 64]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(srcB[q] + kt * 64, (lds_void_t*)(&lds[buf][(64 + (2 * w + q) * 8) * 64]), 16, 0, 0);
-      }
-    };
-    ring_loop<BNS, 4>(H3 / 64, stage, [&](int cur) {
-      const u16* LA = lds[cur];
-      const u16* LB = lds[cur] + 64 * 64;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c = ks * 4 + lq;
-        bf16x8 af[2], bfr[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int ra = wm * 32 + t * 16 + lr, rb = wn * 32 + t * 16 + lr;
-          af[t] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
-          bfr[t] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      }
-    });
-  }
-
-  // ---- gate-gradient epilogue; transposed staging [4 kinds][64 units][64 rows] bf16 = 32 KiB
-  u16* st = lds[0];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int rr = wm * 32 + i * 16 + lq * 4 + e, uu = wn * 32 + jt * 16 + lr;
-        const int b = b0 + rr, j = j0 + uu;
-        const float dh = dy[i][jt][e] + cin[i][jt][e] + acc[i][jt][e];
-        const float r = sr_[i][jt][e], z = sz_[i][jt][e], n = sn_[i][jt][e];
-        const float dn = dh * (1.f - z);
-        const float dz = dh * (hpv[i][jt][e] - n);
-        const float dan = dn * (1.f - n * n);
-        const float dar = dan * sg_[i][jt][e] * r * (1.f - r);
-        const float daz = dz * z * (1.f - z);
-        a.carry_out[(size_t)b * H + j] = z * dh;
-        const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
-        const size_t og = (size_t)b * H3 + j;
-        a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
-        if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
-        st[(0 * 64 + uu) * 64 + rr] = br;
-        st[(1 * 64 + uu) * 64 + rr] = bz;
-        st[(2 * 64 + uu) * 64 + rr] = bn;
-        st[(3 * 64 + uu) * 64 + rr] = bi;
-      }
-  __syncthreads();
-  // 4 kinds x 64 units x 64 rows = 2048 pieces of 8 rows (16 B), 8 per thread
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int q = threadIdx.x + p * 256;
-    const int kind = q >> 9, rem = q & 511, unit = rem >> 3, seg = rem & 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 64 + unit) * 64 + seg * 8]);
-    const int g = kind < 3 ? kind : 2;
-    const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + seg * 8;
-    if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-    if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
-  }
-}
-
-// 8-wave variant: the same 64 x 64 tile, but two wave groups split every 64-deep k-tile by its two
+// tile 64 rows x 64 units over K = 3H (the 4-wave version of this kernel lost to the 8-wave one
+// below: r1_bwd_lds8_ab.json, removed in round 4).
+// 8 waves: two wave groups split every 64-deep k-tile by its two
 // 32-deep k-steps (group g does k-step g), so each wave issues half the LDS-DMA pieces and half the
-// MFMAs of the 4-wave kernel and two waves share each SIMD (one's DMA issue and LDS latency hide
+// MFMAs of a 4-wave kernel and two waves share each SIMD (one's DMA issue and LDS latency hide
 // under the other's MFMAs).  Group 1's partial dh tile is added to group 0's through LDS before the
 // epilogue.
 __global__ void __launch_bounds__(512, 1) gru_bwd_step_lds8_kernel(BwdStepArgs a) {
@@ -918,7 +809,7 @@ constexpr int SKNS = 4;                       // LDS ring: 4 x 32 KiB
 constexpr unsigned kSkSpinLimit = 1u << 21;   // x s_sleep(1): far beyond any real wait
 }
 
-// NS: LDS ring depth (4 x 32 KiB; 5 fills the 160 KiB LDS: A/B switch GK_BWD_SK_NS=5).
+// NS: LDS ring depth (4 x 32 KiB; 3 and 5 measured equal / slower: profiles/r2_h2048_skns3_ab.jsonl).
 // PF (default): the epilogue's fp32 operands (dy, carry, saves, h_{t-1}) are loaded before the K
 // loop, so their latency hides under it instead of following the split-K exchange (h2048 step
 // 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl; GK_BWD_SK_PF=0 reverts).
@@ -1099,163 +990,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
   }
 }
 
-// 64-row split-K backward (A/B switch GK_BWD_SK64=1; rejected: h2048 step 9.37-9.41 -> 10.04-10.05 ms,
-// profiles/r2_h2048_bwd_sk64_ab.jsonl -- unlike the forward, the split-K exchange and the
-// per-workgroup epilogue do not shrink with the tile): tile 64 rows x 128 units over a 1/4 slice of
-// K, 4 waves of 64 rows x 32 units, a 3-deep ring of 24 KiB slots, two workgroups per CU (512 at
-// B = 512, H = 2048: the 64-row forward's trade, twice the k-tile streams in flight per CU).  Same
-// exchange as the 128-row kernel: write-through fp32 partial, monotonic arrival counter, bounded
-// spin; then split s sums the four partials of 16-row group i = s in slab order and runs the
-// gate-gradient epilogue on its 16 x 128 elements (operands loaded before the K loop).
-__global__ void __launch_bounds__(256, 2) gru_bwd_step_sk64_kernel(BwdStepArgs a) {
-  constexpr int S = 4, NS = 3;
-  __shared__ __attribute__((aligned(16))) u16 lds[NS][192 * 64];
-  const int H = a.H, H3 = 3 * a.H;
-  const int bid = blockIdx.x;
-  const int split = (bid >> 3) % S, tile = (bid / (8 * S)) * 8 + (bid & 7);
-  const int ntu = H / 128;
-  const int j0 = (tile % ntu) * 128, b0 = (tile / ntu) * 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;   // K loop: wave w = 64 rows x units 32w..
-  const int lr = lane & 15, lq = lane >> 4;
-  const int srow = lane >> 3, sslot = lane & 7;
-  constexpr int PIECE = 4 * 4 * 2 * 64;           // f32x4 per partial tile: [wave][i][jn][lane]
-  const bool kloop = a.dgh_next != nullptr;
-
-  // epilogue element (piece pp, row e): fragment (wave wp = P >> 1, i = split, jn = P & 1), P = w + 4 pp
-  float pre[2][4][6];
-#pragma unroll
-  for (int pp = 0; pp < 2; ++pp)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int P = w + 4 * pp, wp = P >> 1, jn = P & 1;
-      const size_t o = (size_t)(b0 + split * 16 + lq * 4 + e) * H + j0 + wp * 32 + jn * 16 + lr;
-      pre[pp][e][0] = a.dy[o] + (a.carry_in ? a.carry_in[o] : 0.f);
-      pre[pp][e][1] = a.r[o]; pre[pp][e][2] = a.z[o]; pre[pp][e][3] = a.n[o];
-      pre[pp][e][4] = a.hprev[o]; pre[pp][e][5] = a.ghn[o];
-    }
-
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const sk_rsrc_t rP = sk_rsrc(a.sk_part, (unsigned)(a.sk_part_floats * 4));
-  const size_t tile_base = (size_t)tile * S * PIECE;
-  if (kloop) {
-    const int nk = H3 / 64 / S, kt0 = split * nk;
-    // 24 DMA pieces (8 rows x 128 B) per k-tile, 6 per wave: image rows 0..63 = A (dGh_{t+1}),
-    // 64..191 = B (W_hh^T)
-    const u16* src[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int r = (6 * w + q) * 8 + srow;
-      const int rr = r < 64 ? r : r - 64;
-      const u16* base = r < 64 ? a.dgh_next + (size_t)(b0 + rr) * H3 : a.WhhT + (size_t)(j0 + rr) * H3;
-      src[q] = base + swz(rr, sslot) * 8 + (size_t)kt0 * 64;
-    }
-    auto stage = [&](int buf, int kt) {
-#pragma unroll
-      for (int q = 0; q < 6; ++q)
-        __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][(6 * w + q) * 8 * 64]), 16, 0, 0);
-    };
-    ring_loop<NS, 6>(nk, stage, [&](int cur) {
-      const u16* LA = lds[cur];
-      const u16* LB = lds[cur] + 64 * 64;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c = ks * 4 + lq;
-        bf16x8 af[4], bfr[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ra = i * 16 + lr;
-          af[i] = *reinterpret_cast<const bf16x8*>(&LA[ra * 64 + swz(ra, c) * 8]);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int rb = w * 32 + j * 16 + lr;
-          bfr[j] = *reinterpret_cast<const bf16x8*>(&LB[rb * 64 + swz(rb, c) * 8]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      }
-    });
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const size_t o = tile_base + (size_t)split * PIECE + ((w * 4 + i) * 2 + j) * 64 + lane;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, acc[i][j]), rP, (unsigned)(o * 16), 0, 16);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      unsigned* cnt = a.sk_cnt + (size_t)tile * 16;
-      const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (old / S + 1) * S;
-      unsigned spins = 0;
-      while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > kSkSpinLimit) {
-          if (a.err) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- epilogue: rows 16 split .. 16 split + 15 of the tile; transposed staging [4 kinds][128 units][24]
-  u16* st = lds[0];
-#pragma unroll
-  for (int pp = 0; pp < 2; ++pp) {
-    const int P = w + 4 * pp, wp = P >> 1, jn = P & 1;
-    f32x4 ps = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kloop) {
-#pragma unroll
-      for (int s2 = 0; s2 < S; ++s2) {
-        const size_t o = tile_base + (size_t)s2 * PIECE + ((wp * 4 + split) * 2 + jn) * 64 + lane;
-        ps += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rP, (unsigned)(o * 16), 0, 16));
-      }
-    }
-    const int ut = wp * 32 + jn * 16 + lr;
-    const int j = j0 + ut;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int rq = lq * 4 + e;
-      const int b = b0 + 16 * split + rq;
-      const size_t o = (size_t)b * H + j;
-      const float dh = pre[pp][e][0] + ps[e], r = pre[pp][e][1], z = pre[pp][e][2], n = pre[pp][e][3];
-      const float dn = dh * (1.f - z);
-      const float dz = dh * (pre[pp][e][4] - n);
-      const float dan = dn * (1.f - n * n);
-      const float dar = dan * pre[pp][e][5] * r * (1.f - r);
-      const float daz = dz * z * (1.f - z);
-      a.carry_out[o] = z * dh;
-      const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
-      const size_t og = (size_t)b * H3 + j;
-      a.dgh[og] = br; a.dgh[og + H] = bz; a.dgh[og + 2 * H] = bn;
-      if (a.dgi) { a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi; }
-      st[(0 * 128 + ut) * 24 + rq] = br;
-      st[(1 * 128 + ut) * 24 + rq] = bz;
-      st[(2 * 128 + ut) * 24 + rq] = bn;
-      st[(3 * 128 + ut) * 24 + rq] = bi;
-    }
-  }
-  __syncthreads();
-  // 4 kinds x 128 units x 16 rows = 1024 pieces of 8 rows (16 B), 4 per thread
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int q = tid + p * 256;
-    const int kind = q >> 8, rem = q & 255, unit = rem >> 1, seg = rem & 1;
-    const uint4 v = *reinterpret_cast<const uint4*>(&st[(kind * 128 + unit) * 24 + seg * 8]);
-    const int g = kind < 3 ? kind : 2;
-    const size_t off = (size_t)(g * H + j0 + unit) * a.ldT + a.colT + b0 + 16 * split + seg * 8;
-    if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
-    if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
-  }
-}
+// (A 64-row split-K backward with two workgroups per CU lost to this one: h2048 step 9.37-9.41 ->
+// 10.04-10.05 ms, profiles/r2_h2048_bwd_sk64_ab.jsonl; removed in round 4.)
 
 static int sk_capacity(const void* kernel, int threads = 512) {
   int dev = 0, cus = 0, per = 0;
@@ -1266,11 +1002,7 @@ static int sk_capacity(const void* kernel, int threads = 512) {
 }
 
 int gru_bwd_step_sk_splits(int H, int Bp) {
-  static const bool on = [] {
-    const char* e = std::getenv("GK_BWD_SK");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || H % 128 || Bp % 128) return 0;
+  if (H % 128 || Bp % 128) return 0;
   const int tiles = (H / 128) * (Bp / 128);
   if (tiles % 8) return 0;
   static const int cap4 = sk_capacity((const void*)gru_bwd_step_sk_kernel<4>);
@@ -1278,7 +1010,6 @@ int gru_bwd_step_sk_splits(int H, int Bp) {
   // H = 2048 (K = 6144): 40.3 -> 35.4 us per step (profiles/r1_bwd_step_sk_ab.jsonl).  H = 1024 was
   // a loss before the epilogue operands moved ahead of the K loop (9.50 -> 9.62 ms per h1024_l2 step
   // at B = 1024); with them it gains: 8.67 -> 8.17-8.19 ms (profiles/r2_h1024l2_b1024_sk_ab.jsonl).
-  // GK_BWD_SK_MIN_H=2048 restores the old bound.
   if (H < step_lds_variants().bwd_sk_min_h) return 0;
   if ((3 * H / 64) % 4 == 0 && tiles * 4 <= cap4 && tiles * 4 >= 192) return 4;
   if ((3 * H / 64) % 2 == 0 && tiles * 2 <= cap2 && tiles * 2 >= 192) return 2;
@@ -1286,31 +1017,14 @@ int gru_bwd_step_sk_splits(int H, int Bp) {
 }
 
 StepLdsVariants& step_lds_variants() {
-  static StepLdsVariants v = [] {
-    StepLdsVariants d;
-    auto env = [](const char* name, int& f) { if (const char* e = std::getenv(name)) f = std::atoi(e); };
-    env("GK_STEP_LDS_NS", d.fwd_ns);
-    env("GK_STEP_NT", d.fwd_nt);
-    env("GK_FWD_LDS8", d.fwd8);
-    env("GK_FWD_LDS64", d.fwd64);
-    env("GK_FWD_LDS64_FUSED", d.fwd64_fused);
-    env("GK_FWD_LDS64_ALL", d.fwd64_all);
-    env("GK_BWD_SK64", d.bwd_sk64);
-    env("GK_BWD_SK_MIN_H", d.bwd_sk_min_h);
-    env("GK_BWD_SK_NS", d.bwd_sk_ns);
-    env("GK_BWD_SK_PF", d.bwd_sk_pf);
-    return d;
-  }();
+  static StepLdsVariants v;   // measured-best defaults; tests switch them at run time
   return v;
 }
 
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
-  static const bool big_ok = [] {
-    const char* e = std::getenv("GK_STEP_BIG");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool big_ok = true;
   // big tile: only with the fused input phase on a full round of tiles (without it, the P-table
   // gather moves behind the K loop and it measured slower: profiles/r1_generate_step_kernel_ab.json)
   if (big_ok && a.x_bf && a.Kin % 64 == 0 && a.Bp % 256 == 0 && a.H % 64 == 0 && (a.H / 64) * (a.Bp / 256) >= 256) {
@@ -1322,8 +1036,8 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);
   const StepLdsVariants& v = step_lds_variants();
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
-  if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : v.fwd_ns == 5 ? 5 : 4;
-  const bool nt = v.fwd_nt != 0, eight = v.fwd8 != 0;
+  if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : 4;
+  const bool eight = v.fwd8 != 0;
   const bool big_grid_ok = ns != 2 || v.fwd64_all;   // GK_FWD_LDS64_ALL=1: also where the 2-deep 128-row kernel runs
   if (big_grid_ok && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
     if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
@@ -1339,20 +1053,10 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   }
   if (ns != 2 && !a.x_bf && eight) {
     if (v.fwd8 == 2) hipLaunchKernelGGL((gru_fwd_step_lds8_kernel<FNS, true>), grid, dim3(512), 0, s, a);
-    else if (ns == 5) hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<5>, grid, dim3(512), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<FNS>, grid, dim3(512), 0, s, a);
     return;
   }
-  if (ns != 2 && !a.x_bf && nt) {
-    if (ns == 5) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 5, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, FNS, true>), grid, block, 0, s, a);
-    return;
-  }
-  if (ns == 5) {
-    // 5-deep ring (140 KiB): four k-tiles in flight instead of three
-    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 5>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 5>), grid, block, 0, s, a);
-  } else if (ns == 2) {
+  if (ns == 2) {
     if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 2>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 2>), grid, block, 0, s, a);
   } else {
@@ -1361,39 +1065,17 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   }
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
-  if (step_lds_variants().bwd_sk64 && gru_bwd_step_sk_splits(a.H, a.Bp) == 4 && a.Bp % 64 == 0) {
-    static const int cap64 = sk_capacity((const void*)gru_bwd_step_sk64_kernel, 256);
-    const int tiles = (a.H / 128) * (a.Bp / 64);
-    if (tiles % 8 == 0 && tiles * 4 <= cap64 && a.sk_part && a.sk_cnt &&
-        a.sk_part_floats >= (long)a.H * a.Bp * 4 && a.sk_cnt_words >= (long)tiles * 16) {
-      hipLaunchKernelGGL(gru_bwd_step_sk64_kernel, dim3(tiles * 4), dim3(256), 0, s, a);
-      return;
-    }
-  }
   if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
-      const StepLdsVariants& v = step_lds_variants();
-      const int ns = v.bwd_sk_ns == 5 ? 5 : v.bwd_sk_ns == 3 ? 3 : SKNS;
-      const bool pf = v.bwd_sk_pf != 0;
-      if (S == 4 && ns == 5 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5, true>), dim3(tiles * 4), dim3(512), 0, s, a);
-      else if (S == 4 && ns == 5) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 5>), dim3(tiles * 4), dim3(512), 0, s, a);
-      else if (S == 4 && ns == 3 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, 3, true>), dim3(tiles * 4), dim3(512), 0, s, a);
-      else if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, a);
+      const bool pf = step_lds_variants().bwd_sk_pf != 0;
+      if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, a);
       else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
       else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, a);
       return;
     }
   }
-  static const bool eight = [] {
-    const char* e = std::getenv("GK_BWD_LDS8");
-    return !(e && e[0] == '0');
-  }();
-  if (eight) {
-    hipLaunchKernelGGL(gru_bwd_step_lds8_kernel, dim3(a.H / 64, a.Bp / 64), dim3(512), 0, s, a);
-    return;
-  }
-  hipLaunchKernelGGL(gru_bwd_step_lds_kernel, dim3(a.H / 64, a.Bp / 64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(gru_bwd_step_lds8_kernel, dim3(a.H / 64, a.Bp / 64), dim3(512), 0, s, a);
 }
 
 }  // namespace gk

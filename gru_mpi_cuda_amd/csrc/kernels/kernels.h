@@ -68,19 +68,16 @@ void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
 // workspace: H * Bp * splits fp32 partials, (H/128)(Bp/128) * 16 counter words
 int gru_bwd_step_sk_splits(int H, int Bp);
 // Large-H step-kernel variants (gru_step_lds.hip).  Initialised from the environment (GK_STEP_LDS_NS,
-// GK_STEP_NT, GK_FWD_LDS8, GK_BWD_SK_NS, GK_BWD_SK_PF) on first use; settable at run time so the
+// GK_FWD_LDS8, GK_FWD_LDS64*, GK_BWD_SK_PF, GK_BWD_SK_MIN_H) on first use; settable at run time so the
 // kernel tests cover every variant in one process.  0 / -1 fields mean "automatic".
 struct StepLdsVariants {
-  int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4, 5
-  int fwd_nt = 0;        // forward saves with nontemporal stores
+  int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4
   int fwd8 = 2;          // 8-wave forward (two wave groups split each k-tile): 2 = split epilogue,
                          // 1 = group 0 runs the whole epilogue, 0 = the 4-wave kernel
   int fwd64 = 1;         // 64-row forward tile, two workgroups per CU (1: 3-deep ring, 2: 4-deep)
   int fwd64_fused = 1;   // the 64-row tile also for the fused input phase (layers >= 1 of generation)
   int fwd64_all = 0;     // the 64-row tile also on grids of >= 512 128-row tiles (2-deep 128-row kernel otherwise)
-  int bwd_sk_ns = 4;     // split-K backward LDS ring depth: 4 or 5
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
-  int bwd_sk64 = 0;      // split-K backward on 64-row tiles, two workgroups per CU
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
 };
 StepLdsVariants& step_lds_variants();
@@ -112,23 +109,7 @@ struct SeqFwdArgs {
   float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
   const u16* Whh = nullptr; const float* bhh = nullptr;
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
-  // P as p_slabs K-slice partial tables p_slab floats apart, b_ih0 not included (p_slabs > 1: the
-  // gather sums them and adds bih) -- a split-K table GEMM of 4x the workgroups, each fetching a
-  // quarter of the operands
-  int p_slabs = 1; long p_slab = 0; const float* bih = nullptr;
   const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
-  // layer 0 WITHOUT a P table (Emb != nullptr; gru_fwd_seq_pl_supported): every workgroup computes
-  // the 48 columns of P = Emb · W_ih0^T + b_ih0 it gathers from (its 16 units x 3 gates, all V rows)
-  // into LDS at launch -- the k-sequence of gemm_small, so bitwise the prologue table -- and
-  // transposes its share of the batch (prep, rows 32 rb + ut (mod H/16)) from the pinned staging slot
-  // into ids / labels before its row block's start-up exchange.  No prologue kernel in the step.
-  const u16* Emb = nullptr;        // [V][E] bf16
-  const u16* Wih0 = nullptr;       // [3H][E] bf16 (bias in bih)
-  int V = 0, E = 0;
-  PrepJob prep;                    // prep.in == nullptr: ids already hold the batch
-  // xp = 1 (gru_fwd_seq_xp_supported): layer 0's input projection inside the launch, one step
-  // ahead in the post-publish slack (Emb, Wih0, bih as above; ids from the prologue's batch prep)
-  int xp = 0;
   const float* h0 = nullptr;       // optional fp32 initial state (HSb[0] must hold its bf16)
   unsigned* cnt = nullptr;         // [Bp/32][H/16][16] epoch flags, zero at launch
   unsigned* zero_next = nullptr;   // flag block of the NEXT sequence kernel, zeroed here (nullable)
@@ -136,40 +117,12 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
-  // 1: the publishing wave issues its saves for the backward before its exchange store (one drain for
-  // both) instead of after the signal (GK_FWD_SAVES_IN_DRAIN=1; measured slower, off)
-  int saves_in_drain = 0;
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
 inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 16; }
 bool gru_fwd_seq_supported(int H, int Bp);
-// the table-free layer-0 variant (SeqFwdArgs::Emb): V in {128, 256}, E % 64 == 0, E <= 512, and a
-// row block's batch share fits one pass (T * ceil(32 / (H/16)) <= 1024)
-bool gru_fwd_seq_pl_supported(int H, int Bp, int V, int E, int T);
-bool gru_fwd_seq_xp_supported(int H, int Bp, int E);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
-// Top layer's forward with the FC / softmax-xent / dH pipeline inside the persistent launch
-// (gru_seq.hip, gru_fwd_seq_fc_kernel): replaces fc_xent and the dW_fc product.  V = 256,
-// H in {256, 512} (the row-split forward), Bp % 32 == 0.
-struct FwdFcArgs {
-  const u16* Wfc = nullptr;        // [V][H] bf16
-  const u16* WfcT = nullptr;       // [H][V] bf16
-  const float* bfc = nullptr;      // [V]
-  const int* labels = nullptr;     // [T][Bp] (-1: no loss)
-  const float* inv_count = nullptr;
-  u16* xdl = nullptr;              // dl exchange [T][Bp/32][16][32][16] bf16
-  u16* xdlT = nullptr;             // [T][Bp/32][16][16][32] bf16
-  float* xst = nullptr;            // row statistics [T][Bp/32][16][32][2]
-  float* dy = nullptr;             // [T][Bp][H] fp32: dL/dh of every step (the backward's input)
-  float* dW_part = nullptr;        // [Bp/32][V][H] dW_fc per row block
-  float* db_part = nullptr;        // [Bp/32][V]   db_fc per row block
-  float* loss_part = nullptr;      // [grid] loss partials
-  int V = 0;
-};
-bool gru_fwd_seq_fc_supported(int H, int Bp, int V);
-inline long fwd_fc_xbytes(int T, int Bp) { return (long)T * (Bp / 32) * 16 * (1024 + 1024 + 256); }
-void gru_fwd_seq_fc(const SeqFwdArgs& a, const FwdFcArgs& f, hipStream_t s);
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
 // `lo` at step s and layer `hi` at step s-1 in iteration s = 0..T.  hi's input projection
@@ -186,10 +139,6 @@ void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s);
 
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
-  // top layer alternative to dy (V = 256): dy = dl · W_fc computed in the kernel from the
-  // row-major bf16 dlogits [T][Bp][V] and W_fc^T [H][V] (fc_xent then skips its dH)
-  const u16* dl = nullptr;
-  const u16* WfcT = nullptr;
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
@@ -210,10 +159,6 @@ struct SeqBwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
-  // 1: the publishing wave runs its fused dW_hh / dP MFMAs while its exchange stores drain (before the
-  // signal) instead of after it (GK_BWD_FUSED_IN_DRAIN=1; measured slower, off)
-  int fused_in_drain = 0;
-  int* bump = nullptr;             // [2]: optimiser step counter and fused-tail epoch, +1 each at launch (nullable)
   int T = 0, Bp = 0, H = 0;
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
@@ -446,60 +391,6 @@ struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
     job[n++] = OptCastJob{off, R, C, d, dT, dF, dTF}; } };
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 
-// ------------------------------------------------------------------ fused step tail (tail.hip)
-// Everything after the backward sequence kernel as ONE launch: the layer-0 table gradient dP (its
-// per-row-block partials -> bf16 dP and dP^T), the loss sum, Adam + bf16 refresh of every tensor,
-// and the embedding-side products dW_ih0 = dP^T Emb and dEmb = dP W_ih0, each output tile followed
-// directly by the Adam update of that tile.  One block per work item; the product items come last
-// in the grid and wait (bounded) on per-column-block counters of the dP tiles.
-struct TailArgs {
-  const float* dP_part = nullptr; int nslP = 0, V = 0, H3 = 0;   // [nslP][V][H3] -> dP_bf, dPT_bf
-  // dP_part aliases the W_ih0 gradient slot (data-parallel: the all-reduced dP lives there): the
-  // W_ih0 tiles then keep their gradient to themselves (no write-back over dP still being read)
-  int dP_alias = 0;
-  u16* dP_bf = nullptr; u16* dPT_bf = nullptr;
-  const u16* EmbT = nullptr;       // [E][V]   B operand of dW_ih0
-  const u16* WihT = nullptr;       // [E][H3]  B operand of dEmb
-  int E = 0;
-  float* slab_e = nullptr; int se = 1;   // dEmb K-split partials [se][V][E] (H3 / se % 64 == 0)
-  int jw = -1, je = -1;            // W_ih0 / embedding jobs of the OptCastJobs list (updated by the product items)
-  const float* loss_part = nullptr; int nloss = 0; float* loss = nullptr;
-  unsigned* sync = nullptr;        // tail_sync_words(): monotonic counters, zero before the first launch
-  const unsigned* epoch = nullptr; // launches so far incl. this one (bumped before the launch: SeqBwdArgs::bump)
-  unsigned long long* dbg = nullptr;   // diagnostic (nullable): [nItems][4] = start, wait done, end, wg | xcc << 16
-  int adam_after_dp = 0;           // Adam blocks start once a dP column block is complete (the dP chain first)
-  int fc_after_dp = 0;             // dW_fc blocks likewise (they are off the critical path)
-  // dW_fc = dl^T · H_top and db_fc = row sums of dl^T over nfc K-slices of tokens (0: not in the
-  // tail; the W_fc / b_fc jobs then take their gradient as before).  Slice s goes to slab s of
-  // slab_fc / rs_fc; a tile's LAST slice sums the slabs and runs the Adam of that W_fc tile (and of
-  // its 64 b_fc elements for the first column tile).  Nothing waits for these blocks.
-  const u16* dlT = nullptr; int ldl = 0;    // [V][ldl] bf16 dlogits^T
-  const u16* HTop = nullptr; int ldh = 0;   // [H][ldh] bf16 top-layer h^T (token columns)
-  float* slab_fc = nullptr; float* rs_fc = nullptr;   // [nfc][V][H], [nfc][V]
-  int nfc = 0, tok = 0, H = 0, jf = -1, jb = -1;
-  // The NEXT step's layer-0 table P = Emb·W_ih0^T + b_ih0 from the weights this launch refreshes
-  // (null: the next step's prologue computes it).  One 64 x 64 tile per item, after the Emb rows,
-  // the W_ih0 rows and b_ih0 it reads are refreshed (their refresh stores are write-through then).
-  float* P = nullptr;
-  const u16* EmbR = nullptr;       // [V][E] bf16 row-major copies (the refreshed ones)
-  const u16* WihR = nullptr;       // [H3][E]
-  const float* bih = nullptr;      // [H3] fp32 master of b_ih0
-  int jbi = -1;                    // its job in the OptCastJobs list
-  // The NEXT step's batch preparation (prep.in null: its prologue does it): zero-copy reads of its
-  // pinned staging slot on blocks that wait for nothing, ahead of everything else in the grid.
-  PrepJob prep{nullptr, 0, 0, 0, nullptr, nullptr, nullptr};
-  int nF = 0, nP = 0, nA0 = 0, nW = 0, nE = 0, nPt = 0, nB = 0, nItems = 0;   // filled by tail_step()
-};
-// counters (one 64-B line each): dP column blocks (H3/64), dEmb tiles ((V/64)(E/64)), read-done of
-// Emb^T per E-tile (E/64) and of W_ih^T per (E-tile, K-slice) (8 E/64), dW_fc tiles ((V/64)(H/64)),
-// refreshed Emb row blocks (V/64), refreshed W_ih0 row blocks (H3/64), refreshed b_ih0 (1)
-inline long tail_sync_words(int V, int H3, int E, int H) {
-  return (long)(H3 / 64 + (V / 64) * (E / 64) + 9 * (E / 64) + (V / 64) * (H / 64) + V / 64 + H3 / 64 + 1) * 16;
-}
-// false: the grid cannot hold the waiting product items beside the others (the caller takes the
-// phased tail); true: launched
-bool tail_step(const OptimArgs& a, OptCastJobs& j, TailArgs& t, hipStream_t s);
-int tail_resident_slots();   // workgroups of the tail kernel the device holds at once (0: query failed)
 void fill_f32(float* p, long n, float v, hipStream_t s);
 // placement census: out[b] = HW_REG_XCC_ID of the CU that ran block b
 void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);

@@ -287,21 +287,17 @@ def test_generator_fp32_probs_match_fp64(precision, persist, atol, rtol):
     torch.testing.assert_close(probs[:N].cpu().double(), want, atol=atol, rtol=rtol)
 
 
-@pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll,fc_early", [
-    (1, 256, 256, 8.0, 1, "0"), (2, 128, 256, 0.25, 3, "0"), (1, 512, 512, 1.0, 1, "0"),
-    (2, 512, 256, 0.25, 2, "0"), (2, 512, 256, 64.0, 1, "0"),
-    (1, 512, 512, 8.0, 2, "1"), (2, 512, 256, 0.25, 3, "1")])
-def test_single_graph_step_with_rccl_world1(monkeypatch, layers, E, H, bucket_mb, n_coll, fc_early):
+@pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll", [
+    (1, 256, 256, 8.0, 1), (2, 128, 256, 0.25, 3), (1, 512, 512, 1.0, 1),
+    (2, 512, 256, 0.25, 2), (2, 512, 256, 64.0, 1)])
+def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
     """The whole step as one graph with captured RCCL all-reduces (1-rank communicator) on the
     comm stream: must equal the no-comm step bit for bit (mean over one rank is the identity).
     With a communicator the step all-reduces dP instead of dEmb / dW_ih0 (in the W_ih0 slot when
-    V <= E, else as its own collective) and derives those two after the join (the fused step tail
-    on the averaged dP where it qualifies); small buckets make the top layer's group go out while
-    layer 0 is still in its backward.  fc_early (GK_AR_FC_EARLY=1, off by default): the FC group
-    goes out before the backward sweep, whatever the bucket size."""
+    V <= E, else as its own collective) and derives those two after the join; small buckets make
+    the top layer's group go out while layer 0 is still in its backward."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
-    monkeypatch.setenv("GK_AR_FC_EARLY", fc_early)
     C = load_ext()
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=64, seq=8, seed=3, bucket_mb=bucket_mb)
     x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
@@ -369,51 +365,6 @@ def test_multi_step_graph_matches_single_steps(G, layers, H):
     assert a.t.graph_steps() == G
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
     assert a.loss() == b.loss()
-
-
-@pytest.mark.parametrize("G", [1, 3])
-def test_tail_p_table_tracks_the_weights(monkeypatch, G):
-    """The fused tail leaves the NEXT step's layer-0 table P = Emb·W_ih0^T + b_ih0 behind (and,
-    inside a multi-step graph, its batch).  After steps P matches the refreshed weights; after an
-    external rewrite of the weights (load_state -> refresh_weights) the next launch recomputes it
-    first: bit for bit the same as a trainer with the same history that computes P in every
-    step's prologue as one table (GK_TAIL_P=0, GK_P_SLABS=1; read when a step graph is recorded).
-    (GK_TAIL_P is off by default: measured slower at the headline.)"""
-    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    from gru_mpi_cuda_amd.ops import load_ext
-    monkeypatch.setenv("GK_TAIL", "1")     # the fused step tail (opt-in) is what computes the next P
-    monkeypatch.setenv("GK_TAIL_P", "1")
-    monkeypatch.setenv("GK_FWD_XP", "0")   # both trainers gather from a P table
-    cfg = GRUConfig(vocab=256, embed=256, hidden=256, layers=1, batch=64, seq=8, seed=7)
-    stream = NameStream(cfg.batch, cfg.seq, seed=8)
-    batches = [stream.next() for _ in range(G + 1)]
-
-    def run(tr):
-        if G > 1:
-            tr.steps(batches[:G])
-        else:
-            tr.step(*batches[0])
-    a = HipTrainer(cfg, params=init_params(cfg))
-    run(a)
-    torch.cuda.synchronize()
-    assert a.t.tail_plan()[-1] > 0, a.t.tail_plan()    # the tail computed the next P
-    sd = a.state_dict()
-    got = torch.empty(cfg.vocab, 3 * cfg.hidden, dtype=torch.float32, device="cuda")
-    load_ext().copy_d2d(got.data_ptr(), a.t.buffer("P"), got.numel() * 4)
-    want = sd["embedding"].bfloat16().float() @ sd["weight_ih_l0"].bfloat16().float().T + sd["bias_ih_l0"]
-    torch.testing.assert_close(got.cpu(), want, atol=1e-4, rtol=1e-4)
-    new = {k: v * 0.9 for k, v in sd.items()}
-    a.load_state(new)
-    a.step(*batches[G])
-    monkeypatch.setenv("GK_TAIL_P", "0")
-    monkeypatch.setenv("GK_P_SLABS", "1")   # one table with the bias, as the tail and ensure_p() write it
-    c = HipTrainer(cfg, params=init_params(cfg))
-    run(c)
-    c.load_state(new)
-    c.step(*batches[G])
-    torch.cuda.synchronize()
-    assert c.t.tail_plan()[-1] == 0, c.t.tail_plan()
-    assert torch.equal(a.params, c.params)
 
 
 def test_set_batch_device_matches_host():
@@ -572,15 +523,12 @@ def test_trainer_carry_hidden(monkeypatch, sched, layers, H, B):
     assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
 
 
-@pytest.mark.parametrize("tail", ["0", "1"])
 @pytest.mark.parametrize("layers,H,B,opt", [(1, 512, 256, "adam"), (2, 256, 64, "adam"), (1, 256, 64, "sgd")])
-def test_one_graph_step_equals_phased_step(monkeypatch, layers, H, B, opt, tail):
+def test_one_graph_step_equals_phased_step(layers, H, B, opt):
     """The one-graph step hands optimiser-only slab reductions (dW_hh / bias / dW_fc / dEmb
-    partials) to the fused Adam launch -- or, GK_TAIL=1, to the fused step tail (tail.hip); the
-    phased path (forward_backward, then optimizer_step) reduces them first.  Same partials, same
-    summation order: bitwise-equal weights and grads."""
+    partials) to the fused Adam launch; the phased path (forward_backward, then optimizer_step)
+    reduces them first.  Same partials, same summation order: bitwise-equal weights and grads."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    monkeypatch.setenv("GK_TAIL", tail)
     cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=12, optimizer=opt)
     params = init_params(cfg)
     ds = NameStream(B, cfg.seq, seed=2)
@@ -743,119 +691,6 @@ def test_carry_graph_replay_matches_eager(layers, H, B, synced):
     torch.cuda.synchronize()
     assert torch.equal(g.params, e.params)
     assert g.t.read_error() == 0
-
-
-@pytest.mark.parametrize("G,batch,H", [(1, 64, 512), (4, 80, 512), (3, 64, 256)])
-def test_table_free_forward_matches_prologue_table(monkeypatch, G, batch, H):
-    """Layer 0 through the table-free persistent forward (GK_FWD_PL=1, opt-in: the launch computes its
-    P-table columns and transposes the batch, no prologue kernel) trains bit for bit like the
-    prologue's table + batch kernel (GK_FWD_PL=0, the default), single steps and multi-step graphs,
-    with padded batch rows (80 of 96)."""
-    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=1, batch=batch, seq=8, seed=9)
-    stream = NameStream(cfg.batch, cfg.seq, seed=10)
-    batches = [stream.next() for _ in range(2 * G)]
-    runs = []
-    monkeypatch.setenv("GK_FWD_XP", "0")   # the prologue-table path this variant is bitwise equal to
-    for pl in ("1", "0"):
-        monkeypatch.setenv("GK_FWD_PL", pl)
-        tr = HipTrainer(cfg, params=init_params(cfg))
-        assert ("+pl" in tr.t.plan()) == (pl == "1"), tr.t.plan()
-        if G > 1:
-            tr.steps(batches[:G])
-            tr.steps(batches[G:])
-        else:
-            for x, y in batches:
-                tr.step(x, y)
-        torch.cuda.synchronize()
-        runs.append(tr)
-    a, b = runs
-    torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
-    assert a.loss() == b.loss()
-
-
-@pytest.mark.parametrize("H,B,padded", [(512, 256, False), (512, 64, False), (512, 40, True), (512, 96, True)])
-def test_forward_fc_pipeline_matches_fc_kernel(monkeypatch, H, B, padded):
-    """The top layer's forward with the FC / softmax-xent / dH pipeline inside the persistent launch
-    (GK_FWD_FC=1, opt-in; one layer at H = 512, V = 256) against the separate fc_xent kernel + dW_fc
-    product (GK_FWD_FC=0, the default): loss and every gradient agree to bf16 rounding of dl (the
-    softmax statistics are reduced in a different order), three Adam steps to 1e-2 (Adam turns
-    near-zero gradients into full-size steps); and against the fp64 oracle."""
-    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=1, batch=B, seq=8, seed=13)
-    params = init_params(cfg)
-    if padded:
-        batches = [make_padded_batch(synthetic_names(B, seed=s, max_len=10), cfg.seq) for s in (4, 5, 6)]
-    else:
-        st = NameStream(B, cfg.seq, seed=4)
-        batches = [st.next() for _ in range(3)]
-    res = {}
-    for fc in ("1", "0"):
-        monkeypatch.setenv("GK_FWD_FC", fc)
-        tr = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
-        assert ("+fc" in tr.t.plan()) == (fc == "1"), tr.t.plan()
-        tr.forward_backward(*batches[0])
-        loss, g = tr.loss(), {k: v.clone() for k, v in tr.grad_dict().items()}
-        tr2 = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
-        for x, y in batches:
-            tr2.step(x, y)
-        torch.cuda.synchronize()
-        res[fc] = (loss, g, tr2.state_dict(), tr2.loss())
-    (la, ga, sa, l2a), (lb, gb, sb, l2b) = res["1"], res["0"]
-    assert abs(la - lb) < 1e-4 * abs(lb), (la, lb)
-    for k in gb:
-        assert rel(ga[k], gb[k]) < 5e-3, f"{k}: {rel(ga[k], gb[k]):.2e}"
-    for k in sb:
-        assert rel(sa[k], sb[k]) < 1e-2, f"{k}: {rel(sa[k], sb[k]):.2e}"
-    assert abs(l2a - l2b) < 1e-3 * abs(l2b)
-    p64 = {k: v.double() for k, v in params.items()}
-    x, y = batches[0]
-    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
-    assert abs(la - float(ref_loss)) < 1e-2 * float(ref_loss)
-    for k in ref_g:
-        assert rel(ga[k], ref_g[k]) < 0.04, k
-
-
-@pytest.mark.parametrize("B,padded,G", [(256, False, 1), (96, True, 1), (64, False, 4)])
-def test_forward_input_projection_in_kernel(monkeypatch, B, padded, G):
-    """Layer 0's input projection inside the persistent forward (GK_FWD_XP=1, opt-in, H = E = 512:
-    Emb rows x W_ih0 in the post-publish slack, one step ahead, no P table) against the
-    prologue's P table (GK_FWD_XP=0): loss and gradients agree to fp32 summation order, a few Adam
-    steps (single and multi-step graphs) to Adam's sign sensitivity; and the fp64 oracle."""
-    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    cfg = GRUConfig(vocab=256, embed=512, hidden=512, layers=1, batch=B, seq=8, seed=21)
-    params = init_params(cfg)
-    if padded:
-        batches = [make_padded_batch(synthetic_names(B, seed=s, max_len=10), cfg.seq) for s in range(G + 1)]
-    else:
-        st = NameStream(B, cfg.seq, seed=22)
-        batches = [st.next() for _ in range(G + 1)]
-    res = {}
-    for xp in ("1", "0"):
-        monkeypatch.setenv("GK_FWD_XP", xp)
-        tr = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
-        assert ("+xp" in tr.t.plan()) == (xp == "1"), tr.t.plan()
-        tr.forward_backward(*batches[0])
-        loss, g = tr.loss(), {k: v.clone() for k, v in tr.grad_dict().items()}
-        tr2 = HipTrainer(cfg, params={k: v.clone() for k, v in params.items()})
-        if G > 1:
-            tr2.steps(batches[1:G + 1])
-        else:
-            tr2.step(*batches[1])
-        torch.cuda.synchronize()
-        res[xp] = (loss, g, tr2.state_dict())
-    (la, ga, sa), (lb, gb, sb) = res["1"], res["0"]
-    assert abs(la - lb) < 1e-4 * abs(lb), (la, lb)
-    for k in gb:
-        assert rel(ga[k], gb[k]) < 5e-3, f"{k}: {rel(ga[k], gb[k]):.2e}"
-    for k in sb:
-        assert rel(sa[k], sb[k]) < 1e-2, f"{k}: {rel(sa[k], sb[k]):.2e}"
-    p64 = {k: v.double() for k, v in params.items()}
-    x, y = batches[0]
-    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
-    assert abs(la - float(ref_loss)) < 1e-2 * float(ref_loss)
-    for k in ref_g:
-        assert rel(ga[k], ref_g[k]) < 0.04, k
 
 
 @pytest.mark.parametrize("G", [10, 19])
