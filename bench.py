@@ -35,7 +35,10 @@ def _launch_plan(K: int):
     timed region's synchronize is the only one whose host work the GPU does not hide -- ~20 us for a
     single step, ~5 us per step + 40 us for a group (staging G batches, launching ~8G nodes,
     profiles/r3s5_host_group_launch.txt) -- and every graph boundary costs ~12.8 us
-    (docs/DESIGN.md §6).  K = 20: 2 singles + 2 groups of 9; K = 300: 1 single + 23 groups of 13."""
+    (docs/DESIGN.md §6).  K = 20: 1 single + one group of 19; K = 300: 1 single + 13 groups of 23;
+    K < 2: single steps only."""
+    if K < 2:
+        return 1, 0
     best = None
     for lead in range(0, min(8, K - 1) + 1):
         rest = K - lead
@@ -86,6 +89,8 @@ def main() -> int:
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
+    if args.steps < 1:
+        ap.error("--steps must be >= 1")
 
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:

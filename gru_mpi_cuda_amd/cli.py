@@ -244,10 +244,11 @@ def main(argv=None) -> int:
     g.add_argument("-n", type=int, default=10)
     g.add_argument("--out", default=None, help="names, one per line (non-printables escaped)")
     g.add_argument("--raw-out", default=None, help="raw N x (MAX_LEN+1) output bytes")
-    g.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="bf16x3",
-                   help="bf16x3 (default): the reference's fp32 arithmetic on split-bf16 MFMA products "
-                        "(~2^-16 relative error, same names as the fp64 oracle as often as fp32, ~2x faster); "
-                        "fp32: plain fp32 products; bf16: MFMA fast mode")
+    g.add_argument("--precision", choices=["fp32", "bf16", "bf16x3"], default="fp32",
+                   help="fp32 (default): the reference's fp32 arithmetic (fp32 MFMA products); "
+                        "bf16x3: fp32 arithmetic on split-bf16 MFMA products (~2^-16 relative error per "
+                        "product, ~2x faster; parity with fp32 unpinned on near-tie samples); "
+                        "bf16: MFMA fast mode")
     g.add_argument("--preset", default="ref", help="dims for --fmt ref (headerless blob)")
     _add_model_args(g)
     g.set_defaults(seed=0)

@@ -38,6 +38,13 @@ struct State {
   std::unique_ptr<RcclComm> comm;
   hipStream_t s = nullptr;
   std::string uid_file;
+  // device buffers kept across namegen() calls (grown, never shrunk): the uniforms (the root holds
+  // all N * MAX_LEN, another rank its slice) and the output rows (the root all N, another rank its own)
+  float* rf = nullptr;
+  size_t rf_cap = 0;
+  unsigned char* out = nullptr;
+  size_t out_cap = 0;
+  long allocs = 0;   // device allocations made by namegen() (tests: none after the first call)
 };
 std::unique_ptr<State> S;
 
@@ -105,52 +112,56 @@ static void init_impl(int N, int rng_seed, char* parameter_fname) {
   g.V = st.d.V; g.E = st.d.E; g.H = st.d.H; g.L = st.d.L; g.max_len = st.d.max_len;
   g.sos = st.d.sos; g.eos = st.d.eos;
   g.max_batch = std::max(64, std::min(8192, (N + st.world - 1) / std::max(1, st.world)));
-  // the reference's arithmetic is fp32 (namegensf.cu:233-242, 294-333).  Default: bf16x3 (split-bf16
-  // products, fp32 everywhere else): the same names as the fp64 oracle as often as fp32 over 3 seeds
-  // x 2 reference-shaped presets (profiles/r3_gen_default_decision.jsonl) at 1.9x its speed.
-  // GK_GEN_PRECISION=fp32 selects plain fp32 products, bf16 the bf16 MFMA fast mode.
+  // the reference's arithmetic is fp32 (namegensf.cu:233-242, 294-333), and so is the default here.
+  // GK_GEN_PRECISION=bf16x3 selects split-bf16 products (fp32 everywhere else, ~2^-16 relative error
+  // per product, 1.9x faster at 4096 names; parity with fp32 on near-tie samples unpinned), bf16 the
+  // bf16 MFMA fast mode.
   const char* prec = std::getenv("GK_GEN_PRECISION");
-  g.fp32 = !prec ? 2 : std::string(prec) == "bf16" ? 0 : std::string(prec) == "fp32" ? 1 : 2;
+  g.fp32 = !prec ? 1 : std::string(prec) == "bf16" ? 0 : std::string(prec) == "bf16x3" ? 2 : 1;
   st.gen.reset(new Generator(g, st.params, offsets));
   st.gen->refresh_weights(st.s);
   HIP_CHECK(hipStreamSynchronize(st.s));   // the reference's MPI_Barrier (namegensf.cu:615)
 }
 
+template <class T>
+static T* ensure(T*& p, size_t& cap, size_t n, long& allocs) {
+  if (n > cap) {
+    if (p) HIP_CHECK(hipFree(p));
+    HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
+    cap = n;
+    ++allocs;
+  }
+  return p;
+}
+
+// namegensf.cu:627-890.  The root's uniforms reach every rank as that rank's slice only (grouped
+// ncclSend / ncclRecv: MPI_Scatter at cu:636, with the uneven remainder counts), the generated
+// rows come back to the root the same way (MPI_Gather at cu:889); the buffers persist across calls.
 static void namegen_impl(int N, float* random_floats, char* output) {
   if (!S) throw std::runtime_error("namegen: call namegen_initialize first");
   State& st = *S;
   const int ML = st.d.max_len;
-  int start = 0, count = 0;
-  shard(N, st.rank, st.world, &start, &count);
-  const int per = (N + st.world - 1) / st.world;
-  float* rf = nullptr;
-  unsigned char *slab = nullptr, *all = nullptr;
-  HIP_CHECK(hipMalloc(&rf, (size_t)std::max(N, 1) * ML * 4));
-  HIP_CHECK(hipMalloc(&slab, (size_t)std::max(per, 1) * (ML + 1)));
-  HIP_CHECK(hipMemsetAsync(slab, 0, (size_t)std::max(per, 1) * (ML + 1), st.s));
-  if (st.rank == 0) HIP_CHECK(hipMemcpyAsync(rf, random_floats, (size_t)N * ML * 4, hipMemcpyHostToDevice, st.s));
-  if (st.comm) st.comm->broadcast_f32(rf, (long)N * ML, 0, st.s);   // replaces MPI_Scatter (cu:636)
-  if (count > 0) st.gen->generate(rf + (size_t)start * ML, count, slab, st.s);
-  std::vector<unsigned char> host((size_t)st.world * per * (ML + 1));
-  if (st.comm) {                                                    // replaces MPI_Gather (cu:889)
-    HIP_CHECK(hipMalloc(&all, host.size()));
-    st.comm->allgather_u8(slab, all, (long)per * (ML + 1), st.s);
-    HIP_CHECK(hipMemcpyAsync(host.data(), all, host.size(), hipMemcpyDeviceToHost, st.s));
-  } else {
-    HIP_CHECK(hipMemcpyAsync(host.data(), slab, (size_t)per * (ML + 1), hipMemcpyDeviceToHost, st.s));
+  const bool root = st.rank == 0;
+  std::vector<long> cnt(st.world), dsp(st.world), ocnt(st.world), odsp(st.world);
+  for (int r = 0; r < st.world; ++r) {
+    int s0 = 0, c0 = 0;
+    shard(N, r, st.world, &s0, &c0);
+    cnt[r] = (long)c0 * ML; dsp[r] = (long)s0 * ML;
+    ocnt[r] = (long)c0 * (ML + 1); odsp[r] = (long)s0 * (ML + 1);
   }
+  const int me = st.rank;
+  const long my_names = cnt[me] / std::max(ML, 1);
+  float* rf = ensure(st.rf, st.rf_cap, std::max<size_t>(1, root ? (size_t)N * ML : (size_t)cnt[me]), st.allocs);
+  unsigned char* out = ensure(st.out, st.out_cap, std::max<size_t>(1, root ? (size_t)N * (ML + 1) : (size_t)ocnt[me]),
+                              st.allocs);
+  if (root && N > 0) HIP_CHECK(hipMemcpyAsync(rf, random_floats, (size_t)N * ML * 4, hipMemcpyHostToDevice, st.s));
+  if (st.comm) st.comm->scatterv_f32(rf, cnt.data(), dsp.data(), rf, 0, st.s);
+  // the root's slice sits at its displacement of the full buffer; another rank's at offset 0
+  const size_t in_off = root ? (size_t)dsp[me] : 0, out_off = root ? (size_t)odsp[me] : 0;
+  if (my_names > 0) st.gen->generate(rf + in_off, (int)my_names, out + out_off, st.s);
+  if (st.comm) st.comm->gatherv_u8(out, ocnt.data(), odsp.data(), out, 0, st.s);
+  if (root && N > 0) HIP_CHECK(hipMemcpyAsync(output, out, (size_t)N * (ML + 1), hipMemcpyDeviceToHost, st.s));
   HIP_CHECK(hipStreamSynchronize(st.s));
-  if (st.rank == 0) {
-    std::memset(output, 0, (size_t)N * (ML + 1));
-    for (int r = 0; r < st.world; ++r) {
-      int s0 = 0, c0 = 0;
-      shard(N, r, st.world, &s0, &c0);
-      std::memcpy(output + (size_t)s0 * (ML + 1), host.data() + (size_t)r * per * (ML + 1), (size_t)c0 * (ML + 1));
-    }
-  }
-  (void)hipFree(rf);
-  (void)hipFree(slab);
-  if (all) (void)hipFree(all);
 }
 
 static void finalize_impl() {
@@ -159,6 +170,8 @@ static void finalize_impl() {
   st.gen.reset();
   st.comm.reset();
   if (st.params) (void)hipFree(st.params);
+  if (st.rf) (void)hipFree(st.rf);
+  if (st.out) (void)hipFree(st.out);
   if (st.s) (void)hipStreamDestroy(st.s);
   if (st.rank == 0 && !st.uid_file.empty()) std::remove(st.uid_file.c_str());
   S.reset();
@@ -167,6 +180,7 @@ static void finalize_impl() {
 extern "C" int namegen_rank(void) { return S ? S->rank : launch_env().rank; }
 extern "C" int namegen_world(void) { return S ? S->world : launch_env().world; }
 extern "C" int namegen_max_len(void) { return S ? S->d.max_len : 0; }
+extern "C" long namegen_device_allocs(void) { return S ? S->allocs : 0; }
 
 // C boundary: like the reference's CUDA_CALL, report and exit instead of unwinding into C
 static void fatal(const std::exception& e) {

@@ -29,6 +29,7 @@ void namegen_finalize(void);
 int namegen_rank(void);
 int namegen_world(void);
 int namegen_max_len(void);
+long namegen_device_allocs(void);   /* device allocations made by namegen() so far (buffers persist) */
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,30 @@ void RcclComm::allgather_u16(const unsigned short* send, unsigned short* recv, l
 void RcclComm::allgather_f32(const float* send, float* recv, long n, hipStream_t s) {
   RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclFloat32, C(live()), s));
 }
+void RcclComm::scatterv_f32(const float* send, const long* count, const long* displ, float* recv, int root,
+                            hipStream_t s) {
+  ncclComm_t c = C(live());
+  RCCL_CHECK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < world_; ++r)
+      if (r != root && count[r] > 0) RCCL_CHECK(ncclSend(send + displ[r], (size_t)count[r], ncclFloat32, r, c, s));
+  } else if (count[rank_] > 0) {
+    RCCL_CHECK(ncclRecv(recv, (size_t)count[rank_], ncclFloat32, root, c, s));
+  }
+  RCCL_CHECK(ncclGroupEnd());
+}
+void RcclComm::gatherv_u8(const unsigned char* send, const long* count, const long* displ, unsigned char* recv,
+                          int root, hipStream_t s) {
+  ncclComm_t c = C(live());
+  RCCL_CHECK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < world_; ++r)
+      if (r != root && count[r] > 0) RCCL_CHECK(ncclRecv(recv + displ[r], (size_t)count[r], ncclUint8, r, c, s));
+  } else if (count[rank_] > 0) {
+    RCCL_CHECK(ncclSend(send, (size_t)count[rank_], ncclUint8, root, c, s));
+  }
+  RCCL_CHECK(ncclGroupEnd());
+}
 int RcclComm::count() const {
   int n = 0;
   RCCL_CHECK(ncclCommCount(C(live()), &n));

@@ -31,6 +31,13 @@ class RcclComm {
   // recv[world*n] = concat over ranks of send[n]; bf16 payload moved as 16-bit words
   void allgather_u16(const unsigned short* send, unsigned short* recv, long n, hipStream_t s);
   void allgather_f32(const float* send, float* recv, long n, hipStream_t s);
+  // MPI_Scatterv / MPI_Gatherv as grouped point-to-point transfers (one group launch): rank r's
+  // slice is [displ[r], displ[r] + count[r]) elements of the root's buffer.  Scatter: the root sends
+  // every other rank its slice into that rank's recv (the root's own slice stays where it is);
+  // gather: every other rank sends its send[0 .. count[rank]) into the root's recv at displ[r].
+  void scatterv_f32(const float* send, const long* count, const long* displ, float* recv, int root, hipStream_t s);
+  void gatherv_u8(const unsigned char* send, const long* count, const long* displ, unsigned char* recv, int root,
+                  hipStream_t s);
   int count() const;                  // ncclCommCount: ranks the communicator really has
   // watchdog hook: raises if the communicator reported an asynchronous error
   void check_async_error();

@@ -48,14 +48,19 @@ DEV bf16x8 ld8_sc1s(rsrc_t r, unsigned voff, int soff) {
 // Every cross-workgroup wait is bounded by WALL CLOCK, not by a poll count: workgroups that start
 // late because something else holds their CUs (an RCCL kernel of a data-parallel step waiting for a
 // slow peer, another process's kernel) delay the wait without tripping it.  5 s of the 100 MHz
-// s_memrealtime counter, checked every 64 polls; past it the wait sets the error word and gives up
-// (the step's update is skipped on every rank and the watchdog reports it).
+// s_memrealtime counter, checked every 64 polls; past it the wait sets bit 1 of the error word and
+// gives up (the step's update is skipped on every rank and the watchdog reports it).  Bit 1 is also
+// the give-up signal: every later wait of the launch (any workgroup) sees it at its next check and
+// returns at once, so a grid that is truly not co-resident drains in one budget, not one per wait.
 static constexpr unsigned long long kSpinTicks = 500000000ull;
 struct SpinBudget {
+  const unsigned* err;
   unsigned long long t0 = 0;
   unsigned n = 0;
+  DEV explicit SpinBudget(const unsigned* e) : err(e) {}
   DEV bool expired() {
     if ((n++ & 63u) != 0u) return false;
+    if (err && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) return true;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     if (!t0) { t0 = now; return false; }
     return now - t0 > kSpinTicks;
@@ -73,7 +78,7 @@ static constexpr int kFlagStride = 16;   // uints (64 B)
 DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* err) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    SpinBudget spin;
+    SpinBudget spin(err);
     for (;;) {
       bool ok = true;
       if (lane < nprod) ok = __hip_atomic_load(flags + lane * kFlagStride, __ATOMIC_RELAXED,
@@ -94,7 +99,7 @@ DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* 
 // H/16 producers.  The acquire-at-wavefront fence only pins the following sc1 loads below
 // the poll (no instruction is emitted).
 DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch, unsigned* err) {
-  SpinBudget spin;
+  SpinBudget spin(err);
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
@@ -118,7 +123,7 @@ DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned e
                         LoadK&& loadk) {
   constexpr unsigned all = (1u << NK) - 1u;
   unsigned loaded = 0;
-  SpinBudget spin;
+  SpinBudget spin(err);
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
@@ -155,7 +160,7 @@ DEV void wave_wait_load2(const unsigned* fa, const unsigned* fb, int prod0, unsi
   const unsigned* f = (lane < 32 ? fa : fb) + (size_t)(prod0 + (lane & 31)) * kFlagStride;
   const unsigned ep = lane < 32 ? ea : eb;
   unsigned da = 0, db = 0;
-  SpinBudget spin;
+  SpinBudget spin(err);
   for (;;) {
     bool ok = true;
     if (active) ok = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ep;
@@ -238,7 +243,7 @@ DEV bool row_block_local(unsigned* flags /* the row block's producer lines */, i
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     unsigned v = id + 1u;
-    SpinBudget spin;
+    SpinBudget spin(err);
     for (;;) {
       if (lane < nunit) v = __hip_atomic_load(flags + lane * kFlagStride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__all(v != 0u)) break;

@@ -34,19 +34,19 @@ _MODE = {"bf16": 0, "fp32": 1, "bf16x3": 2}   # GenDims::fp32
 
 
 class HipGenerator:
-    """precision "bf16x3" (default): the fp32-faithful path (IEEE gates and softmax, the reference's
-    arithmetic, namegensf.cu:233-242, 294-333) with its products as bf16 MFMA GEMMs over split
-    operands (x = hi + lo, hi*hi + hi*lo + lo*hi in fp32: ~2^-16 relative error per product, at the
-    bf16 MFMA rate x 1/3).  It names exactly what the fp64 oracle names as often as "fp32" does
-    (100 % over 3 seeds x 2 reference-shaped presets, profiles/r3_gen_default_decision.jsonl) at
-    1.9x its speed at 4096 names;
-    "fp32": fp32 MFMA GEMMs on the fp32 master weights;
+    """precision "fp32" (default): the reference's arithmetic (namegensf.cu:233-242, 294-333) --
+    fp32 MFMA GEMMs on the fp32 master weights, IEEE gates and softmax;
+    "bf16x3": the same with its products as bf16 MFMA GEMMs over split operands (x = hi + lo,
+    hi*hi + hi*lo + lo*hi in fp32: ~2^-16 relative error per product, 1.9x the fp32 speed at 4096
+    names).  Opt-in: 2400 names (profiles/r3_gen_default_decision.jsonl) matched the fp64 oracle
+    as often as fp32, but that sample cannot separate a 2^-16 product error from fp32 on near-tie
+    samples (parity unpinned);
     "bf16": bf16 MFMA fast mode (fused step kernels, bf16 weight copies).
     Small batches run the exact fp32 persistent kernel in both fp32 modes."""
 
     def __init__(self, cfg: GRUConfig, params: Dict[str, torch.Tensor], max_batch: int = 4096,
                  device: Optional[torch.device] = None, flat: Optional[torch.Tensor] = None,
-                 precision: str = "bf16x3"):
+                 precision: str = "fp32"):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         self.precision = precision
@@ -102,9 +102,9 @@ _S: Optional[_State] = None
 
 
 def namegen_initialize(N: int, rng_seed: int, parameter_fname: str, cfg: Optional[GRUConfig] = None,
-                       fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "bf16x3") -> None:
+                       fmt: str = "auto", ctx: Optional[DistCtx] = None, precision: str = "fp32") -> None:
     """namegensf.cu:359-618.  ``rng_seed`` is accepted and unused, as in the reference.
-    ``precision``: "bf16x3" (split-bf16 products, default), "fp32" or "bf16" (fast mode) on the GPU
+    ``precision``: "fp32" (default), "bf16x3" (split-bf16 products) or "bf16" (fast mode) on the GPU
     path (see HipGenerator); the CPU path is the fp32 oracle."""
     global _S
     from ..parallel import dist as gdist

@@ -713,3 +713,55 @@ def test_multi_step_graph_with_rccl_world1(G):
     assert a.t.graph_steps() == G
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
     assert a.loss() == b.loss()
+
+
+def test_bench_shape_matches_oracle_and_cpu_adam():
+    """The headline configuration exactly as bench.py runs it: preset h512 --
+    B = 256, T = 32, E = H = 512, V = 256 -- on the default plan (persistent forward / backward with
+    the fused dW_hh / dP partials, 8 XCD-local row blocks, a T-deep backward exchange).
+      * one step's loss and every gradient against the fp64 manual-BPTT oracle;
+      * three Adam steps against CpuTrainer (fp32): per-step losses and the parameter updates;
+      * the driver's K = 20 launch plan (bench._launch_plan: 1 single-step graph + one 19-step graph)
+        bitwise equal to 20 single-step launches."""
+    from bench import _launch_plan
+    from gru_mpi_cuda_amd.config import preset
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer, CpuTrainer
+    cfg = preset("h512")
+    assert (cfg.batch, cfg.seq, cfg.embed, cfg.hidden, cfg.vocab, cfg.layers) == (256, 32, 512, 512, 256, 1)
+    params = init_params(cfg)
+    ds = NameStream(cfg.batch, cfg.seq, seed=1000)
+    batches = [ds.next() for _ in range(20)]
+    tr = HipTrainer(cfg, params=params)
+    plan = tr.t.plan()
+    assert plan.startswith("fwd=persistent") and "bwd0=persistent+dWhh+dP" in plan, plan
+    x, y = batches[0]
+    tr.forward_backward(x, y)
+    g = tr.grad_dict()
+    p64 = {k: v.double() for k, v in params.items()}
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
+    for k in ref_g:
+        e = rel(g[k], ref_g[k])
+        assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
+    # three Adam steps against the fp32 CPU trainer
+    gt, ct = HipTrainer(cfg, params=params), CpuTrainer(cfg, params=params)
+    for xb, yb in batches[:3]:
+        gt.step(xb, yb)
+        ct.step(xb, yb)
+        assert abs(gt.loss() - ct.loss()) < 1e-2 * ct.loss(), (gt.loss(), ct.loss())
+    sd_g, sd_c = gt.state_dict(), ct.state_dict()
+    for k in sd_c:
+        e = rel(sd_g[k] - params[k], sd_c[k] - params[k])
+        assert e < 0.1, f"{k}: Adam update rel err {e:.4f}"
+    # the driver's launch plan for K = 20
+    G, lead = _launch_plan(20)
+    assert (G, lead) == (19, 1)
+    a, b = HipTrainer(cfg, params=params), HipTrainer(cfg, params=params)
+    a.step(*batches[0])
+    a.steps(batches[1:])
+    for xb, yb in batches:
+        b.step(xb, yb)
+    torch.cuda.synchronize()
+    assert a.t.graph_steps() == 19
+    assert torch.equal(a.params, b.params) and a.loss() == b.loss()
+    assert a.t.read_error() == 0
