@@ -46,6 +46,11 @@ class GRUConfig:
     seed: int = 1234
     carry_hidden: bool = False  # truncated BPTT over a continuous stream: each step starts from the
                                 # previous step's final (detached) hidden state
+    keep_grads: bool = False    # after a one-graph step(), leave the step's full gradient in the grad
+                                # buffer (grad_dict); off, the fused optimiser sums the split-K /
+                                # row-block partials of a tensor in registers and does not write them
+                                # back (7 MB fewer bytes per headline step).  forward_backward() always
+                                # leaves the gradient.
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
     shard_optim: bool = False   # data-parallel ZeRO-1 step: reduce-scatter the gradient, Adam on the

@@ -89,6 +89,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
   // split-K slab: large enough for every weight-gradient product it serves
+  constexpr int kSlots = 2 + 2 * kMaxGroup;   // per-step pair + two multi-step groups
+  size_t o_dst = R((size_t)kSlots * slot_ints() * 4);
   const size_t wmax = std::max({(size_t)V * H, (size_t)3 * H * H, (size_t)V * 3 * H, (size_t)3 * H * E});
   size_t o_sw = R((size_t)splits_ * wmax * 4);
   size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
@@ -111,6 +113,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_skp = sk ? R((size_t)sk_part_floats_ * 4) : 0, o_skc = sk ? R((size_t)sk_cnt_words_ * 4) : 0;
   (void)any_bwd;
   arena_.commit();   // zero-filled: HS[0] = h_init = 0, HT columns [0,Bp) = 0
+  d_stage_ = arena_.get<int>(o_dst);
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
   slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
   slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
@@ -160,7 +163,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   events_.resize(64 + 8 * C_ * L);
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  constexpr int kSlots = 2 + 2 * kMaxGroup;   // per-step pair + two multi-step groups
+  HIP_CHECK(hipStreamCreateWithFlags(&sx_, hipStreamNonBlocking));
   HIP_CHECK(hipHostMalloc(&h_stage_, kSlots * (2 * tok + 16) * sizeof(int)));
   std::memset(h_stage_, 0, kSlots * (2 * tok + 16) * sizeof(int));
   // The staging events only tell the host that the graph which read a pinned slot has finished;
@@ -174,6 +177,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   for (auto& e : group_done_) {
     HIP_CHECK(hipEventCreateWithFlags(&e, stage_flags));
     HIP_CHECK(hipEventRecord(e, s0_));
+  }
+  for (auto* ev : {&copy_done_[0], &copy_done_[1], &group_copy_done_[0], &group_copy_done_[1]}) {
+    HIP_CHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(*ev, sx_));
   }
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocCoherent | hipHostMallocMapped));
   std::memset(err_host_, 0, 64);
@@ -192,11 +199,14 @@ Trainer::~Trainer() {
   for (auto& g : g_group_) g.reset();
   for (auto& e : stage_done_) if (e) (void)hipEventDestroy(e);
   for (auto& e : group_done_) if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {copy_done_[0], copy_done_[1], group_copy_done_[0], group_copy_done_[1]})
+    if (e) (void)hipEventDestroy(e);
   wd_.reset();   // the watchdog thread reads err_host_
   if (h_stage_) (void)hipHostFree(h_stage_);
   if (err_host_) (void)hipHostFree(err_host_);
   if (s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
+  if (sx_) (void)hipStreamDestroy(sx_);
   if (sc_) (void)hipStreamDestroy(sc_);
 }
 
@@ -270,13 +280,22 @@ void Trainer::refresh_weights(hipStream_t s) {
 void Trainer::set_batch(const int* x, const int* y, int B, hipStream_t s) {
   if (B > Bp_ || B <= 0) throw std::runtime_error("set_batch: batch larger than the trainer was built for");
   (void)s;
-  // Batch-major ids/labels are written into a pinned staging slot; the step graph captured
-  // against that slot reads it zero-copy in its first kernel (prep_batch: transpose + pad), so
-  // there is no SDMA copy and no per-element host transpose.  The slot is reused only after
-  // the graph that last read it has completed (stage_done_, recorded after each launch).
+  // Batch-major ids/labels are written into a pinned staging slot and copied to the device slot by
+  // one DMA on the copy stream, off the step's critical path; the step graph captured against that
+  // slot reads the device copy in its first kernel (prep_batch: transpose + pad).  The slot pair is
+  // reused only after the graph that last read it has completed (stage_done_, recorded after each
+  // launch), which also means its copy is done.
   const int slot = (stage_slot_ ^= 1);
   HIP_CHECK(hipEventSynchronize(stage_done_[slot]));
   fill_slot(slot, x, y, B);
+  copy_slots(slot, 1, copy_done_[slot]);
+}
+
+void Trainer::copy_slots(int first, int n, hipEvent_t done) {
+  const size_t off = (size_t)first * slot_ints();
+  HIP_CHECK(hipMemcpyAsync(d_stage_ + off, h_stage_ + off, (size_t)n * slot_ints() * sizeof(int),
+                           hipMemcpyHostToDevice, sx_));
+  HIP_CHECK(hipEventRecord(done, sx_));
 }
 
 void Trainer::fill_slot(int slot, const int* x, const int* y, int B) {
@@ -491,6 +510,7 @@ OptimArgs Trainer::optim_args() const {
   a.err = err_; a.err_host = err_host_dev_;
   a.lr = o_.lr; a.b1 = o_.b1; a.b2 = o_.b2; a.eps = o_.eps; a.wd = o_.wd; a.sgd = o_.sgd;
   a.sched = o_.sched; a.warmup = o_.warmup; a.total = o_.total; a.lr_min = o_.lr_min;
+  a.keep_g = o_.keep_grads;
   return a;
 }
 
@@ -592,7 +612,8 @@ void Trainer::record_opt(hipStream_t s) {
 void Trainer::forward_backward(hipStream_t s) {
   GK_TRACE("gk.forward_backward");
   const int slot = stage_slot_;
-  stage_src_ = h_stage_ + (size_t)slot * slot_ints();
+  stage_src_ = dev_slot(slot);
+  HIP_CHECK(hipStreamWaitEvent(s, copy_done_[slot], 0));
   if (!use_graph_) {
     // eager: run on the internal streams, ordered after / before the caller's stream
     hipEvent_t a = events_.back();
@@ -712,7 +733,8 @@ void Trainer::step(hipStream_t s) {
     return;
   }
   const int slot = stage_slot_;
-  stage_src_ = h_stage_ + (size_t)slot * slot_ints();
+  stage_src_ = dev_slot(slot);
+  HIP_CHECK(hipStreamWaitEvent(s, copy_done_[slot], 0));
   Graph& g = g_step_[slot];
   if (!g.ready()) {
     GK_TRACE("gk.capture_step_graph");
@@ -749,6 +771,7 @@ void Trainer::set_batches(const int* x, const int* y, int B, int n) {
   HIP_CHECK(hipEventSynchronize(group_done_[gp]));   // the group graph that last read these slots is done
   const size_t per = (size_t)B * d_.T;
   for (int j = 0; j < n; ++j) fill_slot(group_slot(gp, j), x + j * per, y + j * per, B);
+  copy_slots(group_slot(gp, 0), n, group_copy_done_[gp]);   // the group's slots are contiguous
 }
 
 void Trainer::step_group(hipStream_t s) {
@@ -761,7 +784,7 @@ void Trainer::step_group(hipStream_t s) {
     g.begin(s0_);
     try {
       for (int j = 0; j < group_; ++j) {
-        stage_src_ = h_stage_ + (size_t)group_slot(gp, j) * slot_ints();
+        stage_src_ = dev_slot(group_slot(gp, j));
         record_step_body();
       }
     } catch (...) {
@@ -775,6 +798,7 @@ void Trainer::step_group(hipStream_t s) {
     }
     g.end(s0_);
   }
+  HIP_CHECK(hipStreamWaitEvent(s, group_copy_done_[gp], 0));
   g.launch(s);
   HIP_CHECK(hipEventRecord(group_done_[gp], s));
   if (wd_) wd_->watch(group_done_[gp]);

@@ -31,6 +31,7 @@ struct OptCfg {
   int sgd = 0;
   int sched = 0, warmup = 0, total = 0;   // OptimArgs::sched / warmup / total
   float lr_min = 0.f;
+  int keep_grads = 1;   // OptimArgs::keep_g
 };
 
 class Trainer {
@@ -92,14 +93,22 @@ class Trainer {
   Graph g_fb_[2], g_opt_;          // one forward/backward graph per staging slot
   bool use_graph_ = true;
   bool overlap_ = true;
-  // pinned host staging, 2 slots of [16 hdr][Bp*T x][Bp*T y] (batch-major); the step graph's
-  // first kernel reads its slot zero-copy.  Graph k is captured against slot k.
+  // batch staging, slots of [16 hdr][Bp*T x][Bp*T y] (batch-major): the host fills a pinned slot,
+  // one DMA on the copy stream sx_ moves it to the same slot of the device staging d_stage_ while the
+  // previous graph still runs, and the step graph's first kernel reads the DEVICE slot (no pinned
+  // host memory read inside a step).  Graph k is captured against slot k.
   int* h_stage_ = nullptr;
+  int* d_stage_ = nullptr;
+  hipStream_t sx_ = nullptr;
   hipEvent_t stage_done_[2] = {nullptr, nullptr};
+  hipEvent_t copy_done_[2] = {nullptr, nullptr};       // per-step slots 0, 1 reached the device
+  hipEvent_t group_copy_done_[2] = {nullptr, nullptr}; // a multi-step slot group reached the device
   int stage_slot_ = 0;
-  const int* stage_src_ = nullptr;   // slot the graph being recorded reads
+  const int* stage_src_ = nullptr;   // device slot the graph being recorded reads
   size_t slot_ints() const { return 16 + 2 * (size_t)Bp_ * d_.T; }
+  const int* dev_slot(int slot) const { return d_stage_ + (size_t)slot * slot_ints(); }
   void fill_slot(int slot, const int* x, const int* y, int B);
+  void copy_slots(int first, int n, hipEvent_t done);   // pinned -> device, on sx_
   // single-graph step (prep + fwd/bwd + in-graph RCCL all-reduce + optimiser)
   Graph g_step_[2];
   Graph g_group_[2];
@@ -208,6 +217,7 @@ class Trainer {
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
   int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks)
+  bool top_dy_bf16_ = false;     // the recorded step's fc_xent writes the top layer's dy in bf16
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }

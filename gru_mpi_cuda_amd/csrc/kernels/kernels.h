@@ -139,6 +139,7 @@ void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s);
 
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
+  const u16* dyb = nullptr;        // [T][Bp][H] bf16 alternative to dy (the top layer under fc_xent's bf16 dH)
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
@@ -177,6 +178,7 @@ struct FcXentArgs {
   // fused dH = dlogits · W_fc (nullable): dy [M][H] fp32 from WT = W_fc^T [H][V] bf16
   const u16* WT = nullptr;
   float* dy = nullptr;
+  int dy_bf16 = 0;                 // 8-wave V = 256 kernel: dy holds bf16 [M][H] instead of fp32
   int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
   // FT-layout copies of W [V][H] and W^T [H][V] (ft_offset): required by the 8-wave V = 256 kernel
   const u16* Wf = nullptr;
@@ -343,6 +345,9 @@ struct OptimArgs {
   // at step `total` (models/cpu_ref.py lr_at is the host twin)
   int sched = 0, warmup = 0, total = 0;
   float lr_min = 0.f;
+  // 1: a gradient summed from slabs (OptCastJob::gsl) is also written to g (observable); 0: it stays
+  // in registers (the one-graph step without GRUConfig.keep_grads)
+  int keep_g = 1;
 };
 void adam_step(const OptimArgs& a, hipStream_t s);
 void bump_step(int* step, hipStream_t s);

@@ -1,12 +1,10 @@
-// Device-side optimiser pieces shared by the standalone Adam/cast launch (misc.hip) and the fused
-// step-tail kernel (tail.hip): the learning-rate schedule, the step error-word gate, the
-// deterministic split-K slab sum and the Adam/SGD update of float4 groups.
+// Device-side optimiser pieces of the fused Adam/cast launch (misc.hip): the learning-rate schedule,
+// the step error-word gate, the deterministic split-K slab sum and the Adam/SGD update of float4
+// groups.
 //
-// SC1 = true: every gradient / slab load is an L1-bypassing `sc1` buffer load.  The tail kernel
-// produces some gradients inside the same launch (written by other workgroups with sc1 stores,
-// published through an agent-scope counter): MI355X_MICROARCH.md 'Valid forms' row 1 -- sc1
-// stores, one atomic add per producing workgroup after every storing wave's vmcnt(0), an sc1 poll,
-// then sc1 loads only.
+// SC1 = true: every gradient / slab load is an L1-bypassing `sc1` buffer load, for a gradient
+// produced inside the same launch by other workgroups (sc1 stores published through an agent-scope
+// counter: MI355X_MICROARCH.md 'Valid forms' row 1).  The standalone launch uses SC1 = false.
 #pragma once
 #include "common.h"
 
@@ -99,7 +97,7 @@ DEV float4 job_grad4(const OptimArgs& a, const OptCastJob& J, long i) {
   }
   const long n = J.R ? (long)J.R * J.C : (long)J.C;
   const float4 g = sum_slabs4<SC1>(J.gsl, n, J.nsl, (size_t)(i * 4 - J.off));
-  reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
+  if (a.keep_g) reinterpret_cast<float4*>(const_cast<float*>(a.g))[i] = g;
   return g;
 }
 

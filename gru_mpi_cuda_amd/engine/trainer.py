@@ -64,7 +64,8 @@ class HipTrainer:
         opt = dict(lr=cfg.lr, beta1=cfg.beta1, beta2=cfg.beta2, eps=cfg.eps,
                    weight_decay=cfg.weight_decay, clip_norm=cfg.clip_norm,
                    sgd=int(cfg.optimizer == "sgd"), lr_sched=LR_SCHEDS.index(cfg.lr_sched),
-                   warmup_steps=cfg.warmup_steps, total_steps=cfg.total_steps, lr_min=cfg.lr_min)
+                   warmup_steps=cfg.warmup_steps, total_steps=cfg.total_steps, lr_min=cfg.lr_min,
+                   keep_grads=int(cfg.keep_grads))
         self.t = self.C.Trainer(dims, opt, self.params.data_ptr(), self.grads.data_ptr(),
                                 self.m.data_ptr(), self.v.data_ptr(), self.layout.total, offsets)
         self.t.set_use_graph(use_graph)

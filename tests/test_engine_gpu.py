@@ -529,7 +529,8 @@ def test_one_graph_step_equals_phased_step(layers, H, B, opt):
     partials) to the fused Adam launch; the phased path (forward_backward, then optimizer_step)
     reduces them first.  Same partials, same summation order: bitwise-equal weights and grads."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
-    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=12, optimizer=opt)
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=8, seed=12, optimizer=opt,
+                    keep_grads=True)
     params = init_params(cfg)
     ds = NameStream(B, cfg.seq, seed=2)
     batches = [ds.next() for _ in range(3)]
@@ -542,6 +543,12 @@ def test_one_graph_step_equals_phased_step(layers, H, B, opt):
     torch.cuda.synchronize()
     assert torch.equal(a.grads, b.grads)
     assert torch.equal(a.params, b.params)
+    # without keep_grads the fused optimiser does not write the summed partials back: same update
+    c = HipTrainer(cfg.replace(keep_grads=False), params=params)
+    for x, y in batches:
+        c.step(x, y)
+    torch.cuda.synchronize()
+    assert torch.equal(c.params, b.params)
 
 
 @pytest.mark.parametrize("layers,V,E,H,B,T", [(1, 256, 40, 96, 5, 7), (3, 256, 64, 160, 33, 5),
@@ -620,7 +627,8 @@ def test_trainer_lr_schedule_matches_cpu():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.models.cpu_ref import lr_at
     cfg = GRUConfig(vocab=256, embed=128, hidden=256, layers=1, batch=64, seq=8, lr=5e-2, seed=2,
-                    optimizer="sgd", lr_sched="cosine", warmup_steps=2, total_steps=6, lr_min=5e-3)
+                    optimizer="sgd", lr_sched="cosine", warmup_steps=2, total_steps=6, lr_min=5e-3,
+                    keep_grads=True)
     params = init_params(cfg)
     ds = NameStream(cfg.batch, cfg.seq, seed=5)
     tr = HipTrainer(cfg, params=params)
