@@ -86,6 +86,8 @@ def main() -> int:
                          "costs (_launch_plan: a few single-step launches first, so the first launch after "
                          "the timed region's synchronize is cheap, then groups).  Reported as graph_steps "
                          "and lead_single_steps.")
+    ap.add_argument("--variant", action="append", default=[], metavar="KEY=INT",
+                    help="large-H step-kernel variant (StepLdsVariants field, kernels.h), for A/B runs; repeatable")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -129,6 +131,9 @@ def main() -> int:
 
     if args.impl == "hip":
         from gru_mpi_cuda_amd.engine.trainer import make_trainer
+        if args.variant and ctx.device.type == "cuda":
+            from gru_mpi_cuda_amd.ops import load_ext
+            load_ext().set_step_lds_variants({k: int(v) for k, v in (x.split("=", 1) for x in args.variant)})
         from gru_mpi_cuda_amd.parallel.rccl import make_comm
         comm = make_comm(ctx) if ctx.device.type == "cuda" else None
         if comm is None and args.rccl_self and ctx.device.type == "cuda":

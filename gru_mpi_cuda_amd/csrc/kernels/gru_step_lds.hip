@@ -818,11 +818,24 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) 
   static_assert(!PF || S == 4, "prefetch holds one epilogue quarter");
   __shared__ __attribute__((aligned(16))) u16 lds[NS][256 * 64];
   const int H = a.H, H3 = 3 * a.H;
-  // block -> (tile, split): the S splits of a tile are 8 blocks apart (one XCD under the
-  // dispatcher's round-robin placement: a speed choice, the exchange does not depend on it)
+  // block -> (tile, split), a speed choice only (the exchange does not depend on placement):
+  //  sk_map 0: the S splits of a tile are 8 blocks apart (one XCD under the dispatcher's round-robin
+  //            placement): an XCD streams 2 unit tiles x every row tile over ALL of K (9 MB at B = 512,
+  //            H = 2048 -- more than its 4 MB L2);
+  //  sk_map 1: XCD x (= bid % 8) takes split x % S of every row tile of 1/(8/S) of the unit tiles:
+  //            one K-slice of the operands (4.5 MB), the S partners of a tile on S different XCDs.
   const int bid = blockIdx.x;
-  const int split = (bid >> 3) % S, tile = (bid / (8 * S)) * 8 + (bid & 7);
   const int ntu = H / 128;
+  int split, tile;
+  if (a.sk_map == 1) {
+    const int ntr = a.Bp / 128, x = bid & 7, i = bid >> 3, G = 8 / S;
+    split = x % S;
+    const int ut = i / ntr + (ntu / G) * (x / S), rt = i % ntr;
+    tile = rt * ntu + ut;
+  } else {
+    split = (bid >> 3) % S;
+    tile = (bid / (8 * S)) * 8 + (bid & 7);
+  }
   const int j0 = (tile % ntu) * 128, b0 = (tile / ntu) * 128;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;             // K loop: wave = 64 rows x 32 units
@@ -1068,10 +1081,14 @@ void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
   if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
-      const bool pf = step_lds_variants().bwd_sk_pf != 0;
-      if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, a);
-      else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, a);
+      const StepLdsVariants& v = step_lds_variants();
+      const bool pf = v.bwd_sk_pf != 0;
+      BwdStepArgs b = a;
+      // the across-XCD order needs whole unit-tile groups per XCD
+      b.sk_map = (v.bwd_sk_map == 1 && (a.H / 128) % (8 / S) == 0) ? 1 : 0;
+      if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, b);
+      else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, b);
+      else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, b);
       return;
     }
   }

@@ -61,6 +61,7 @@ struct BwdStepArgs {
   long sk_part_floats = 0;
   unsigned* sk_cnt = nullptr;
   long sk_cnt_words = 0;
+  int sk_map = 0;                  // block -> (tile, split) order (gru_bwd_step_sk_kernel)
   unsigned* err = nullptr;
 };
 void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
@@ -78,6 +79,7 @@ struct StepLdsVariants {
   int fwd64_fused = 1;   // the 64-row tile also for the fused input phase (layers >= 1 of generation)
   int fwd64_all = 0;     // the 64-row tile also on grids of >= 512 128-row tiles (2-deep 128-row kernel otherwise)
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
+  int bwd_sk_map = 0;    // split-K backward block order: 0 splits of a tile on one XCD, 1 splits across XCDs
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
 };
 StepLdsVariants& step_lds_variants();

@@ -261,7 +261,7 @@ def test_fwd_step_fused_64row(step_variants, H, Bp):
     test_fwd_step(step_variants, "fused", H, Bp, 2)
 
 
-@pytest.mark.parametrize("var", [dict(bwd_sk_pf=1), dict(bwd_sk_pf=0)])
+@pytest.mark.parametrize("var", [dict(bwd_sk_pf=1), dict(bwd_sk_pf=0), dict(bwd_sk_pf=1, bwd_sk_map=1)])
 @pytest.mark.parametrize("first", [False, True])
 def test_bwd_step_sk_variants(step_variants, first, var):
     step_variants.set_step_lds_variants(var)
