@@ -407,7 +407,7 @@ def test_reduce_slabs_cast(ext, R, C, splits):
     (768, 512, 2048, 4, False, False, 0, True), (1024, 1024, 3072, 1, False, True, 0, False),
     (512, 256, 4096, 8, False, False, 64, True), (2304, 1280, 576, 1, True, True, 32, False),
     (1536, 512, 8192, 4, False, False, 0, True), (512, 768, 1024, 1, False, False, 0, True)])
-@pytest.mark.parametrize("mfma", ["16", "32"])
+@pytest.mark.parametrize("mfma", ["16", "32", "r"])
 def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, rowsum, mfma):
     """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
     operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
