@@ -28,6 +28,8 @@ def main() -> int:
     ap.add_argument("--sizes-mb", default="0.25,1,2,4,5.25,8,16,32,64")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-plan", action="store_true",
+                    help="skip the headline step's collective plan (the configuration the driver's N-GPU run records)")
     args = ap.parse_args()
 
     import torch
@@ -42,6 +44,8 @@ def main() -> int:
     dev = ctx.device
     stream = torch.cuda.current_stream(dev)
     n_ranks = ctx.world
+    if not args.no_plan:
+        _headline_plan(ctx, comm, stream, args)
     for mb in (float(x) for x in args.sizes_mb.split(",")):
         n = int(mb * (1 << 20) / 4) // 64 * 64
         buf = torch.ones(n, device=dev)
@@ -74,6 +78,51 @@ def main() -> int:
             print(json.dumps(row), flush=True)
     gdist.shutdown()
     return 0
+
+
+def _headline_plan(ctx, comm, stream, args) -> None:
+    """The exact collectives the headline step graph records at this world size (bench.py's config:
+    preset h512, 256 sequences per GPU, default bucket_mb): Trainer::allreduce_log after one captured
+    step -- (offset, floats) of each ncclAllReduce(avg), the last one grouped with the error-word max --
+    and the same sizes replayed inside a captured hipGraph (how the step issues them), so the driver's
+    first 8-GPU run has its collective cost measured in the form it will run."""
+    import numpy as np
+    import torch
+    from gru_mpi_cuda_amd.config import preset
+    from gru_mpi_cuda_amd.engine.trainer import make_trainer
+    from gru_mpi_cuda_amd.utils.data import NameStream
+    base = preset("h512")
+    cfg = base.replace(batch=base.batch * ctx.world)
+    tr = make_trainer(cfg, ctx, comm=comm)
+    x, y = NameStream(base.batch, cfg.seq, seed=1000 + ctx.rank).next()
+    tr.step(x, y)
+    torch.cuda.synchronize(ctx.device)
+    log = [(int(o), int(n)) for o, n in tr.t.allreduce_log()]
+    buf = torch.ones(max([n for _, n in log] + [1]), device=ctx.device)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(ctx.device)
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for _, n in log:
+                comm.allreduce_avg_f32(buf.data_ptr(), n, side.cuda_stream)
+    for _ in range(args.warmup):
+        g.replay()
+    torch.cuda.synchronize(ctx.device)
+    ts = []
+    for _ in range(args.iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3)
+    if ctx.is_main:
+        mb = sum(n for _, n in log) * 4 / 2 ** 20
+        print(json.dumps({"headline_step_collectives": [{"offset": o, "floats": n, "mb": round(n * 4 / 2 ** 20, 3)}
+                                                         for o, n in log],
+                          "total_mb": round(mb, 3), "bucket_mb": cfg.bucket_mb, "ranks": ctx.world,
+                          "plan": tr.t.plan(), "in_graph_replay_us_median": round(float(np.median(ts)), 2)}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -314,7 +314,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
-    a.dy = GP(const float, d, "dy"); a.dyb = GP(const u16, d, "dyb");
+    a.dy = GP(const float, d, "dy");
     a.sr = GP(const float, d, "sr"); a.sz = GP(const float, d, "sz"); a.sn = GP(const float, d, "sn");
     a.sghn = GP(const float, d, "sghn"); a.HSf = GP(const float, d, "HSf");
     a.HT = GP(const u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0); a.WhhT = GP(const u16, d, "WhhT");
@@ -342,7 +342,7 @@ PYBIND11_MODULE(_C, m) {
     a.dl = GP(u16, d, "dl"); a.dlT = GP(u16, d, "dlT"); a.loss_part = GP(float, d, "loss_part");
     a.M = get<int>(d, "M", 0); a.H = get<int>(d, "H", 0); a.V = get<int>(d, "V", 0);
     a.ldT = get<int>(d, "ldT", 0); a.colT = get<int>(d, "colT", 0);
-    a.WT = GP(const u16, d, "WT"); a.dy = GP(float, d, "dy"); a.dy_bf16 = get<int>(d, "dy_bf16", 0);
+    a.WT = GP(const u16, d, "WT"); a.dy = GP(float, d, "dy");
     a.dbg = GP(unsigned long long, d, "dbg");
     a.Wf = GP(const u16, d, "Wf"); a.WTf = GP(const u16, d, "WTf");
     if (a.M % 32 || a.V % 64 || a.V > 512 || a.H % 32 || a.ldT % 8 || a.colT % 8)

@@ -217,7 +217,6 @@ class Trainer {
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
   int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks)
-  bool top_dy_bf16_ = false;     // the recorded step's fc_xent writes the top layer's dy in bf16
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }

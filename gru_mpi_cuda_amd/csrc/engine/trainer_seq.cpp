@@ -124,7 +124,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
   // is zeroed by a memset instead.  The arena starts zeroed for the first step.
   nloss_ = (int)(tok / 32);
-  top_dy_bf16_ = false;
   {
     // layer-0 input projection folded into a [V][3H] table: Gi(t,b) = P[x(t,b)], launched together
     // with the batch preparation (independent work, one graph node)
@@ -202,10 +201,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     } else if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
       f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
-      // bf16 dy for a persistent top layer (its backward kernel reads it as SeqBwdArgs::dyb): half
-      // the store and load bytes of the largest tensor this kernel writes
-      f.dy_bf16 = (seq_[L - 1].bwd && fc_xent_fused_ok(V, H, (int)tok)) ? 1 : 0;
-      top_dy_bf16_ = f.dy_bf16 != 0;
       fc_xent(f, s);
     } else {
       fc_xent(f, s);
@@ -247,7 +242,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (q.bwd) {
       SeqBwdArgs a;
       a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
-      if (l == L - 1 && top_dy_bf16_) { a.dyb = reinterpret_cast<const u16*>(y.dy); a.dy = nullptr; }
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
       a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;

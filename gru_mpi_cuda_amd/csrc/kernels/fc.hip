@@ -392,24 +392,13 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) dacc[r][c] = mfma16(af[r], bt[kk][c], dacc[r][c]);
     }
-    if (a.dy_bf16) {
-      u16* dyb = reinterpret_cast<u16*>(a.dy);
 #pragma unroll
-      for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            dyb[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = f2bf(dacc[r][c][i]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            a.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = dacc[r][c][i];
-    }
+        for (int i = 0; i < 4; ++i)
+          a.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + n0 + c * 16 + lr] = dacc[r][c][i];
   }
   STAMP();
   __syncthreads();
@@ -698,7 +687,6 @@ void fc_xent(const FcXentArgs& a, hipStream_t s) {
     }
     return;
   }
-  if (a.dy_bf16) throw std::runtime_error("fc_xent: bf16 dy needs the 8-wave V = 256 kernel (fc_xent_fused_ok)");
   const int NW = a.V / 64;
   if (a.dy && (a.H % (16 * NW) || a.V % 128 || !a.WT))
     throw std::runtime_error("fc_xent: fused dH needs H % (V/4) == 0, V % 128 == 0 and W_fc^T");

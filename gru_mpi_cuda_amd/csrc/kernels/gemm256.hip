@@ -302,134 +302,19 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// 256 x 256 tiles on a 4-deep ring of 32-deep k-tiles (the 2-buffer 64-deep
-// pipeline above leaves ONE k-tile in flight while a tile's 64 MFMAs run, so every tile's LDS-DMA
-// latency that exceeds its compute shows up as a stall; here three 32 KiB tiles are in flight, each
-// with three tiles' compute to land).  Same 128 KiB of LDS, same wave layout and accumulators.
-//   * a 32-deep row is 64 B: 16-B chunk c of row r lives in slot c ^ (2 ((r >> 3) & 1)).  ds_read_b128
-//     serves a fragment read (16 rows, chunk l >> 4) in 4 lane groups; with this swizzle each group
-//     touches 16 distinct (bank quad, row mod 4) pairs -- conflict-free (exhaustive check over the
-//     four groups, scripts/ note in docs/DESIGN.md §3.3).  LDS-DMA writes lane-linear, so the swizzle
-//     is applied on the per-lane source chunk.
-//   * per k-tile a wave issues 4 LDS-DMA instructions (1 KiB each) and runs 2 groups of 16 MFMAs;
-//     the wait before tile kt is vmcnt(8): the two younger tiles stay in flight.
-DEV int swz32(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
-template <bool BIAS, bool ACC, bool RS>
-__global__ void __launch_bounds__(512, 1) gemm256r_kernel(GemmArgs a, int ntn, int ntm, int kper) {
-  constexpr int NS = 4, BK = 32;
-  __shared__ __attribute__((aligned(16))) u16 lds[NS][2][256 * BK];   // [slot][A | B][256 rows x 32]
-  const int id = xcd_remap256(blockIdx.x, gridDim.x);
-  constexpr int kGroupM = 4;
-  const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
-  const int per_group = kGroupM * ntn, first_m = (pid / per_group) * kGroupM;
-  const int gm = min(ntm - first_m, kGroupM);
-  const int tm = first_m + (pid % per_group) % gm, tn = (pid % per_group) / gm;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  const int lr = lane & 15, lq = lane >> 4;
-  const int row0 = tm * kBM, col0 = tn * kBN;
-  const int kbeg = sp * kper, nk = kper / BK;
-
-  // staging: instruction q (0..3) of wave w covers 16 rows of operand op = q >> 1:
-  // rows 16 (2w + (q & 1)) .. + 15; lane l -> row + (l >> 2), LDS slot l & 3
-  const u16* src[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int op = q >> 1, r = 16 * (2 * w + (q & 1)) + (lane >> 2);
-    const int c = swz32(r, lane & 3);
-    src[q] = (op == 0 ? a.A + (size_t)(row0 + r) * a.lda : a.B + (size_t)(col0 + r) * a.ldb) + kbeg + c * 8;
-  }
-  auto stage = [&](int slot, int kt) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(src[q] + kt * BK,
-                                       (lds256_t*)(&lds[slot][q >> 1][(16 * (2 * w + (q & 1))) * BK]), 16, 0, 0);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto rdA = [&](int slot, int i) {
-    const int r = wr * 128 + i * 16 + lr;
-    return *reinterpret_cast<const bf16x8*>(&lds[slot][0][r * BK + swz32(r, lq) * 8]);
-  };
-  auto rdB = [&](int slot, int j) {
-    const int r = wc * 64 + j * 16 + lr;
-    return *reinterpret_cast<const bf16x8*>(&lds[slot][1][r * BK + swz32(r, lq) * 8]);
-  };
-  const bool do_rs = RS && tn == 0 && wc == 0;
-  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) stage(t, t);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt % NS;
-    // tile kt landed: at most min(2, nk - 1 - kt) younger tiles (4 instructions each) still in flight
-    const int younger = min(NS - 2, nk - 1 - kt);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();   // tile kt visible to every wave; every wave is done with slot (kt + 3) % 4
-    if (kt + NS - 1 < nk) stage((kt + NS - 1) % NS, kt + NS - 1);
-    bf16x8 fa0[4], fa1[4], fb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa0[i] = rdA(cur, i);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = rdB(cur, j);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa1[i] = rdA(cur, 4 + i);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa0[i], fb[j], acc[i][j]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 + i][j] = mfma16(fa1[i], fb[j], acc[4 + i][j]);
-    if (do_rs) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { rs[i] = add_sum8(fa0[i], rs[i]); rs[4 + i] = add_sum8(fa1[i], rs[4 + i]); }
-    }
-  }
-  if (do_rs) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      float v = rs[t];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + wr * 128 + t * 16 + lane] = v;
-    }
-  }
-  float* C = a.C + (size_t)sp * a.M * a.ldc;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = col0 + wc * 64 + j * 16 + lr;
-    const float bb = BIAS ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = row0 + wr * 128 + i * 16 + lq * 4 + e;
-        float* dst = C + (size_t)row * a.ldc + col;
-        const float v = acc[i][j][e] + bb;
-        if (ACC) *dst += v; else *dst = v;
-      }
-  }
-}
+// (Round 4: the same tile on a 4-deep ring of 32-deep k-tiles -- three 32 KiB tiles in flight
+// instead of one 64 KiB tile, conflict-free 64-B-row swizzle c ^ 2((r >> 3) & 1) -- measured slower on
+// every shape: h2048 dW_hh 1032 vs 1122 TF at split 4, sq8192 1190 vs 1254 TF
+// (profiles/r4_gemm256_ring.jsonl); removed.  Twice the barriers per MFMA cost more than the deeper
+// prefetch gained.)
 
 // Which form (GK_GEMM256_MFMA=16 / 32 forces one; read per launch so tests and benches switch it
 // in-process).  Default: 32x32x16 only for short K-slices (<= 256), where it measured faster --
 // h2048 dH 65536 x 2048 x 256: 438 vs 360 TF -- and 16x16x32 elsewhere (sq8192 1284 vs 1203 TF,
 // h2048 dW_hh 4-way split 1139 vs 1073 TF; profiles/r3_gemm256_m32.jsonl)
-// 'r': the 4-deep ring of 32-deep k-tiles (gemm256r_kernel)
 static int gemm256_mfma(int kper) {
   const char* e = std::getenv("GK_GEMM256_MFMA");
-  if (e && e[0]) return e[0] == 'r' ? 'r' : std::atoi(e);
+  if (e && e[0]) return std::atoi(e);
   return kper <= 256 ? 32 : 16;
 }
 
@@ -451,7 +336,6 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
 #define GK_L(B_, A_, R_)                                                                                   \
   do {                                                                                                     \
     if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (form == 'r') hipLaunchKernelGGL((gemm256r_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
     else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);           \
   } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate

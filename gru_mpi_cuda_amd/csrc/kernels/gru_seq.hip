@@ -774,7 +774,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) int idsL[NTP > 0 ? 32 : 1];
   auto load_saves = [&](int t) {
     const size_t o = ((size_t)t * Bp + b) * H + j;
-    sv[0] = a.dyb ? __uint_as_float((unsigned)a.dyb[o] << 16) : a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
     sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
     if constexpr (NTP > 0) svid = a.ids[(size_t)t * Bp + b];   // this thread's row id (fused dP)
   };

@@ -79,7 +79,8 @@ struct StepLdsVariants {
   int fwd64_fused = 1;   // the 64-row tile also for the fused input phase (layers >= 1 of generation)
   int fwd64_all = 0;     // the 64-row tile also on grids of >= 512 128-row tiles (2-deep 128-row kernel otherwise)
   int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
-  int bwd_sk_map = 0;    // split-K backward block order: 0 splits of a tile on one XCD, 1 splits across XCDs
+  int bwd_sk_map = 1;    // split-K backward block order: 1 splits across XCDs (h2048 9.46-9.47 vs 9.49 ms,
+                         // profiles/r4_h2048_skmap.jsonl), 0 the 4 splits of a tile on one XCD
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
 };
 StepLdsVariants& step_lds_variants();
@@ -141,7 +142,6 @@ void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s);
 
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
-  const u16* dyb = nullptr;        // [T][Bp][H] bf16 alternative to dy (the top layer under fc_xent's bf16 dH)
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
@@ -180,7 +180,6 @@ struct FcXentArgs {
   // fused dH = dlogits · W_fc (nullable): dy [M][H] fp32 from WT = W_fc^T [H][V] bf16
   const u16* WT = nullptr;
   float* dy = nullptr;
-  int dy_bf16 = 0;                 // 8-wave V = 256 kernel: dy holds bf16 [M][H] instead of fp32
   int M = 0, H = 0, V = 0, ldT = 0, colT = 0;
   // FT-layout copies of W [V][H] and W^T [H][V] (ft_offset): required by the 8-wave V = 256 kernel
   const u16* Wf = nullptr;

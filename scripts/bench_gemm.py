@@ -56,13 +56,12 @@ for name, M, N, K, sp in SHAPES:
     ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 34 else None
     variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
     # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32)
-    # algo "5r": the 256 x 256 kernel on a 4-deep ring of 32-deep k-tiles (GK_GEMM256_MFMA=r)
-    variants += [(x, k) for a_, k in list(variants) if a_ == 5 for x in ("5m", "5r")]
+    variants += [("5m", k) for a_, k in variants if a_ == 5]
     if os.environ.get("GEMM_ONLY256"):
-        variants = [v for v in variants if v[0] in (5, "5m", "5r")]
+        variants = [v for v in variants if v[0] in (5, "5m")]
     for algo, ks in variants:
-        os.environ["GK_GEMM256_MFMA"] = {"5m": "32", "5r": "r"}.get(algo, "16")
-        algo_arg = 5 if algo in ("5m", "5r") else algo
+        os.environ["GK_GEMM256_MFMA"] = "32" if algo == "5m" else "16"
+        algo_arg = 5 if algo == "5m" else algo
         if ks > 1 and Cs.shape[0] < ks:
             Cs = torch.empty(ks, M, N, device=dev)
         d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,

@@ -279,11 +279,11 @@ def test_bwd_step_dgit_n_only(ext, H, Bp, algo, sk):
     test_bwd_step(ext, False, H, Bp, algo, sk, n_only=True)
 
 
-@pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256", "fused_dh_bf16"])
+@pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256"])
 @pytest.mark.parametrize("H", [256, 320, 512, 1024])
 def test_fc_xent(ext, mode, H):
     fused_dh = mode.startswith("fused_dh")
-    if mode in ("dl_v256", "fused_dh_bf16") and H % 512:
+    if mode == "dl_v256" and H % 512:
         pytest.skip("the 8-wave kernel is for H in (512, 1024)")
     M, V = 128, 256
     X = bf(rnd(M, H, seed=1))
@@ -305,8 +305,6 @@ def test_fc_xent(ext, mode, H):
         Wf, WTf = ft_layout(W), ft_layout(WT)
         d.update(WT=WT.data_ptr(), dy=dy.data_ptr(), Wf=Wf.data_ptr(), WTf=WTf.data_ptr())
         del d["dl"]
-        if mode == "fused_dh_bf16":   # the persistent top layer's dy: bf16 [M][H] in the same buffer
-            d["dy_bf16"] = 1
     if mode == "dl_v256":   # persistent-backward path: 8-wave kernel, row-major dl, no dH
         from gru_mpi_cuda_amd.ops import ft_layout
         Wf = ft_layout(W)
@@ -326,9 +324,6 @@ def test_fc_xent(ext, mode, H):
     torch.testing.assert_close(dlT[:, M:].T, dl, atol=0, rtol=0)
     if mode == "fused_dh":   # dH = dlogits(bf16) · W_fc, fp32 accumulate
         torch.testing.assert_close(dy, dl.float() @ W.float(), atol=1e-5, rtol=1e-3)
-    if mode == "fused_dh_bf16":   # ... rounded to bf16 once
-        got = dy.view(torch.bfloat16).flatten()[:M * H].view(M, H).float()
-        torch.testing.assert_close(got, (dl.float() @ W.float()).bfloat16().float(), atol=1e-5, rtol=1e-2)
 
 
 @pytest.mark.parametrize("H", [128, 512, 1024])   # 512/1024: 8-wave kernel on the FT copy of W_fc
@@ -407,7 +402,7 @@ def test_reduce_slabs_cast(ext, R, C, splits):
     (768, 512, 2048, 4, False, False, 0, True), (1024, 1024, 3072, 1, False, True, 0, False),
     (512, 256, 4096, 8, False, False, 64, True), (2304, 1280, 576, 1, True, True, 32, False),
     (1536, 512, 8192, 4, False, False, 0, True), (512, 768, 1024, 1, False, False, 0, True)])
-@pytest.mark.parametrize("mfma", ["16", "32", "r"])
+@pytest.mark.parametrize("mfma", ["16", "32"])
 def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, rowsum, mfma):
     """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
     operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
