@@ -308,10 +308,17 @@ PYBIND11_MODULE(_C, m) {
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    if (get<int>(d, "big", 0)) {   // the large-H persistent forward (gru_seq_big.hip)
+      if (!gru_fwd_seq_big_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq(big): shape not supported");
+      gru_fwd_seq_big(a, S(s));
+      HIP_LAUNCH_CHECK();
+      return;
+    }
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
+  m.def("fwd_seq_big_supported", &gru_fwd_seq_big_supported);
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
     a.dy = GP(const float, d, "dy");

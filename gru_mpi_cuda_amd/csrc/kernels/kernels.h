@@ -127,6 +127,13 @@ inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 
 bool gru_fwd_seq_supported(int H, int Bp);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 
+// Persistent forward for large H with a large batch (gru_seq_big.hip): 256 workgroups of 128 rows x
+// 32 units x 3 gates, W_hh streamed from L2 each step, h exchanged through T-deep per-producer tiles
+// of `xch` (T x Bp x H bf16) with epoch flags in `cnt` (zeroed before the launch).  Needs
+// (Bp/128)(H/32) == 256, H % 256 == 0, H >= 1024.
+bool gru_fwd_seq_big_supported(int H, int Bp);
+void gru_fwd_seq_big(const SeqFwdArgs& a, hipStream_t s);
+
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
 // `lo` at step s and layer `hi` at step s-1 in iteration s = 0..T.  hi's input projection
 // W_ih · h_lo(t) + b_ih is computed in the kernel from the same exchange tiles lo's next step reads

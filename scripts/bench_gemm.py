@@ -55,6 +55,8 @@ for name, M, N, K, sp in SHAPES:
     row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp}
     ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 34 else None
     variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
+    # algo 3: the one-shot small GEMM at the K-slices it takes (h512 step products)
+    variants += [(3, k) for k in (1, 2, 4, 6, 8, 16) if K % k == 0 and (K // k) in (128, 192, 256, 512, 1024, 1536, 2048)]
     # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32)
     variants += [("5m", k) for a_, k in variants if a_ == 5]
     if os.environ.get("GEMM_ONLY256"):
@@ -66,7 +68,7 @@ for name, M, N, K, sp in SHAPES:
             Cs = torch.empty(ks, M, N, device=dev)
         d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,
                  splits=ks, algo=algo_arg)
-        tag = f"algo{algo}" + (f"s{ks}" if algo_arg == 5 else "")
+        tag = f"algo{algo}" + (f"s{ks}" if algo_arg in (3, 5) else "")
         try:
             us = timeit(lambda: C.gemm_nt(d, s))
         except RuntimeError as e:

@@ -104,6 +104,37 @@ def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H, blaslt):
         assert e < 0.04, f"{k}: rel err {e:.4f} ({plan})"
 
 
+@pytest.mark.parametrize("layers,B,H,E", [(1, 512, 2048, 128), (2, 1024, 1024, 128)])
+def test_trainer_grads_big_persistent_forward(layers, B, H, E):
+    """Large H with a large batch takes the persistent big-tile forward (gru_seq_big.hip) with the
+    per-step backward: full gradients against the fp64 oracle, and the loss against the all-per-step
+    schedule (GK_PERSIST=0)."""
+    import os
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=4 if H >= 2048 else 3, seed=6)
+    params = init_params(cfg)
+    x, y = NameStream(B, cfg.seq, seed=9).next()
+    tr = HipTrainer(cfg, params=params)
+    assert tr.t.plan().startswith("fwd=persistent-big"), tr.t.plan()
+    tr.forward_backward(x, y)
+    assert tr.t.read_error() == 0
+    g = tr.grad_dict()
+    p64 = {k: v.double() for k, v in params.items()}
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    assert abs(tr.loss() - float(ref_loss)) < 1e-2 * float(ref_loss)
+    for k in ref_g:
+        e = rel(g[k], ref_g[k])
+        assert e < 0.04, f"{k}: rel err {e:.4f} ({tr.t.plan()})"
+    os.environ["GK_PERSIST"] = "0"
+    try:
+        st = HipTrainer(cfg, params=params)
+    finally:
+        del os.environ["GK_PERSIST"]
+    assert "persistent" not in st.t.plan()
+    st.forward_backward(x, y)
+    assert abs(st.loss() - tr.loss()) < 1e-4 * abs(st.loss())
+
+
 def test_trainer_adam_step_and_learning():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer, CpuTrainer
     cfg = GRUConfig(vocab=256, embed=128, hidden=128, layers=1, batch=64, seq=16, time_chunks=2, lr=3e-3, seed=1)
