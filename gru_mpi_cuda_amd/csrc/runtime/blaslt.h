@@ -13,7 +13,8 @@ using u16 = unsigned short;
 // Create the handle and the workspace (call before any stream capture; idempotent).
 void blaslt_init();
 // Smallest GEMM (2*M*N*K, in GFLOP) routed to the library under algo 0; env GK_BLASLT_MIN_GFLOP,
-// default 60; GK_BLASLT=0 disables the library entirely.
+// default 60.  The library is OFF by default (gemm256 took the weight gradients in round 2);
+// GK_BLASLT=1 enables it.
 double blaslt_min_gflop();
 bool blaslt_enabled();
 // C[M][N] (ldc) = A[M][K] (lda) . B[N][K]^T (ldb), fp32 out, fp32 accumulation (C += with

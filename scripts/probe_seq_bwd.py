@@ -38,14 +38,9 @@ if fuse_w:
         d["HF"] = HF.data_ptr()
 if fuse_p:
     d.update(ids=ids.data_ptr(), dP_part=dPp.data_ptr())
-if int(os.environ.get("DL", 0)):   # top layer: dy = dl · W_fc inside the kernel
-    dl = (torch.randn(T, Bp, V, device=dev) * 0.01).bfloat16()
-    WfcT = (torch.randn(H, V, device=dev) / V ** 0.5).bfloat16()
-    del d["dy"]
-    d.update(dl=dl.data_ptr(), WfcT=WfcT.data_ptr())
 if not (fuse_w and fuse_p):
     d.update(dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), ldG=T * Bp)
-res = {"H": H, "Bp": Bp, "fuse_w": fuse_w, "fuse_p": fuse_p, "dl": int(os.environ.get("DL", 0))}
+res = {"H": H, "Bp": Bp, "fuse_w": fuse_w, "fuse_p": fuse_p}
 for mode in ("plain", "dbg"):
     if mode == "dbg":
         d["dbg"] = dbg.data_ptr()

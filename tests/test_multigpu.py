@@ -185,8 +185,9 @@ def test_dp_adam_five_steps_equals_one_gpu(tmp_path, n):
 
 def test_dp_adam_five_steps_one_rank_twin(tmp_path):
     """1-GPU twin of the Adam DP test: the same worker with a 1-rank RCCL communicator (the
-    data-parallel graph: grouped collectives + error word) against no communicator (the fused step
-    tail: another fp32 summation order for dW_fc), 5 Adam steps."""
+    data-parallel graph: grouped collectives + error word, slab sums materialised before the
+    collective) against no communicator (the slab sums inside the fused Adam launch: another fp32
+    summation order for dW_fc), 5 Adam steps."""
     worker = tmp_path / "worker.py"
     worker.write_text(WORKER)
     a, b = str(tmp_path / "nocomm.pt"), str(tmp_path / "comm1.pt")
