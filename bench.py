@@ -87,7 +87,7 @@ def main() -> int:
                          "the timed region's synchronize is cheap, then groups).  Reported as graph_steps "
                          "and lead_single_steps.")
     ap.add_argument("--variant", action="append", default=[], metavar="KEY=INT",
-                    help="large-H step-kernel variant (StepLdsVariants field, kernels.h), for A/B runs; repeatable")
+                    help="kernel / step-plan variant (StepLdsVariants field, kernels.h), for A/B runs; repeatable")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()

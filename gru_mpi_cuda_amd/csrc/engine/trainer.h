@@ -217,6 +217,9 @@ class Trainer {
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;
+  // the dW_fc GEMM held back to run inside the embedding-side launch (StepLdsVariants::dwfc_group)
+  GemmArgs fc_held_;
+  bool fc_held_on_ = false;
   int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks)
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:

@@ -4,7 +4,8 @@
 //   -> fused FC + softmax-xent over all B*T tokens -> dH GEMM -> dW_fc split-K GEMM
 //   -> [per layer, top-down: backward sequence kernel with fused dW_hh / dP / bias partials
 //       -> (l>0) dW_ih GEMM + dX GEMM]
-//   -> one multi-tensor reduction of all partial slabs -> dW_ih0 / dEmb GEMMs -> loss.
+//   -> one multi-tensor reduction of all partial slabs (+ loss) -> dW_ih0 / dEmb GEMMs (single GPU:
+//      with the dW_fc K-slices in the same launch).
 //
 // Every layer falls back to the per-timestep kernels when its shape cannot be made
 // co-resident (gru_*_seq_supported), so any config still runs -- just slower.
@@ -118,6 +119,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   const long tok = (long)T * B;
   const long fw = seq_flag_words(H, B);
   ev_next_ = 0;
+  fc_held_on_ = false;
   if (dp) { ar_ready_ = ar_launched_ = 0; ar_busy_ = false; ar_log_.clear(); }
   // Flag blocks: forward(l) at cnt_ + l*fw, backward(l) at cnt_ + (L+l)*fw.  Each persistent
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
@@ -234,7 +236,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ws.splits = (int)(tok / kslice); ws.algo = 3;
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
     }
-    gemm_nt(w, s);
+    // single GPU, slabs summed inside Adam: nothing reads dW_fc before the optimiser, so its
+    // K-slices can join the dW_ih0 / dEmb launch after the backward sweep (one launch fewer; its
+    // latency-bound tiles run beside theirs)
+    fc_held_on_ = !dp && defer_slabs_ && sp <= 8 && w.algo == 3 && step_lds_variants().dwfc_group;
+    if (fc_held_on_) fc_held_ = w;
+    else gemm_nt(w, s);
     tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
     tail.add(rs_fc2_, sp, V, G("fc.bias"));
   }
@@ -380,10 +387,16 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   if (H3 % V == 0 && H3 / V <= splits_) {
     GemmArgs es = e;
     es.splits = H3 / V;
+    // the held dW_fc K-slices (4-chunk tiles) first: they are the long ones
+    const GemmArgs three[3] = {fc_held_, g, es};
+    const bool with_fc = fc_held_on_ && gemm_small_group_depth(three, 3) == gemm_small_kblocks(g);
     const int nkb = gemm_small_kblocks(g);
     if (nkb && nkb == gemm_small_kblocks(es)) {
       const GemmArgs pair[2] = {g, es};
-      gemm_small_group(pair, 2, s);
+      if (fc_held_on_ && !with_fc) gemm_nt(fc_held_, s);
+      if (with_fc) gemm_small_group(three, 3, s);
+      else gemm_small_group(pair, 2, s);
+      fc_held_on_ = false;
       SlabJobs r;
       slab_job(r, slab_e_, es.splits, (long)V * E, G("embedding"));
       if (r.n) reduce_slabs_multi(r, s);
@@ -391,6 +404,8 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
       return;
     }
   }
+  if (fc_held_on_) gemm_nt(fc_held_, s);
+  fc_held_on_ = false;
   const GemmArgs both[2] = {g, e};
   if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
     gemm_lds_group(both, 2, s);   // one launch for both small products

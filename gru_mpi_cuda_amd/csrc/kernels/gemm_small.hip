@@ -10,6 +10,7 @@
 //   * LDS: NKB x (64 + 64) rows x 128 B = NKB x 16 KiB (NKB <= 8: two workgroups per CU up to 4);
 //   * split-K slabs, fused bias (unsplit) and fused row sums of A as in gemm_lds;
 //   * grouped launch for several independent products (dW_ih0 and dEmb share one).
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include "kernels.h"
@@ -40,7 +41,7 @@ DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_rs = ROWSUM && tn == 0 && wn == 0;
+  const bool do_rs = ROWSUM && a.rowsumA && tn == 0 && wn == 0;
   float rs[2] = {0.f, 0.f};
   for (int ch = 0; ch < nch; ++ch) {
   const int kbeg = (sp * nch + ch) * NKB * 64;
@@ -118,15 +119,27 @@ __global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_kernel(GemmA
   gemm_small_body<NKB, BIAS, ROWSUM>(a, xcd_remap_s(blockIdx.x, gridDim.x), ntn, ntm, lds, nch);
 }
 
-struct SmallGroup { GemmArgs job[4]; int start[5]; int ntn[4], ntm[4]; int n; };
+// Jobs share the chunk depth NKB; each streams its K-slice as nch[k] chunks.  per_xcd: every job's
+// tile count is a multiple of 8, and each XCD runs 1/8 of EVERY job (job k's blocks occupy local
+// slots [xs[k], xs[k+1]) of each XCD, job 0 first in dispatch order, consecutive job ids on one XCD as
+// in xcd_remap_s) -- a long job (a 4-chunk dW_fc K-slice) is spread over the chip instead of
+// filling the first XCDs; else ids are dealt as one range (xcd_remap_s) and cut at start[k].
+struct SmallGroup { GemmArgs job[4]; int start[5], xs[5]; int ntn[4], ntm[4], nch[4]; int n, per_xcd; };
 
 template <int NKB, bool BIAS, bool ROWSUM>
 __global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_group_kernel(SmallGroup g) {
   __shared__ __attribute__((aligned(16))) u16 lds[NKB][2][64 * 64];
-  const int id = xcd_remap_s(blockIdx.x, gridDim.x);
-  int k = 0;
-  while (k + 1 < g.n && id >= g.start[k + 1]) ++k;
-  gemm_small_body<NKB, BIAS, ROWSUM>(g.job[k], id - g.start[k], g.ntn[k], g.ntm[k], lds);
+  int k = 0, id;
+  if (g.per_xcd) {
+    const int x = blockIdx.x % 8, loc = blockIdx.x / 8;
+    while (k + 1 < g.n && loc >= g.xs[k + 1]) ++k;
+    id = x * (g.xs[k + 1] - g.xs[k]) + (loc - g.xs[k]);
+  } else {
+    const int gid = xcd_remap_s(blockIdx.x, gridDim.x);
+    while (k + 1 < g.n && gid >= g.start[k + 1]) ++k;
+    id = gid - g.start[k];
+  }
+  gemm_small_body<NKB, BIAS, ROWSUM>(g.job[k], id, g.ntn[k], g.ntm[k], lds, g.nch[k]);
 }
 
 // + trailing blocks running the batch transpose (gemm_with_prep in gemm_lds.hip)
@@ -209,23 +222,43 @@ void gemm_small_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
 #undef GP_CASE
 }
 
+int gemm_small_group_depth(const GemmArgs* jobs, int n) {
+  int nkb = 0;
+  for (int k = 0; k < n; ++k) {
+    const int kb = gemm_small_kblocks(jobs[k]);
+    if (!kb) return 0;
+    nkb = k ? std::min(nkb, kb) : kb;
+  }
+  while (nkb > 8) nkb = nkb % 8 ? 0 : 8;   // chunks of <= 8 blocks (gemm_small's K-slice rule)
+  if (nkb != 2 && nkb != 3 && nkb != 4 && nkb != 8) return 0;
+  for (int k = 0; k < n; ++k)
+    if (gemm_small_kblocks(jobs[k]) % nkb) return 0;
+  return nkb;
+}
+
 void gemm_small_group(const GemmArgs* jobs, int n, hipStream_t s) {
   if (n < 1 || n > 4) throw std::runtime_error("gemm_small_group: 1..4 jobs");
   SmallGroup g;
   g.n = n;
   int tot = 0;
-  int nch0 = 1;
-  const int nkb = small_blocks(jobs[0], &nch0);
-  const bool bias = jobs[0].bias && jobs[0].splits == 1, rs = jobs[0].rowsumA != nullptr;
-  if (nch0 != 1) throw std::runtime_error("gemm_small_group: K-slices up to 512 only");
+  const int nkb = gemm_small_group_depth(jobs, n);
+  const bool bias = jobs[0].bias && jobs[0].splits == 1;
+  bool rs = false;
+  g.per_xcd = 1;
+  g.xs[0] = 0;
   for (int k = 0; k < n; ++k) {
     const GemmArgs& a = jobs[k];
-    if (!nkb || gemm_small_kblocks(a) != nkb || (a.bias && a.splits == 1) != bias || (a.rowsumA != nullptr) != rs)
+    if (!nkb || (a.bias && a.splits == 1) != bias)
       throw std::runtime_error("gemm_small_group: job " + std::to_string(k) + " incompatible");
+    rs = rs || a.rowsumA != nullptr;
     g.job[k] = a;
     g.ntn[k] = a.N / 64; g.ntm[k] = a.M / 64;
+    g.nch[k] = gemm_small_kblocks(a) / nkb;
     g.start[k] = tot;
-    tot += g.ntn[k] * g.ntm[k] * a.splits;
+    const int nt = g.ntn[k] * g.ntm[k] * a.splits;
+    tot += nt;
+    if (nt % 8) g.per_xcd = 0;
+    g.xs[k + 1] = g.xs[k] + nt / 8;
   }
   g.start[n] = tot;
   dispatch_nkb(nkb, bias, rs, SmallGroupLaunch{g, tot, s});

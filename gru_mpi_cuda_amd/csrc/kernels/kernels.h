@@ -68,9 +68,10 @@ void gru_bwd_step(const BwdStepArgs& a, hipStream_t s);
 // split-K count the backward LDS step kernel would use for (H, Bp): 0 = the 64 x 64 kernel;
 // workspace: H * Bp * splits fp32 partials, (H/128)(Bp/128) * 16 counter words
 int gru_bwd_step_sk_splits(int H, int Bp);
-// Large-H step-kernel variants (gru_step_lds.hip).  Initialised from the environment (GK_STEP_LDS_NS,
-// GK_FWD_LDS8, GK_FWD_LDS64*, GK_BWD_SK_PF, GK_BWD_SK_MIN_H) on first use; settable at run time so the
-// kernel tests cover every variant in one process.  0 / -1 fields mean "automatic".
+// Run-time kernel / step-plan variants: the measured-best defaults, settable at run time
+// (set_step_lds_variants, bench.py --variant) so one process can test or A/B every variant.  The
+// large-H step-kernel fields are read per launch (gru_step_lds.hip), the plan fields when a step
+// graph is recorded.  0 fields mean "automatic" where noted.
 struct StepLdsVariants {
   int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4
   int fwd8 = 2;          // 8-wave forward (two wave groups split each k-tile): 2 = split epilogue,
@@ -82,6 +83,8 @@ struct StepLdsVariants {
   int bwd_sk_map = 1;    // split-K backward block order: 1 splits across XCDs (h2048 9.46-9.47 vs 9.49 ms,
                          // profiles/r4_h2048_skmap.jsonl), 0 the 4 splits of a tile on one XCD
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
+  int dwfc_group = 1;    // single-GPU step: the dW_fc K-slices run after the backward sweep inside the
+                         // dW_ih0 / dEmb launch (one launch fewer), 0: their own launch before it
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -324,7 +327,10 @@ void gemm_lds(const GemmArgs& a, hipStream_t s);
 // at once; for the latency-bound small products.  kblocks = 64-deep blocks per K-slice, 0 = unsupported
 int gemm_small_kblocks(const GemmArgs& a);
 void gemm_small(const GemmArgs& a, hipStream_t s);
-void gemm_small_group(const GemmArgs* jobs, int n, hipStream_t s);   // same kblocks / flags, n <= 4
+// up to 4 independent small GEMMs in one launch: the jobs' K-slices must be multiples of one chunk
+// depth (gemm_small_group_depth != 0; longer slices stream as several chunks), same bias mode
+int gemm_small_group_depth(const GemmArgs* jobs, int n);
+void gemm_small_group(const GemmArgs* jobs, int n, hipStream_t s);
 
 // sum `splits` slabs [splits][n] -> dst[n] (optionally also as bf16 and/or accumulate)
 void reduce_slabs(const float* src, int splits, long n, float* dst, hipStream_t s);
@@ -376,6 +382,7 @@ struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0; int* bump = nul
   void add_cast(const float* s, int splits, int R, int C, float* d, u16* bf, u16* bfT) {
     job[n++] = SlabJob{s, d, (long)R * C, splits, bf, bfT, R, C}; } };
 void reduce_slabs_multi(SlabJobs& j, hipStream_t s);
+int reduce_slabs_blocks(SlabJobs& j);   // fills j.blk_start, returns the launch's block count
 // "FT" (fragment-tiled) bf16 layout of a K-contiguous [R][K] matrix: element (r, k) at
 //   ((r/16 * K/32 + k/32) * 64 + (r%16) + 16*((k%32)/8)) * 8 + k%8
 // i.e. every 16x32 MFMA operand fragment is 1 KB contiguous in lane order, so a fragment load is

@@ -260,4 +260,61 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
   }
 }
 
+// One block's share of a multi-tensor slab reduction (reduce_slabs_multi): block b of the prefix sum
+// over the jobs' block counts; tile: 16 x 72 u16 of LDS for the transposed bf16 copies.  Blocks past
+// the last job do nothing.
+DEV void reduce_multi_body(const SlabJobs& j, int b, u16 (*tile)[72]) {
+  if (b >= j.blk_start[j.n]) return;
+  int k = 0;
+  while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
+  if (j.bump && b == 0 && threadIdx.x == 0) *j.bump += 1;
+  const SlabJob& J = j.job[k];
+  if (J.bf || J.bfT) {   // 16x64 tile (one float4 per thread): slab sum -> fp32 / bf16 / bf16 transposed
+    // 16-row tiles: 4x the workgroups of 64x64 ones, so the slab loads of a 256 x 1536 dP reach
+    // every CU (96 blocks of 64x64 left most of the chip idle)
+    const int tiles_c = J.C / 64, t = b - j.blk_start[k];
+    const int r0 = (t / tiles_c) * 16, c0 = (t % tiles_c) * 64;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const size_t o = (size_t)(r0 + ty) * J.C + c0 + 4 * tx;
+    const float4 acc = sum_slabs4(J.src, J.n, J.splits, o);
+    if (J.dst) *reinterpret_cast<float4*>(J.dst + o) = acc;
+    uint2 w;
+    w.x = (unsigned)f2bf(acc.x) | ((unsigned)f2bf(acc.y) << 16);
+    w.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
+    if (J.bf) *reinterpret_cast<uint2*>(J.bf + o) = w;
+    if (!J.bfT) return;
+    *reinterpret_cast<uint2*>(&tile[ty][4 * tx]) = w;
+    __syncthreads();
+    if (threadIdx.x < 128) {   // 64 columns x 2 pieces of 8 rows (16 B)
+      const int col = threadIdx.x >> 1, seg = threadIdx.x & 1;
+      u16 v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
+      *reinterpret_cast<uint4*>(J.bfT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
+    }
+    return;
+  }
+  const long n4 = J.n / 4;
+  const long nb = j.blk_start[k + 1] - j.blk_start[k];
+  for (long i = (b - j.blk_start[k]) * (long)blockDim.x + threadIdx.x; i < n4; i += nb * blockDim.x)
+    reinterpret_cast<float4*>(J.dst)[i] = sum_slabs4(J.src, J.n, J.splits, (size_t)i * 4);
+  if (b == j.blk_start[k]) {
+    if (J.n < 4) {   // tiny job (e.g. the loss: many one-float partials): one wave, fixed order
+      if (threadIdx.x < 64)
+        for (long i = 0; i < J.n; ++i) {
+          float acc = 0.f;
+          for (int s = threadIdx.x; s < J.splits; s += 64) acc += J.src[(size_t)s * J.n + i];
+          acc = wave_sum(acc);
+          if (threadIdx.x == 0) J.dst[i] = acc;
+        }
+    } else {
+      for (long i = n4 * 4 + threadIdx.x; i < J.n; i += blockDim.x) {
+        float acc = 0.f;
+        for (int s = 0; s < J.splits; ++s) acc += J.src[(size_t)s * J.n + i];
+        J.dst[i] = acc;
+      }
+    }
+  }
+}
+
 }  // namespace gk

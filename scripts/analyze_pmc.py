@@ -43,11 +43,16 @@ def main(root: str) -> None:
                       + c.get("TCC_EA0_WRREQ_64B_sum", 0.0) * 64) / 2 ** 20,
             cu_busy_cycles=busy)))
     rows.sort(reverse=True)
-    print(f"{'kernel':60s} {'MFMA%':>7s} {'bf16GF':>9s} {'LDSconf%':>9s} {'fetchMB':>9s} {'writeMB':>9s}")
+    # per dispatch: each counter group's run sees every kernel's dispatches once (groups are separate
+    # runs of the same program), so the dispatch count of one group divides the sums
+    print(f"{'kernel':60s} {'disp':>5s} {'MFMA%':>7s} {'bf16GF/d':>9s} {'LDSconf%':>9s} {'fetchMB/d':>10s} {'writeMB/d':>10s}")
     for gui, k, d in rows:
         f = lambda v, fmt: (fmt % v) if v is not None else "-"  # noqa: E731
-        print(f"{k:60s} {f(d['mfma_util_pct'], '%7.1f')} {d['mfma_bf16_gflop']:9.2f} "
-              f"{f(d['lds_conflict_pct'], '%9.2f')} {d['fetch_MB']:9.1f} {d['write_MB']:9.1f}")
+        n = max(1, len({x for x in nd[k] if "/g1/" in x[0]}) or 1)
+        nf = max(1, len({x for x in nd[k] if "/g3/" in x[0]}) or 1)
+        nw = max(1, len({x for x in nd[k] if "/g4/" in x[0]}) or 1)
+        print(f"{k:60s} {n:5d} {f(d['mfma_util_pct'], '%7.1f')} {d['mfma_bf16_gflop'] / n:9.3f} "
+              f"{f(d['lds_conflict_pct'], '%9.2f')} {d['fetch_MB'] / nf:10.2f} {d['write_MB'] / nw:10.2f}")
 
 
 if __name__ == "__main__":

@@ -804,3 +804,31 @@ def test_bench_shape_matches_oracle_and_cpu_adam():
     assert a.t.graph_steps() == 19
     assert torch.equal(a.params, b.params) and a.loss() == b.loss()
     assert a.t.read_error() == 0
+
+
+@pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 256, 128)])
+def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
+    """StepLdsVariants.dwfc_group: the single-GPU step runs the dW_fc K-slices after the backward
+    sweep inside the dW_ih0 / dEmb launch (4 chunks of 256 instead of 2 of 512: the same k order), so
+    the weights after three Adam steps equal the own-launch plan bit for bit."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=H, hidden=H, layers=layers, batch=B, seq=32, seed=3)
+    params = init_params(cfg)
+    ds = NameStream(B, cfg.seq, seed=4)
+    batches = [ds.next() for _ in range(3)]
+    out = []
+    try:
+        for v in (0, 1):
+            C.set_step_lds_variants(dict(dwfc_group=v))
+            tr = HipTrainer(cfg, params=params)
+            for x, y in batches:
+                tr.step(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((tr.params.clone(), tr.loss()))
+    finally:
+        C.set_step_lds_variants(saved)
+    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
