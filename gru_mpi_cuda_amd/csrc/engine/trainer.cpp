@@ -68,7 +68,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   }
   // large H with a big batch: the persistent big-tile forward where the register-resident one does
   // not fit (GK_PERSIST=0 turns every persistent kernel off)
-  fwd_big_ = allow && !persist_fwd_ && gru_fwd_seq_big_supported(H, B);
+  fwd_big_ = allow && !persist_fwd_ && step_lds_variants().fwd_big && gru_fwd_seq_big_supported(H, B);
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);
   if (const char* xl = std::getenv("GK_XCD_LOCAL")) xcd_local_ = std::atoi(xl) != 0;
   if (step_algo_ == 2 && !gru_step_lds_ok(H, B)) step_algo_ = 0;
@@ -87,6 +87,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     q.fuse_w = allow && H <= 512 && gru_bwd_seq_supported(H, B, true, q.fuse_p);
     q.bwd = allow && gru_bwd_seq_supported(H, B, q.fuse_w, q.fuse_p);
     if (!q.bwd) q.fuse_w = q.fuse_p = false;
+    q.big = allow && !q.bwd && step_lds_variants().bwd_big && gru_bwd_seq_big_supported(H, B) &&
+            seq_flag_words(H, B) >= 8192;
     any_bwd |= q.bwd;
   }
   splits_ = 8;
@@ -109,8 +111,12 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   // per-step backward on the split-K LDS kernel: partial tiles + monotonic arrival counters
   // (shared by all layers: their step kernels run one after another on one stream)
   int sk = 0;
-  for (int l = 0; l < L; ++l)
-    if (!seq_[l].bwd) sk = gru_bwd_step_sk_splits(H, B);
+  bool any_big = false;
+  for (int l = 0; l < L; ++l) {
+    if (!seq_[l].bwd && !seq_[l].big) sk = gru_bwd_step_sk_splits(H, B);
+    any_big |= seq_[l].big;
+  }
+  size_t o_bp = any_big ? R((size_t)gru_bwd_seq_big_part_floats(H, B) * 4) : 0;
   sk_part_floats_ = sk ? (long)H * B * sk : 0;
   sk_cnt_words_ = sk ? (long)(H / 128) * (B / 64) * 16 : 0;   // 64-row tiles (gru_bwd_step_sk64) need twice the 128-row count
   size_t o_skp = sk ? R((size_t)sk_part_floats_ * 4) : 0, o_skc = sk ? R((size_t)sk_cnt_words_ * 4) : 0;
@@ -127,6 +133,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     seq_[l].dbih_part = seq_[l].bwd ? arena_.get<float>(o_pbi[l]) : nullptr;
   }
   dP_part_ = seq_[0].fuse_p ? arena_.get<float>(o_pP) : nullptr;
+  bpart_ = any_big ? arena_.get<float>(o_bp) : nullptr;
   sk_part_ = sk ? arena_.get<float>(o_skp) : nullptr;
   sk_cnt_ = sk ? arena_.get<unsigned>(o_skc) : nullptr;
 

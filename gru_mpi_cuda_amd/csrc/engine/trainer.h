@@ -190,6 +190,7 @@ class Trainer {
   // persistent-sequence path
   struct SeqPlan {
     bool bwd = false, fuse_w = false, fuse_p = false;
+    bool big = false;    // large H: the persistent split-K backward (gru_seq_big.hip) instead of T step kernels
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
     u16* HF = nullptr;   // fragment-tiled h for the fused dW_hh (SeqFwdArgs::HF)
   };
@@ -201,6 +202,7 @@ class Trainer {
   bool persist_fwd_ = false;
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   bool fwd_big_ = false;       // large H, large batch: the persistent 128 x 96-tile forward (gru_seq_big.hip)
+  float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;
   int splits_ = 8;

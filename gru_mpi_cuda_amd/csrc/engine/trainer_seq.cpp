@@ -264,6 +264,16 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       gru_bwd_seq(a, s);
+    } else if (q.big) {
+      SeqBwdArgs a;
+      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; a.HSf = y.HSf;
+      a.WhhT = y.WhhT; a.xbuf = xbuf_; a.part = bpart_;
+      a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)tok; a.dgi = y.dgi;
+      a.dgiT_n_only = l == 0 && dgiT_share_;
+      a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
+      a.T = T; a.Bp = B; a.H = H;
+      fill_f32(reinterpret_cast<float*>(a.cnt), 8192, 0.f, s);
+      gru_bwd_seq_big(a, s);
     } else {
       for (int t = T - 1; t >= 0; --t) bwd_step(l, t, s);
     }
@@ -423,7 +433,7 @@ std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
                   (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : fwd_big_ ? "persistent-big" : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
-    p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : "per-step");
+    p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : seq_[l].big ? "persistent-big" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";
     if (seq_[l].fuse_p) p += "+dP";
   }

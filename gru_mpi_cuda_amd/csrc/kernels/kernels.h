@@ -85,6 +85,8 @@ struct StepLdsVariants {
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
   int dwfc_group = 1;    // single-GPU step: the dW_fc K-slices run after the backward sweep inside the
                          // dW_ih0 / dEmb launch (one launch fewer), 0: their own launch before it
+  int fwd_big = 1;       // large H x large batch: the persistent big-tile forward (0: T step kernels)
+  int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -172,10 +174,19 @@ struct SeqBwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
+  float* part = nullptr;           // large-H kernel: split-K partial tiles (gru_bwd_seq_big_part_floats)
+  int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
   int T = 0, Bp = 0, H = 0;
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s);
+// Persistent backward for large H with a large batch (gru_seq_big.hip): 64 tiles of 128 rows x 128
+// units x 4 K-slices = 256 workgroups, dGh exchanged through the T-deep `xbuf` ([T][Bp][3H] bf16),
+// split-K partials through `part`, epoch flags in cnt[0, 8192) (zeroed before the launch); writes
+// dghT / dgiT (ldG >= T * Bp, column t * Bp + b) and the optional row-major dgi.  (H/128)(Bp/128) = 64.
+bool gru_bwd_seq_big_supported(int H, int Bp);
+long gru_bwd_seq_big_part_floats(int H, int Bp);
+void gru_bwd_seq_big(const SeqBwdArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ FC + softmax
 struct FcXentArgs {

@@ -106,9 +106,9 @@ def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H, blaslt):
 
 @pytest.mark.parametrize("layers,B,H,E", [(1, 512, 2048, 128), (2, 1024, 1024, 128)])
 def test_trainer_grads_big_persistent_forward(layers, B, H, E):
-    """Large H with a large batch takes the persistent big-tile forward (gru_seq_big.hip) with the
-    per-step backward: full gradients against the fp64 oracle, and the loss against the all-per-step
-    schedule (GK_PERSIST=0)."""
+    """Large H with a large batch takes the persistent big-tile forward and the persistent split-K
+    backward (gru_seq_big.hip): full gradients against the fp64 oracle, and loss + gradients against
+    the all-per-step schedule (GK_PERSIST=0: the step kernels)."""
     import os
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=4 if H >= 2048 else 3, seed=6)
@@ -116,6 +116,7 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
     x, y = NameStream(B, cfg.seq, seed=9).next()
     tr = HipTrainer(cfg, params=params)
     assert tr.t.plan().startswith("fwd=persistent-big"), tr.t.plan()
+    assert all(f"bwd{l}=persistent-big" in tr.t.plan() for l in range(layers)), tr.t.plan()
     tr.forward_backward(x, y)
     assert tr.t.read_error() == 0
     g = tr.grad_dict()
@@ -133,6 +134,10 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
     assert "persistent" not in st.t.plan()
     st.forward_backward(x, y)
     assert abs(st.loss() - tr.loss()) < 1e-4 * abs(st.loss())
+    gs = st.grad_dict()
+    for k in gs:
+        e = rel(g[k], gs[k])
+        assert e < 1e-2, f"{k}: persistent vs per-step rel err {e:.5f}"
 
 
 def test_trainer_adam_step_and_learning():
