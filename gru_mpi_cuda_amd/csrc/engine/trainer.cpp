@@ -591,7 +591,10 @@ void Trainer::record_opt(hipStream_t s) {
       j.add(off_.at("bias_ih_l" + k), 0, 3 * H, nullptr, nullptr);
       j.add(off_.at("bias_hh_l" + k), 0, 3 * H, nullptr, nullptr);
     }
-    j.add(off_.at("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
+    // the plain W_fc / W_fc^T copies only where a kernel reads them: the fused V = 256 FC kernel of the
+    // sequence step reads the fragment-tiled copies only
+    const bool plain = overlap_ || fc_split_ || !(V == 256 && (H == 512 || H == 1024));
+    j.add(off_.at("fc.weight"), V, H, plain ? Wfc : nullptr, plain ? WfcT : nullptr, WfcF, WfcTF);
     j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
     // deferred slab reductions: summed inside the Adam launch where a job covers exactly the
     // gradient segment; anything else is reduced first
