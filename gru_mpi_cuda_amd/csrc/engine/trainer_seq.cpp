@@ -178,6 +178,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     } else if (fwd_big_) {
       SeqFwdArgs a = fwd_args(l);   // (flags zeroed by fwd_args: the big kernel's partner runs per-step)
       a.zero_next = nullptr; a.zero_words = 0; a.HF = nullptr;
+      a.xch_acquire = step_lds_variants().big_acq;
       gru_fwd_seq_big(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
@@ -272,6 +273,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dgiT_n_only = l == 0 && dgiT_share_;
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
       a.T = T; a.Bp = B; a.H = H;
+      a.xch_acquire = step_lds_variants().big_acq;
       fill_f32(reinterpret_cast<float*>(a.cnt), 8192, 0.f, s);
       gru_bwd_seq_big(a, s);
     } else {

@@ -95,6 +95,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
   const rsrc_g rX = mk_rsrc(a.xch, (unsigned)((size_t)T * xstep * 2));
   const rsrc_g rH0 = mk_rsrc(a.HSb, (unsigned)((size_t)Bp * H * 2));   // HS[0] (h_init, row-major)
   unsigned* const flags = a.cnt + (size_t)rg * ncg * kFlag;
+  const bool acq = a.xch_acquire != 0;
   auto stage = [&](int buf, int kt, int t) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -104,7 +105,8 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
         const int c = swz(r, sslot);
         if (t > 0) {   // producer 2 kt + c / 4, its tile [128][32]: row r, units 8 (c % 4) ..
           const unsigned off = (unsigned)((((size_t)(t - 1) * nrg + rg) * ncg + 2 * kt + (c >> 2)) * 4096 + r * 32 + (c & 3) * 8) * 2;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);   // aux 16 = sc1
+          if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
+          else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);     // aux 16 = sc1
         } else {
           const unsigned off = (unsigned)(((size_t)(b0 + r) * H + kt * 64 + c * 8) * 2);
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rH0, dst, 16, off, 0, 0, 0);
@@ -136,15 +138,23 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
               ok = __hip_atomic_load(flags + lane * kFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t;
             if (__all(ok)) break;
             __builtin_amdgcn_s_sleep(1);
-            if ((n++ & 63u) == 0u) {
-              if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
+            if ((n++ & 63u) == 0u) {   // (first check: the clock only, as gru_seq.hip SpinBudget)
               const unsigned long long now = __builtin_amdgcn_s_memrealtime();
               if (!t0) t0 = now;
+              else if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
               else if (now - t0 > kSpinTicks) {
                 if (lane == 0 && a.err) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
               }
             }
+          }
+          // acquire (MI355X_MICROARCH.md 'Inter-workgroup visibility': release-side sc1 stores + drain,
+          // consumer agent acquire by one wave, vmcnt(0), barrier, then plain loads): the row group's h
+          // is fetched into this XCD's L2 once and shared by its workgroups, where sc1 loads would
+          // fetch it from the memory side once per workgroup
+          if (acq) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
         }
         __syncthreads();
@@ -305,6 +315,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   const rsrc_g rP = mk_rsrc(a.part, (unsigned)((size_t)2 * 64 * kBS * kPiece * 16));
   unsigned* const gflag = a.cnt;
   unsigned* const pflag = a.cnt + 4096;
+  const bool acq = a.xch_acquire != 0;
   // epilogue items: row quarter `split`, piece P = w + 8 pp -> (wnp, ii, jn), 4 rows e each
   const int sq = split, wmq = sq >> 1, ibq = 2 * (sq & 1);
   float carry[2][4];
@@ -325,7 +336,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       const int col = (kt0 + kt) * 64 + swz(rr, sslot) * 8;
       if (w < 4) {
         const unsigned off = (unsigned)((((size_t)(t + 1) * Bp + b0 + rr) * H3 + col) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);   // aux 16 = sc1
+        if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);     // aux 16 = sc1
       } else {
         __builtin_amdgcn_global_load_lds(a.WhhT + (size_t)(j0 + rr) * H3 + col, dst, 16, 0, 0);
       }
@@ -340,10 +352,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
                                                 __HIP_MEMORY_SCOPE_AGENT) >= target;
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
-      if ((n++ & 63u) == 0u) {
-        if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
+      if ((n++ & 63u) == 0u) {   // (first check: the clock only)
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         if (!t0) t0 = now;
+        else if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
         else if (now - t0 > kSpinTicks) {
           if (lane == 0 && a.err) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -379,11 +391,16 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       // dGh_{t+1}: column block cb of this slice (gate cb / ntu, unit tile cb % ntu) x 4 row quarters
-      if (w == 0)
+      if (w == 0) {
         spin_until(gflag, 4 * ncb, 16, ep, [&](int l) {
           const int cb = split * ncb + (l >> 2);
           return (rt * ntu + cb % ntu) * kBS + (l & 3);
         });
+        if (acq) {   // as the forward: plain A loads behind one wave's agent acquire, shared in L2
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
       __syncthreads();
 #pragma unroll
       for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);

@@ -87,6 +87,7 @@ struct StepLdsVariants {
                          // dW_ih0 / dEmb launch (one launch fewer), 0: their own launch before it
   int fwd_big = 1;       // large H x large batch: the persistent big-tile forward (0: T step kernels)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
+  int big_acq = 1;       // the large-H persistent kernels read the exchange behind an agent acquire (0: sc1 loads)
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -125,6 +126,8 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
+  int xch_acquire = 1;             // large-H kernels: exchange read by plain loads behind an agent acquire
+                                   // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -175,6 +178,7 @@ struct SeqBwdArgs {
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
   float* part = nullptr;           // large-H kernel: split-K partial tiles (gru_bwd_seq_big_part_floats)
+  int xch_acquire = 1;             // large-H kernel: as SeqFwdArgs::xch_acquire
   int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
   int T = 0, Bp = 0, H = 0;
 };

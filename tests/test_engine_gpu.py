@@ -138,6 +138,21 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
     for k in gs:
         e = rel(g[k], gs[k])
         assert e < 1e-2, f"{k}: persistent vs per-step rel err {e:.5f}"
+    # the exchange read through sc1 loads instead of plain loads behind the agent acquire: the same
+    # bytes, so the same gradients bit for bit (a stale line on either path would differ)
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    C.set_step_lds_variants(dict(big_acq=0))
+    try:
+        sc = HipTrainer(cfg, params=params)
+        sc.forward_backward(x, y)
+        assert sc.t.read_error() == 0
+        g1 = sc.grad_dict()
+    finally:
+        C.set_step_lds_variants(saved)
+    for k in g1:
+        assert torch.equal(g1[k], g[k]), k
 
 
 def test_trainer_adam_step_and_learning():
