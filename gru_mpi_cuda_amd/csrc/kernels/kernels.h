@@ -85,7 +85,9 @@ struct StepLdsVariants {
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
   int dwfc_group = 1;    // single-GPU step: the dW_fc K-slices run after the backward sweep inside the
                          // dW_ih0 / dEmb launch (one launch fewer), 0: their own launch before it
-  int fwd_big = 1;       // large H x large batch: the persistent big-tile forward (0: T step kernels)
+  int fwd_big = 0;       // large H x large batch: the persistent big-tile forward instead of T step kernels
+                         // (h2048: 3.04-3.20 ms per forward vs 2.89 for the 64-row step kernels,
+                         // profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
   int big_acq = 1;       // the large-H persistent kernels read the exchange behind an agent acquire (0: sc1 loads)
 };

@@ -111,10 +111,17 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
     the all-per-step schedule (GK_PERSIST=0: the step kernels)."""
     import os
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=4 if H >= 2048 else 3, seed=6)
     params = init_params(cfg)
     x, y = NameStream(B, cfg.seq, seed=9).next()
-    tr = HipTrainer(cfg, params=params)
+    saved = C.step_lds_variants()
+    C.set_step_lds_variants(dict(fwd_big=1))   # (off by default: the step kernels measured faster)
+    try:
+        tr = HipTrainer(cfg, params=params)
+    finally:
+        C.set_step_lds_variants(saved)
     assert tr.t.plan().startswith("fwd=persistent-big"), tr.t.plan()
     assert all(f"bwd{l}=persistent-big" in tr.t.plan() for l in range(layers)), tr.t.plan()
     tr.forward_backward(x, y)
@@ -140,10 +147,7 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
         assert e < 1e-2, f"{k}: persistent vs per-step rel err {e:.5f}"
     # the exchange read through sc1 loads instead of plain loads behind the agent acquire: the same
     # bytes, so the same gradients bit for bit (a stale line on either path would differ)
-    from gru_mpi_cuda_amd.ops import load_ext
-    C = load_ext()
-    saved = C.step_lds_variants()
-    C.set_step_lds_variants(dict(big_acq=0))
+    C.set_step_lds_variants(dict(big_acq=0, fwd_big=1))
     try:
         sc = HipTrainer(cfg, params=params)
         sc.forward_backward(x, y)
