@@ -75,11 +75,15 @@ def _link(objs, out, shared=True, libs=()):
     newest = max(os.path.getmtime(o) for o in objs)
     if os.path.exists(out) and os.path.getmtime(out) >= newest:
         return
-    cmd = [HIPCC, f"--offload-arch={ARCH}", *(["-shared"] if shared else []), "-fPIC", *objs, "-o", out,
+    # link to a temporary name, then rename: a reader (a tree snapshot, a running process loading the
+    # library) sees the old file or the new one, never a partly written one
+    tmp = out + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *(["-shared"] if shared else []), "-fPIC", *objs, "-o", tmp,
            "-L/opt/rocm/lib", *libs, "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
 
 
 HOST_TOOL = ["capi/ckpt_check.cpp", "capi/ckpt_reader.cpp"]

@@ -301,7 +301,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       j.add(loss_part_, nloss_, 1, loss_);
       j.bump = step_;
     }
-    if (j.n) reduce_slabs_multi(j, s);
+    if (l == 0 && fc_held_on_ && step_lds_variants().dwfc_group == 2 && gemm_small_kblocks(fc_held_) % 4 == 0) {
+      gemm_small_with_slabs(fc_held_, j, s);   // the held dW_fc K-slices beside layer 0's reduce
+      fc_held_on_ = false;
+    } else if (j.n) {
+      reduce_slabs_multi(j, s);
+    }
     if (!q.fuse_w)
       wgrad_gemm(y.dghT, (int)tok, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
                  q.bwd ? nullptr : G("bias_hh_l" + k), s);

@@ -833,8 +833,9 @@ def test_bench_shape_matches_oracle_and_cpu_adam():
 @pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 256, 128)])
 def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
     """StepLdsVariants.dwfc_group: the single-GPU step runs the dW_fc K-slices after the backward
-    sweep inside the dW_ih0 / dEmb launch (4 chunks of 256 instead of 2 of 512: the same k order), so
-    the weights after three Adam steps equal the own-launch plan bit for bit."""
+    sweep inside the dW_ih0 / dEmb launch (1) or the slab-reduce launch (2) -- 4 chunks of 256 instead
+    of 2 of 512: the same k order -- so the weights after three Adam steps equal the own-launch plan
+    (0) bit for bit."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
@@ -845,7 +846,7 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
     batches = [ds.next() for _ in range(3)]
     out = []
     try:
-        for v in (0, 1):
+        for v in (0, 1, 2):
             C.set_step_lds_variants(dict(dwfc_group=v))
             tr = HipTrainer(cfg, params=params)
             for x, y in batches:
@@ -855,4 +856,5 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
             out.append((tr.params.clone(), tr.loss()))
     finally:
         C.set_step_lds_variants(saved)
-    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
+    for o in out[1:]:
+        assert torch.equal(out[0][0], o[0]) and out[0][1] == o[1]
