@@ -105,7 +105,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   for (int l = 0; l < L; ++l) {
     if (seq_[l].fuse_w) o_pw[l] = R((size_t)nrb * 3 * H * H * 4);
     if (seq_[l].fuse_w && persist_fwd_) o_hf[l] = R((tok + B) * H * 2);
-    if (seq_[l].bwd) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
+    if (seq_[l].bwd || seq_[l].big) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
   }
   size_t o_pP = seq_[0].fuse_p ? R((size_t)nrb * V * 3 * H * 4) : 0;
   // per-step backward on the split-K LDS kernel: partial tiles + monotonic arrival counters
@@ -129,8 +129,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   for (int l = 0; l < L; ++l) {
     seq_[l].dWhh_part = seq_[l].fuse_w ? arena_.get<float>(o_pw[l]) : nullptr;
     seq_[l].HF = o_hf[l] ? arena_.get<u16>(o_hf[l]) : nullptr;   // zero-filled: HF[0] = h_init
-    seq_[l].dbhh_part = seq_[l].bwd ? arena_.get<float>(o_pbh[l]) : nullptr;
-    seq_[l].dbih_part = seq_[l].bwd ? arena_.get<float>(o_pbi[l]) : nullptr;
+    seq_[l].dbhh_part = (seq_[l].bwd || seq_[l].big) ? arena_.get<float>(o_pbh[l]) : nullptr;
+    seq_[l].dbih_part = (seq_[l].bwd || seq_[l].big) ? arena_.get<float>(o_pbi[l]) : nullptr;
   }
   dP_part_ = seq_[0].fuse_p ? arena_.get<float>(o_pP) : nullptr;
   bpart_ = any_big ? arena_.get<float>(o_bp) : nullptr;

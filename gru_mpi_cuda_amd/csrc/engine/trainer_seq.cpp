@@ -21,10 +21,12 @@ static bool ar_span() { return true; }
 
 // Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
 // split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
-// 128 x 128 split-K path only.  GK_WGRAD_GEMM overrides the default.
+// 128 x 128 split-K path only; default (0) "auto": hipBLASLt for the products with >= 8 M outputs and
+// >= 60 GFLOP (dW_hh at H = 2048: one unsplit library GEMM, no slabs; h2048 step 8.93 -> 8.68 ms,
+// profiles/r4_h2048_wgrad_ab.jsonl), gemm256 for the rest.  GK_WGRAD_GEMM overrides it.
 static int wgrad_engine() {   // read at record time (tests switch it per trainer)
   const char* v = std::getenv("GK_WGRAD_GEMM");
-  if (!v || !*v) return 256;
+  if (!v || !*v) return 0;
   if (std::string(v) == "lib") return 1;
   if (std::string(v) == "128") return 128;
   return 256;
@@ -47,7 +49,14 @@ static int gemm256_splits(int M, int N, int K) {
 
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
-  if (wgrad_engine() == 256) {
+  const int eng = wgrad_engine();
+  if (eng == 0 && (double)M * N >= 8e6 && 2.0 * M * N * (double)K >= 60e9) {
+    GemmArgs w;   // one unsplit library GEMM straight into the gradient (+ a row-sum pass for the bias)
+    w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
+    w.M = M; w.N = N; w.K = K;
+    if (gemm_library(w, s)) return;
+  }
+  if (eng == 256 || eng == 0) {
     GemmArgs w;
     w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.M = M; w.N = N; w.K = K;
     const int sp = gemm256_splits(M, N, K);
@@ -271,6 +280,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.WhhT = y.WhhT; a.xbuf = xbuf_; a.part = bpart_;
       a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)tok; a.dgi = y.dgi;
       a.dgiT_n_only = l == 0 && dgiT_share_;
+      a.dbhh_part = q.dbhh_part; a.dbih_part = l == 0 ? q.dbih_part : nullptr;   // (l > 0: from the dW_ih GEMM)
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
       a.T = T; a.Bp = B; a.H = H;
       a.xch_acquire = step_lds_variants().big_acq;
@@ -284,14 +294,14 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // weight gradients not accumulated inside the sequence kernel
     SlabJobs j;
     if (q.fuse_w) slab_job(j, q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
-    if (q.bwd) slab_job(j, q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
+    if (q.bwd || q.big) slab_job(j, q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
     // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail -- or, when the
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
       if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
       else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     }
-    if (l == 0 && q.bwd) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
+    if (l == 0 && (q.bwd || q.big)) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
     // all-reduced with it), else with layer 0's reduce
     if (dp ? l == L - 1 : l == 0)
@@ -301,15 +311,10 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       j.add(loss_part_, nloss_, 1, loss_);
       j.bump = step_;
     }
-    if (l == 0 && fc_held_on_ && step_lds_variants().dwfc_group == 2 && gemm_small_kblocks(fc_held_) % 4 == 0) {
-      gemm_small_with_slabs(fc_held_, j, s);   // the held dW_fc K-slices beside layer 0's reduce
-      fc_held_on_ = false;
-    } else if (j.n) {
-      reduce_slabs_multi(j, s);
-    }
+    if (j.n) reduce_slabs_multi(j, s);
     if (!q.fuse_w)
       wgrad_gemm(y.dghT, (int)tok, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
-                 q.bwd ? nullptr : G("bias_hh_l" + k), s);
+                 (q.bwd || q.big) ? nullptr : G("bias_hh_l" + k), s);
     if (l == 0) {
       if (!q.fuse_p) {
         GemmArgs p;   // dP = onehot(x)^T · dGi, split-K then reduce
@@ -321,7 +326,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
         gemm_nt(p, s);
         float* dPd = dp ? dP_target() : dP_;
         reduce_slabs(slab_w_, sp, (long)V * H3, dPd, s);
-        if (!q.bwd) colsum(dPd, V, H3, G("bias_ih_l0"), s);
+        if (!q.bwd && !q.big) colsum(dPd, V, H3, G("bias_ih_l0"), s);
       }
       if (dp) {   // layer 0's group [W_hh0, b_hh0, b_ih0, dP] closes the step's collectives
         ar_ready_ = group_end(0);

@@ -164,7 +164,7 @@ void rowsum_bf16(const u16* A, int lda, int M, int K, float* out, hipStream_t s)
   hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(M), dim3(256), 0, s, A, lda, K, out);
 }
 
-static bool gemm_library(const GemmArgs& a, hipStream_t s) {
+bool gemm_library(const GemmArgs& a, hipStream_t s) {
   if (!gemm_library_ok(a)) return false;
   if (!blaslt_gemm_nt(a.A, a.lda, a.B, a.ldb, a.C, a.ldc, a.M, a.N, a.K, a.accumulate != 0, s)) return false;
   if (a.rowsumA) hipLaunchKernelGGL(rowsum_bf16_kernel, dim3(a.M), dim3(256), 0, s, a.A, a.lda, a.K, a.rowsumA);

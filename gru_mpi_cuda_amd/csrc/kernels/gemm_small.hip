@@ -15,7 +15,6 @@
 #include <string>
 #include "kernels.h"
 #include "common.h"
-#include "optim_dev.h"
 
 namespace gk {
 
@@ -156,22 +155,6 @@ __global__ void __launch_bounds__(256, NKB <= 4 ? 2 : 1) gemm_small_prep_kernel(
   gemm_small_body<NKB, BIAS, false>(a, xcd_remap_s(blockIdx.x, ng), ntn, ntm, lds, nch);
 }
 
-// + leading blocks running a multi-tensor slab reduction (reduce_slabs_multi's jobs, whose 16 x 72
-// transpose tile aliases the GEMM's LDS): one launch for a memory-bound reduce and a latency-bound
-// GEMM that does not depend on it.  nslab is a multiple of 8, so GEMM block b - nslab sits on the
-// XCD xcd_remap_s assumes.
-template <int NKB, bool ROWSUM>
-__global__ void __launch_bounds__(256, 2) gemm_small_slabs_kernel(GemmArgs a, int ntn, int ntm, int nch,
-                                                                  SlabJobs j, int nslab) {
-  __shared__ __attribute__((aligned(16))) u16 lds[NKB][2][64 * 64];
-  const int b = blockIdx.x;
-  if (b < nslab) {
-    reduce_multi_body(j, b, reinterpret_cast<u16 (*)[72]>(&lds[0][0][0]));
-    return;
-  }
-  gemm_small_body<NKB, false, ROWSUM>(a, xcd_remap_s(b - nslab, gridDim.x - nslab), ntn, ntm, lds, nch);
-}
-
 // 64-deep blocks per chunk (0 = unsupported); *nch = chunks per K-slice (slices of n x 512 stream)
 static int small_blocks(const GemmArgs& a, int* nch) {
   *nch = 1;
@@ -237,16 +220,6 @@ void gemm_small_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
     return;
   switch (nkb) { GP_CASE(2) GP_CASE(3) GP_CASE(4) GP_CASE(8) default: break; }
 #undef GP_CASE
-}
-
-void gemm_small_with_slabs(const GemmArgs& g, SlabJobs& j, hipStream_t s) {
-  const int kb = gemm_small_kblocks(g);
-  if (!kb || kb % 4 || (g.bias && g.splits == 1)) throw std::runtime_error("gemm_small_with_slabs: unsupported GEMM");
-  const int nslab = (reduce_slabs_blocks(j) + 7) / 8 * 8;
-  const int ntn = g.N / 64, ntm = g.M / 64, nch = kb / 4;
-  const dim3 grid(nslab + ntn * ntm * g.splits), block(256);
-  if (g.rowsumA) hipLaunchKernelGGL((gemm_small_slabs_kernel<4, true>), grid, block, 0, s, g, ntn, ntm, nch, j, nslab);
-  else hipLaunchKernelGGL((gemm_small_slabs_kernel<4, false>), grid, block, 0, s, g, ntn, ntm, nch, j, nslab);
 }
 
 int gemm_small_group_depth(const GemmArgs* jobs, int n) {

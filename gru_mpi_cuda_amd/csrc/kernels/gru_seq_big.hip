@@ -323,6 +323,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
     for (int e = 0; e < 4; ++e) carry[pp][e] = 0.f;
+  // bias gradients of the quarter's 32 rows, summed over all steps: [16-row half ii][dar, daz,
+  // dan * r, dan][128 units] in LDS beside the ring, each slot owned by one lane (no atomics: the
+  // sums are deterministic)
+  __shared__ float bacc[2][4][128];
+  for (int i = tid; i < 2 * 4 * 128; i += 512) (&bacc[0][0][0])[i] = 0.f;
   auto item_off = [&](int pp, int e) {
     const int P = w + 8 * pp, wnp = P >> 2, ii = (P >> 1) & 1, jn = P & 1;
     return (size_t)(b0 + 32 * sq + ii * 16 + lq * 4 + e) * H + j0 + wnp * 32 + jn * 16 + lr;
@@ -390,6 +395,12 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // W_hh^T rows of the first ring slots do not depend on the exchange: waves 4-7 put them in flight
+      // before the wait (each wave's vmcnt counts only its own pieces, so the ring's waits still hold)
+      if (w >= 4) {
+#pragma unroll
+        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
+      }
       // dGh_{t+1}: column block cb of this slice (gate cb / ntu, unit tile cb % ntu) x 4 row quarters
       if (w == 0) {
         spin_until(gflag, 4 * ncb, 16, ep, [&](int l) {
@@ -402,8 +413,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
         }
       }
       __syncthreads();
+      if (w < 4) {
 #pragma unroll
-      for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
+        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
+      }
       for (int kt = 0; kt < nk; ++kt) {
         const int ahead = min(kBNS - 2, nk - 1 - kt);
         if (ahead >= 2) vmwait<8>(); else if (ahead == 1) vmwait<4>(); else vmwait<0>();
@@ -468,6 +481,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
     for (int pp = 0; pp < 2; ++pp) {
       const int P = w + 8 * pp, wnp = P >> 2, ii = (P >> 1) & 1, jn = P & 1;
       const int uu = wnp * 32 + jn * 16 + lr;
+      float bs[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rq = ii * 16 + lq * 4 + e;
@@ -480,6 +494,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
         const float dar = dan * ghn * r * (1.f - r);
         const float daz = dz * z * (1.f - z);
         carry[pp][e] = z * dh;
+        bs[0] += dar; bs[1] += daz; bs[2] += dan * r; bs[3] += dan;
         const u16 br = f2bf(dar), bz = f2bf(daz), bn = f2bf(dan * r), bi = f2bf(dan);
         stR[(0 * 32 + rq) * kRowPad + uu] = br;
         stR[(1 * 32 + rq) * kRowPad + uu] = bz;
@@ -489,6 +504,15 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
         stT[(1 * 128 + uu) * 40 + rq] = bz;
         stT[(2 * 128 + uu) * 40 + rq] = bn;
         stT[(3 * 128 + uu) * 40 + rq] = bi;
+      }
+      if (a.dbhh_part || a.dbih_part) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = bs[q];
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          if (lq == 0) bacc[ii][q][uu] += v;
+        }
       }
     }
     __syncthreads();
@@ -526,6 +550,16 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       if (kind < 3 && a.dghT) *reinterpret_cast<uint4*>(a.dghT + off) = v;
       if (a.dgiT && (kind == 3 || (kind < 2 && !a.dgiT_n_only))) *reinterpret_cast<uint4*>(a.dgiT + off) = v;
     }
+  }
+  // ---- bias-gradient partials of this workgroup's 32 rows ("row block" rt * 4 + split of
+  // dbhh_part / dbih_part [Bp/32][3H]): the two 16-row halves' LDS sums
+  if (a.dbhh_part || a.dbih_part) {
+    __syncthreads();
+    const int q = tid >> 7, u = tid & 127;
+    const float v = bacc[0][q][u] + bacc[1][q][u];
+    const size_t rb = (size_t)(b0 / 32 + sq) * H3;
+    if (a.dbhh_part && q < 3) a.dbhh_part[rb + q * H + j0 + u] = v;
+    if (a.dbih_part && q != 2) a.dbih_part[rb + (q == 3 ? 2 : q) * H + j0 + u] = v;
   }
 }
 

@@ -85,8 +85,9 @@ struct StepLdsVariants {
   int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
   int dwfc_group = 1;    // single-GPU step: the dW_fc K-slices run after the backward sweep inside the
                          // dW_ih0 / dEmb launch (one launch fewer; 0.2183-0.2226 vs 0.2255-0.2274 ms,
-                         // profiles/r4_dwfc_group_ab.jsonl), 2: inside the slab-reduce launch before
-                         // it, 0: their own launch before the backward
+                         // profiles/r4_dwfc_group_ab.jsonl), 0: their own launch before the backward.
+                         // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
+                         // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
   int fwd_big = 0;       // large H x large batch: the persistent big-tile forward instead of T step kernels
                          // (h2048: 3.04-3.20 ms per forward vs 2.89 for the 64-row step kernels,
                          // profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl)
@@ -332,6 +333,9 @@ struct GemmArgs {
 // algo 0 sends plain (no one-hot, no bias, unsplit) products of >= GK_BLASLT_MIN_GFLOP to hipBLASLt
 bool gemm_library_ok(const GemmArgs& a);
 bool gemm_library_wanted(const GemmArgs& a);
+// the product on hipBLASLt (+ the row-sum pass when rowsumA): false, with nothing launched, when the
+// library has no algorithm for the shape
+bool gemm_library(const GemmArgs& a, hipStream_t s);
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
 bool gemm256_ok(const GemmArgs& a);
@@ -402,9 +406,6 @@ struct SlabJobs { SlabJob job[24]; int blk_start[25]; int n = 0; int* bump = nul
     job[n++] = SlabJob{s, d, (long)R * C, splits, bf, bfT, R, C}; } };
 void reduce_slabs_multi(SlabJobs& j, hipStream_t s);
 int reduce_slabs_blocks(SlabJobs& j);   // fills j.blk_start, returns the launch's block count
-// a gemm_small product (K-slices of a multiple of 256, no bias) and a slab reduction in ONE launch:
-// the reduction's blocks first, then the GEMM's 64 x 64 tiles (4-block chunks, two workgroups per CU)
-void gemm_small_with_slabs(const GemmArgs& g, SlabJobs& j, hipStream_t s);
 // "FT" (fragment-tiled) bf16 layout of a K-contiguous [R][K] matrix: element (r, k) at
 //   ((r/16 * K/32 + k/32) * 64 + (r%16) + 16*((k%32)/8)) * 8 + k%8
 // i.e. every 16x32 MFMA operand fragment is 1 KB contiguous in lane order, so a fragment load is

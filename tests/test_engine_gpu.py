@@ -833,9 +833,8 @@ def test_bench_shape_matches_oracle_and_cpu_adam():
 @pytest.mark.parametrize("layers,H,B", [(1, 512, 256), (2, 256, 128)])
 def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
     """StepLdsVariants.dwfc_group: the single-GPU step runs the dW_fc K-slices after the backward
-    sweep inside the dW_ih0 / dEmb launch (1) or the slab-reduce launch (2) -- 4 chunks of 256 instead
-    of 2 of 512: the same k order -- so the weights after three Adam steps equal the own-launch plan
-    (0) bit for bit."""
+    sweep inside the dW_ih0 / dEmb launch (1) -- 4 chunks of 256 instead of 2 of 512: the same k
+    order -- so the weights after three Adam steps equal the own-launch plan (0) bit for bit."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
@@ -846,7 +845,7 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
     batches = [ds.next() for _ in range(3)]
     out = []
     try:
-        for v in (0, 1, 2):
+        for v in (0, 1):
             C.set_step_lds_variants(dict(dwfc_group=v))
             tr = HipTrainer(cfg, params=params)
             for x, y in batches:
