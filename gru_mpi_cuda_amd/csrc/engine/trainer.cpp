@@ -15,8 +15,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     : d_(d), o_(o), params_(params), grads_(grads), m_(m), v_(v), nflat_(nflat), off_(offsets) {
   if (d_.V % 64 || d_.E % 64 || d_.H % 64)
     throw std::runtime_error("HIP engine needs vocab, embed and hidden to be multiples of 64");
-  blaslt_init();   // library handle + workspace now, never inside the step-graph capture
   Bp_ = round_up(std::max(d_.B, 1), 64);
+  // library handle + workspace now, never inside the step-graph capture (also where the weight-
+  // gradient engine will route dW_hh to the library)
+  blaslt_init(wgrad_prefers_library(3 * d_.H, d_.H, (long)d_.T * Bp_));
   C_ = std::max(1, d_.chunks);
   while (C_ > 1 && d_.T % C_) --C_;
   Tc_ = d_.T / C_;

@@ -50,7 +50,7 @@ static int gemm256_splits(int M, int N, int K) {
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
   const int eng = wgrad_engine();
-  if (eng == 0 && (double)M * N >= 8e6 && 2.0 * M * N * (double)K >= 60e9) {
+  if (eng == 0 && wgrad_prefers_library(M, N, K)) {
     GemmArgs w;   // one unsplit library GEMM straight into the gradient (+ a row-sum pass for the bias)
     w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
     w.M = M; w.N = N; w.K = K;

@@ -46,8 +46,11 @@ template <int N> DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N)
 }  // namespace
 
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[kNS][(128 + 96) * 64];
-  __shared__ __attribute__((aligned(16))) u16 st[128 * 32];   // the step's bf16 h tile [row][unit]
+  // ONE __shared__ object: with a second one hipcc cannot tell the ring's LDS-DMA writes from the
+  // other object's reads and drains vmcnt(0) before every ds_read (cdna_hip_programming.md §5 4a)
+  __shared__ __attribute__((aligned(16))) u16 lds_all[kNS * (128 + 96) * 64 + 128 * 32];
+  u16 (*lds)[(128 + 96) * 64] = reinterpret_cast<u16 (*)[(128 + 96) * 64]>(lds_all);
+  u16* st = lds_all + kNS * (128 + 96) * 64;   // the step's bf16 h tile [row][unit]
   const int H = a.H, Bp = a.Bp, T = a.T;
   const int nrg = Bp / 128, ncg = H / 32;
   const int bid = blockIdx.x, xcd = bid & 7, ib = bid >> 3;
@@ -296,7 +299,9 @@ DEV int big_bwd_ntu(int H) { return H / 128; }
 }  // namespace
 
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[kBNS][256 * 64];
+  // ONE __shared__ object (ring + bias accumulators): see the forward
+  __shared__ __attribute__((aligned(16))) u16 lds_all[kBNS * 256 * 64 + 2 * 4 * 128 * 2];
+  u16 (*lds)[256 * 64] = reinterpret_cast<u16 (*)[256 * 64]>(lds_all);
   const int H = a.H, H3 = 3 * H, Bp = a.Bp, T = a.T;
   const int ntu = big_bwd_ntu(H), ntr = Bp / 128;
   const int bid = blockIdx.x, x = bid & 7, ib = bid >> 3;
@@ -326,7 +331,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   // bias gradients of the quarter's 32 rows, summed over all steps: [16-row half ii][dar, daz,
   // dan * r, dan][128 units] in LDS beside the ring, each slot owned by one lane (no atomics: the
   // sums are deterministic)
-  __shared__ float bacc[2][4][128];
+  float (*bacc)[4][128] = reinterpret_cast<float (*)[4][128]>(lds_all + kBNS * 256 * 64);
   for (int i = tid; i < 2 * 4 * 128; i += 512) (&bacc[0][0][0])[i] = 0.f;
   auto item_off = [&](int pp, int e) {
     const int P = w + 8 * pp, wnp = P >> 2, ii = (P >> 1) & 1, jn = P & 1;

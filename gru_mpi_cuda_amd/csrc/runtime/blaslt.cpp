@@ -100,8 +100,8 @@ void* workspace_for(State& s, hipStream_t stream) {
 
 }  // namespace
 
-void blaslt_init() {
-  if (!blaslt_enabled()) return;
+void blaslt_init(bool force) {
+  if (!force && !blaslt_enabled()) return;
   State& s = st();
   std::lock_guard<std::mutex> g(s.mu);
   init_locked(s);

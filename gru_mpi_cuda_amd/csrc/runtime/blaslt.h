@@ -11,7 +11,9 @@ namespace gk {
 using u16 = unsigned short;
 
 // Create the handle and the workspace (call before any stream capture; idempotent).
-void blaslt_init();
+// force: create the handle and workspace even when GK_BLASLT is off (a caller that routes some of its
+// own products to the library, e.g. the trainer's weight-gradient engine)
+void blaslt_init(bool force = false);
 // Smallest GEMM (2*M*N*K, in GFLOP) routed to the library under algo 0; env GK_BLASLT_MIN_GFLOP,
 // default 60.  The library is OFF by default (gemm256 took the weight gradients in round 2);
 // GK_BLASLT=1 enables it.

@@ -1,7 +1,7 @@
 #!/bin/bash
 # fused bias partials in the large-H backward + auto library dW_hh: tests, h2048 / h1024_l2 benches, trace
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread -k "big_persistent or dwfc or bench_shape" > gpurun_out/r4_c7_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread -k "big_persistent or dwfc or bench_shape or wgrad_library" > gpurun_out/r4_c7_tests.log 2>&1
 rc=$?; tail -7 gpurun_out/r4_c7_tests.log; [ $rc -ne 0 ] && exit $rc
 out=gpurun_out/r4_c7_ab.jsonl
 b() { timeout -k 10 300 python bench.py --steps 6 --warmup 2 "$@" 2>/dev/null | grep '^{'; }

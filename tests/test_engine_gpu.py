@@ -857,3 +857,29 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
         C.set_step_lds_variants(saved)
     for o in out[1:]:
         assert torch.equal(out[0][0], o[0]) and out[0][1] == o[1]
+
+
+def test_wgrad_library_engine_matches_gemm256():
+    """The auto weight-gradient engine sends dW_hh at H = 2048 over >= 2384 tokens (>= 8 M outputs,
+    >= 60 GFLOP) to one unsplit hipBLASLt GEMM, captured in the step graph; it must agree with the
+    gemm256 split-K path (GK_WGRAD_GEMM=256) on every gradient."""
+    import os
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    cfg = GRUConfig(vocab=256, embed=128, hidden=2048, layers=1, batch=512, seq=8, seed=4)
+    params = init_params(cfg)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=5).next()
+    grads = []
+    for eng in ("", "256"):
+        if eng:
+            os.environ["GK_WGRAD_GEMM"] = eng
+        try:
+            tr = HipTrainer(cfg, params=params)
+            tr.forward_backward(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            grads.append(tr.grad_dict())
+        finally:
+            os.environ.pop("GK_WGRAD_GEMM", None)
+    for k in grads[0]:
+        e = rel(grads[0][k], grads[1][k])
+        assert e < 1e-3, f"{k}: library vs gemm256 rel err {e:.2e}"
