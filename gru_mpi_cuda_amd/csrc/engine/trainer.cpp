@@ -68,9 +68,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     const char* fw = std::getenv("GK_FWD_WAVE");
     fwd_wave_ = persist_fwd_ && L >= 2 && !(fw && fw[0] == '0') && gru_fwd_seq2_supported(H, B);
   }
-  // large H with a big batch: the persistent big-tile forward where the register-resident one does
-  // not fit (GK_PERSIST=0 turns every persistent kernel off)
-  fwd_big_ = allow && !persist_fwd_ && step_lds_variants().fwd_big && gru_fwd_seq_big_supported(H, B);
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);
   if (const char* xl = std::getenv("GK_XCD_LOCAL")) xcd_local_ = std::atoi(xl) != 0;
   if (step_algo_ == 2 && !gru_step_lds_ok(H, B)) step_algo_ = 0;

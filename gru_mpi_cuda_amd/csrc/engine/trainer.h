@@ -205,7 +205,6 @@ class Trainer {
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
-  bool fwd_big_ = false;       // large H, large batch: the persistent 128 x 96-tile forward (gru_seq_big.hip)
   float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;

@@ -184,11 +184,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ++l;
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
-    } else if (fwd_big_) {
-      SeqFwdArgs a = fwd_args(l);   // (flags zeroed by fwd_args: the big kernel's partner runs per-step)
-      a.zero_next = nullptr; a.zero_words = 0; a.HF = nullptr;
-      a.xch_acquire = step_lds_variants().big_acq;
-      gru_fwd_seq_big(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
     }
@@ -443,7 +438,7 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
 
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
-                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : fwd_big_ ? "persistent-big" : "per-step");
+                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : seq_[l].big ? "persistent-big" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";

@@ -1,27 +1,12 @@
-// Persistent large-H forward recurrence: ONE launch runs all T steps of a layer
-// whose per-step GEMM is a real GEMM (B = 512 rows, H = 2048: 12.9 GFLOP per step), where the
-// register-resident persistent kernels of gru_seq.hip do not fit and the per-step kernels of
-// gru_step_lds.hip pay a launch, a grid ramp and a drain per timestep.
+// Persistent large-H backward recurrence: ONE launch runs all T backward steps
+// of a layer whose per-step GEMM is a real GEMM (B = 512 rows, H = 2048: dh = dGh . W_hh is 12.9
+// GFLOP per step), where the register-resident persistent kernels of gru_seq.hip do not fit and the
+// per-step kernels of gru_step_lds.hip pay a launch, a grid ramp and a drain per timestep.
 //
-// Decomposition (256 workgroups, one per CU, 512 threads): workgroup (rg, cg) owns batch rows
-// [128 rg, +128) x units [32 cg, +32) (x 3 gates: the 128 x 96 tile of gru_fwd_step_lds8_kernel,
-// whose K loop and split epilogue it reuses).  All row groups of a unit group run on one XCD
-// (cg = 8-block stripe of bid % 8), so the W_hh slice they all stream (96 x H bf16) is read from
-// HBM once per XCD and served by its L2 after that.
-//
-// Per step t:
-//   1. wave 0 polls the epoch flags of the row group's H/32 producers (one lane each, sc1 loads,
-//      bounded by wall clock): step t needs h_{t-1} of its 128 rows from every unit group;
-//   2. the K loop streams A = h_{t-1} (the producers' exchange tiles, LDS-DMA with sc1) and
-//      B = W_hh gate rows (plain LDS-DMA, L2-resident) through a 4-deep LDS ring;
-//   3. gates epilogue (group 0 / 1 split as in the step kernel), the new bf16 h tile [128][32] is
-//      staged in LDS and published: 512 x 16-B sc1 stores (whole lines of this producer's own 8 KB
-//      tile of the T-deep exchange buffer), every wave drains, a barrier, one flag store (epoch t+1)
-//      -- MI355X_MICROARCH.md 'Valid forms' row 1;
-//   4. only then the stores nobody in this launch reads: fp32 h, bf16 row-major h, the transposed h
-//      (weight-gradient GEMM operand) and the r / z / n / gh_n saves of the backward.
-// The exchange slots are T-deep (a fresh address every step: no consumer L2 holds a stale line) and
-// the flags are zeroed before the launch (epochs restart at every launch).
+// (Round 4 also built the forward twin -- 256 workgroups of 128 rows x 32 units x 3 gates, W_hh
+// streamed through a 4-deep LDS ring, T-deep per-producer h tiles with epoch flags.  Correct, and
+// slower than the 64-row step kernels: h2048 forward 3.04-3.34 ms vs 2.89-2.97, step 9.24 vs 8.69-8.72
+// ms, profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl, r4_h2048_h1024_big_ab.jsonl; removed.)
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -34,8 +19,6 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void_g;
 typedef __amdgpu_buffer_rsrc_t rsrc_g;
 typedef unsigned int u32x4_g __attribute__((ext_vector_type(4)));
-constexpr int kNS = 4;                        // LDS ring: 4 x (128 + 96) rows x 128 B = 112 KiB
-constexpr int kFlag = 16;                     // uints per producer flag line (64 B)
 constexpr unsigned long long kSpinTicks = 500000000ull;   // 5 s of s_memrealtime (100 MHz)
 
 DEV int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
@@ -45,233 +28,6 @@ DEV rsrc_g mk_rsrc(const void* p, unsigned bytes) {
 template <int N> DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 }  // namespace
 
-__global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
-  // ONE __shared__ object: with a second one hipcc cannot tell the ring's LDS-DMA writes from the
-  // other object's reads and drains vmcnt(0) before every ds_read (cdna_hip_programming.md §5 4a)
-  __shared__ __attribute__((aligned(16))) u16 lds_all[kNS * (128 + 96) * 64 + 128 * 32];
-  u16 (*lds)[(128 + 96) * 64] = reinterpret_cast<u16 (*)[(128 + 96) * 64]>(lds_all);
-  u16* st = lds_all + kNS * (128 + 96) * 64;   // the step's bf16 h tile [row][unit]
-  const int H = a.H, Bp = a.Bp, T = a.T;
-  const int nrg = Bp / 128, ncg = H / 32;
-  const int bid = blockIdx.x, xcd = bid & 7, ib = bid >> 3;
-  const int cg = xcd * (ncg / 8) + ib / nrg, rg = ib % nrg;
-  const int j0 = cg * 32, b0 = rg * 128;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, grp = w >> 2, wl = w & 3;
-  const int wm = wl >> 1, wn = wl & 1;
-  const int lr = lane & 15, lq = lane >> 4;
-  const int srow = lane >> 3, sslot = lane & 7;
-  const int u = j0 + wn * 16 + lr;
-  // fragment i (rows wm*64 + 16 i ..) is finished by group i / 2 (the step kernel's split epilogue):
-  // per-item state is indexed by k = i % 2 of the group's own fragments (compile-time indices only:
-  // every group-dependent choice below is a two-way dispatch on grp, never a runtime array index)
-  float bh[3], hp[2][4], gi[2][4][3];
-#pragma unroll
-  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
-  auto row_of = [&](int i, int e) { return b0 + wm * 64 + i * 16 + lq * 4 + e; };
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) hp[k][e] = a.h0 ? a.h0[(size_t)row_of(2 * grp + k, e) * H + u] : 0.f;
-  // input projection of step t for the owned items (P table gathered by id, or Gi rows)
-  auto load_gi = [&](int t) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int b = row_of(2 * grp + k, e);
-        const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) gi[k][e][g] = src[g * H + u];
-      }
-  };
-
-  // staging: piece p (image rows 8p .. 8p+7) of a k-tile, 4 per wave: A rows for p < 16, W rows after
-  // (waves 4-7's fourth piece duplicates their first: 28 pieces over 32 slots)
-  int pc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    int p = w + 8 * q;
-    if (p >= 28) p = w;
-    pc[q] = p;
-  }
-  const size_t xstep = (size_t)nrg * ncg * 4096;                 // exchange elements per step
-  const rsrc_g rX = mk_rsrc(a.xch, (unsigned)((size_t)T * xstep * 2));
-  const rsrc_g rH0 = mk_rsrc(a.HSb, (unsigned)((size_t)Bp * H * 2));   // HS[0] (h_init, row-major)
-  unsigned* const flags = a.cnt + (size_t)rg * ncg * kFlag;
-  const bool acq = a.xch_acquire != 0;
-  auto stage = [&](int buf, int kt, int t) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = pc[q], r = p * 8 + srow;
-      lds_void_g* dst = (lds_void_g*)(&lds[buf][p * 8 * 64]);
-      if (p < 16) {
-        const int c = swz(r, sslot);
-        if (t > 0) {   // producer 2 kt + c / 4, its tile [128][32]: row r, units 8 (c % 4) ..
-          const unsigned off = (unsigned)((((size_t)(t - 1) * nrg + rg) * ncg + 2 * kt + (c >> 2)) * 4096 + r * 32 + (c & 3) * 8) * 2;
-          if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
-          else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);     // aux 16 = sc1
-        } else {
-          const unsigned off = (unsigned)(((size_t)(b0 + r) * H + kt * 64 + c * 8) * 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rH0, dst, 16, off, 0, 0, 0);
-        }
-      } else {
-        const int rb = r - 128;
-        const u16* src = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + kt * 64 + swz(rb, sslot) * 8;
-        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-      }
-    }
-  };
-  const int nk = H / 64;
-  if (a.ids || a.Gi) load_gi(0);
-
-  for (int t = 0; t < T; ++t) {
-    f32x4 acc[4][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (t > 0 || a.h0) {
-      if (t > 0) {   // h_{t-1} of the row group: every producer's flag at epoch >= t
-        if (w == 0) {
-          unsigned long long t0 = 0;
-          unsigned n = 0;
-          for (;;) {
-            bool ok = true;
-            if (lane < ncg)
-              ok = __hip_atomic_load(flags + lane * kFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t;
-            if (__all(ok)) break;
-            __builtin_amdgcn_s_sleep(1);
-            if ((n++ & 63u) == 0u) {   // (first check: the clock only, as gru_seq.hip SpinBudget)
-              const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-              if (!t0) t0 = now;
-              else if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
-              else if (now - t0 > kSpinTicks) {
-                if (lane == 0 && a.err) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-            }
-          }
-          // acquire (MI355X_MICROARCH.md 'Inter-workgroup visibility': release-side sc1 stores + drain,
-          // consumer agent acquire by one wave, vmcnt(0), barrier, then plain loads): the row group's h
-          // is fetched into this XCD's L2 once and shared by its workgroups, where sc1 loads would
-          // fetch it from the memory side once per workgroup
-          if (acq) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-        }
-        __syncthreads();
-      }
-      // 4-deep ring: 3 k-tiles in flight, one barrier per k-tile
-#pragma unroll
-      for (int s = 0; s < kNS - 1; ++s) stage(s, s, t);
-      for (int kt = 0; kt < nk; ++kt) {
-        const int ahead = min(kNS - 2, nk - 1 - kt);
-        if (ahead >= 2) vmwait<8>(); else if (ahead == 1) vmwait<4>(); else vmwait<0>();
-        lds_barrier();
-        if (kt + kNS - 1 < nk) stage((kt + kNS - 1) % kNS, kt + kNS - 1, t);
-        const u16* LA = lds[kt % kNS];
-        const u16* LB = LA + 128 * 64;
-        const int c = grp * 4 + lq;
-        bf16x8 af[4], bfr[3];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = wm * 64 + i * 16 + lr;
-          af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
-        }
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          const int r = g * 32 + wn * 16 + lr;
-          bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
-      }
-      __syncthreads();   // every wave done with the ring: it now holds the cross-group partials
-      // the non-owning group's partials -> LDS -> the owner: [4 waves][12 tiles][64 lanes] f32x4
-      f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);
-      auto swap = [&](auto G) {
-        constexpr int mine = decltype(G)::value * 2, other = 2 - mine;
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int g = 0; g < 3; ++g) red[(wl * 12 + (other + k) * 3 + g) * 64 + lane] = acc[other + k][g];
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-          for (int g = 0; g < 3; ++g) acc[mine + k][g] += red[(wl * 12 + (mine + k) * 3 + g) * 64 + lane];
-      };
-      if (grp == 0) swap(std::integral_constant<int, 0>{}); else swap(std::integral_constant<int, 1>{});
-    }
-    // pass 1: h for the owned items -> hp, the bf16 h tile into LDS
-    auto pass1 = [&](auto G) {
-      constexpr int mine = decltype(G)::value * 2;
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float ghr = acc[mine + k][0][e] + bh[0], ghz = acc[mine + k][1][e] + bh[1];
-          const float ghn = acc[mine + k][2][e] + bh[2];
-          const float r = sigmoidf_(gi[k][e][0] + ghr);
-          const float z = sigmoidf_(gi[k][e][1] + ghz);
-          const float n = tanhf_(gi[k][e][2] + r * ghn);
-          const float h = n + z * (hp[k][e] - n);
-          hp[k][e] = h;
-          st[(wm * 64 + (mine + k) * 16 + lq * 4 + e) * 32 + wn * 16 + lr] = f2bf(h);
-        }
-    };
-    if (grp == 0) pass1(std::integral_constant<int, 0>{}); else pass1(std::integral_constant<int, 1>{});
-    __syncthreads();
-    // publish: this producer's [128][32] tile, 16 B per thread, write-through; drain; one flag
-    const u32x4_g hv4 = *reinterpret_cast<const u32x4_g*>(&st[tid * 8]);
-    {
-      const unsigned off = (unsigned)((((size_t)t * nrg + rg) * ncg + cg) * 4096 + tid * 8) * 2;
-      __builtin_amdgcn_raw_buffer_store_b128(hv4, rX, off, 0, 16);   // aux 16 = sc1
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (tid == 0)
-      __hip_atomic_store(flags + cg * kFlag, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // pass 2 (after the signal): the saves of the backward, gates recomputed from the accumulators
-    // (cheaper than holding five values per item in registers across the publish)
-    auto pass2 = [&](auto G) {
-      constexpr int mine = decltype(G)::value * 2;
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const size_t o = (size_t)row_of(mine + k, e) * H + u;
-          a.HSf[(size_t)(t + 1) * Bp * H + o] = hp[k][e];
-          if (a.sr) {
-            const float ghn = acc[mine + k][2][e] + bh[2];
-            const float r = sigmoidf_(gi[k][e][0] + acc[mine + k][0][e] + bh[0]);
-            const float z = sigmoidf_(gi[k][e][1] + acc[mine + k][1][e] + bh[1]);
-            const float n = tanhf_(gi[k][e][2] + r * ghn);
-            const size_t so = (size_t)t * Bp * H + o;
-            a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = ghn;
-          }
-        }
-    };
-    if (grp == 0) pass2(std::integral_constant<int, 0>{}); else pass2(std::integral_constant<int, 1>{});
-    // row-major bf16 h: row tid / 4, units 8 (tid % 4) ..
-    *reinterpret_cast<u32x4_g*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (tid >> 2)) * H + j0 + (tid & 3) * 8) = hv4;
-    if (a.HT) {   // transposed: unit tid / 16, rows 8 (tid % 16) ..
-      const int unit = tid >> 4, seg = tid & 15;
-      u16 v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
-      *reinterpret_cast<uint4*>(a.HT + (size_t)(j0 + unit) * a.ldT + (size_t)(t + 1) * Bp + b0 + seg * 8) =
-          *reinterpret_cast<const uint4*>(v);
-    }
-    // the next step's input projection (its loads retire before the next K loop's first wait)
-    if (t + 1 < T && (a.ids || a.Gi)) load_gi(t + 1);
-    __syncthreads();   // st is rewritten by the next step's epilogue
-  }
-}
-
 // ==================================================================== persistent large-H backward
 // ONE launch runs all T backward steps of a layer at large H with a large batch (B = 512, H = 2048:
 // dh = dGh_{t+1} . W_hh is 512 x 2048 x 6144 per step), replacing T launches of the split-K step
@@ -280,8 +36,9 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_big_kernel(SeqFwdArgs a) {
 //     sk_map 1 (XCD x takes split x % 4 of every row tile of half the unit tiles);
 //   * per step t (descending): wave 0 polls the epoch flags of the dGh_{t+1} producers of this
 //     workgroup's A operand (its 128 rows x K-slice: 4 row-quarter producers of each of the slice's
-//     128-column blocks); the K loop streams A (T-deep exchange, sc1) and W_hh^T (plain) through a
-//     4-deep LDS ring; the fp32 partial tile goes out write-through (parity-double-buffered), one
+//     128-column blocks), then (xch_acquire) one agent acquire; the K loop streams A (T-deep
+//     exchange: plain loads behind the acquire, or sc1) and W_hh^T (plain, its first ring slots issued
+//     before the wait) through a 4-deep LDS ring; the fp32 partial tile goes out write-through (parity-double-buffered), one
 //     flag per (tile, split), and the S partners wait for each other;
 //   * the epilogue runs on row quarter `split` of the tile: partials summed in split order (the same
 //     sum whoever runs it), the gate gradients, carry = z * dh kept in REGISTERS across steps (the
@@ -567,27 +324,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
     if (a.dbih_part && q != 2) a.dbih_part[rb + (q == 3 ? 2 : q) * H + j0 + u] = v;
   }
 }
-
-bool gru_fwd_seq_big_supported(int H, int Bp) {
-  if (H % 256 || Bp % 128 || H < 1024) return false;
-  const int nrg = Bp / 128, ncg = H / 32;
-  if (nrg * ncg != 256 || ncg > 64) return false;   // one workgroup per CU, <= 64 producers per row group
-  int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gru_fwd_seq_big_kernel, 512, 0) != hipSuccess) return false;
-  return ncu * per >= nrg * ncg;
-}
-
-void gru_fwd_seq_big(const SeqFwdArgs& a, hipStream_t s) {
-  if (!gru_fwd_seq_big_supported(a.H, a.Bp) || !a.xch || !a.cnt || !a.HSb || !a.HSf || !a.Whh || !a.bhh ||
-      (!a.ids == !a.Gi) || (a.ids && !a.P))
-    throw std::runtime_error("gru_fwd_seq_big: unsupported shape or incomplete arguments");
-  if ((size_t)a.T * a.Bp * a.H * 2 >= (1ull << 32) || (size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 33))
-    throw std::runtime_error("gru_fwd_seq_big: exchange exceeds the 4 GB buffer range");
-  hipLaunchKernelGGL(gru_fwd_seq_big_kernel, dim3((a.Bp / 128) * (a.H / 32)), dim3(512), 0, s, a);
-}
-
 
 bool gru_bwd_seq_big_supported(int H, int Bp) {
   if (H % 256 || Bp % 128 || H < 1024) return false;

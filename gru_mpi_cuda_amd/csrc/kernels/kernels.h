@@ -88,11 +88,9 @@ struct StepLdsVariants {
                          // profiles/r4_dwfc_group_ab.jsonl), 0: their own launch before the backward.
                          // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
                          // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
-  int fwd_big = 0;       // large H x large batch: the persistent big-tile forward instead of T step kernels
-                         // (h2048: 3.04-3.20 ms per forward vs 2.89 for the 64-row step kernels,
-                         // profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
-  int big_acq = 1;       // the large-H persistent kernels read the exchange behind an agent acquire (0: sc1 loads)
+  int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
+                         // (0: sc1 loads; measured equal, profiles/r4_h2048_big_acq_ab.jsonl)
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -131,8 +129,6 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
-  int xch_acquire = 1;             // large-H kernels: exchange read by plain loads behind an agent acquire
-                                   // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -140,12 +136,6 @@ inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 
 bool gru_fwd_seq_supported(int H, int Bp);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
 
-// Persistent forward for large H with a large batch (gru_seq_big.hip): 256 workgroups of 128 rows x
-// 32 units x 3 gates, W_hh streamed from L2 each step, h exchanged through T-deep per-producer tiles
-// of `xch` (T x Bp x H bf16) with epoch flags in `cnt` (zeroed before the launch).  Needs
-// (Bp/128)(H/32) == 256, H % 256 == 0, H >= 1024.
-bool gru_fwd_seq_big_supported(int H, int Bp);
-void gru_fwd_seq_big(const SeqFwdArgs& a, hipStream_t s);
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer
 // `lo` at step s and layer `hi` at step s-1 in iteration s = 0..T.  hi's input projection
@@ -183,7 +173,8 @@ struct SeqBwdArgs {
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
   float* part = nullptr;           // large-H kernel: split-K partial tiles (gru_bwd_seq_big_part_floats)
-  int xch_acquire = 1;             // large-H kernel: as SeqFwdArgs::xch_acquire
+  int xch_acquire = 1;             // large-H kernel: exchange read by plain loads behind an agent acquire
+                                   // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
   int T = 0, Bp = 0, H = 0;
 };

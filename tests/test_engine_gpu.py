@@ -105,10 +105,10 @@ def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H, blaslt):
 
 
 @pytest.mark.parametrize("layers,B,H,E", [(1, 512, 2048, 128), (2, 1024, 1024, 128)])
-def test_trainer_grads_big_persistent_forward(layers, B, H, E):
-    """Large H with a large batch takes the persistent big-tile forward and the persistent split-K
-    backward (gru_seq_big.hip): full gradients against the fp64 oracle, and loss + gradients against
-    the all-per-step schedule (GK_PERSIST=0: the step kernels)."""
+def test_trainer_grads_big_persistent_backward(layers, B, H, E):
+    """Large H with a large batch takes the persistent split-K backward (gru_seq_big.hip) after the
+    64-row forward step kernels: full gradients against the fp64 oracle, and loss + gradients against
+    the all-per-step schedule (GK_PERSIST=0: the split-K step kernels)."""
     import os
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
@@ -116,13 +116,7 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=4 if H >= 2048 else 3, seed=6)
     params = init_params(cfg)
     x, y = NameStream(B, cfg.seq, seed=9).next()
-    saved = C.step_lds_variants()
-    C.set_step_lds_variants(dict(fwd_big=1))   # (off by default: the step kernels measured faster)
-    try:
-        tr = HipTrainer(cfg, params=params)
-    finally:
-        C.set_step_lds_variants(saved)
-    assert tr.t.plan().startswith("fwd=persistent-big"), tr.t.plan()
+    tr = HipTrainer(cfg, params=params)
     assert all(f"bwd{l}=persistent-big" in tr.t.plan() for l in range(layers)), tr.t.plan()
     tr.forward_backward(x, y)
     assert tr.t.read_error() == 0
@@ -147,7 +141,8 @@ def test_trainer_grads_big_persistent_forward(layers, B, H, E):
         assert e < 1e-2, f"{k}: persistent vs per-step rel err {e:.5f}"
     # the exchange read through sc1 loads instead of plain loads behind the agent acquire: the same
     # bytes, so the same gradients bit for bit (a stale line on either path would differ)
-    C.set_step_lds_variants(dict(big_acq=0, fwd_big=1))
+    saved = C.step_lds_variants()
+    C.set_step_lds_variants(dict(big_acq=0))
     try:
         sc = HipTrainer(cfg, params=params)
         sc.forward_backward(x, y)
