@@ -50,6 +50,10 @@ class Arena {
     if (base_) return;
     HIP_CHECK(hipMalloc(&base_, size_ ? size_ : 256));
     HIP_CHECK(hipMemset(base_, 0, size_ ? size_ : 256));
+    // hipMemset is asynchronous on the null stream, and the engines' non-blocking streams do not
+    // wait for it: without this a first batch copied on the trainer's copy stream could land before
+    // the zero-fill and be wiped (a loss of 0 in one GPU-suite run)
+    HIP_CHECK(hipDeviceSynchronize());
   }
   template <class T> T* get(size_t off) const { return reinterpret_cast<T*>(static_cast<char*>(base_) + off); }
   size_t bytes() const { return size_; }
