@@ -60,7 +60,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     x.sih = l > 0 ? R((size_t)C_ * 3 * H * K * 4) : 0; x.rih = l > 0 ? R((size_t)C_ * 3 * H * 4) : 0;
   }
   // ---- persistent-sequence path (gru_seq.hip): decided per layer from the occupancy query
-  const int nrb = B / 32;
   const char* pe = std::getenv("GK_PERSIST");
   const bool allow = !(pe && pe[0] == '0');
   persist_fwd_ = allow && gru_fwd_seq_supported(H, B);
@@ -88,6 +87,10 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     if (!q.bwd) q.fuse_w = q.fuse_p = false;
     q.big = allow && !q.bwd && step_lds_variants().bwd_big && gru_bwd_seq_big_supported(H, B) &&
             seq_flag_words(H, B) >= 8192;
+    // 32-row blocks that cannot be XCD-local (Bp/32 not a multiple of 8) but 16-row ones can
+    q.rows16 = q.bwd && !q.fuse_w && (B / 32) % 8 != 0 && (B / 16) % 8 == 0 && step_lds_variants().bwd16 &&
+               gru_bwd_seq16_supported(H, B, q.fuse_p);
+    q.nrb = q.rows16 ? B / 16 : B / 32;
     any_bwd |= q.bwd;
   }
   splits_ = 8;
@@ -102,11 +105,14 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_se = R((size_t)splits_ * V * E * 4);
   std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0), o_hf(L, 0);
   for (int l = 0; l < L; ++l) {
-    if (seq_[l].fuse_w) o_pw[l] = R((size_t)nrb * 3 * H * H * 4);
+    if (seq_[l].fuse_w) o_pw[l] = R((size_t)seq_[l].nrb * 3 * H * H * 4);
     if (seq_[l].fuse_w && persist_fwd_) o_hf[l] = R((tok + B) * H * 2);
-    if (seq_[l].bwd || seq_[l].big) { o_pbh[l] = R((size_t)nrb * 3 * H * 4); o_pbi[l] = R((size_t)nrb * 3 * H * 4); }
+    if (seq_[l].bwd || seq_[l].big) {
+      o_pbh[l] = R((size_t)seq_[l].nrb * 3 * H * 4);
+      o_pbi[l] = R((size_t)seq_[l].nrb * 3 * H * 4);
+    }
   }
-  size_t o_pP = seq_[0].fuse_p ? R((size_t)nrb * V * 3 * H * 4) : 0;
+  size_t o_pP = seq_[0].fuse_p ? R((size_t)seq_[0].nrb * V * 3 * H * 4) : 0;
   // per-step backward on the split-K LDS kernel: partial tiles + monotonic arrival counters
   // (shared by all layers: their step kernels run one after another on one stream)
   int sk = 0;

@@ -191,6 +191,8 @@ class Trainer {
   struct SeqPlan {
     bool bwd = false, fuse_w = false, fuse_p = false;
     bool big = false;    // large H: the persistent split-K backward (gru_seq_big.hip) instead of T step kernels
+    bool rows16 = false; // the persistent backward on 16-row blocks (gru_seq16.hip)
+    int nrb = 0;         // row blocks of the backward's bias / dP / dW_hh partials
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
     u16* HF = nullptr;   // fragment-tiled h for the fused dW_hh (SeqFwdArgs::HF)
   };

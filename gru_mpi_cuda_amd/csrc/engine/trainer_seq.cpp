@@ -124,7 +124,7 @@ void Trainer::slab_job(SlabJobs& j, const float* src, int splits, long n, float*
 
 void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
-  const int H3 = 3 * H, nrb = B / 32;
+  const int H3 = 3 * H;
   const long tok = (long)T * B;
   const long fw = seq_flag_words(H, B);
   ev_next_ = 0;
@@ -268,7 +268,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
-      gru_bwd_seq(a, s);
+      if (q.rows16) gru_bwd_seq16(a, s); else gru_bwd_seq(a, s);
     } else if (q.big) {
       SeqBwdArgs a;
       a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; a.HSf = y.HSf;
@@ -288,15 +288,15 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (dp && q.bwd) ar_flush(s, false);
     // weight gradients not accumulated inside the sequence kernel
     SlabJobs j;
-    if (q.fuse_w) slab_job(j, q.dWhh_part, nrb, (long)H3 * H, G("weight_hh_l" + k));
-    if (q.bwd || q.big) slab_job(j, q.dbhh_part, nrb, H3, G("bias_hh_l" + k));
+    if (q.fuse_w) slab_job(j, q.dWhh_part, q.nrb, (long)H3 * H, G("weight_hh_l" + k));
+    if (q.bwd || q.big) slab_job(j, q.dbhh_part, q.nrb, H3, G("bias_hh_l" + k));
     // layer 0's dP goes straight to the bf16 (+ transposed) GEMM operands of the tail -- or, when the
     // tail runs after the data-parallel all-reduce, to fp32 dP (the tensor that is all-reduced)
     if (l == 0 && q.fuse_p) {
-      if (dp) j.add(dP_part_, nrb, (long)V * H3, dP_target());
-      else j.add_cast(dP_part_, nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
+      if (dp) j.add(dP_part_, q.nrb, (long)V * H3, dP_target());
+      else j.add_cast(dP_part_, q.nrb, V, H3, nullptr, dP_bf_, dPT_bf_);
     }
-    if (l == 0 && (q.bwd || q.big)) slab_job(j, q.dbih_part, nrb, H3, G("bias_ih_l0"));
+    if (l == 0 && (q.bwd || q.big)) slab_job(j, q.dbih_part, q.nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
     // all-reduced with it), else with layer 0's reduce
     if (dp ? l == L - 1 : l == 0)
@@ -440,7 +440,8 @@ std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
                   (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
-    p += " bwd" + std::to_string(l) + "=" + (seq_[l].bwd ? "persistent" : seq_[l].big ? "persistent-big" : "per-step");
+    p += " bwd" + std::to_string(l) + "=" +
+         (seq_[l].bwd ? (seq_[l].rows16 ? "persistent16" : "persistent") : seq_[l].big ? "persistent-big" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";
     if (seq_[l].fuse_p) p += "+dP";
   }

@@ -89,6 +89,8 @@ struct StepLdsVariants {
                          // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
                          // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
+  int bwd16 = 1;         // persistent backward on 16-row blocks where 32-row blocks are not XCD-local
+                         // (H = 1024, Bp = 128: the config-4 shard)
   int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
                          // (0: sc1 loads; measured equal, profiles/r4_h2048_big_acq_ab.jsonl)
 };
@@ -180,6 +182,11 @@ struct SeqBwdArgs {
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s);
+// The same backward on 16-row row blocks x 32 units (gru_seq16.hip): 8 XCD-local row blocks at
+// Bp = 128, half the streamed dGh per workgroup; H = 1024, no fused dW_hh.  Bias / dP partials are
+// per 16-row block: dbhh_part / dbih_part [Bp/16][3H], dP_part [Bp/16][V][3H].
+bool gru_bwd_seq16_supported(int H, int Bp, bool fuse_p);
+void gru_bwd_seq16(const SeqBwdArgs& a, hipStream_t s);
 // Persistent backward for large H with a large batch (gru_seq_big.hip): 64 tiles of 128 rows x 128
 // units x 4 K-slices = 256 workgroups, dGh exchanged through the T-deep `xbuf` ([T][Bp][3H] bf16),
 // split-K partials through `part`, epoch flags in cnt[0, 8192) (zeroed before the launch); writes

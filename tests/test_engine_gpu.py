@@ -878,3 +878,36 @@ def test_wgrad_library_engine_matches_gemm256():
     for k in grads[0]:
         e = rel(grads[0][k], grads[1][k])
         assert e < 1e-3, f"{k}: library vs gemm256 rel err {e:.2e}"
+
+
+def test_bwd16_matches_32_row_backward():
+    """The config-4 shard (L = 2, H = 1024, Bp = 128) takes the persistent backward on 16-row blocks
+    (gru_seq16.hip: 8 XCD-local row blocks).  Each wave covers the same K-slice in the same k order
+    as the 32-row kernel, so dGh -- and everything the weight-gradient GEMMs make from it -- is
+    bitwise the same; the fused dP and the bias sums group their rows differently (fp32 rounding)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=256, hidden=1024, layers=2, batch=128, seq=8, seed=12)
+    params = init_params(cfg)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=13).next()
+    out = []
+    try:
+        for v in (1, 0):
+            C.set_step_lds_variants(dict(bwd16=v))
+            tr = HipTrainer(cfg, params=params)
+            assert ("bwd0=persistent16" in tr.t.plan()) == (v == 1), tr.t.plan()
+            tr.forward_backward(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((tr.grad_dict(), tr.loss()))
+    finally:
+        C.set_step_lds_variants(saved)
+    (g16, l16), (g32, l32) = out
+    assert l16 == l32
+    for k in ("weight_hh_l0", "weight_hh_l1", "weight_ih_l1"):
+        assert torch.equal(g16[k], g32[k]), k
+    for k in g32:
+        e = rel(g16[k], g32[k])
+        assert e < 1e-4, f"{k}: 16-row vs 32-row rel err {e:.2e}"
