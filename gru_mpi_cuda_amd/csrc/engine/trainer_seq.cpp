@@ -387,6 +387,26 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
 // below overwrites that slot (same stream).
 void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   const int V = d_.V, E = d_.E, H3 = 3 * d_.H;
+  // data-parallel, slab sums deferred into Adam: the one-shot GEMMs stage the all-reduced fp32 dP
+  // themselves (no cast launch), and dW_ih0 goes to a one-slab buffer that Adam reads -- dP lives in
+  // the W_ih0 gradient slot, so the GEMM must not write there while its other blocks read dP
+  if (dP_fp32 && defer_slabs_ && H3 % V == 0 && H3 / V <= splits_) {
+    GemmArgs g;   // dW_ih0 = dP^T · Emb
+    g.A32 = dP_fp32; g.a32_trans = 1; g.lda = H3; g.B = EmbT; g.ldb = V; g.C = slab_w_; g.ldc = E;
+    g.M = H3; g.N = E; g.K = V;
+    GemmArgs es;  // dEmb = dP · W_ih0, K-slices of V into slab_e_
+    es.A32 = dP_fp32; es.lda = H3; es.B = Ls_[0].WihT; es.ldb = H3; es.C = slab_e_; es.ldc = E;
+    es.M = V; es.N = E; es.K = H3; es.splits = H3 / V;
+    const int nkb = gemm_small_kblocks(g);
+    if (nkb && nkb == gemm_small_kblocks(es)) {
+      const GemmArgs pair[2] = {g, es};
+      gemm_small_group(pair, 2, s);
+      slab_job(deferred_, slab_w_, 1, (long)H3 * E, G("weight_ih_l0"));
+      slab_job(deferred_, slab_e_, es.splits, (long)V * E, G("embedding"));
+      HIP_LAUNCH_CHECK();
+      return;
+    }
+  }
   if (dP_fp32) {
     CastJobs j;
     j.add(dP_fp32, V, H3, dP_bf_, dPT_bf_);

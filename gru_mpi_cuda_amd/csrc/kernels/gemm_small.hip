@@ -54,11 +54,41 @@ DEV void gemm_small_body(const GemmArgs& a, int id, int ntn, int ntm, u16 (*lds)
       const int r = w * 16 + q * 8 + srow;
       const int c = sslot ^ ((r >> 1) & 7);
       const size_t ko = (size_t)kbeg + kb * 64 + c * 8;
-      __builtin_amdgcn_global_load_lds(a.A + (size_t)(row0 + r) * a.lda + ko,
-                                       (lds_void_s*)(&lds[kb][0][(w * 16 + q * 8) * 64]), 16, 0, 0);
+      if (!a.A32)
+        __builtin_amdgcn_global_load_lds(a.A + (size_t)(row0 + r) * a.lda + ko,
+                                         (lds_void_s*)(&lds[kb][0][(w * 16 + q * 8) * 64]), 16, 0, 0);
       __builtin_amdgcn_global_load_lds(a.B + (size_t)(col0 + r) * a.ldb + ko,
                                        (lds_void_s*)(&lds[kb][1][(w * 16 + q * 8) * 64]), 16, 0, 0);
     }
+  if (a.A32) {
+    // fp32 A: float4 loads, rounded to bf16 into the same swizzled image (chunk c of row r in slot
+    // c ^ ((r >> 1) & 7)); per 64 x 64 block 1024 float4, 4 per thread
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int q = tid + 256 * p;
+        if (!a.a32_trans) {   // row r, k 4q4 .. +3 of the block (8-B LDS writes)
+          const int r = q >> 4, k4 = (q & 15) * 4;
+          const float4 v = *reinterpret_cast<const float4*>(a.A32 + (size_t)(row0 + r) * a.lda + kbeg + kb * 64 + k4);
+          const int c = (k4 >> 3) ^ ((r >> 1) & 7);
+          uint2 u;
+          u.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+          u.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+          *reinterpret_cast<uint2*>(&lds[kb][0][r * 64 + c * 8 + (k4 & 7)]) = u;
+        } else {              // A32[k][m]: k = q / 16 of the block, rows m 4(q % 16) .. +3
+          const int k = q >> 4, m4 = (q & 15) * 4;
+          const float4 v = *reinterpret_cast<const float4*>(a.A32 + (size_t)(kbeg + kb * 64 + k) * a.lda + row0 + m4);
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = m4 + i, c = (k >> 3) ^ ((r >> 1) & 7);
+            lds[kb][0][r * 64 + c * 8 + (k & 7)] = f2bf(e[i]);
+          }
+        }
+      }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -165,7 +195,8 @@ static int small_blocks(const GemmArgs& a, int* nch) {
   if (nkb > 8 && nkb % 8 == 0 && nkb <= 32) { *nch = nkb / 8; nkb = 8; }
   if (nkb != 2 && nkb != 3 && nkb != 4 && nkb != 8) return 0;
   if ((a.lda % 8) || (a.ldb % 8)) return 0;
-  if ((reinterpret_cast<uintptr_t>(a.A) | reinterpret_cast<uintptr_t>(a.B)) & 15) return 0;
+  if ((reinterpret_cast<uintptr_t>(a.A32 ? (const void*)a.A32 : (const void*)a.A) |
+       reinterpret_cast<uintptr_t>(a.B)) & 15) return 0;
   return nkb;
 }
 int gemm_small_kblocks(const GemmArgs& a) {

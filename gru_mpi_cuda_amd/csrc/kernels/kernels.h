@@ -324,6 +324,9 @@ struct GemmArgs {
   // layer 0's dP reads the r/z gate rows of dGi^T from dGh^T, where they are identical
   const u16* B2 = nullptr; int b2_row = 0;
   int raster = 0;                  // LDS 128x128 kernel tile order: 0 auto (shorter dimension fast), 1 column-fast
+  // gemm_small / gemm_small_group only: A taken from an fp32 matrix, rounded to bf16 while staging
+  // (no separate cast pass): A[m][k] = A32[m * lda + k], or with a32_trans A32[k * lda + m]
+  const float* A32 = nullptr; int a32_trans = 0;
   int algo = 0;                    // 0 auto, 1 register-direct 64x64 tiles, 2 LDS-staged 128x128,
                                    // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel),
                                    // 5 LDS-staged 256x256 (gemm256.hip)
