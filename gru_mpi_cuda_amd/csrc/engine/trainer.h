@@ -208,6 +208,7 @@ class Trainer {
   bool persist_fwd_ = false;
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
+  bool fwd64p_ = false;        // large H, large batch: the persistent 64-row forward (gru_seq_big.hip)
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;
   int splits_ = 8;

@@ -184,6 +184,11 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ++l;
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
+    } else if (fwd64p_) {
+      SeqFwdArgs a = fwd_args(l);   // (flags zeroed by fwd_args: the partner backward is not the 32-row kernel)
+      a.zero_next = nullptr; a.zero_words = 0; a.HF = nullptr;
+      a.xch_acquire = step_lds_variants().big_acq;
+      gru_fwd_seq64(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
     }
@@ -458,7 +463,7 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
 
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
-                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
+                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : fwd64p_ ? "persistent64" : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" +
          (seq_[l].bwd ? (seq_[l].rows16 ? "persistent16" : "persistent") : seq_[l].big ? "persistent-big" : "per-step");

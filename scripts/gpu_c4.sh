@@ -12,3 +12,13 @@ for i in 1 2 3; do
   done
 done
 bash scripts/gpu_prof.sh c4_bwd16 --preset h1024_l2 --per-gpu-batch 128 --steps 5 --warmup 2 | head -8
+timeout -k 10 600 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 200 --timeout-method thread -k "rccl or sharded or world1" > gpurun_out/dp_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/dp_tests.log; [ $rc -ne 0 ] && exit $rc
+for i in 1 2; do
+  for f in "" "--rccl-self"; do
+    l=$(timeout -k 10 300 python bench.py --steps 20 --warmup 5 $f 2>/dev/null | grep '^{') || exit 1
+    echo "{\"form\": \"$f\", \"bench\": $l}" >> gpurun_out/dp_struct_ab.jsonl
+    echo "[$f] $(echo $l | python3 -c 'import json,sys; print(json.load(sys.stdin)["ms_per_step"])')"
+  done
+done
+bash scripts/gpu_prof.sh r4_rccl_self2 --rccl-self --steps 20 --warmup 5 | head -12
