@@ -152,6 +152,20 @@ def test_trainer_grads_big_persistent_backward(layers, B, H, E):
         C.set_step_lds_variants(saved)
     for k in g1:
         assert torch.equal(g1[k], g[k]), k
+    # the persistent 64-row forward (fwd64p) runs the 64-row step kernel's k order and epilogue, so
+    # the whole step is bitwise the step-kernel forward's
+    if C.fwd_seq64_supported(H, B):
+        C.set_step_lds_variants(dict(fwd64p=1))
+        try:
+            fp = HipTrainer(cfg, params=params)
+            assert "fwd=persistent64" in fp.t.plan(), fp.t.plan()
+            fp.forward_backward(x, y)
+            assert fp.t.read_error() == 0
+            g2 = fp.grad_dict()
+        finally:
+            C.set_step_lds_variants(saved)
+        for k in g2:
+            assert torch.equal(g2[k], g[k]), k
 
 
 def test_trainer_adam_step_and_learning():
