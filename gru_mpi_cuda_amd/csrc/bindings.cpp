@@ -252,7 +252,7 @@ PYBIND11_MODULE(_C, m) {
     py::dict d;
     d["fwd_ns"] = v.fwd_ns; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
     d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["bwd_sk_map"] = v.bwd_sk_map;
-    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16; d["fwd64p"] = v.fwd64p;
+    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -272,7 +272,6 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd_big") v.bwd_big = x;
       else if (k == "big_acq") v.big_acq = x;
       else if (k == "bwd16") v.bwd16 = x;
-      else if (k == "fwd64p") v.fwd64p = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
   });
@@ -314,18 +313,11 @@ PYBIND11_MODULE(_C, m) {
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
-    if (get<int>(d, "seq64", 0)) {   // the persistent 64-row large-H forward (gru_seq_big.hip)
-      if (!gru_fwd_seq64_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq(seq64): shape not supported");
-      gru_fwd_seq64(a, S(s));
-      HIP_LAUNCH_CHECK();
-      return;
-    }
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
     HIP_LAUNCH_CHECK();
   });
   m.def("bwd_seq_big_supported", &gru_bwd_seq_big_supported);
-  m.def("fwd_seq64_supported", &gru_fwd_seq64_supported);
   m.def("bwd_seq", [](py::dict d, uintptr_t s) {
     SeqBwdArgs a;
     a.dy = GP(const float, d, "dy");

@@ -63,7 +63,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const char* pe = std::getenv("GK_PERSIST");
   const bool allow = !(pe && pe[0] == '0');
   persist_fwd_ = allow && gru_fwd_seq_supported(H, B);
-  fwd64p_ = allow && !persist_fwd_ && step_lds_variants().fwd64p && gru_fwd_seq64_supported(H, B);
   {
     const char* fw = std::getenv("GK_FWD_WAVE");
     fwd_wave_ = persist_fwd_ && L >= 2 && !(fw && fw[0] == '0') && gru_fwd_seq2_supported(H, B);

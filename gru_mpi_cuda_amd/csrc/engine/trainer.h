@@ -208,7 +208,6 @@ class Trainer {
   bool persist_fwd_ = false;
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
-  bool fwd64p_ = false;        // large H, large batch: the persistent 64-row forward (gru_seq_big.hip)
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)
   std::vector<SeqPlan> seq_;
   int splits_ = 8;
@@ -219,7 +218,7 @@ class Trainer {
   long sk_part_floats_ = 0, sk_cnt_words_ = 0;
   int xcd_local_ = 1;          // persistent kernels may use the L2-local hand-off (GK_XCD_LOCAL=0: never)
   // layer 0's per-step backward writes only the n-gate rows of dGi^T; the one-hot dP GEMM reads the
-  // r/z rows from dGh^T, where they are identical (GK_DGIT_SHARE=0: write and read all of dGi^T)
+  // r/z rows from dGh^T, where they are identical (measured: profiles/r2_h2048_dgit_share_ab.jsonl)
   bool dgiT_share_ = false;
   u16* xbuf_ = nullptr;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;

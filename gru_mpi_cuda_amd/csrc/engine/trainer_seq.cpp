@@ -184,11 +184,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ++l;
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
-    } else if (fwd64p_) {
-      SeqFwdArgs a = fwd_args(l);   // (flags zeroed by fwd_args: the partner backward is not the 32-row kernel)
-      a.zero_next = nullptr; a.zero_words = 0; a.HF = nullptr;
-      a.xch_acquire = step_lds_variants().big_acq;
-      gru_fwd_seq64(a, s);
     } else {
       for (int t = 0; t < T; ++t) fwd_step(l, t, s);
     }
@@ -361,7 +356,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
         // persistent backward kernel (joined before the embedding tail).  Neither waits on the
         // other -- the RCCL kernel only on its peers, the sequence kernel only on its own
         // workgroups -- so if the collective's workgroups cannot co-reside they run after it
-        // (no overlap, no deadlock).  GK_AR_SPAN=0: joined before the persistent kernel.
+        // (no overlap, no deadlock).  (Joined before the persistent kernel instead: equal at one rank.)
         // The fork comes after the dX GEMM below, so the collective starts beside the sequence
         // kernel rather than beside that bandwidth-bound GEMM.
         if (!seq_[l - 1].bwd) ar_flush(s, false);
@@ -463,7 +458,7 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
 
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
-                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : fwd64p_ ? "persistent64" : "per-step");
+                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" +
          (seq_[l].bwd ? (seq_[l].rows16 ? "persistent16" : "persistent") : seq_[l].big ? "persistent-big" : "per-step");

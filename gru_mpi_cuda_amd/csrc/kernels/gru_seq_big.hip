@@ -6,7 +6,10 @@
 // (Round 4 also built the forward twin -- 256 workgroups of 128 rows x 32 units x 3 gates, W_hh
 // streamed through a 4-deep LDS ring, T-deep per-producer h tiles with epoch flags.  Correct, and
 // slower than the 64-row step kernels: h2048 forward 3.04-3.34 ms vs 2.89-2.97, step 9.24 vs 8.69-8.72
-// ms, profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl, r4_h2048_h1024_big_ab.jsonl; removed.)
+// ms, profiles/r4_h2048_big_v1_ab.jsonl, r4_h2048_big_acq_ab.jsonl, r4_h2048_h1024_big_ab.jsonl; removed.
+// A second try on the 64-row step kernel's tile -- two workgroups per CU, 512 co-resident, the same
+// k order and epilogue -- was correct and slower still: h2048 9.37-9.40 vs 8.77-8.81 ms, h1024_l2 x
+// 1024 equal, profiles/r4_h2048_h1024_fwd64_ab.jsonl; removed.)
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -27,218 +30,6 @@ DEV rsrc_g mk_rsrc(const void* p, unsigned bytes) {
 }
 template <int N> DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 }  // namespace
-
-// ==================================================================== persistent large-H forward, 64-row tiles
-// The 64-row forward step kernel's tile (gru_step_lds.hip gru_fwd_step_lds64_kernel: 64 rows x 32
-// units x 3 gates, 4 waves of 32 x 16, a 3-deep ring of 20 KiB, two workgroups per CU -- one's
-// epilogue under the other's K loop) with all T steps in one launch: (H/32) x (Bp/64) = 512
-// workgroups at h2048 / h1024_l2 x 1024, all co-resident.  The unit group is the fast block index,
-// so an XCD streams the W_hh slices of 1/8 of the unit groups (3.1 MB at H = 2048).  Per step:
-// wave 0 polls the epoch flags of the row group's H/32 producers (sc1), then (xch_acquire) one agent
-// acquire, a barrier, the K loop streams A = h_{t-1} of the 64 rows from the producers' [64][32]
-// exchange tiles (T-deep) and B = W_hh; the bf16 h tile is staged in LDS and published (256 x 16-B
-// sc1 stores, drain, barrier, one flag), and only then go the saves the backward reads (h fp32 and
-// bf16, h^T, r / z / n / gh_n recomputed from the live accumulators) and the next step's inputs.
-namespace {
-constexpr int kF64NS = 3;   // LDS ring: 3 x (64 + 96) rows x 128 B = 60 KiB
-}
-
-__global__ void __launch_bounds__(256, 2) gru_fwd_seq64_kernel(SeqFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[kF64NS][(64 + 96) * 64];   // one object: st aliases slot 0
-  const int H = a.H, Bp = a.Bp, T = a.T;
-  const int nrg = Bp / 64, ncg = H / 32;
-  const int cg = blockIdx.x % ncg, rg = blockIdx.x / ncg;
-  const int j0 = cg * 32, b0 = rg * 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int lr = lane & 15, lq = lane >> 4;
-  const int srow = lane >> 3, sslot = lane & 7;
-  const int u = j0 + wn * 16 + lr;
-  const bool acq = a.xch_acquire != 0;
-  auto row_of = [&](int i, int e) { return b0 + wm * 32 + i * 16 + lq * 4 + e; };
-  float bh[3], hp[2][4], gi[2][4][3];
-#pragma unroll
-  for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) hp[i][e] = a.h0 ? a.h0[(size_t)row_of(i, e) * H + u] : 0.f;
-  auto load_gi = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int b = row_of(i, e);
-        const float* src = a.ids ? a.P + (size_t)a.ids[(size_t)t * Bp + b] * 3 * H : a.Gi + ((size_t)t * Bp + b) * 3 * H;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) gi[i][e][g] = src[g * H + u];
-      }
-  };
-  const size_t xstep = (size_t)nrg * ncg * 2048;   // exchange elements per step: [nrg][ncg][64][32]
-  const rsrc_g rX = mk_rsrc(a.xch, (unsigned)((size_t)T * xstep * 2));
-  const rsrc_g rH0 = mk_rsrc(a.HSb, (unsigned)((size_t)Bp * H * 2));   // HS[0] = h_init, row-major bf16
-  unsigned* const flags = a.cnt + (size_t)rg * ncg * 16;
-  // 20 LDS-DMA pieces (8 image rows) per k-tile, 5 per wave: image rows 0..63 = A, 64..159 = W_hh
-  auto stage = [&](int buf, int kt, int t) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      const int p = 5 * w + q, r = p * 8 + srow;
-      lds_void_g* dst = (lds_void_g*)(&lds[buf][p * 8 * 64]);
-      if (p < 8) {
-        const int c = swz(r, sslot);   // the logical 16-B chunk this lane's slot holds
-        if (t > 0) {   // producer 2 kt + c / 4 of the row group, its tile row r, units 8 (c % 4) ..
-          const unsigned off = (unsigned)(((((size_t)(t - 1) * nrg + rg) * ncg + 2 * kt + (c >> 2)) * 2048 + r * 32 + (c & 3) * 8) * 2);
-          if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);
-          else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);   // aux 16 = sc1
-        } else {
-          const unsigned off = (unsigned)(((size_t)(b0 + r) * H + kt * 64 + c * 8) * 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rH0, dst, 16, off, 0, 0, 0);
-        }
-      } else {
-        const int rb = r - 64;
-        const u16* src = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + kt * 64 + swz(rb, sslot) * 8;
-        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-      }
-    }
-  };
-  const int nk = H / 64;
-  if (a.ids || a.Gi) load_gi(0);
-
-  for (int t = 0; t < T; ++t) {
-    f32x4 acc[2][3];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (t > 0) {   // h_{t-1} of the row group: every producer's flag at epoch >= t
-      if (w == 0) {
-        unsigned long long t0 = 0;
-        unsigned n = 0;
-        for (;;) {
-          bool ok = true;
-          if (lane < ncg) ok = __hip_atomic_load(flags + lane * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)t;
-          if (__all(ok)) break;
-          __builtin_amdgcn_s_sleep(1);
-          if ((n++ & 63u) == 0u) {   // (first check: the clock only, as gru_seq.hip SpinBudget)
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (!t0) t0 = now;
-            else if (a.err && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) break;
-            else if (now - t0 > kSpinTicks) {
-              if (lane == 0 && a.err) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-        }
-        if (acq) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
-      __syncthreads();
-    }
-    if (t > 0 || a.h0) {
-      // 3-deep ring: 2 k-tiles in flight, one barrier per k-tile (5 pieces per wave per k-tile)
-#pragma unroll
-      for (int s2 = 0; s2 < kF64NS - 1; ++s2) stage(s2, s2, t);
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) vmwait<5>(); else vmwait<0>();
-        lds_barrier();
-        if (kt + kF64NS - 1 < nk) stage((kt + kF64NS - 1) % kF64NS, kt + kF64NS - 1, t);
-        const u16* LA = lds[kt % kF64NS];
-        const u16* LB = LA + 64 * 64;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int c = ks * 4 + lq;
-          bf16x8 af[2], bfr[3];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int r = wm * 32 + i * 16 + lr;
-            af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
-          }
-#pragma unroll
-          for (int g = 0; g < 3; ++g) {
-            const int r = g * 32 + wn * 16 + lr;
-            bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
-          }
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
-        }
-      }
-      __syncthreads();   // every wave is done with the ring: slot 0 becomes the h staging tile
-    }
-    u16* st = lds[0];   // [64 rows][32 units] bf16
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
-        const float r = sigmoidf_(gi[i][e][0] + ghr);
-        const float z = sigmoidf_(gi[i][e][1] + ghz);
-        const float n = tanhf_(gi[i][e][2] + r * ghn);
-        const float h = n + z * (hp[i][e] - n);
-        hp[i][e] = h;
-        st[(wm * 32 + i * 16 + lq * 4 + e) * 32 + wn * 16 + lr] = f2bf(h);
-      }
-    __syncthreads();
-    // publish: this producer's [64][32] tile, 16 B per thread, write-through; drain; one flag
-    const u32x4_g hv4 = *reinterpret_cast<const u32x4_g*>(&st[tid * 8]);
-    {
-      const unsigned off = (unsigned)(((((size_t)t * nrg + rg) * ncg + cg) * 2048 + tid * 8) * 2);
-      __builtin_amdgcn_raw_buffer_store_b128(hv4, rX, off, 0, 16);   // aux 16 = sc1
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + cg * 16, (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // after the signal: the saves of the backward (gates recomputed from the live accumulators)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const size_t o = (size_t)row_of(i, e) * H + u;
-        a.HSf[(size_t)(t + 1) * Bp * H + o] = hp[i][e];
-        if (a.sr) {
-          const float ghn = acc[i][2][e] + bh[2];
-          const float r = sigmoidf_(gi[i][e][0] + acc[i][0][e] + bh[0]);
-          const float z = sigmoidf_(gi[i][e][1] + acc[i][1][e] + bh[1]);
-          const float n = tanhf_(gi[i][e][2] + r * ghn);
-          const size_t so = (size_t)t * Bp * H + o;
-          a.sr[so] = r; a.sz[so] = z; a.sn[so] = n; a.sghn[so] = ghn;
-        }
-      }
-    // row-major bf16 h: row tid / 4, units 8 (tid % 4) ..
-    *reinterpret_cast<u32x4_g*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (tid >> 2)) * H + j0 + (tid & 3) * 8) = hv4;
-    if (a.HT) {   // transposed: unit tid / 8, rows 8 (tid % 8) ..
-      const int unit = tid >> 3, seg = tid & 7;
-      u16 v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
-      *reinterpret_cast<uint4*>(a.HT + (size_t)(j0 + unit) * a.ldT + (size_t)(t + 1) * Bp + b0 + seg * 8) =
-          *reinterpret_cast<const uint4*>(v);
-    }
-    if (t + 1 < T && (a.ids || a.Gi)) load_gi(t + 1);
-    __syncthreads();   // st (ring slot 0) is refilled by the next step's K loop
-  }
-}
-
-bool gru_fwd_seq64_supported(int H, int Bp) {
-  if (H % 64 || Bp % 64 || H < 1024 || H / 32 > 64) return false;
-  int dev = 0, ncu = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gru_fwd_seq64_kernel, 256, 0) != hipSuccess) return false;
-  return (long)ncu * per >= (long)(H / 32) * (Bp / 64);
-}
-
-void gru_fwd_seq64(const SeqFwdArgs& a, hipStream_t s) {
-  if (!gru_fwd_seq64_supported(a.H, a.Bp) || !a.xch || !a.cnt || !a.HSb || !a.HSf || !a.Whh || !a.bhh ||
-      (!a.ids == !a.Gi) || (a.ids && !a.P))
-    throw std::runtime_error("gru_fwd_seq64: unsupported shape or incomplete arguments");
-  if ((size_t)a.T * a.Bp * a.H * 2 >= (1ull << 32))
-    throw std::runtime_error("gru_fwd_seq64: exchange exceeds the 4 GB buffer range");
-  hipLaunchKernelGGL(gru_fwd_seq64_kernel, dim3((a.H / 32) * (a.Bp / 64)), dim3(256), 0, s, a);
-}
 
 // ==================================================================== persistent large-H backward
 // ONE launch runs all T backward steps of a layer at large H with a large batch (B = 512, H = 2048:

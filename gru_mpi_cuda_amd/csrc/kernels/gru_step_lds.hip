@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
   }
 }
 
-// 64-row forward (default where the 128-row tile would give one workgroup per CU; GK_FWD_LDS64=0
+// 64-row forward (default where the 128-row tile would give one workgroup per CU; StepLdsVariants::fwd64 = 0
 // reverts, 2 = 4-deep ring): tile 64 rows x 32 units x 3 gates, 4 waves of 32 rows x 16 units, a
 // 3-deep ring of 20 KiB slots, two workgroups per CU.  At B = 512, H = 2048 that is 512 workgroups:
 // twice the k-tile streams in flight per CU of the 128-row tile, for 1.4x its L2 bytes per FLOP
@@ -358,7 +358,7 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
   }
 }
 
-// 8-wave forward (default; GK_FWD_LDS8=0 reverts; h2048 step 9.84 -> 9.75-9.78 ms,
+// 8-wave forward (default; StepLdsVariants::fwd8 = 0 reverts; h2048 step 9.84 -> 9.75-9.78 ms,
 // profiles/r2_h2048_fwd8_ab.jsonl): the same 128 x 96 tile, but two wave groups split
 // every 64-deep k-tile by its two 32-deep k-steps (group g does k-step g), as the 8-wave backward
 // kernel does: each wave issues half the LDS-DMA pieces and half the MFMAs, and two waves share a
@@ -812,7 +812,7 @@ constexpr unsigned kSkSpinLimit = 1u << 21;   // x s_sleep(1): far beyond any re
 // NS: LDS ring depth (4 x 32 KiB; 3 and 5 measured equal / slower: profiles/r2_h2048_skns3_ab.jsonl).
 // PF (default): the epilogue's fp32 operands (dy, carry, saves, h_{t-1}) are loaded before the K
 // loop, so their latency hides under it instead of following the split-K exchange (h2048 step
-// 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl; GK_BWD_SK_PF=0 reverts).
+// 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl; StepLdsVariants::bwd_sk_pf = 0 reverts).
 template <int S, int NS = SKNS, bool PF = false>
 __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) {
   static_assert(!PF || S == 4, "prefetch holds one epilogue quarter");
@@ -1051,13 +1051,13 @@ void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
   int ns = grid.x * grid.y >= 512 ? 2 : 4;
   if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : 4;
   const bool eight = v.fwd8 != 0;
-  const bool big_grid_ok = ns != 2 || v.fwd64_all;   // GK_FWD_LDS64_ALL=1: also where the 2-deep 128-row kernel runs
+  const bool big_grid_ok = ns != 2 || v.fwd64_all;   // fwd64_all: also where the 2-deep 128-row kernel runs
   if (big_grid_ok && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
     if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<3>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     return;
   }
-  // fused input phase (layers >= 1 of batched generation) on 64-row tiles (GK_FWD_LDS64_FUSED=0
+  // fused input phase (layers >= 1 of batched generation) on 64-row tiles (StepLdsVariants::fwd64_fused = 0
   // reverts): reference model at 1024 names 55.8-56.1 -> 54.3-54.9 us per char
   // (profiles/r2_generate_fwd64_fused_ab.txt)
   if (big_grid_ok && a.x_bf && v.fwd64_fused && a.Bp % 64 == 0 && a.Kin % 64 == 0) {

@@ -89,7 +89,6 @@ struct StepLdsVariants {
                          // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
                          // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
-  int fwd64p = 0;        // large H x large batch: the persistent 64-row forward instead of T step kernels
   int bwd16 = 1;         // persistent backward on 16-row blocks where 32-row blocks are not XCD-local
                          // (H = 1024, Bp = 128: the config-4 shard)
   int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
@@ -132,19 +131,12 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
-  int xch_acquire = 1;             // large-H kernel: exchange read by plain loads behind an agent acquire
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
 inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 16; }
 bool gru_fwd_seq_supported(int H, int Bp);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
-// Persistent large-H forward on the 64-row step kernel's tile (gru_seq_big.hip): (H/32) x (Bp/64)
-// workgroups of 256 threads, two per CU, all co-resident; h exchanged through T-deep [64][32] tiles
-// of `xch` (T x Bp x H bf16), epoch flags in `cnt` (zeroed before the launch).  H % 64 == 0,
-// H >= 1024, Bp % 64 == 0.
-bool gru_fwd_seq64_supported(int H, int Bp);
-void gru_fwd_seq64(const SeqFwdArgs& a, hipStream_t s);
 
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer

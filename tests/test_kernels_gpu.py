@@ -517,59 +517,3 @@ def test_fwd_seq2_two_layer_wavefront(ext, H, B, T, carry):
     torch.testing.assert_close(bufs[1]["HSb"][1:].float(), H1, atol=2e-2, rtol=0)
     HT1 = bufs[1]["HT"].view(H, T + 1, B)[:, 1:].permute(1, 2, 0).float()
     torch.testing.assert_close(HT1, H1, atol=2e-2, rtol=0)
-
-
-@pytest.mark.parametrize("H,B,T,mode", [(2048, 512, 4, "table"), (1024, 1024, 3, "gi"), (2048, 512, 3, "carry"),
-                                        (1024, 1024, 1, "table"), (1024, 128, 3, "table")])
-def test_fwd_seq64(ext, H, B, T, mode):
-    """The persistent large-H forward on 64-row tiles (gru_seq_big.hip gru_fwd_seq64_kernel: (H/32) x
-    (Bp/64) workgroups, two per CU, h exchanged through per-producer tiles + epoch flags) against a
-    torch fp32 recurrence on the same bf16 operands: h (fp32, row-major bf16, transposed bf16), the
-    r / z / n / gh_n saves; P-table, Gi-row and carried-state inputs."""
-    if not ext.fwd_seq64_supported(H, B):
-        pytest.skip("shape not co-resident")
-    V = 256
-    g = torch.Generator(device="cpu").manual_seed(7)
-    R = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)
-    Whh = bf(R(3 * H, H, sc=H ** -0.5))
-    bhh = R(3 * H, sc=0.1)
-    if mode == "gi":
-        Gi = R(T, B, 3 * H, sc=0.5)
-    else:
-        P = R(V, 3 * H, sc=0.5)
-        ids = torch.randint(0, V, (T, B), generator=g, dtype=torch.int32).to(DEV)
-        Gi = P[ids.long()]
-    h0 = R(B, H, sc=0.5) if mode == "carry" else torch.zeros(B, H, device=DEV)
-    err = torch.zeros(16, device=DEV, dtype=torch.int32)
-    HSb = torch.zeros(T + 1, B, H, device=DEV, dtype=torch.bfloat16)
-    HSb[0] = h0.to(torch.bfloat16)
-    HSf = torch.zeros(T + 1, B, H, device=DEV)
-    HSf[0] = h0
-    HT = torch.zeros(H, (T + 1) * B, device=DEV, dtype=torch.bfloat16)
-    xch = torch.zeros(T, B, H, device=DEV, dtype=torch.bfloat16)
-    sv = [torch.zeros(T, B, H, device=DEV) for _ in range(4)]
-    cnt = torch.zeros((B // 64) * (H // 32) * 16 + 64, device=DEV, dtype=torch.int32)
-    d = dict(HSb=HSb.data_ptr(), xch=xch.data_ptr(), HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * B,
-             sr=sv[0].data_ptr(), sz=sv[1].data_ptr(), sn=sv[2].data_ptr(), sghn=sv[3].data_ptr(),
-             Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), cnt=cnt.data_ptr(), err=err.data_ptr(), T=T, Bp=B, H=H, seq64=1)
-    if mode == "gi":
-        d["Gi"] = Gi.data_ptr()
-    else:
-        d.update(P=P.data_ptr(), ids=ids.data_ptr())
-    if mode == "carry":
-        d["h0"] = h0.data_ptr()
-    ext.fwd_seq(d, S())
-    torch.cuda.synchronize()
-    assert int(err[0]) == 0
-    h = h0.clone()
-    for t in range(T):
-        gh = h.to(torch.bfloat16).float() @ Whh.float().t() + bhh
-        gi_r, gi_z, gi_n = torch.chunk(Gi[t], 3, dim=1)
-        gh_r, gh_z, gh_n = torch.chunk(gh, 3, dim=1)
-        r = torch.sigmoid(gi_r + gh_r); z = torch.sigmoid(gi_z + gh_z); n = torch.tanh(gi_n + r * gh_n)
-        h = n + z * (h - n)
-        torch.testing.assert_close(HSf[t + 1], h, atol=5e-3, rtol=0)
-        for k, ref in enumerate((r, z, n, gh_n)):
-            torch.testing.assert_close(sv[k][t], ref, atol=5e-3, rtol=0)
-        torch.testing.assert_close(HSb[t + 1].float(), h, atol=2e-2, rtol=0)
-        torch.testing.assert_close(HT.view(H, T + 1, B)[:, t + 1].t().float(), h, atol=2e-2, rtol=0)
