@@ -252,7 +252,7 @@ PYBIND11_MODULE(_C, m) {
     py::dict d;
     d["fwd_ns"] = v.fwd_ns; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
     d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["bwd_sk_map"] = v.bwd_sk_map;
-    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16; d["dwfc256"] = v.dwfc256;
+    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -272,7 +272,6 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd_big") v.bwd_big = x;
       else if (k == "big_acq") v.big_acq = x;
       else if (k == "bwd16") v.bwd16 = x;
-      else if (k == "dwfc256") v.dwfc256 = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
   });

@@ -241,19 +241,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       ws.splits = (int)(tok / kslice); ws.algo = 3;
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
     }
-    // large products (H = 2048 over 64 K tokens): the 256 x 256 kernel on >= 2048-deep K-slices
-    // fills a whole wave (8 tiles x 32 splits at h2048) where the 128 x 128 split stops at 8 slabs
-    // of 32 tiles (0.35 PF)
-    if (w.algo != 3 && step_lds_variants().dwfc256 && V % 256 == 0 && H % 256 == 0) {
-      const int t256 = (V / 256) * (H / 256);
-      int s256 = 1;
-      while (s256 * 2 <= kFcSplitsMax && t256 * s256 < 256 && tok % (s256 * 2) == 0 && tok / (s256 * 2) >= 2048 &&
-             (tok / (s256 * 2)) % 64 == 0)
-        s256 *= 2;
-      GemmArgs w2 = w;
-      w2.splits = s256; w2.algo = 5;
-      if (t256 * s256 >= 256 && gemm256_ok(w2)) { w = w2; sp = s256; }
-    }
+    // (gemm256 on 2048-deep K-slices at h2048 -- 8 tiles x 32 splits -- measured equal: the GEMM
+    // 194 -> 173 us, its 32 slabs given back in the reduce; profiles/r4_h2048_dwfc256_ab.jsonl)
     // single GPU, slabs summed inside Adam: nothing reads dW_fc before the optimiser, so its
     // K-slices can join the dW_ih0 / dEmb launch after the backward sweep (one launch fewer; its
     // latency-bound tiles run beside theirs)

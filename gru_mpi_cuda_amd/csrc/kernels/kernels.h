@@ -89,7 +89,6 @@ struct StepLdsVariants {
                          // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
                          // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
-  int dwfc256 = 1;       // dW_fc on gemm256 K-slices where they fill a wave (h2048), else the 128 x 128 split
   int bwd16 = 1;         // persistent backward on 16-row blocks where 32-row blocks are not XCD-local
                          // (H = 1024, Bp = 128: the config-4 shard)
   int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
