@@ -335,6 +335,12 @@ PYBIND11_MODULE(_C, m) {
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     // "unchecked": skip the co-residency query and go straight to the dispatch table (tests its
     // unmatched-variant error without launching anything)
+    if (get<int>(d, "rows16", 0)) {   // the 16-row-block backward (gru_seq16.hip)
+      if (!gru_bwd_seq16_supported(a.H, a.Bp, a.dP_part != nullptr)) throw std::runtime_error("bwd_seq(rows16): shape not supported");
+      gru_bwd_seq16(a, S(s));
+      HIP_LAUNCH_CHECK();
+      return;
+    }
     if (!get<int>(d, "unchecked", 0) &&
         !gru_bwd_seq_supported(a.H, a.Bp, a.dWhh_part != nullptr, a.dP_part != nullptr))
       throw std::runtime_error("bwd_seq: shape not supported");

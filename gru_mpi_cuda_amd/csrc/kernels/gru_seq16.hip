@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
 
   for (int t = T - 1; t >= 0; --t) {
     const int s = T - 1 - t;
+    stamp(a.dbg, s, 0);
     f32x4 acc[2];
     acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc[1] = acc[0];
@@ -87,6 +88,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
         const int so = (int)((((slot + (size_t)((c0 % H) / 32)) * 3 + (size_t)(c0 / H)) * 512) * 2);
         af[kk] = ld8_sc1s(rX, xlane, so);
       });
+      stamp(a.dbg, s, 1);
 #pragma unroll
       for (int kk = 0; kk < NKW3; ++kk) {
         acc[0] = mfma16(af[kk], bwL[kk][tid], acc[0]);
@@ -101,6 +103,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) part[w][u][i * 64 + lane] = acc[u][i];
     __syncthreads();
+    stamp(a.dbg, s, 2);
     float dh = dy + carry;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) dh += part[ww][uh][reg * 64 + ln];
@@ -119,6 +122,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
       if (col == 0) idsL[row] = idc;
     }
     __syncthreads();
+    stamp(a.dbg, s, 3);
     if (w == 0) {
       // publish dGh_t as 3 gate blocks of [16 rows][32 units] (1 KB each, whole lines of its own)
       const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (3 * 16 * 32);
@@ -134,6 +138,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
         if (loc) signal_flag_local(fl, (unsigned)(s + 1));
         else signal_flag(fl, (unsigned)(s + 1));
       }
+      stamp(a.dbg, s, 4);
     } else if (w <= 4 && a.dghT) {
       // transposed copies for the weight-gradient GEMMs: 32 units x 16 rows per kind
       const int g = w - 1;          // 0..3 : dGh r, z, n and dGi n
@@ -148,6 +153,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
       const size_t og = ((size_t)t * Bp + b) * H3 + j;
       a.dgi[og] = br; a.dgi[og + H] = bz; a.dgi[og + 2 * H] = bi;
     }
+    stamp(a.dbg, s, 5);
     if constexpr (NTP > 0) {
       // dP += onehot(x_t)^T dGi_t over this block's 16 rows: A = dGi^T [unit][row] (K = rows, the
       // upper 16 of the 32-deep MFMA zero), B = one-hot [row][vocab column]
@@ -180,6 +186,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
         }
       }
     }
+    stamp(a.dbg, s, 6);
   }
 
   if constexpr (NTP > 0) {

@@ -7,8 +7,9 @@ from gru_mpi_cuda_amd.ops import load_ext
 
 C = load_ext()
 dev = torch.device("cuda", 0)
-H, Bp, T, V = int(os.environ.get("H", 512)), int(os.environ.get("B", 256)), 32, 256
-H3, nrb = 3 * H, Bp // 32
+H, Bp, T, V = int(os.environ.get("H", 512)), int(os.environ.get("B", 256)), int(os.environ.get("T", 32)), 256
+R16 = int(os.environ.get("R16", 0))     # 1: the 16-row-block kernel (gru_seq16.hip)
+H3, nrb = 3 * H, Bp // (16 if R16 else 32)
 fuse_w, fuse_p = int(os.environ.get("FW", 1)), int(os.environ.get("FP", 1))
 s = torch.cuda.current_stream().cuda_stream
 f = lambda *sh: torch.randn(*sh, device=dev) * 0.1          # noqa: E731
@@ -31,7 +32,7 @@ dbg = torch.zeros(2 * 4096 * 8, device=dev, dtype=torch.int64)
 d = dict(allow_local=int(os.environ.get("LOCAL", 1)), dy=dy.data_ptr(), sr=sr.data_ptr(), sz=sz.data_ptr(), sn=sn.data_ptr(), sghn=sghn.data_ptr(),
          HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp, WhhT=WhhT.data_ptr(), xbuf=xbuf.data_ptr(),
          dbhh_part=dbh.data_ptr(), dbih_part=dbi.data_ptr(), cnt=cnt.data_ptr(), err=err.data_ptr(),
-         T=T, Bp=Bp, H=H, V=V)
+         T=T, Bp=Bp, H=H, V=V, rows16=R16)
 if fuse_w:
     d["dWhh_part"] = dWp.data_ptr()
     if int(os.environ.get("HF", 1)):
@@ -40,7 +41,7 @@ if fuse_p:
     d.update(ids=ids.data_ptr(), dP_part=dPp.data_ptr())
 if not (fuse_w and fuse_p):
     d.update(dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), ldG=T * Bp)
-res = {"H": H, "Bp": Bp, "fuse_w": fuse_w, "fuse_p": fuse_p}
+res = {"H": H, "Bp": Bp, "fuse_w": fuse_w, "fuse_p": fuse_p, "rows16": R16}
 for mode in ("plain", "dbg"):
     if mode == "dbg":
         d["dbg"] = dbg.data_ptr()
