@@ -252,7 +252,7 @@ PYBIND11_MODULE(_C, m) {
     py::dict d;
     d["fwd_ns"] = v.fwd_ns; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
     d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["bwd_sk_map"] = v.bwd_sk_map;
-    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16;
+    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -272,6 +272,8 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd_big") v.bwd_big = x;
       else if (k == "big_acq") v.big_acq = x;
       else if (k == "bwd16") v.bwd16 = x;
+      else if (k == "bwd_xring") v.bwd_xring = x;
+      else if (k == "fwd_xring") v.fwd_xring = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
   });
@@ -287,6 +289,7 @@ PYBIND11_MODULE(_C, m) {
       a.h0 = GP(const float, d, "h0");
       a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
       a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+      a.xring = get<int>(d, "xring", 0);
       a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
       if (!a.xch || !a.cnt || !a.HSb || !a.HSf || !a.Whh || !a.bhh) throw std::runtime_error("fwd_seq2: HSb/HSf/xch/cnt/Whh/bhh required");
       return a;
@@ -312,6 +315,7 @@ PYBIND11_MODULE(_C, m) {
     a.h0 = GP(const float, d, "h0");
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+    a.xring = get<int>(d, "xring", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));
@@ -331,7 +335,7 @@ PYBIND11_MODULE(_C, m) {
     a.dbih_part = GP(float, d, "dbih_part"); a.ids = GP(const int, d, "ids");
     a.dP_part = GP(float, d, "dP_part"); a.V = get<int>(d, "V", 0);
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err"); a.dbg = GP(unsigned long long, d, "dbg");
-    a.allow_local = get<int>(d, "allow_local", 1);
+    a.allow_local = get<int>(d, "allow_local", 1); a.xring = get<int>(d, "xring", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     // "unchecked": skip the co-residency query and go straight to the dispatch table (tests its
     // unmatched-variant error without launching anything)

@@ -155,6 +155,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (l == 0) { a.P = Ptab_; a.ids = ids_; }
     else a.Gi = y.Gi;
     a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
+    a.xring = step_lds_variants().fwd_xring;
     if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
     a.T = T; a.Bp = B; a.H = H;
     if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
@@ -270,6 +271,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
+      a.xring = step_lds_variants().bwd_xring;
       if (q.rows16) gru_bwd_seq16(a, s); else gru_bwd_seq(a, s);
     } else if (q.big) {
       SeqBwdArgs a;

@@ -69,6 +69,10 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   float hp = a.h0 ? a.h0[(size_t)b * H + j] : 0.f;
   const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
   const rsrc_t rX = make_rsrc(a.xch, (unsigned)((size_t)T * Bp * H * 2));
+  // exchange ring: the slot of step t is reused at step t + xr.  Safe for xr >= 2: a producer writes
+  // step t only after every producer of its row block published step t - 1, i.e. finished reading
+  // the tiles of step t - 2 -- the ones the write replaces when xr = 2.
+  const int xr = a.xring >= 2 ? a.xring : T;
   const unsigned sv_bytes = (unsigned)((size_t)T * Bp * H * 4);   // < 4 GB: checked on the host
   const rsrc_t rHSf = make_rsrc(a.HSf, sv_bytes + (unsigned)(Bp * H * 4));
   const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
@@ -103,7 +107,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       if (t > 0) {
         // h_t from the producers' exchange tiles (written at step t-1); unit u = k0 + 32kk + lk
         // lives in tile u/16 at column u%16
-        const size_t slot = ((size_t)(t - 1) * nrb + rbk) * nunit;
+        const size_t slot = ((size_t)((t - 1) % xr) * nrb + rbk) * nunit;
         wave_wait_load<NKW>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
                             (unsigned)t, a.err, [&](int kk) {
           const int u = k0 + kk * 32 + lk;
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
       // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
-      const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
+      const unsigned xo = (unsigned)((((size_t)(t % xr) * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
       unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
       if (loc) {
         st16_plain(rX, xo, v);
@@ -267,6 +271,10 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
   const unsigned hs_bytes = (unsigned)((size_t)(T + 1) * Bp * H * 2), x_bytes = (unsigned)((size_t)T * Bp * H * 2);
   const rsrc_t rH0 = make_rsrc(L0.HSb, hs_bytes), rX0 = make_rsrc(L0.xch, x_bytes);
   const rsrc_t rH1 = make_rsrc(L1.HSb, hs_bytes), rX1 = make_rsrc(L1.xch, x_bytes);
+  // exchange rings as gru_fwd_seq_kernel's (L0.xring for both layers): lo's tile of step t is read in
+  // iteration t + 1, hi's in t + 2; a slot is rewritten xr steps later, after every producer of the
+  // row block published the iteration in which it was last read
+  const int xr = L0.xring >= 2 ? L0.xring : T;
   zero_next_flags(L0.zero_next, L0.zero_words);
   zero_next_flags(L1.zero_next, L1.zero_words);
   unsigned* const fl0 = L0.cnt + (size_t)rbk * nunit * kFlagStride;
@@ -280,7 +288,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
   const unsigned hl = (unsigned)((lr * H + lk) * 2);
   auto stage_x = [&](int st, int kk, int ts) {
     const rsrc_t rX = st == 0 ? rX0 : rX1;
-    const int so = (int)((((size_t)ts * nrb + rbk) * nunit + (k0 + kk * 32) / 16) * 1024);
+    const int so = (int)((((size_t)(ts % xr) * nrb + rbk) * nunit + (k0 + kk * 32) / 16) * 1024);
 #pragma unroll
     for (int r = 0; r < 2; ++r)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (lds_void*)(&stage[w][st][kk][r][0]), 16, xl, so + r * 512, 0, 16);
@@ -426,7 +434,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
       if (ly == 0 ? do0 : do1) {
         const SeqFwdArgs& Y = ly == 0 ? L0 : L1;
         const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[ly][lane >> 1][(lane & 1) * 8]);
-        const unsigned xo = (unsigned)((((size_t)t * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
+        const unsigned xo = (unsigned)((((size_t)(t % xr) * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
         unsigned* fl = (ly == 0 ? fl0 : fl1) + (size_t)ut * kFlagStride;
         const rsrc_t rX = ly == 0 ? rX0 : rX1;
         if (loc) {
@@ -523,6 +531,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   f32x4 accP[3][NTP > 0 ? NTP : 1];
   zero_acc(accW);
   zero_acc(accP);
+  // exchange ring (SeqBwdArgs::xring, gru_seq16.hip): the slot of step t is reused at step t - xr
+  const int xr = a.xring >= 2 ? a.xring : T;
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)(((lk >> 4) * 3 * 512 + lr * 16 + (lk & 15)) * 2);   // exchange lane offset
   zero_next_flags(a.zero_next, a.zero_words);
@@ -556,7 +566,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       // slot t+1 at column (c/H)*16 + c%16
       // 32-column k-steps never straddle a gate (H % 32 == 0): gate c0 / H and producer tile
       // (c0 % H) / 16 are wave-uniform (scalar offset); the lane part is fixed for the launch
-      const size_t slot = ((size_t)(t + 1) * nrb + rbk) * nunit;
+      const size_t slot = ((size_t)((t + 1) % xr) * nrb + rbk) * nunit;
       wave_wait_load<NKW3>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW3,
                            ((k0 + 16 * lane) % H) / 16, (unsigned)s, a.err, [&](int kk) {
         if constexpr (kScalarX) {
@@ -658,7 +668,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       // publish the dGh_t tile as 3 gate blocks of [32 rows][16 units] (1 KB each, whole lines of its
       // own): a consumer's 16-row fragment of one gate is then 512 contiguous bytes per producer
       // (8 full lines per load instruction instead of 16-row x 96-B strided pieces)
-      const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (3 * 32 * 16);
+      const size_t tile = (((size_t)(t % xr) * nrb + rbk) * nunit + ut) * (3 * 32 * 16);
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[g][lane >> 1][(lane & 1) * 8]);

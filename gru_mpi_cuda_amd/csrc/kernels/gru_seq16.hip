@@ -58,6 +58,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
   f32x4 accP[3][2][NTP > 0 ? NTP : 1];
 #pragma unroll
   for (int g = 0; g < 3; ++g) zero_acc(accP[g]);
+  // exchange ring: the slot of step t is reused at step t - xr.  Safe for xr >= 2: a producer writes
+  // step t only after every producer of its row block published step t + 1, i.e. finished reading
+  // the tiles of step t + 2 -- the ones the write replaces when xr = 2.
+  const int xr = a.xring >= 2 ? a.xring : T;
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)((lr * 32 + lk) * 2);   // fragment lane offset in a 1-KB gate block
   zero_next_flags(a.zero_next, a.zero_words);
@@ -81,7 +85,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
     if (s > 0) {
       // k-step kk: columns c0 = k0 + 32 kk .. +31 = gate c0 / H, units of producer (c0 % H) / 32
       bf16x8 af[NKW3];
-      const size_t slot = ((size_t)(t + 1) * nrb + rbk) * nunit;
+      const size_t slot = ((size_t)((t + 1) % xr) * nrb + rbk) * nunit;
       wave_wait_load1<NKW3>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < NKW3,
                             ((k0 + 32 * lane) % H) / 32, (unsigned)s, a.err, [&](int kk) {
         const int c0 = k0 + kk * 32;
@@ -125,7 +129,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
     stamp(a.dbg, s, 3);
     if (w == 0) {
       // publish dGh_t as 3 gate blocks of [16 rows][32 units] (1 KB each, whole lines of its own)
-      const size_t tile = (((size_t)t * nrb + rbk) * nunit + ut) * (3 * 16 * 32);
+      const size_t tile = (((size_t)(t % xr) * nrb + rbk) * nunit + ut) * (3 * 16 * 32);
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(&srow[g][lane >> 2][(lane & 3) * 8]);

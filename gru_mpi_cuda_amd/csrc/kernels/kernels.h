@@ -93,6 +93,9 @@ struct StepLdsVariants {
                          // (H = 1024, Bp = 128: the config-4 shard)
   int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
                          // (0: sc1 loads; measured equal, profiles/r4_h2048_big_acq_ab.jsonl)
+  int bwd_xring = 4;     // persistent backward (32- and 16-row): dGh exchange as a ring of this many
+                         // slots instead of one per step (0); docs/DESIGN.md §3.1d
+  int fwd_xring = 0;     // persistent forward (one- and two-layer): the same for the h exchange
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -131,6 +134,7 @@ struct SeqFwdArgs {
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
+  int xring = 0;                   // h exchange as a ring of xring slots (>= 2; 0 = one per step)
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -159,8 +163,8 @@ struct SeqBwdArgs {
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
   const u16* HF = nullptr;         // SeqFwdArgs::HF of the same layer: preferred over HT when set
   const u16* WhhT = nullptr;       // [H][3H]
-  u16* xbuf = nullptr;             // dGh exchange, one slot per step (no WAR reuse), tiled per producer:
-                                   // [T][Bp/32][H/16][3 gates][32 rows][16 units] bf16
+  u16* xbuf = nullptr;             // dGh exchange, tiled per producer, one slot per step or a ring of
+                                   // xring slots: [T or xring][Bp/32][H/16][3 gates][32 rows][16 units] bf16
   u16* dghT = nullptr; u16* dgiT = nullptr; int ldG = 0;   // [3H][ldG] transposed copies (nullable)
   u16* dgi = nullptr;              // [T][Bp][3H] row-major dGi (nullable)
   float* dWhh_part = nullptr;      // [Bp/32][3H][H] fused dW_hh partials (nullable = not fused)
@@ -178,6 +182,8 @@ struct SeqBwdArgs {
   int xch_acquire = 1;             // large-H kernel: exchange read by plain loads behind an agent acquire
                                    // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
+  int xring = 0;                   // step / 16-row kernels: exchange slots reused every xring steps
+                                   // (>= 2; 0 = one per step; StepLdsVariants::bwd_xring)
   int T = 0, Bp = 0, H = 0;
 };
 bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p);

@@ -32,7 +32,7 @@ dbg = torch.zeros(2 * 4096 * 8, device=dev, dtype=torch.int64)
 d = dict(allow_local=int(os.environ.get("LOCAL", 1)), dy=dy.data_ptr(), sr=sr.data_ptr(), sz=sz.data_ptr(), sn=sn.data_ptr(), sghn=sghn.data_ptr(),
          HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp, WhhT=WhhT.data_ptr(), xbuf=xbuf.data_ptr(),
          dbhh_part=dbh.data_ptr(), dbih_part=dbi.data_ptr(), cnt=cnt.data_ptr(), err=err.data_ptr(),
-         T=T, Bp=Bp, H=H, V=V, rows16=R16)
+         T=T, Bp=Bp, H=H, V=V, rows16=R16, xring=int(os.environ.get("XR", 0)))
 if fuse_w:
     d["dWhh_part"] = dWp.data_ptr()
     if int(os.environ.get("HF", 1)):
@@ -41,7 +41,7 @@ if fuse_p:
     d.update(ids=ids.data_ptr(), dP_part=dPp.data_ptr())
 if not (fuse_w and fuse_p):
     d.update(dghT=dghT.data_ptr(), dgiT=dgiT.data_ptr(), ldG=T * Bp)
-res = {"H": H, "Bp": Bp, "fuse_w": fuse_w, "fuse_p": fuse_p, "rows16": R16}
+res = {"H": H, "Bp": Bp, "T": T, "fuse_w": fuse_w, "fuse_p": fuse_p, "rows16": R16, "xring": int(os.environ.get("XR", 0))}
 for mode in ("plain", "dbg"):
     if mode == "dbg":
         d["dbg"] = dbg.data_ptr()
