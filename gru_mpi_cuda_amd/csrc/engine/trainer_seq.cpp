@@ -180,6 +180,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       w2.hi = fwd_args(l + 1);
       w2.hi.Gi = nullptr;
       w2.hi.xch = xbuf_ + (size_t)T * B * H;   // xbuf_ holds 3 layers' worth of exchange tiles
+      w2.lo.xring = w2.hi.xring = 0;   // (a ring measured equal here: profiles/r4_fwd_xring_ab.jsonl)
       w2.Wih = Ls_[l + 1].Wih; w2.bih = P("bias_ih_l" + std::to_string(l + 1));
       gru_fwd_seq2(w2, s);
       ++l;

@@ -95,7 +95,8 @@ struct StepLdsVariants {
                          // (0: sc1 loads; measured equal, profiles/r4_h2048_big_acq_ab.jsonl)
   int bwd_xring = 4;     // persistent backward (32- and 16-row): dGh exchange as a ring of this many
                          // slots instead of one per step (0); docs/DESIGN.md §3.1d
-  int fwd_xring = 0;     // persistent forward (one- and two-layer): the same for the h exchange
+  int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
+                         // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
 };
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
