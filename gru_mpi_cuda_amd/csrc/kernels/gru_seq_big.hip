@@ -77,6 +77,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   const int ncb = H3 / kBS / 128;                    // 128-column blocks per slice
   const size_t slot = (size_t)Bp * H3;               // exchange elements per step
   const rsrc_g rX = mk_rsrc(a.xbuf, (unsigned)((size_t)T * slot * 2));
+  // exchange ring (SeqBwdArgs::xring): dGh_t in slot t % xr.  A workgroup publishes dGh_t only after
+  // its S partners' step-t partials, whose K-slices together need dGh_{t+1} from every workgroup of
+  // the row tile, each of which published it after its own step-(t+1) reads of dGh_{t+2}: the slot
+  // being rewritten (t + 2 for xr = 2) has no reader left.
+  const int xr = a.xring >= 2 ? a.xring : T;
   const rsrc_g rP = mk_rsrc(a.part, (unsigned)((size_t)2 * 64 * kBS * kPiece * 16));
   unsigned* const gflag = a.cnt;
   unsigned* const pflag = a.cnt + 4096;
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       lds_void_g* dst = (lds_void_g*)(&lds[buf][(4 * w + q) * 8 * 64]);
       const int col = (kt0 + kt) * 64 + swz(rr, sslot) * 8;
       if (w < 4) {
-        const unsigned off = (unsigned)((((size_t)(t + 1) * Bp + b0 + rr) * H3 + col) * 2);
+        const unsigned off = (unsigned)((((size_t)((t + 1) % xr) * Bp + b0 + rr) * H3 + col) * 2);
         if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
         else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);     // aux 16 = sc1
       } else {
@@ -287,7 +292,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       for (int p = 0; p < 3; ++p) {
         const int q = tid + 512 * p, g = q >> 9, rq = (q >> 4) & 31, seg = q & 15;
         const u32x4_g v = *reinterpret_cast<const u32x4_g*>(&stR[(g * 32 + rq) * kRowPad + seg * 8]);
-        const unsigned off = (unsigned)((((size_t)t * Bp + b0 + 32 * sq + rq) * H3 + g * H + j0 + seg * 8) * 2);
+        const unsigned off = (unsigned)((((size_t)(t % xr) * Bp + b0 + 32 * sq + rq) * H3 + g * H + j0 + seg * 8) * 2);
         __builtin_amdgcn_raw_buffer_store_b128(v, rX, off, 0, 16);   // aux 16 = sc1
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -911,3 +911,39 @@ def test_bwd16_matches_32_row_backward():
     for k in g32:
         e = rel(g16[k], g32[k])
         assert e < 1e-4, f"{k}: 16-row vs 32-row rel err {e:.2e}"
+
+
+@pytest.mark.parametrize("layers,B,H,E,T,plan", [
+    (1, 256, 512, 512, 16, "bwd0=persistent"),          # headline kernels (32-row fwd / bwd)
+    (2, 128, 1024, 256, 12, "bwd0=persistent16"),       # config-4 shard: 16-row backward, wavefront fwd
+    (1, 512, 2048, 128, 7, "bwd0=persistent-big"),      # large-H split-K backward
+])
+def test_exchange_ring_matches_one_slot_per_step(layers, B, H, E, T, plan):
+    """The persistent kernels' exchange as a ring of 2 slots (the smallest the hand-off allows, see
+    docs/DESIGN.md §3.1 "Exchange rings") and of 4 (the default) against one slot per step: the same
+    bytes reach the same MFMAs, so the loss and every gradient must be bitwise equal -- a slot
+    rewritten while a reader still needed it would show up here (T > ring depth throughout)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=T, seed=21)
+    params = init_params(cfg)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=22).next()
+    out = []
+    try:
+        for xr in (0, 2, 4):
+            C.set_step_lds_variants(dict(bwd_xring=xr, fwd_xring=xr))
+            tr = HipTrainer(cfg, params=params)
+            assert plan in tr.t.plan(), tr.t.plan()
+            tr.forward_backward(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((tr.loss(), tr.grad_dict()))
+    finally:
+        C.set_step_lds_variants(saved)
+    (l0, g0) = out[0]
+    for l, g in out[1:]:
+        assert l == l0
+        for k in g0:
+            assert torch.equal(g[k], g0[k]), k
