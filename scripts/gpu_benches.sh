@@ -19,5 +19,5 @@ run h2048_b512 --preset h2048 --per-gpu-batch 512 --steps 6 --warmup 2
 run rccl_self --rccl-self --steps 20 --warmup 5
 timeout -k 10 300 python bench/bench_generate.py --names 32,256,4096 --modes engine,engine_fp32 > gpurun_out/gen.jsonl 2>/dev/null || exit 1
 cat gpurun_out/gen.jsonl
-bash scripts/gpu_prof.sh r4_h512_xring --steps 20 --warmup 5 | head -10
-bash scripts/gpu_prof.sh r4_c4_xring --preset h1024_l2 --per-gpu-batch 128 --steps 5 --warmup 2 | head -14
+bash scripts/gpu_prof.sh r4_h512_final --steps 20 --warmup 5 | head -10
+bash scripts/gpu_prof.sh r4_c4_final --preset h1024_l2 --per-gpu-batch 128 --steps 5 --warmup 2 | head -14
