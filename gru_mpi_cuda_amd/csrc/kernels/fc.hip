@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   }
   int* ys = reinterpret_cast<int*>(dlr + FROWS * LDR);           // [32] labels of the block
   if (tid < FROWS) ys[tid] = ylab;
-  __syncthreads();
+  lds_barrier();   // LDS hand-off only: the weight loads stay in flight
   STAMP();
 
   // ---- logits: 32 rows x this wave's 32 columns, K = H in chunks of 8 k-steps (2 in flight)
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       const float m = max16(fmaxf(acc[r][0][i], acc[r][1][i]));
       if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
     }
-  __syncthreads();
+  lds_barrier();   // LDS hand-off only: the weight loads stay in flight
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
       const float e = sum16(__expf(acc[r][0][i] - m) + __expf(acc[r][1][i] - m));
       if (lr == 0) red[NW * 32 + w * 32 + row] = e;
     }
-  __syncthreads();
+  lds_barrier();   // LDS hand-off only: the weight loads stay in flight
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
         dlr[row * LDR + col] = db;
       }
     }
-  __syncthreads();
+  lds_barrier();   // LDS hand-off only: the weight loads stay in flight
   STAMP();
   // per-row nll (one thread per row; the statistics are still in LDS)
   if (tid < FROWS) {
