@@ -40,6 +40,38 @@ def ext_path() -> str:
     return os.path.join(HERE, "_C" + suffix)
 
 
+def hash_path() -> str:
+    """Sidecar written next to the extension by every build: the source hash it was built from."""
+    return ext_path() + ".srchash"
+
+
+def source_hash() -> str:
+    """sha256 over every native source under csrc/ (path + bytes, sorted) plus the build target and
+    flags.  A built ``_C`` / ``libnamegen.so`` is only trusted when its sidecar carries this value, so a
+    test, the smoke check or the bench can never silently run an older build than the tree."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(("arch=%s;flags=%s" % (ARCH, " ".join(_FLAG_BASE))).encode())
+    for root, dirs, files in os.walk(CSRC):
+        dirs.sort()
+        for f in sorted(files):
+            if f.endswith((".h", ".hpp", ".hip", ".cpp", ".cc")):
+                path = os.path.join(root, f)
+                h.update(os.path.relpath(path, CSRC).encode() + b"\0")
+                with open(path, "rb") as fh:
+                    h.update(fh.read())
+                h.update(b"\0")
+    return h.hexdigest()
+
+
+def built_hash() -> str | None:
+    try:
+        with open(hash_path()) as fh:
+            return fh.read().strip() or None
+    except OSError:
+        return None
+
+
 def _headers():
     for root, _, files in os.walk(CSRC):
         for f in files:
@@ -47,28 +79,46 @@ def _headers():
                 yield os.path.join(root, f)
 
 
-def _newest_header() -> float:
-    return max((os.path.getmtime(h) for h in _headers()), default=0.0)
+_FLAG_BASE = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-result"]
 
 
 def _flags(extra=()):
     import pybind11
-    return [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result",
+    return [f"--offload-arch={ARCH}", *_FLAG_BASE,
             f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
             "-I/opt/rocm/include", *extra]
 
 
-def _compile(src: str, force: bool, hdr_time: float) -> str:
+def _headers_digest() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(_headers()):
+        h.update(os.path.relpath(p, CSRC).encode() + b"\0")
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _compile(src: str, force: bool, hdr_digest: str) -> str:
+    """Compile one source unless its object was built from exactly these bytes: the object's stamp
+    file holds sha256(source + every header + flags) -- content, not mtimes, so a checkout, a copy or
+    a clock skew can never leave an object older than its source looking current."""
+    import hashlib
     out = os.path.join(OBJ, src.replace("/", "_") + ".o")
     path = os.path.join(CSRC, src)
-    if not force and os.path.exists(out):
-        t = os.path.getmtime(out)
-        if t >= os.path.getmtime(path) and t >= hdr_time:
-            return out
+    with open(path, "rb") as fh:
+        digest = hashlib.sha256(fh.read() + hdr_digest.encode() + " ".join(_FLAG_BASE + [ARCH]).encode()).hexdigest()
+    stamp = out + ".src"
+    if not force and os.path.exists(out) and os.path.exists(stamp):
+        with open(stamp) as fh:
+            if fh.read().strip() == digest:
+                return out
     cmd = [HIPCC, *_flags(), "-c", path, "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    with open(stamp, "w") as fh:
+        fh.write(digest + "\n")
     return out
 
 
@@ -115,7 +165,7 @@ def build_host_tools(force: bool = False) -> list:
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
-    hdr = _newest_header()
+    hdr = _headers_digest()
     srcs = KERNELS + ENGINE + PYBIND + [s for s in CAPI + DRIVER if os.path.exists(os.path.join(CSRC, s))]
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
     with ThreadPoolExecutor(jobs) as ex:
@@ -132,8 +182,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
                   libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl", "-lhipblaslt", "-lrocprofiler-sdk-roctx",
                         f"-Wl,-rpath,{os.path.join(HERE, 'bin')}", "-Wl,-rpath,$ORIGIN"])
     build_host_tools(force)
+    tmp = hash_path() + ".tmp"
+    with open(tmp, "w") as fh:
+        fh.write(source_hash() + "\n")
+    os.replace(tmp, hash_path())
     if verbose:
-        print(f"[build_ext] {ext_path()} ({len(srcs)} sources, arch {ARCH})")
+        print(f"[build_ext] {ext_path()} ({len(srcs)} sources, arch {ARCH}, src {built_hash()[:16]})")
     return ext_path()
 
 

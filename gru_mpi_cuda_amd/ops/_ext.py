@@ -17,7 +17,28 @@ def ext_available() -> bool:
     return os.path.exists(ext_path())
 
 
+class StaleExtensionError(ImportError):
+    """The built extension does not match the native sources in the tree."""
+
+
+def check_fresh() -> str:
+    """Source hash of the tree if the built extension was built from it; raises StaleExtensionError
+    otherwise (missing sidecar = unknown provenance = stale)."""
+    from ..build_ext import built_hash, source_hash, hash_path
+    want, have = source_hash(), built_hash()
+    if want != have:
+        raise StaleExtensionError(
+            f"native extension is STALE: csrc/ hashes to {want[:16]} but {hash_path()} records "
+            f"{(have or 'nothing')[:16]}; rebuild with `python -m gru_mpi_cuda_amd.build_ext` "
+            "(GK_EXT_REBUILD=1 rebuilds on load)")
+    return want
+
+
 def load_ext(build_if_missing: bool = True):
+    """Import ``_C``.  A missing extension is built when ``build_if_missing``; a stale one (sources
+    changed since the build) is rebuilt only where that is safe and asked for -- no GPU visible
+    (this build container) or GK_EXT_REBUILD=1 -- and otherwise refused loudly: a GPU run never
+    exercises an older binary than the sources it claims to test."""
     global _EXT
     if _EXT is not None:
         return _EXT
@@ -28,6 +49,15 @@ def load_ext(build_if_missing: bool = True):
             raise ImportError(f"native extension missing at {ext_path()}; run "
                               "`python -m gru_mpi_cuda_amd.build_ext`")
         build()
+    try:
+        check_fresh()
+    except StaleExtensionError:
+        rebuild = os.environ.get("GK_EXT_REBUILD")
+        if rebuild == "1" or (rebuild != "0" and build_if_missing and not torch.cuda.is_available()):
+            build()
+            check_fresh()
+        else:
+            raise
     try:
         _EXT = importlib.import_module("gru_mpi_cuda_amd._C")
     except ImportError as e:
