@@ -250,9 +250,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("step_lds_variants", []() {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
-    d["fwd_ns"] = v.fwd_ns; d["fwd8"] = v.fwd8; d["fwd64"] = v.fwd64; d["fwd64_fused"] = v.fwd64_fused; d["fwd64_all"] = v.fwd64_all;
-    d["bwd_sk_pf"] = v.bwd_sk_pf; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["bwd_sk_map"] = v.bwd_sk_map;
-    d["dwfc_group"] = v.dwfc_group; d["bwd_big"] = v.bwd_big; d["big_acq"] = v.big_acq; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring;
+    d["fwd64"] = v.fwd64; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["dwfc_group"] = v.dwfc_group;
+    d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -260,17 +259,10 @@ PYBIND11_MODULE(_C, m) {
     for (auto kv : d) {
       const std::string k = py::str(kv.first);
       const int x = kv.second.cast<int>();
-      if (k == "fwd_ns") v.fwd_ns = x;
-      else if (k == "fwd8") v.fwd8 = x;
-      else if (k == "fwd64") v.fwd64 = x;
-      else if (k == "fwd64_fused") v.fwd64_fused = x;
-      else if (k == "fwd64_all") v.fwd64_all = x;
-      else if (k == "bwd_sk_pf") v.bwd_sk_pf = x;
+      if (k == "fwd64") v.fwd64 = x;
       else if (k == "bwd_sk_min_h") v.bwd_sk_min_h = x;
-      else if (k == "bwd_sk_map") v.bwd_sk_map = x;
       else if (k == "dwfc_group") v.dwfc_group = x;
       else if (k == "bwd_big") v.bwd_big = x;
-      else if (k == "big_acq") v.big_acq = x;
       else if (k == "bwd16") v.bwd16 = x;
       else if (k == "bwd_xring") v.bwd_xring = x;
       else if (k == "fwd_xring") v.fwd_xring = x;

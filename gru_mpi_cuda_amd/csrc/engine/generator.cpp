@@ -277,9 +277,13 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
       a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab32_; a.rf = rf_; a.out = out_; a.probs = probe_;
       a.ws = pws_; a.sync = psync_; a.err = err_; a.dbg = persist_dbg_;
       a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
-      if (inject_) {
-        static const unsigned kBit = 32u;
-        HIP_CHECK(hipMemcpyAsync(err_, &kBit, 4, hipMemcpyHostToDevice, s));
+      if (inject_) {   // test hook: OR the spin-limit bit into the word (earlier batches' bits stay)
+        unsigned cur = 0;
+        HIP_CHECK(hipMemcpyAsync(&cur, err_, 4, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        cur |= 32u;
+        HIP_CHECK(hipMemcpyAsync(err_, &cur, 4, hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
         inject_ = false;
       }
       gen_persist_f32(a, s);
@@ -319,7 +323,9 @@ unsigned Generator::read_error() {
   unsigned e[4] = {0, 0, 0, 0};
   HIP_CHECK(hipDeviceSynchronize());
   HIP_CHECK(hipMemcpy(e, err_, 16, hipMemcpyDeviceToHost));
-  if (e[0])
+  // reporting is the caller's (HipGenerator / the C API raise or print it); the detail line is a debug aid
+  const char* dbg = std::getenv("GK_GEN_DEBUG");
+  if (e[0] && dbg && dbg[0] && dbg[0] != '0')
     std::fprintf(stderr, "[generator] error word %u: id %d (0x%08x) at row %u\n", e[0], (int)e[1], e[1], e[2]);
   return e[0];
 }

@@ -283,7 +283,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dbhh_part = q.dbhh_part; a.dbih_part = l == 0 ? q.dbih_part : nullptr;   // (l > 0: from the dW_ih GEMM)
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
       a.T = T; a.Bp = B; a.H = H;
-      a.xch_acquire = step_lds_variants().big_acq;
       a.xring = step_lds_variants().bwd_xring;
       fill_f32(reinterpret_cast<float*>(a.cnt), 8192, 0.f, s);
       gru_bwd_seq_big(a, s);

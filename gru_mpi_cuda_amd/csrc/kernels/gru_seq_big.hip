@@ -39,8 +39,8 @@ template <int N> DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N)
 //     sk_map 1 (XCD x takes split x % 4 of every row tile of half the unit tiles);
 //   * per step t (descending): wave 0 polls the epoch flags of the dGh_{t+1} producers of this
 //     workgroup's A operand (its 128 rows x K-slice: 4 row-quarter producers of each of the slice's
-//     128-column blocks), then (xch_acquire) one agent acquire; the K loop streams A (T-deep
-//     exchange: plain loads behind the acquire, or sc1) and W_hh^T (plain, its first ring slots issued
+//     128-column blocks), then one agent acquire; the K loop streams A (the exchange ring: plain
+//     loads behind the acquire) and W_hh^T (plain, its first ring slots issued
 //     before the wait) through a 4-deep LDS ring; the fp32 partial tile goes out write-through (parity-double-buffered), one
 //     flag per (tile, split), and the S partners wait for each other;
 //   * the epilogue runs on row quarter `split` of the tile: partials summed in split order (the same
@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   const int nk = H3 / 64 / kBS, kt0 = split * nk;   // k-tiles per slice
   const int ncb = H3 / kBS / 128;                    // 128-column blocks per slice
   const size_t slot = (size_t)Bp * H3;               // exchange elements per step
-  const rsrc_g rX = mk_rsrc(a.xbuf, (unsigned)((size_t)T * slot * 2));
+  const int nslot = a.xring >= 2 && a.xring < T ? a.xring : T;   // slots addressed (ring or T-deep)
+  const rsrc_g rX = mk_rsrc(a.xbuf, (unsigned)((size_t)nslot * slot * 2));
   // exchange ring (SeqBwdArgs::xring): dGh_t in slot t % xr.  A workgroup publishes dGh_t only after
   // its S partners' step-t partials, whose K-slices together need dGh_{t+1} from every workgroup of
   // the row tile, each of which published it after its own step-(t+1) reads of dGh_{t+2}: the slot
@@ -85,7 +86,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   const rsrc_g rP = mk_rsrc(a.part, (unsigned)((size_t)2 * 64 * kBS * kPiece * 16));
   unsigned* const gflag = a.cnt;
   unsigned* const pflag = a.cnt + 4096;
-  const bool acq = a.xch_acquire != 0;
   // epilogue items: row quarter `split`, piece P = w + 8 pp -> (wnp, ii, jn), 4 rows e each
   const int sq = split, wmq = sq >> 1, ibq = 2 * (sq & 1);
   float carry[2][4];
@@ -111,8 +111,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       const int col = (kt0 + kt) * 64 + swz(rr, sslot) * 8;
       if (w < 4) {
         const unsigned off = (unsigned)((((size_t)((t + 1) % xr) * Bp + b0 + rr) * H3 + col) * 2);
-        if (acq) __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
-        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 16);     // aux 16 = sc1
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, dst, 16, off, 0, 0, 0);   // behind the acquire
       } else {
         __builtin_amdgcn_global_load_lds(a.WhhT + (size_t)(j0 + rr) * H3 + col, dst, 16, 0, 0);
       }
@@ -177,10 +176,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
           const int cb = split * ncb + (l >> 2);
           return (rt * ntu + cb % ntu) * kBS + (l & 3);
         });
-        if (acq) {   // as the forward: plain A loads behind one wave's agent acquire, shared in L2
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // plain A loads behind one wave's agent acquire, shared in the XCD's L2 (sc1 loads instead --
+        // one fetch per workgroup from the memory side -- measured equal, r4_h2048_big_acq_ab.jsonl;
+        // that switch was removed in round 5)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
       if (w < 4) {
@@ -351,7 +351,9 @@ void gru_bwd_seq_big(const SeqBwdArgs& a, hipStream_t s) {
   if (!gru_bwd_seq_big_supported(a.H, a.Bp) || !a.xbuf || !a.cnt || !a.part || !a.dy || !a.sr || !a.sz ||
       !a.sn || !a.sghn || !a.HSf || !a.WhhT || a.ldG < a.T * a.Bp)
     throw std::runtime_error("gru_bwd_seq_big: unsupported shape or incomplete arguments");
-  if ((size_t)a.T * a.Bp * 3 * a.H * 2 >= (1ull << 32))
+  // only min(T, xring) slots of the exchange are addressed when a ring is active
+  const size_t slots = a.xring >= 2 && a.xring < a.T ? (size_t)a.xring : (size_t)a.T;
+  if (slots * a.Bp * 3 * a.H * 2 >= (1ull << 32))
     throw std::runtime_error("gru_bwd_seq_big: exchange exceeds the 4 GB buffer range");
   hipLaunchKernelGGL(gru_bwd_seq_big_kernel, dim3(256), dim3(512), 0, s, a);
 }

@@ -358,157 +358,9 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
   }
 }
 
-// 8-wave forward (default; StepLdsVariants::fwd8 = 0 reverts; h2048 step 9.84 -> 9.75-9.78 ms,
-// profiles/r2_h2048_fwd8_ab.jsonl): the same 128 x 96 tile, but two wave groups split
-// every 64-deep k-tile by its two 32-deep k-steps (group g does k-step g), as the 8-wave backward
-// kernel does: each wave issues half the LDS-DMA pieces and half the MFMAs, and two waves share a
-// SIMD.  Group 1's partial accumulators join group 0's through LDS; group 0 runs the epilogue.
-// 28 DMA pieces per k-tile: waves 0-3 issue 4, waves 4-7 issue 3 plus a duplicate of their first
-// (same source, same LDS bytes), so every wave's vmcnt arithmetic counts 4 per k-tile.
-// SE (split epilogue, fwd8 = 2): the groups swap half of their partial tiles instead of group 1
-// handing all of them over, and each runs the epilogue for its two 16-row fragments (i = 2 grp,
-// 2 grp + 1) -- eight waves store the outputs instead of four.
-template <int NS, bool SE = false>
-__global__ void __launch_bounds__(512, 1) gru_fwd_step_lds8_kernel(FwdStepArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 lds[NS][(128 + 96) * 64];
-  const int H = a.H;
-  const int j0 = blockIdx.x * 32, b0 = blockIdx.y * 128;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, grp = w >> 2, wl = w & 3;
-  const int wm = wl >> 1, wn = wl & 1;
-  const int lr = lane & 15, lq = lane >> 4;
-  const int srow = lane >> 3, sslot = lane & 7;
-  const int u = j0 + wn * 16 + lr;
-
-  float gi[4][4][3], bh[3], hp[4][4];
-  // fragment i's epilogue runs in group 0, or (SE) in group i / 2
-  auto own = [&](int i) { return SE ? (i >> 1) == grp : grp == 0; };
-  if (SE || grp == 0) {
-#pragma unroll
-    for (int g = 0; g < 3; ++g) bh[g] = a.bhh[g * H + u];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (own(i))
-#pragma unroll
-        for (int e = 0; e < 4; ++e) hp[i][e] = a.hprev_f[(size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * H + u];
-    const float* src[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) src[i][e] = a.Gi + (size_t)(b0 + wm * 64 + i * 16 + lq * 4 + e) * 3 * H;
-    if (a.ids) {
-      const int4* id4 = reinterpret_cast<const int4*>(a.ids + b0 + wm * 64 + lq * 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (own(i)) {
-          const int4 v = id4[i * 4];
-          src[i][0] = a.P + (size_t)v.x * 3 * H; src[i][1] = a.P + (size_t)v.y * 3 * H;
-          src[i][2] = a.P + (size_t)v.z * 3 * H; src[i][3] = a.P + (size_t)v.w * 3 * H;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (own(i))
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int g = 0; g < 3; ++g) gi[i][e][g] = src[i][e][g * H + u];
-  }
-
-  f32x4 acc[4][3];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int g = 0; g < 3; ++g) acc[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // piece p (image rows 8p..8p+7): A rows (h_{t-1}) for p < 16, B rows (W_hh gate rows) after
-  const u16* src[4];
-  int dst[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    int p = w + 8 * q;
-    if (p >= 28) p = w;                       // waves 4-7: duplicate of the first piece
-    const int r = p * 8 + srow;
-    if (p < 16) {
-      src[q] = a.hprev_bf + (size_t)(b0 + r) * H + swz(r, sslot) * 8;
-    } else {
-      const int rb = r - 128;
-      src[q] = a.Whh + (size_t)((rb >> 5) * H + j0 + (rb & 31)) * H + swz(rb, sslot) * 8;
-    }
-    dst[q] = p * 8 * 64;
-  }
-  auto stage = [&](int buf, int kt) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds(src[q] + kt * 64, (lds_void_t*)(&lds[buf][dst[q]]), 16, 0, 0);
-  };
-  ring_loop<NS, 4>(H / 64, stage, [&](int cur) {
-    const u16* LA = lds[cur];
-    const u16* LB = lds[cur] + 128 * 64;
-    const int c = grp * 4 + lq;
-    bf16x8 af[4], bfr[3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wm * 64 + i * 16 + lr;
-      af[i] = *reinterpret_cast<const bf16x8*>(&LA[r * 64 + swz(r, c) * 8]);
-    }
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-      const int r = g * 32 + wn * 16 + lr;
-      bfr[g] = *reinterpret_cast<const bf16x8*>(&LB[r * 64 + swz(r, c) * 8]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) acc[i][g] = mfma16(af[i], bfr[g], acc[i][g]);
-  });
-  // group 1 -> LDS -> group 0 (ring_loop ended with a barrier: the ring is free)
-  // [4 waves][12 tiles][64 lanes] = 48 KiB; fragment i's tile of wave wl sits at (wl*12 + 3i + g)
-  f32x4* red = reinterpret_cast<f32x4*>(&lds[0][0]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (!own(i))
-#pragma unroll
-      for (int g = 0; g < 3; ++g) red[(wl * 12 + i * 3 + g) * 64 + lane] = acc[i][g];
-  __syncthreads();
-  u16* st = lds[NS - 1];     // [128 rows][32 units]; NS >= 3 keeps it clear of the 48 KiB above
-  if (SE || grp == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (own(i))
-#pragma unroll
-        for (int g = 0; g < 3; ++g) acc[i][g] += red[(wl * 12 + i * 3 + g) * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (own(i))
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int rr = wm * 64 + i * 16 + lq * 4 + e;
-        const int b = b0 + rr;
-        const float ghr = acc[i][0][e] + bh[0], ghz = acc[i][1][e] + bh[1], ghn = acc[i][2][e] + bh[2];
-        const float r = sigmoidf_(gi[i][e][0] + ghr);
-        const float z = sigmoidf_(gi[i][e][1] + ghz);
-        const float n = tanhf_(gi[i][e][2] + r * ghn);
-        const float h = n + z * (hp[i][e] - n);
-        const size_t o = (size_t)b * H + u;
-        a.h_f[o] = h;
-        const u16 hb = f2bf(h);
-        a.h_bf[o] = hb;
-        if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
-        st[rr * 32 + wn * 16 + lr] = hb;
-      }
-  }
-  if (a.hT) {
-    __syncthreads();
-    // 32 units x 128 rows: 512 x 16-B pieces, 1 per thread
-    const int q = threadIdx.x;
-    const int unit = q >> 4, seg = q & 15;
-    u16 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = st[(seg * 8 + k) * 32 + unit];
-    *reinterpret_cast<uint4*>(a.hT + (size_t)(j0 + unit) * a.ldT + a.colT + b0 + seg * 8) =
-        *reinterpret_cast<const uint4*>(v);
-  }
-}
+// (Round 2's 8-wave variant of the 128 x 96 forward tile -- two wave groups splitting each k-tile,
+// h2048 9.84 -> 9.71 ms, profiles/r2_h2048_fwd8_ab.jsonl -- was removed in round 5: the 64-row tile
+// below took every grid it served, so no default plan launched it.)
 
 // ==================================================================== forward, big batch
 // Tile 256 rows x 64 units x 3 gates for big-batch steps (batched generation: 4096+ names): 8 waves
@@ -812,7 +664,7 @@ constexpr unsigned kSkSpinLimit = 1u << 21;   // x s_sleep(1): far beyond any re
 // NS: LDS ring depth (4 x 32 KiB; 3 and 5 measured equal / slower: profiles/r2_h2048_skns3_ab.jsonl).
 // PF (default): the epilogue's fp32 operands (dy, carry, saves, h_{t-1}) are loaded before the K
 // loop, so their latency hides under it instead of following the split-K exchange (h2048 step
-// 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl; StepLdsVariants::bwd_sk_pf = 0 reverts).
+// 10.36-10.50 -> 9.82-9.85 ms, profiles/r2_h2048_step_variants_ab.jsonl); always on at S = 4.
 template <int S, int NS = SKNS, bool PF = false>
 __global__ void __launch_bounds__(512, 1) gru_bwd_step_sk_kernel(BwdStepArgs a) {
   static_assert(!PF || S == 4, "prefetch holds one epilogue quarter");
@@ -1037,57 +889,36 @@ StepLdsVariants& step_lds_variants() {
 bool gru_step_lds_ok(int H, int Bp) { return H >= 256 && H % 64 == 0 && Bp % 128 == 0; }
 
 void gru_fwd_step_lds(const FwdStepArgs& a, hipStream_t s) {
-  constexpr bool big_ok = true;
   // big tile: only with the fused input phase on a full round of tiles (without it, the P-table
   // gather moves behind the K loop and it measured slower: profiles/r1_generate_step_kernel_ab.json)
-  if (big_ok && a.x_bf && a.Kin % 64 == 0 && a.Bp % 256 == 0 && a.H % 64 == 0 && (a.H / 64) * (a.Bp / 256) >= 256) {
-    const dim3 grid(a.H / 64, a.Bp / 256), block(512);
-    if (a.x_bf) hipLaunchKernelGGL(gru_fwd_step_big_kernel<true>, grid, block, 0, s, a);
-    else hipLaunchKernelGGL(gru_fwd_step_big_kernel<false>, grid, block, 0, s, a);
+  if (a.x_bf && a.Kin % 64 == 0 && a.Bp % 256 == 0 && a.H % 64 == 0 && (a.H / 64) * (a.Bp / 256) >= 256) {
+    hipLaunchKernelGGL(gru_fwd_step_big_kernel<true>, dim3(a.H / 64, a.Bp / 256), dim3(512), 0, s, a);
     return;
   }
   const dim3 grid(a.H / 32, a.Bp / 128), block(256);
-  const StepLdsVariants& v = step_lds_variants();
-  int ns = grid.x * grid.y >= 512 ? 2 : 4;
-  if (v.fwd_ns) ns = v.fwd_ns == 2 ? 2 : 4;
-  const bool eight = v.fwd8 != 0;
-  const bool big_grid_ok = ns != 2 || v.fwd64_all;   // fwd64_all: also where the 2-deep 128-row kernel runs
-  if (big_grid_ok && !a.x_bf && v.fwd64 && a.Bp % 64 == 0) {
-    if (v.fwd64 == 2) hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<4>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
+  // grids of >= 512 128-row tiles: the 2-deep 128-row kernel, two workgroups per CU (the 64-row tile
+  // there measured 74-75 -> 88 us per char at 2048 names, profiles/r2_generate_fwd64_all_ab.txt).
+  // Smaller grids: the 64-row tile, two workgroups per CU, 3-deep ring (h2048 9.72 -> 9.43-9.47 ms,
+  // profiles/r2_h2048_fwd64_ab.jsonl; fused input phase 55.8 -> 54.3-54.9 us per char at 1024 names,
+  // r2_generate_fwd64_fused_ab.txt).  StepLdsVariants::fwd64 = 0 keeps the 128-row kernel everywhere.
+  const bool small_grid = grid.x * grid.y < 512;
+  if (small_grid && step_lds_variants().fwd64 && a.Bp % 64 == 0 && (!a.x_bf || a.Kin % 64 == 0)) {
+    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds64_kernel<3, true>), dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(gru_fwd_step_lds64_kernel<3>, dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
     return;
   }
-  // fused input phase (layers >= 1 of batched generation) on 64-row tiles (StepLdsVariants::fwd64_fused = 0
-  // reverts): reference model at 1024 names 55.8-56.1 -> 54.3-54.9 us per char
-  // (profiles/r2_generate_fwd64_fused_ab.txt)
-  if (big_grid_ok && a.x_bf && v.fwd64_fused && a.Bp % 64 == 0 && a.Kin % 64 == 0) {
-    hipLaunchKernelGGL((gru_fwd_step_lds64_kernel<3, true>), dim3(a.H / 32, a.Bp / 64), dim3(256), 0, s, a);
-    return;
-  }
-  if (ns != 2 && !a.x_bf && eight) {
-    if (v.fwd8 == 2) hipLaunchKernelGGL((gru_fwd_step_lds8_kernel<FNS, true>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL(gru_fwd_step_lds8_kernel<FNS>, grid, dim3(512), 0, s, a);
-    return;
-  }
-  if (ns == 2) {
-    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 2>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 2>), grid, block, 0, s, a);
-  } else {
-    if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, FNS>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, FNS>), grid, block, 0, s, a);
-  }
+  if (a.x_bf) hipLaunchKernelGGL((gru_fwd_step_lds_kernel<true, 2>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((gru_fwd_step_lds_kernel<false, 2>), grid, block, 0, s, a);
 }
 void gru_bwd_step_lds(const BwdStepArgs& a, hipStream_t s) {
   if (const int S = gru_bwd_step_sk_splits(a.H, a.Bp)) {
     const int tiles = (a.H / 128) * (a.Bp / 128);
     if (a.sk_part && a.sk_cnt && a.sk_part_floats >= (long)a.H * a.Bp * S && a.sk_cnt_words >= (long)tiles * 16) {
-      const StepLdsVariants& v = step_lds_variants();
-      const bool pf = v.bwd_sk_pf != 0;
       BwdStepArgs b = a;
-      // the across-XCD order needs whole unit-tile groups per XCD
-      b.sk_map = (v.bwd_sk_map == 1 && (a.H / 128) % (8 / S) == 0) ? 1 : 0;
-      if (S == 4 && pf) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, b);
-      else if (S == 4) hipLaunchKernelGGL(gru_bwd_step_sk_kernel<4>, dim3(tiles * 4), dim3(512), 0, s, b);
+      // splits across XCDs where whole unit-tile groups fit per XCD (h2048 9.46-9.47 vs 9.49 ms,
+      // profiles/r4_h2048_skmap.jsonl), else the splits of a tile 8 blocks apart
+      b.sk_map = (a.H / 128) % (8 / S) == 0 ? 1 : 0;
+      if (S == 4) hipLaunchKernelGGL((gru_bwd_step_sk_kernel<4, SKNS, true>), dim3(tiles * 4), dim3(512), 0, s, b);
       else hipLaunchKernelGGL(gru_bwd_step_sk_kernel<2>, dim3(tiles * 2), dim3(512), 0, s, b);
       return;
     }

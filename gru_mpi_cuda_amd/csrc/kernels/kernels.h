@@ -73,31 +73,22 @@ int gru_bwd_step_sk_splits(int H, int Bp);
 // large-H step-kernel fields are read per launch (gru_step_lds.hip), the plan fields when a step
 // graph is recorded.  0 fields mean "automatic" where noted.
 struct StepLdsVariants {
-  int fwd_ns = 0;        // forward LDS ring depth: 0 auto (2 or 4), 2, 4
-  int fwd8 = 2;          // 8-wave forward (two wave groups split each k-tile): 2 = split epilogue,
-                         // 1 = group 0 runs the whole epilogue, 0 = the 4-wave kernel
-  int fwd64 = 1;         // 64-row forward tile, two workgroups per CU (1: 3-deep ring, 2: 4-deep)
-  int fwd64_fused = 1;   // the 64-row tile also for the fused input phase (layers >= 1 of generation)
-  int fwd64_all = 0;     // the 64-row tile also on grids of >= 512 128-row tiles (2-deep 128-row kernel otherwise)
-  int bwd_sk_pf = 1;     // split-K backward: epilogue operands loaded before the K loop
-  int bwd_sk_map = 1;    // split-K backward block order: 1 splits across XCDs (h2048 9.46-9.47 vs 9.49 ms,
-                         // profiles/r4_h2048_skmap.jsonl), 0 the 4 splits of a tile on one XCD
-  int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward (read per call)
+  int fwd64 = 1;         // large-H forward step kernel: the 64-row tile (two workgroups per CU) on grids
+                         // of < 512 128-row tiles; 0 = the 128-row 2-deep kernel everywhere
+  int bwd_sk_min_h = 1024;  // smallest H that takes the split-K backward step kernel (read per call)
   int dwfc_group = 1;    // single-GPU step: the dW_fc K-slices run after the backward sweep inside the
                          // dW_ih0 / dEmb launch (one launch fewer; 0.2183-0.2226 vs 0.2255-0.2274 ms,
                          // profiles/r4_dwfc_group_ab.jsonl), 0: their own launch before the backward.
-                         // (Inside the slab-reduce launch instead measured slower, 0.2175-0.2196 vs
-                         // 0.2145-0.2152 ms, profiles/r4_dwfc_group2_ab.jsonl; removed.)
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
   int bwd16 = 1;         // persistent backward on 16-row blocks where 32-row blocks are not XCD-local
                          // (H = 1024, Bp = 128: the config-4 shard)
-  int big_acq = 1;       // the large-H persistent backward reads the exchange behind an agent acquire
-                         // (0: sc1 loads; measured equal, profiles/r4_h2048_big_acq_ab.jsonl)
   int bwd_xring = 4;     // persistent backward (32- and 16-row): dGh exchange as a ring of this many
                          // slots instead of one per step (0); docs/DESIGN.md §3.1d
   int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
                          // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
 };
+// (Round 5 removed the measured-equal / marginal switches fwd_ns, fwd8, fwd64 = 2, fwd64_fused,
+// fwd64_all, bwd_sk_pf, bwd_sk_map and big_acq with the code only they reached; docs/DESIGN.md §7.)
 StepLdsVariants& step_lds_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
 bool gru_step_lds_ok(int H, int Bp);
@@ -180,7 +171,6 @@ struct SeqBwdArgs {
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
   float* part = nullptr;           // large-H kernel: split-K partial tiles (gru_bwd_seq_big_part_floats)
-  int xch_acquire = 1;             // large-H kernel: exchange read by plain loads behind an agent acquire
                                    // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
   int xring = 0;                   // step / 16-row kernels: exchange slots reused every xring steps

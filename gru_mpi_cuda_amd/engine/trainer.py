@@ -80,6 +80,11 @@ class HipTrainer:
                 self.t.set_shard_optim(True)
         self.t.refresh_weights(self._stream())
         self._one_graph = True
+        # does the flat gradient buffer hold the last step's full gradient?  Not after a one-graph
+        # step() / steps() without cfg.keep_grads: the fused Adam then sums the split-K / row-block
+        # partials in registers and never writes them back (and in data-parallel mode the W_ih0 slot
+        # holds the all-reduced dP) -- grad_dict() refuses instead of returning stale values
+        self._grads_valid = False
         # host thread watching each launched step, the communicator and the step
         # error word (a persistent kernel's spin limit: that step's update is skipped on device)
         wd = int(cfg.watchdog_ms)
@@ -106,6 +111,7 @@ class HipTrainer:
         s = self._stream()
         self.t.set_batch(x, y, s)
         self.t.forward_backward(s)
+        self._grads_valid = True
 
     def allreduce_grads(self) -> None:
         if self.comm is None:
@@ -122,13 +128,16 @@ class HipTrainer:
 
     def step(self, x: np.ndarray, y: np.ndarray) -> None:
         """Whole step = one hipGraph replay: batch prep, forward, softmax-xent, BPTT, weight
-        gradients, bucketed RCCL all-reduce (if data-parallel) and Adam + bf16 weight refresh."""
+        gradients, bucketed RCCL all-reduce (if data-parallel) and Adam + bf16 weight refresh.
+        The flat gradient buffer (grad_dict) holds the step's gradient afterwards only with
+        ``cfg.keep_grads``; otherwise grad_dict() raises until the next forward_backward()."""
         s = self._stream()
         self.t.set_batch(x, y, s)
         self.check_watchdog()
         if self._one_graph:
             try:
                 self.t.step(s)
+                self._grads_valid = bool(self.cfg.keep_grads)
                 return
             except RuntimeError as e:   # e.g. RCCL refusing stream capture: fall back, loudly
                 if self.comm is None:
@@ -141,6 +150,7 @@ class HipTrainer:
         self.t.forward_backward(s)
         self.allreduce_grads()
         self.t.optimizer_step(s)
+        self._grads_valid = True
 
     def steps(self, batches) -> None:
         """len(batches) whole steps as ONE graph launch (Trainer::set_graph_steps): the graph boundary
@@ -157,6 +167,7 @@ class HipTrainer:
         self.check_watchdog()
         try:
             self.t.step_group(s)
+            self._grads_valid = bool(self.cfg.keep_grads)
         except RuntimeError as e:   # e.g. a collective refusing capture: one graph per step, loudly
             import sys
             print(f"[gru_mpi_cuda_amd] multi-step graph unavailable ({e}); one graph per step", file=sys.stderr)
@@ -196,6 +207,11 @@ class HipTrainer:
         return self._unpad({k: v.cpu() for k, v in from_flat(self.icfg, self.params).items()})
 
     def grad_dict(self) -> Dict[str, torch.Tensor]:
+        """The last forward_backward()'s gradient (or the last step()'s with ``cfg.keep_grads``)."""
+        if not self._grads_valid:
+            raise RuntimeError("grad_dict(): the gradient buffer does not hold the last step's gradient "
+                               "(one-graph step() without keep_grads: the fused optimiser never writes it "
+                               "back); set GRUConfig.keep_grads=True or call forward_backward()")
         torch.cuda.synchronize(self.dev)
         return self._unpad({k: v.cpu() for k, v in from_flat(self.icfg, self.grads).items()})
 

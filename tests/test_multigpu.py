@@ -273,7 +273,8 @@ CAPI_WORKER_N = 203   # N % P != 0 for P = 2, 4, 8 (the reference drops those na
 def test_capi_namegen_identical_across_world_sizes(tmp_path, n):
     """SURVEY §3.2 invariant on the native C API (no Python in the path): bin/namegen under the
     one-process-per-GPU launcher writes byte-identical names at world 1 and world n, including
-    N % n != 0 (RCCL broadcast of the uniforms + all-gather of the name slabs)."""
+    N % n != 0 (RcclComm::scatterv_f32 of each rank's uniforms, gatherv_u8 of its name rows:
+    grouped ncclSend / ncclRecv with the uneven remainder counts)."""
     if n > _gpus():
         pytest.skip(f"needs {n} GPUs")
     from gru_mpi_cuda_amd.config import GRUConfig
