@@ -302,6 +302,162 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Phased form (round 5, cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4+T5): the same
+// 256 x 256 x 64 tile, 2 (M) x 4 (N) waves of 128 x 64, two 64 KiB k-tile buffers -- but the k-tile is
+// four PHASES, each {this phase's fragment reads + one 16 KiB half-tile of LDS-DMA staging -> raw
+// s_barrier -> lgkmcnt(0) -> setprio(1) 16 MFMAs setprio(0) -> raw s_barrier}, and the staging runs
+// two k-tiles ahead with a COUNTED vmcnt: never vmcnt(0) in the loop, two half-tiles stay in flight
+// across every k-tile boundary (the vmcnt(0) + __syncthreads per k-tile of gemm256_kernel drains the
+// whole pipeline once per k-tile).
+//
+// A wave's output is 4 quadrants of 64 x 32 (A sub-tile sa = rows 64 sa.., B sub-tile sb = cols
+// 32 sb..); phase order per k-tile (A0,B0) (A0,B1) (A1,B1) (A1,B0), so the reads are A0+B0 (12
+// ds_read_b128), B1 (4), A1 (8), none -- every fragment is read once per k-tile (A in one 32-VGPR
+// set, B0 / B1 16 each).  Buffer c = kt & 1 holds k-tile kt; halves 0/1 = A rows 0-127 / 128-255,
+// 2/3 = B rows 0-127 / 128-255.  A k-tile's B halves are last read in its phase 2, its A halves in
+// phase 3 (each wave retires its reads with lgkmcnt(0) before its MFMAs, and the phase's closing
+// barrier follows), so k-tile kt + 2 is staged into the same buffer as B0h in phase 3, B1h in
+// phase 4, A0h in phase 1 and A1h in phase 2 of k-tile kt + 1; phase 4 of k-tile u waits with
+// vmcnt(4) (k-tile u + 1 landed, u + 2's two B halves in flight) before its first barrier, so every
+// wave's k-tile u + 1 reads (phase 1 of u + 1, after that barrier and phase 4's closing one) see
+// all eight waves' DMA (RAW: wait, then barrier, then read).
+template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <bool BIAS, bool ACC, bool RS>
+__global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+  __shared__ __attribute__((aligned(16))) u16 lds[2][4][128 * 64];   // ONE array (§5 item 4a)
+  const int id = xcd_remap256(blockIdx.x, gridDim.x);
+  constexpr int kGroupM = 4;
+  const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
+  const int per_group = kGroupM * ntn, first_m = (pid / per_group) * kGroupM;
+  const int gm = min(ntm - first_m, kGroupM);
+  const int tm = first_m + (pid % per_group) % gm, tn = (pid % per_group) / gm;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int row0 = tm * kBM, col0 = tn * kBN;
+  const int kbeg = sp * kper, nk = kper / kBK;
+
+  // staging: wave w's instruction q of half h covers rows (2w + q) * 8 .. + 7 of that half
+  const int srow = lane >> 3, sslot = lane & 7;
+  const u16* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = (2 * w + q) * 8 + srow;
+      const int c = sslot ^ ((r >> 1) & 7);
+      src[h][q] = h < 2 ? a.A + (size_t)(row0 + h * 128 + r) * a.lda + kbeg + c * 8
+                        : a.B + (size_t)(col0 + (h - 2) * 128 + r) * a.ldb + kbeg + c * 8;
+    }
+  auto stage = [&](int kt, int h) {   // half h of k-tile kt into buffer kt & 1
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds(src[h][q] + kt * kBK, (lds256_t*)(&lds[kt & 1][h][(2 * w + q) * 8 * 64]),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int bh = 2 + (wc >> 1), bo = (wc & 1) * 64;
+  // fragment reads: A sub-tile sa (rows 64 sa + 16 i + lr of half wr), B sub-tile sb (rows
+  // bo + 32 sb + 16 j + lr of half bh), k-step ks (chunk 4 ks + lq), swizzled as staged
+  auto rdA = [&](int buf, int sa, int i, int ks) {
+    const int r = sa * 64 + i * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][wr][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  auto rdB = [&](int buf, int sb, int j, int ks) {
+    const int r = bo + sb * 32 + j * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][bh][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+  };
+  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];   // [k-step][tile]
+  const bool do_rs = RS && tn == 0 && wc == 0;   // wave-uniform
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#define GK_RA(buf, sa) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[ks][i] = rdA(buf, sa, i, ks); }
+#define GK_RB(dst, buf, sb) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[ks][j] = rdB(buf, sb, j, ks); }
+#define GK_MMA(sa, fb, sb) { \
+    __builtin_amdgcn_s_setprio(1); \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) \
+        acc[(sa) * 4 + i][(sb) * 2 + j] = mfma16(fa[ks][i], fb[ks][j], acc[(sa) * 4 + i][(sb) * 2 + j]); \
+    __builtin_amdgcn_s_setprio(0); }
+#define GK_RS(sa) { if (do_rs) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+      rs[(sa) * 4 + i] = add_sum8(fa[ks][i], rs[(sa) * 4 + i]); } }
+#define GK_SYNC() { __builtin_amdgcn_s_barrier(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+                    __builtin_amdgcn_sched_barrier(0); }
+#define GK_END() { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); }
+
+  // prologue: k-tile 0 whole, k-tile 1's B halves; wait for k-tile 0
+  stage(0, 2); stage(0, 3); stage(0, 0); stage(0, 1);
+  if (nk > 1) { stage(1, 2); stage(1, 3); vmwait256<4>(); } else { vmwait256<0>(); }
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int c = kt & 1;
+    // phase 1: (A0, B0)
+    GK_RA(c, 0); GK_RB(fb0, c, 0);
+    if (kt + 1 < nk) stage(kt + 1, 0);
+    GK_SYNC();
+    GK_MMA(0, fb0, 0);
+    GK_RS(0);
+    GK_END();
+    // phase 2: (A0, B1)
+    GK_RB(fb1, c, 1);
+    if (kt + 1 < nk) stage(kt + 1, 1);
+    GK_SYNC();
+    GK_MMA(0, fb1, 1);
+    GK_END();
+    // phase 3: (A1, B1); this buffer's B halves are free: k-tile kt + 2's B0h
+    GK_RA(c, 1);
+    if (kt + 2 < nk) stage(kt + 2, 2);
+    GK_SYNC();
+    GK_MMA(1, fb1, 1);
+    GK_RS(1);
+    GK_END();
+    // phase 4: (A1, B0); k-tile kt + 2's B1h, then wait for k-tile kt + 1
+    if (kt + 2 < nk) { stage(kt + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    GK_MMA(1, fb0, 0);
+    GK_END();
+  }
+#undef GK_RA
+#undef GK_RB
+#undef GK_MMA
+#undef GK_RS
+#undef GK_SYNC
+#undef GK_END
+
+  if (do_rs) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float v = rs[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + wr * 128 + t * 16 + lane] = v;
+    }
+  }
+  float* C = a.C + (size_t)sp * a.M * a.ldc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + wc * 64 + j * 16 + lr;
+    const float bb = BIAS ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + wr * 128 + i * 16 + lq * 4 + e;
+        float* dst = C + (size_t)row * a.ldc + col;
+        const float v = acc[i][j][e] + bb;
+        if (ACC) *dst += v; else *dst = v;
+      }
+  }
+}
+
 // (Round 4: the same tile on a 4-deep ring of 32-deep k-tiles -- three 32 KiB tiles in flight
 // instead of one 64 KiB tile, conflict-free 64-B-row swizzle c ^ 2((r >> 3) & 1) -- measured slower on
 // every shape: h2048 dW_hh 1032 vs 1122 TF at split 4, sq8192 1190 vs 1254 TF
@@ -316,6 +472,11 @@ static int gemm256_mfma(int kper) {
   const char* e = std::getenv("GK_GEMM256_MFMA");
   if (e && e[0]) return std::atoi(e);
   return kper <= 256 ? 32 : 16;
+}
+// 1: the phased pipeline (gemm256p_kernel) for the 16x16x32 form; GK_GEMM256_PHASED=0 keeps gemm256_kernel
+static bool gemm256_phased() {
+  const char* e = std::getenv("GK_GEMM256_PHASED");
+  return !(e && e[0] == '0');
 }
 
 bool gemm256_ok(const GemmArgs& a) {
@@ -333,9 +494,11 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   const int ntn = a.N / kBN, ntm = a.M / kBM, kper = a.K / a.splits;
   const dim3 grid(ntn * ntm * a.splits), block(512);
   const int form = gemm256_mfma(kper);
+  const bool phased = gemm256_phased();
 #define GK_L(B_, A_, R_)                                                                                   \
   do {                                                                                                     \
     if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
     else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);           \
   } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate
