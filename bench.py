@@ -71,6 +71,8 @@ def main() -> int:
                     help="at 1 GPU, still record the gradient collectives (1-rank RCCL communicator) "
                          "to time the data-parallel step structure")
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--dp-pipeline", type=int, choices=[-1, 0, 1], default=None,
+                    help="one-layer data-parallel tail: -1 auto (pipelined at world > 1), 0 one collective, 1 pipelined")
     ap.add_argument("--shard-optim", action="store_true",
                     help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
     ap.add_argument("--min-warmup", type=int, default=300,
@@ -125,6 +127,8 @@ def main() -> int:
         cfg = cfg.replace(bucket_mb=args.bucket_mb)
     if args.shard_optim:
         cfg = cfg.replace(shard_optim=True)
+    if args.dp_pipeline is not None:
+        cfg = cfg.replace(dp_pipeline=args.dp_pipeline)
 
     stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
     pool = [stream.next() for _ in range(8)]
@@ -211,6 +215,7 @@ def main() -> int:
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
                        "overlap": cfg.overlap, "plan": plan, "shard_optim": cfg.shard_optim,
+                       "dp_pipeline": (tr.t.dp_pipeline() if args.impl == "hip" and hasattr(tr, "t") else 0),
                        "collectives": (len(tr.t.allreduce_log()) if args.impl == "hip" and comm is not None
                                        and hasattr(tr, "t") else 0)},
             "rccl_ranks": comm.count() if comm is not None else (world if ctx.backend != "none" else 1),

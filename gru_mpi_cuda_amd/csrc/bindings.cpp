@@ -126,6 +126,8 @@ PYBIND11_MODULE(_C, m) {
       .def("read_error", &Trainer::read_error)
       .def("enable_watchdog", &Trainer::enable_watchdog)
       .def("set_shard_optim", &Trainer::set_shard_optim)
+      .def("set_dp_pipeline", &Trainer::set_dp_pipeline)
+      .def("dp_pipeline", &Trainer::dp_pipeline)
       .def("shard_optim", &Trainer::shard_optim)
       .def("shard_chunk", &Trainer::shard_chunk)
       .def("gather_opt_state", [](Trainer& t, uintptr_t s) { t.gather_opt_state(S(s)); })

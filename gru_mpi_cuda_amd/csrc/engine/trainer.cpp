@@ -577,7 +577,9 @@ void Trainer::gather_opt_state(hipStream_t s) {
   comm_->allgather_f32(v_ + o, v_, c, s);
 }
 
-void Trainer::record_opt(hipStream_t s) {
+void Trainer::record_opt(hipStream_t s, int part) {
+  if (part != 0 && o_.clip > 0.f)
+    throw std::runtime_error("record_opt: a split optimiser launch cannot clip (needs the global norm)");
   if (o_.clip > 0.f) {
     sumsq_partials(grads_, nflat_, norm_parts_, 256, s);
     clip_scale_finalize(norm_parts_, 256, o_.clip, gscale_, s);
@@ -588,19 +590,23 @@ void Trainer::record_opt(hipStream_t s) {
     // one launch: update every tensor and write its bf16 (+ transposed) MFMA copies from the
     // freshly updated registers (no second pass over the fp32 master weights)
     OptCastJobs j;
-    j.add(off_.at("embedding"), V, E, Emb, EmbT);
-    for (int l = 0; l < d_.L; ++l) {
-      const std::string k = std::to_string(l);
-      j.add(off_.at("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
-      j.add(off_.at("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
-      j.add(off_.at("bias_ih_l" + k), 0, 3 * H, nullptr, nullptr);
-      j.add(off_.at("bias_hh_l" + k), 0, 3 * H, nullptr, nullptr);
+    if (part != 2) {
+      j.add(off_.at("embedding"), V, E, Emb, EmbT);
+      for (int l = 0; l < d_.L; ++l) {
+        const std::string k = std::to_string(l);
+        j.add(off_.at("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
+        j.add(off_.at("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
+        j.add(off_.at("bias_ih_l" + k), 0, 3 * H, nullptr, nullptr);
+        j.add(off_.at("bias_hh_l" + k), 0, 3 * H, nullptr, nullptr);
+      }
     }
-    // the plain W_fc / W_fc^T copies only where a kernel reads them: the fused V = 256 FC kernel of the
-    // sequence step reads the fragment-tiled copies only
-    const bool plain = overlap_ || fc_split_ || !(V == 256 && (H == 512 || H == 1024));
-    j.add(off_.at("fc.weight"), V, H, plain ? Wfc : nullptr, plain ? WfcT : nullptr, WfcF, WfcTF);
-    j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
+    if (part != 1) {
+      // the plain W_fc / W_fc^T copies only where a kernel reads them: the fused V = 256 FC kernel of
+      // the sequence step reads the fragment-tiled copies only
+      const bool plain = overlap_ || fc_split_ || !(V == 256 && (H == 512 || H == 1024));
+      j.add(off_.at("fc.weight"), V, H, plain ? Wfc : nullptr, plain ? WfcT : nullptr, WfcF, WfcTF);
+      j.add(off_.at("fc.bias"), 0, V, nullptr, nullptr);
+    }
     // deferred slab reductions: summed inside the Adam launch where a job covers exactly the
     // gradient segment; anything else is reduced first
     SlabJobs rest;
@@ -619,6 +625,7 @@ void Trainer::record_opt(hipStream_t s) {
     if (rest.n) reduce_slabs_multi(rest, s);
     adam_cast_multi(a, j, s);
   } else {
+    if (part != 0) throw std::runtime_error("record_opt: split optimiser launches need V, E, H % 64 == 0");
     if (deferred_.n) reduce_slabs_multi(deferred_, s);
     adam_step(a, s);
     refresh_weights(s);
@@ -688,6 +695,22 @@ void Trainer::set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& bu
   g_step_[1].reset();
   g_group_[0].reset();
   g_group_[1].reset();
+}
+
+void Trainer::set_dp_pipeline(int mode) {
+  if (mode < -1 || mode > 1) throw std::runtime_error("set_dp_pipeline: -1 (auto), 0 or 1");
+  dp_pipe_ = mode;
+  g_step_[0].reset();
+  g_step_[1].reset();
+  g_group_[0].reset();
+  g_group_[1].reset();
+}
+
+bool Trainer::dp_pipe_on() const {
+  if (!comm_ || overlap_ || shard_opt_ || d_.L != 1 || o_.clip > 0.f) return false;
+  const int V = d_.V, E = d_.E, H = d_.H;
+  if (V % 64 || E % 64 || H % 64 || !dP_inplace_) return false;
+  return dp_pipe_ == 1 || (dp_pipe_ == -1 && comm_->world() > 1);
 }
 
 long Trainer::group_end(int l) const {
@@ -832,10 +855,12 @@ void Trainer::record_step_body() {
     return;
   }
   deferred_.n = 0;
+  opt_in_fb_ = false;
   if (dp_overlap()) {
     // readiness-ordered collectives on the comm stream, overlapped with the rest of the
     // backward; joined before the optimiser (the embedding-side tail runs after the join)
     record_fb_seq(s0_, /*dp=*/true);
+    if (opt_in_fb_) { opt_in_fb_ = false; return; }   // the pipelined tail recorded its own Adam launches
   } else {
     defer_slabs_ = !overlap_ && !comm_ && o_.clip <= 0.f;
     if (overlap_) record_fb(s0_); else record_fb_seq(s0_);

@@ -71,7 +71,8 @@ class Trainer {
   void slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst);
   void record_carry(hipStream_t s);     // HS[T] -> HS[0] of every layer and copy (carry_ only)
   bool carry_ = false;
-  void record_opt(hipStream_t s0);
+  // part: 0 every tensor, 1 every tensor but the FC pair, 2 the FC pair only (pipelined DP tail)
+  void record_opt(hipStream_t s0, int part = 0);
   void fwd_step(int l, int t, hipStream_t s);
   void bwd_step(int l, int t, hipStream_t s);
   hipEvent_t ev();
@@ -136,6 +137,17 @@ class Trainer {
   bool ar_flush(hipStream_t s, bool force, bool with_err = false);
   void ar_join(hipStream_t s);
   float* dP_target() { return dP_inplace_ ? G("weight_ih_l0") : dP_; }
+  // Pipelined data-parallel tail (one-layer models, where every gradient but FC's is ready only when
+  // the persistent backward ends): three readiness buckets instead of one exposed collective --
+  //   reduce [W_hh0, b_hh0, b_ih0, dP] slabs -> AR1 (+ error word) on the comm stream
+  //   | beside it: dW_fc K-slices -> reduce -> AR2 (FC pair) on the comm stream
+  //   join AR1 -> dW_ih0 / dEmb from the averaged dP -> Adam (all but FC) | beside it: AR2
+  //   join AR2 -> Adam (FC pair).
+  // dp_pipe_: -1 auto (on at world > 1), 0 one collective (the single-bucket step), 1 on.
+  int dp_pipe_ = -1;
+  bool dp_pipe_on() const;
+  bool opt_in_fb_ = false;   // record_fb_seq recorded the optimiser itself (pipelined tail)
+  void record_dp_tail_l1(hipStream_t s, SlabJobs& j, const SlabJobs& fc_tail);
   hipStream_t sc_ = nullptr;
   long min_bucket_ = 0, ar_ready_ = 0, ar_launched_ = 0;
   bool ar_busy_ = false, dP_inplace_ = false;
@@ -151,6 +163,9 @@ class Trainer {
   void set_comm(RcclComm* c, const std::vector<std::pair<long, long>>& buckets, long min_bucket_floats);
   // collectives recorded into the last captured step graph (tests / plan printing)
   const std::vector<std::pair<long, long>>& allreduce_log() const { return ar_log_; }
+  // pipelined data-parallel tail (see dp_pipe_): -1 auto, 0 off, 1 on; takes effect at the next capture
+  void set_dp_pipeline(int mode);
+  int dp_pipeline() const { return dp_pipe_on() ? 1 : 0; }
   // Sharded optimiser step (ZeRO-1 style, data-parallel only; call after set_comm).  The step graph
   // reduce-scatters the flat fp32 gradient in place (rank r owns floats [r*c, (r+1)*c), c a multiple
   // of 4; the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the masters and

@@ -248,7 +248,10 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // single GPU, slabs summed inside Adam: nothing reads dW_fc before the optimiser, so its
     // K-slices can join the dW_ih0 / dEmb launch after the backward sweep (one launch fewer; its
     // latency-bound tiles run beside theirs)
-    fc_held_on_ = !dp && defer_slabs_ && sp <= 8 && w.algo == 3 && step_lds_variants().dwfc_group;
+    // pipelined data-parallel tail (dp_pipe_on): the K-slices run after the backward too, beside the
+    // first collective (record_dp_tail_l1)
+    fc_held_on_ = (dp && dp_pipe_on()) ||
+                  (!dp && defer_slabs_ && sp <= 8 && w.algo == 3 && step_lds_variants().dwfc_group);
     if (fc_held_on_) fc_held_ = w;
     else gemm_nt(w, s);
     tail.add(slab_fc2_, sp, (long)V * H, G("fc.weight"));
@@ -303,13 +306,20 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     if (l == 0 && (q.bwd || q.big)) slab_job(j, q.dbih_part, q.nrb, H3, G("bias_ih_l0"));
     // dW_fc / db_fc slabs: with the top layer's group when data-parallel (the FC group is
-    // all-reduced with it), else with layer 0's reduce
-    if (dp ? l == L - 1 : l == 0)
+    // all-reduced with it), else with layer 0's reduce; the pipelined tail reduces them on their own
+    const bool pipe = dp && l == 0 && dp_pipe_on();
+    if ((dp ? l == L - 1 : l == 0) && !pipe)
       for (int k2 = 0; k2 < tail.n; ++k2)
         slab_job(j, tail.job[k2].src, tail.job[k2].splits, tail.job[k2].n, tail.job[k2].dst);
     if (l == 0) {   // + the loss partials and the optimiser step counter
       j.add(loss_part_, nloss_, 1, loss_);
       j.bump = step_;
+    }
+    if (pipe) {   // one-layer data-parallel: the bucketed, pipelined tail records the rest of the step
+      if (!q.fuse_p || !q.fuse_w) throw std::runtime_error("pipelined data-parallel tail: needs the fused dW_hh / dP backward");
+      record_dp_tail_l1(s, j, tail);
+      HIP_LAUNCH_CHECK();
+      return;
     }
     if (j.n) reduce_slabs_multi(j, s);
     if (!q.fuse_w)
@@ -385,6 +395,59 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     record_emb_tail(s, seq_[0].fuse_p ? nullptr : dP_);
   }
   HIP_LAUNCH_CHECK();
+}
+
+// The pipelined one-layer data-parallel tail (Trainer::dp_pipe_).  j holds the
+// backward's slab jobs (W_hh0, b_hh0, b_ih0 partials, dP -> the W_ih0 slot, loss); fc_tail the dW_fc /
+// db_fc K-slice slabs of the held FC GEMM.  Three readiness buckets of the flat gradient (layout:
+// fc.weight, fc.bias | weight_hh_l0, bias_hh_l0, bias_ih_l0 | dP in the weight_ih_l0 slot):
+//   s : reduce(j)                         c : AR1 = [W_hh0 .. dP] + error word (max over ranks)
+//   s : dW_fc K-slices -> reduce(fc)      c : AR2 = [fc.weight, fc.bias]
+//   s : join AR1 -> dW_ih0 / dEmb (one grouped launch on the averaged fp32 dP) -> Adam(all but FC)
+//   s : join AR2 -> Adam(FC)
+// At world W, AR1 (4.6 MB at the headline) runs beside the dW_fc GEMM and its reduce, AR2 beside the
+// embedding GEMMs and the first Adam launch, instead of one 5.25 MB collective with nothing beside
+// it.  Every per-element sum is the single-bucket step's (same reduce kernel and order, the same GEMM
+// k order, Adam per element), so at one rank the result is bitwise that step's
+// (tests/test_engine_gpu.py::test_dp_pipelined_tail_world1).  Reference: the reference's only
+// parallel layer is scatter -> compute -> gather around the name loop (namegensf.cu:628-636, 889).
+void Trainer::record_dp_tail_l1(hipStream_t s, SlabJobs& j, const SlabJobs& fc_tail) {
+  const long r0 = off_.at("weight_hh_l0"), r1 = group_end(0);
+  if (j.n) reduce_slabs_multi(j, s);
+  hipEvent_t e = ev();
+  HIP_CHECK(hipEventRecord(e, s));          // fork AR1 after the reduce
+  HIP_CHECK(hipStreamWaitEvent(sc_, e, 0));
+  comm_->allreduce_avg_f32_err(grads_ + r0, r1 - r0, err_, sc_);
+  ar_log_.push_back({r0, r1 - r0});
+  hipEvent_t ar1 = ev();
+  HIP_CHECK(hipEventRecord(ar1, sc_));
+  // beside AR1: the dW_fc K-slices (held back from before the backward) and their slab reduce
+  if (!fc_held_on_) throw std::runtime_error("pipelined data-parallel tail: the dW_fc GEMM was not held");
+  gemm_nt(fc_held_, s);
+  fc_held_on_ = false;
+  if (fc_tail.n) {
+    SlabJobs f;
+    for (int k = 0; k < fc_tail.n; ++k) f.job[f.n++] = fc_tail.job[k];
+    reduce_slabs_multi(f, s);
+  }
+  hipEvent_t e2 = ev();
+  HIP_CHECK(hipEventRecord(e2, s));
+  HIP_CHECK(hipStreamWaitEvent(sc_, e2, 0));
+  comm_->allreduce_avg_f32(grads_, r0, sc_);   // [fc.weight, fc.bias] (offset 0: readiness order)
+  ar_log_.push_back({0, r0});
+  hipEvent_t ar2 = ev();
+  HIP_CHECK(hipEventRecord(ar2, sc_));
+  // join AR1: the embedding-side GEMMs from the averaged dP, then Adam on everything but the FC pair
+  HIP_CHECK(hipStreamWaitEvent(s, ar1, 0));
+  defer_slabs_ = true;
+  record_emb_tail(s, dP_target());
+  record_opt(s, 1);
+  defer_slabs_ = false;
+  // join AR2: Adam on the FC pair
+  HIP_CHECK(hipStreamWaitEvent(s, ar2, 0));
+  record_opt(s, 2);
+  ar_busy_ = false;
+  opt_in_fb_ = true;
 }
 
 // dEmb = dP · W_ih0 and dW_ih0 = dP^T · Emb from the layer-0 table gradient dP.  dP_fp32 may

@@ -78,6 +78,7 @@ class HipTrainer:
                             max(1024, int(cfg.bucket_mb * (1 << 20) / 4)))
             if cfg.shard_optim:
                 self.t.set_shard_optim(True)
+            self.t.set_dp_pipeline(int(cfg.dp_pipeline))
         self.t.refresh_weights(self._stream())
         self._one_graph = True
         # does the flat gradient buffer hold the last step's full gradient?  Not after a one-graph
@@ -287,16 +288,41 @@ class CpuTrainer:
     def error_word(self) -> int:
         return self._err
 
+    def _pipelined(self) -> bool:
+        """CPU twin of Trainer::dp_pipe_on (one-layer data-parallel pipelined tail)."""
+        c = self.cfg
+        return (self.ctx.world > 1 and c.layers == 1 and self.shard is None and c.clip_norm <= 0
+                and c.dp_pipeline in (-1, 1))
+
     def allreduce_grads(self) -> None:
+        import torch.distributed as dist
+        if self._pipelined():
+            # twin of Trainer::record_dp_tail_l1: AR1 = [W_hh0 .. end) with the error word, then
+            # AR2 = the FC pair (the device step all-reduces dP where this path has dW_ih0 / dEmb)
+            r0 = self.layout["weight_hh_l0"].offset
+            w1 = dist.all_reduce(self.flat_g[r0:], op=dist.ReduceOp.SUM, async_op=True)
+            e = torch.tensor([self._err], dtype=torch.int64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            self._err = int(e.item())
+            w2 = dist.all_reduce(self.flat_g[:r0], op=dist.ReduceOp.SUM, async_op=True)
+            w1.wait()
+            w2.wait()
+            self.flat_g.div_(self.ctx.world)
+            return
         allreduce_mean_buckets(self.flat_g, self.buckets, self.ctx.world)
         if self.ctx.world > 1:   # max over ranks, like the device word in the last collective
-            import torch.distributed as dist
             e = torch.tensor([self._err], dtype=torch.int64)
             dist.all_reduce(e, op=dist.ReduceOp.MAX)
             self._err = int(e.item())
 
     def optimizer_step(self) -> None:
         if self._err:   # a step that failed on any rank is skipped on every rank
+            return
+        if self.shard is None and self._pipelined():   # Adam(all but FC), then Adam(FC), one step
+            fc = ("fc.weight", "fc.bias")
+            self.opt.step({k: v for k, v in self.params.items() if k not in fc},
+                          {k: v for k, v in self.gviews.items() if k not in fc})
+            self.opt.step({k: self.params[k] for k in fc}, {k: self.gviews[k] for k in fc}, advance=False)
             return
         if self.shard is None:
             self.opt.step(self.params, self.gviews)

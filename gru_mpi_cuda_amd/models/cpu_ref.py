@@ -167,13 +167,18 @@ class Adam:
         self.m = {k: torch.zeros_like(v) for k, v in params.items()}
         self.v = {k: torch.zeros_like(v) for k, v in params.items()}
 
-    def step(self, params: Params, grads: Params) -> None:
+    def step(self, params: Params, grads: Params, advance: bool = True) -> None:
+        """advance=False: a further part of the SAME step (the pipelined data-parallel tail updates
+        the FC pair in a second launch with the step counter of the first)."""
         c = self.cfg
         scale = 1.0
         if c.clip_norm > 0:
+            if not advance:
+                raise ValueError("a split optimiser step cannot clip (needs the global norm)")
             norm = torch.sqrt(sum((g.double() ** 2).sum() for g in grads.values())).item()
             scale = min(1.0, c.clip_norm / (norm + 1e-6))
-        self.step_n += 1
+        if advance:
+            self.step_n += 1
         lr = lr_at(c, self.step_n)
         if c.optimizer == "sgd":
             for k in params:

@@ -7,3 +7,4 @@ for i in a b c; do
 done
 cat $out
 bash scripts/gpu_prof.sh r5_base --steps 20 --warmup 5 | head -12
+bash scripts/gpu_gemm.sh

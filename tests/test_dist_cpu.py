@@ -103,6 +103,53 @@ def test_dp_training_equals_single_rank(tmp_path, world):
         torch.testing.assert_close(a[k], b[k], atol=1e-4, rtol=1e-4)
 
 
+def _pipe_worker(rank, world, port, outdir, steps, pipe):
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=16, hidden=24, layers=1, batch=8, seq=6, lr=1e-2, dp_pipeline=pipe)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1))
+    assert tr._pipelined() == (world > 1 and pipe != 0)
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    per = cfg.batch // world
+    for _ in range(steps):
+        x, y = ds.next()
+        tr.step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    if rank == 0:
+        m, v, n = tr.opt_state()
+        torch.save({"p": tr.state_dict(), "m": m, "v": v, "n": n}, os.path.join(outdir, f"pipe{pipe}_{world}.pt"))
+    gdist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_pipelined_tail_equals_single_bucket(tmp_path, world):
+    """CPU twin of the one-layer pipelined data-parallel tail (Trainer::record_dp_tail_l1): two
+    readiness buckets (W_hh0 .. end with the error word, then the FC pair) and Adam in two parts of
+    ONE step equal the single-bucket step at the same world size -- bitwise at world 2, where a
+    two-rank sum has one order; at 4 gloo's ring order follows the buffer's chunking, so to fp32
+    rounding -- and one rank with the whole batch."""
+    ctx = mp.get_context("spawn")
+    for w, pipe in ((world, 1), (world, 0), (1, 1)):
+        port = _free_port()
+        procs = [ctx.Process(target=_pipe_worker, args=(r, w, port, str(tmp_path), 4, pipe)) for r in range(w)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(180)
+            assert p.exitcode == 0
+    a = torch.load(tmp_path / f"pipe1_{world}.pt", weights_only=True)
+    b = torch.load(tmp_path / f"pipe0_{world}.pt", weights_only=True)
+    one = torch.load(tmp_path / "pipe1_1.pt", weights_only=True)
+    assert a["n"] == b["n"] == one["n"] == 4
+    tol = dict(atol=0, rtol=0) if world == 2 else dict(atol=1e-6, rtol=1e-4)
+    for k in a["p"]:
+        torch.testing.assert_close(a["p"][k], b["p"][k], **tol)
+        torch.testing.assert_close(a["p"][k], one["p"][k], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(a["m"], b["m"], **tol)
+    torch.testing.assert_close(a["v"], b["v"], **(tol if world == 2 else dict(atol=1e-9, rtol=1e-3)))
+
+
 def _shard_worker(rank, world, port, outdir, steps, shard):
     _env(rank, world, port)
     from gru_mpi_cuda_amd.parallel import dist as gdist

@@ -324,6 +324,48 @@ def test_generator_fp32_probs_match_fp64(precision, persist, atol, rtol):
     torch.testing.assert_close(probs[:N].cpu().double(), want, atol=atol, rtol=rtol)
 
 
+@pytest.mark.parametrize("E,H,group", [(256, 256, 1), (512, 512, 1), (128, 256, 4)])
+def test_dp_pipelined_tail_world1(E, H, group):
+    """The bucketed, pipelined one-layer data-parallel tail (Trainer::record_dp_tail_l1: AR1 = W_hh0 ..
+    dP beside the dW_fc K-slices, AR2 = the FC pair beside the embedding GEMMs and the first Adam
+    launch) on a 1-rank communicator: bitwise the single-bucket DP step (params, loss, Adam moments)
+    and close to the no-comm step, over single-step and multi-step graphs; two collectives."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=1, batch=64, seq=8, seed=3)
+    ds = NameStream(cfg.batch, cfg.seq, seed=4)
+    batches = [ds.next() for _ in range(2 * group)]
+    runs = {}
+    for mode in ("pipe", "mono", "none"):
+        comm = None if mode == "none" else C.RcclComm(C.RcclComm.unique_id(), 0, 1)
+        tr = HipTrainer(cfg.replace(dp_pipeline=1 if mode == "pipe" else 0), params=init_params(cfg), comm=comm)
+        if comm is not None:
+            assert tr.t.dp_pipeline() == (1 if mode == "pipe" else 0)
+        if group == 1:
+            for x, y in batches:
+                tr.step(x, y)
+        else:
+            tr.steps(batches[:group])
+            tr.steps(batches[group:])
+        assert tr._one_graph, "in-graph RCCL all-reduce fell back"
+        if mode == "pipe":
+            log = tr.t.allreduce_log()
+            assert len(log) == 2 and log[1][0] == 0, log
+        torch.cuda.synchronize()
+        assert tr.t.read_error() == 0
+        runs[mode] = (tr.params.clone(), tr.loss(), tr.m.clone(), tr.v.clone())
+    for a, b in zip(runs["pipe"], runs["mono"]):   # the single-bucket DP step: bit for bit
+        if isinstance(a, float):
+            assert a == b
+        else:
+            torch.testing.assert_close(a, b, atol=0, rtol=0)
+    # the no-comm step sums the dW_fc slabs inside the Adam launch (another fp32 order): close
+    assert abs(runs["pipe"][1] - runs["none"][1]) < 1e-4 * abs(runs["none"][1])
+    d = (runs["pipe"][0] - runs["none"][0]).abs()
+    assert d.max().item() <= 2 * cfg.lr * 2 * group + 1e-6 and (d > 1e-6).float().mean().item() < 1e-3
+
+
 @pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll", [
     (1, 256, 256, 8.0, 1), (2, 128, 256, 0.25, 3), (1, 512, 512, 1.0, 1),
     (2, 512, 256, 0.25, 2), (2, 512, 256, 64.0, 1)])
