@@ -228,9 +228,10 @@ DEV void fc2_load_wt(bf16x8 (&bt)[8][4], const u16* WTf, int n0, int lane) {
     for (int c = 0; c < 4; ++c) bt[kk][c] = ld8(WTf + ((size_t)((n0 / 16 + c) * 8 + kk) * 64 + lane) * 8);
 }
 
-// DH = false (the persistent backward path): no dH here -- the backward sequence kernel computes
-// dy = dl · W_fc itself from the row-major bf16 dl this kernel writes (its MFMA pipe is idle while
-// it waits on the recurrence), so the W_fc^T stream, the dH MFMAs and the fp32 dy store go away.
+// DH = true (every default plan): dH = dl · W_fc fused, the dlogits never leave LDS.  DH = false
+// writes the row-major bf16 dl instead and leaves dH to a GEMM (a round-2 plan computed dy inside
+// the backward sequence kernel from it: fc_xent 16.3 -> 11.4 us but the backward +7-10 us,
+// profiles/r2_bwd_dh_ab.jsonl; that consumer was removed in round 4).
 template <int HH, bool DH>
 __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
