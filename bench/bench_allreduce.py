@@ -10,8 +10,12 @@ prints one JSON line per size with time, algorithm bandwidth (bytes / time) and 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bench_allreduce.py
     python bench/bench_allreduce.py            # 1 GPU: a 1-rank communicator (plumbing / launch cost)
 
-The headline model's per-step gradient traffic is one ~5.25 MB collective (dP in the W_ih0 slot,
-W_hh, biases, W_fc): the 4-8 MB rows are the ones that set the data-parallel step overhead.
+The headline model's per-step gradient traffic is ~5.25 MB (dP in the W_ih0 slot, W_hh, biases,
+W_fc).  At world > 1 the one-layer step records it as the pipelined tail's two readiness buckets
+(Trainer::record_dp_tail_l1): AR1 = W_hh0, b_hh0, b_ih0, dP (4.6 MB, with the error word) beside
+the dW_fc K-slices, AR2 = the FC pair (0.5 MB) beside the embedding GEMMs and the first Adam launch;
+`--dp-pipeline 0` (bench.py) restores one collective after the backward.  The plan row below prints
+the exact collectives of the captured step at this world size.
 """
 from __future__ import annotations
 
@@ -121,7 +125,8 @@ def _headline_plan(ctx, comm, stream, args) -> None:
         print(json.dumps({"headline_step_collectives": [{"offset": o, "floats": n, "mb": round(n * 4 / 2 ** 20, 3)}
                                                          for o, n in log],
                           "total_mb": round(mb, 3), "bucket_mb": cfg.bucket_mb, "ranks": ctx.world,
-                          "plan": tr.t.plan(), "in_graph_replay_us_median": round(float(np.median(ts)), 2)}),
+                          "plan": tr.t.plan(), "dp_pipeline": tr.t.dp_pipeline(),
+                          "in_graph_replay_us_median": round(float(np.median(ts)), 2)}),
               flush=True)
 
 

@@ -27,7 +27,8 @@ dbg = torch.zeros(2 * 4096 * 8, device=dev, dtype=torch.int64)
 d = dict(allow_local=int(os.environ.get("LOCAL", 1)), HSb=HSb.data_ptr(), xch=xch.data_ptr(), HSf=HSf.data_ptr(), HT=HT.data_ptr(), ldT=(T + 1) * Bp,
          sr=sv[0].data_ptr(), sz=sv[1].data_ptr(), sn=sv[2].data_ptr(), sghn=sv[3].data_ptr(),
          Whh=Whh.data_ptr(), bhh=bhh.data_ptr(), P=P.data_ptr(), ids=ids.data_ptr(),
-         cnt=cnt.data_ptr(), err=err.data_ptr(), T=T, Bp=Bp, H=H)
+         cnt=cnt.data_ptr(), err=err.data_ptr(), T=T, Bp=Bp, H=H,
+         xring=int(os.environ.get("XR", 4)), tag=int(os.environ.get("TAG", 0)))
 res = {}
 for mode in ("plain", "dbg"):
     if mode == "dbg":
@@ -35,6 +36,7 @@ for mode in ("plain", "dbg"):
     times = []
     for it in range(20):
         cnt.zero_()
+        xch.zero_()   # the tagged ring starts zeroed (in the engine: the backward zeroes it)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -44,6 +46,7 @@ for mode in ("plain", "dbg"):
         times.append(e0.elapsed_time(e1) * 1000)
     res[mode + "_us"] = float(np.median(times[5:]))
 res["err"] = int(err[0])
+res["xring"], res["tag"] = d["xring"], d["tag"]
 st = dbg.view(2, 4096, 8)[:, :T, :7].cpu().numpy().astype(np.float64) * 10.0   # ns
 for wg in (0, 1):
     x = st[wg]
