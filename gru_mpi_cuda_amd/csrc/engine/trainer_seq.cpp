@@ -32,15 +32,17 @@ static int wgrad_engine() {   // read at record time (tests switch it per traine
   return 256;
 }
 
-// split-K depth for gemm256: the one that fills whole waves of 256 workgroups best (ties: the
-// shallower, fewer slabs), K-slices at least 2048 deep
+// split-K depth for gemm256: the one that fills whole waves of 256 workgroups best with the tile
+// gemm256 picks for it (256 or 192 rows, gemm256_tile_rows; ties: the shallower, fewer slabs),
+// K-slices at least 2048 deep
 static int gemm256_splits(int M, int N, int K) {
-  const int tiles = (M / 256) * (N / 256);
   int best = 0;
   double best_fill = 0.0;
   for (int sp = 1; sp <= 8; sp *= 2) {
     if (K % sp || (K / sp) % 64 || (sp > 1 && K / sp < 2048)) continue;
-    const int wg = tiles * sp, rounds = (wg + 255) / 256;
+    const int bm = gemm256_tile_rows(M, N, K, sp);
+    if (!bm) continue;
+    const int wg = (M / bm) * (N / 256) * sp, rounds = (wg + 255) / 256;
     const double fill = (double)wg / (rounds * 256);
     if (fill > best_fill + 1e-9) { best_fill = fill; best = sp; }
   }

@@ -324,9 +324,19 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 // all eight waves' DMA (RAW: wait, then barrier, then read).
 template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <bool BIAS, bool ACC, bool RS>
+// BM = 256 or 192 rows of A per tile (192: M = 3H products at 3H % 256 != 0 or whose 256-row grid
+// leaves part of a round idle -- dW_hh at H = 2048 is 32 x 8 = 256 tiles of 192 rows, one full round,
+// against 24 x 8 = 192 of 256; gemm256_tile_rows picks by fill).  Waves are 2 (M) x 4 (N) with a
+// (BM / 2) x 64 output: RT = BM / 32 row tiles of 16, a quadrant is RT / 2 of them x 2 column tiles.
+// LDS per buffer: A [BM][64] + B [256][64] bf16, staged in 1-KiB pieces of 8 rows (one wave
+// instruction each): A BM / 64 pieces per wave, B 4.
+template <int BM, bool BIAS, bool ACC, bool RS>
 __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
-  __shared__ __attribute__((aligned(16))) u16 lds[2][4][128 * 64];   // ONE array (§5 item 4a)
+  constexpr int RT = BM / 32, QR = RT / 2;          // row tiles per wave / per quadrant
+  constexpr int NA = BM / 64, NB = 4;                // staging pieces per wave: A, B
+  constexpr int NA1 = (NA + 1) / 2;                  // A pieces in phase 1 (the rest in phase 2)
+  constexpr int AOFF = 0, BOFF = BM * 64;            // element offsets inside a buffer
+  __shared__ __attribute__((aligned(16))) u16 lds[2][(BM + 256) * 64];   // ONE array (§5 item 4a)
   const int id = xcd_remap256(blockIdx.x, gridDim.x);
   constexpr int kGroupM = 4;
   const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
@@ -336,90 +346,110 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int lr = lane & 15, lq = lane >> 4;
-  const int row0 = tm * kBM, col0 = tn * kBN;
+  const int row0 = tm * BM, col0 = tn * kBN;
   const int kbeg = sp * kper, nk = kper / kBK;
 
-  // staging: wave w's instruction q of half h covers rows (2w + q) * 8 .. + 7 of that half
+  // staging: piece q of wave w covers image rows (NA w + q) * 8 .. + 7 of A, (NB w + q) * 8 .. of B
   const int srow = lane >> 3, sslot = lane & 7;
-  const u16* src[4][2];
+  const u16* srcA[NA];
+  const u16* srcB[NB];
 #pragma unroll
-  for (int h = 0; h < 4; ++h)
+  for (int q = 0; q < NA; ++q) {
+    const int r = (NA * w + q) * 8 + srow;
+    srcA[q] = a.A + (size_t)(row0 + r) * a.lda + kbeg + (sslot ^ ((r >> 1) & 7)) * 8;
+  }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = (2 * w + q) * 8 + srow;
-      const int c = sslot ^ ((r >> 1) & 7);
-      src[h][q] = h < 2 ? a.A + (size_t)(row0 + h * 128 + r) * a.lda + kbeg + c * 8
-                        : a.B + (size_t)(col0 + (h - 2) * 128 + r) * a.ldb + kbeg + c * 8;
-    }
-  auto stage = [&](int kt, int h) {   // half h of k-tile kt into buffer kt & 1
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      __builtin_amdgcn_global_load_lds(src[h][q] + kt * kBK, (lds256_t*)(&lds[kt & 1][h][(2 * w + q) * 8 * 64]),
-                                       16, 0, 0);
+  for (int q = 0; q < NB; ++q) {
+    const int r = (NB * w + q) * 8 + srow;
+    srcB[q] = a.B + (size_t)(col0 + r) * a.ldb + kbeg + (sslot ^ ((r >> 1) & 7)) * 8;
+  }
+  auto stA = [&](int kt, int q) {
+    __builtin_amdgcn_global_load_lds(srcA[q] + kt * kBK, (lds256_t*)(&lds[kt & 1][AOFF + (NA * w + q) * 8 * 64]), 16, 0, 0);
+  };
+  auto stB = [&](int kt, int q) {
+    __builtin_amdgcn_global_load_lds(srcB[q] + kt * kBK, (lds256_t*)(&lds[kt & 1][BOFF + (NB * w + q) * 8 * 64]), 16, 0, 0);
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[RT][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int bh = 2 + (wc >> 1), bo = (wc & 1) * 64;
-  // fragment reads: A sub-tile sa (rows 64 sa + 16 i + lr of half wr), B sub-tile sb (rows
-  // bo + 32 sb + 16 j + lr of half bh), k-step ks (chunk 4 ks + lq), swizzled as staged
+  const int arow = wr * (BM / 2), brow = (wc >> 1) * 128 + (wc & 1) * 64;
+  // fragment reads: A sub-tile sa (rows arow + 16 (QR sa + i) + lr), B sub-tile sb (rows
+  // brow + 32 sb + 16 j + lr), k-step ks (chunk 4 ks + lq), swizzled as staged
   auto rdA = [&](int buf, int sa, int i, int ks) {
-    const int r = sa * 64 + i * 16 + lr, c = ks * 4 + lq;
-    return *reinterpret_cast<const bf16x8*>(&lds[buf][wr][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+    const int r = arow + (QR * sa + i) * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][AOFF + r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
   };
   auto rdB = [&](int buf, int sb, int j, int ks) {
-    const int r = bo + sb * 32 + j * 16 + lr, c = ks * 4 + lq;
-    return *reinterpret_cast<const bf16x8*>(&lds[buf][bh][r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
+    const int r = brow + sb * 32 + j * 16 + lr, c = ks * 4 + lq;
+    return *reinterpret_cast<const bf16x8*>(&lds[buf][BOFF + r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
   };
-  bf16x8 fa[2][4], fb0[2][2], fb1[2][2];   // [k-step][tile]
+  bf16x8 fa[2][QR], fb0[2][2], fb1[2][2];   // [k-step][tile]
   const bool do_rs = RS && tn == 0 && wc == 0;   // wave-uniform
-  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#define GK_RA(buf, sa) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[ks][i] = rdA(buf, sa, i, ks); }
+  float rs[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) rs[i] = 0.f;
+#define GK_RA(buf, sa) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < QR; ++i) fa[ks][i] = rdA(buf, sa, i, ks); }
 #define GK_RB(dst, buf, sb) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int j = 0; j < 2; ++j) dst[ks][j] = rdB(buf, sb, j, ks); }
 #define GK_MMA(sa, fb, sb) { \
     __builtin_amdgcn_s_setprio(1); \
-    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < QR; ++i) \
       _Pragma("unroll") for (int j = 0; j < 2; ++j) \
-        acc[(sa) * 4 + i][(sb) * 2 + j] = mfma16(fa[ks][i], fb[ks][j], acc[(sa) * 4 + i][(sb) * 2 + j]); \
+        acc[(sa) * QR + i][(sb) * 2 + j] = mfma16(fa[ks][i], fb[ks][j], acc[(sa) * QR + i][(sb) * 2 + j]); \
     __builtin_amdgcn_s_setprio(0); }
-#define GK_RS(sa) { if (do_rs) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i) \
-      rs[(sa) * 4 + i] = add_sum8(fa[ks][i], rs[(sa) * 4 + i]); } }
+#define GK_RS(sa) { if (do_rs) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < QR; ++i) \
+      rs[(sa) * QR + i] = add_sum8(fa[ks][i], rs[(sa) * QR + i]); } }
 #define GK_SYNC() { __builtin_amdgcn_s_barrier(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                     __builtin_amdgcn_sched_barrier(0); }
 #define GK_END() { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); }
 
-  // prologue: k-tile 0 whole, k-tile 1's B halves; wait for k-tile 0
-  stage(0, 2); stage(0, 3); stage(0, 0); stage(0, 1);
-  if (nk > 1) { stage(1, 2); stage(1, 3); vmwait256<4>(); } else { vmwait256<0>(); }
+  // prologue: k-tile 0 whole, k-tile 1's B pieces; wait for k-tile 0
+#pragma unroll
+  for (int q = 0; q < NB; ++q) stB(0, q);
+#pragma unroll
+  for (int q = 0; q < NA; ++q) stA(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) stB(1, q);
+    vmwait256<NB>();
+  } else {
+    vmwait256<0>();
+  }
   __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
     const int c = kt & 1;
-    // phase 1: (A0, B0)
+    // phase 1: (A0, B0); k-tile kt + 1's first A pieces
     GK_RA(c, 0); GK_RB(fb0, c, 0);
-    if (kt + 1 < nk) stage(kt + 1, 0);
+    if (kt + 1 < nk) {
+#pragma unroll
+      for (int q = 0; q < NA1; ++q) stA(kt + 1, q);
+    }
     GK_SYNC();
     GK_MMA(0, fb0, 0);
     GK_RS(0);
     GK_END();
-    // phase 2: (A0, B1)
+    // phase 2: (A0, B1); the rest of k-tile kt + 1's A pieces
     GK_RB(fb1, c, 1);
-    if (kt + 1 < nk) stage(kt + 1, 1);
+    if (kt + 1 < nk) {
+#pragma unroll
+      for (int q = NA1; q < NA; ++q) stA(kt + 1, q);
+    }
     GK_SYNC();
     GK_MMA(0, fb1, 1);
     GK_END();
-    // phase 3: (A1, B1); this buffer's B halves are free: k-tile kt + 2's B0h
+    // phase 3: (A1, B1); this buffer's B rows are free: half of k-tile kt + 2's B pieces
     GK_RA(c, 1);
-    if (kt + 2 < nk) stage(kt + 2, 2);
+    if (kt + 2 < nk) { stB(kt + 2, 0); stB(kt + 2, 1); }
     GK_SYNC();
     GK_MMA(1, fb1, 1);
     GK_RS(1);
     GK_END();
-    // phase 4: (A1, B0); k-tile kt + 2's B1h, then wait for k-tile kt + 1
-    if (kt + 2 < nk) { stage(kt + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); }
+    // phase 4: (A1, B0); the other half, then wait for k-tile kt + 1 (k-tile kt + 2's 4 B pieces
+    // stay in flight)
+    if (kt + 2 < nk) { stB(kt + 2, 2); stB(kt + 2, 3); vmwait256<NB>(); } else { vmwait256<0>(); }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     GK_MMA(1, fb0, 0);
@@ -434,11 +464,11 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
 
   if (do_rs) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
+    for (int t = 0; t < RT; ++t) {
       float v = rs[t];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + wr * 128 + t * 16 + lane] = v;
+      if (lane < 16) a.rowsumA[(size_t)sp * a.M + row0 + arow + t * 16 + lane] = v;
     }
   }
   float* C = a.C + (size_t)sp * a.M * a.ldc;
@@ -447,10 +477,10 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
     const int col = col0 + wc * 64 + j * 16 + lr;
     const float bb = BIAS ? a.bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < RT; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = row0 + wr * 128 + i * 16 + lq * 4 + e;
+        const int row = row0 + arow + i * 16 + lq * 4 + e;
         float* dst = C + (size_t)row * a.ldc + col;
         const float v = acc[i][j][e] + bb;
         if (ACC) *dst += v; else *dst = v;
@@ -479,27 +509,46 @@ static bool gemm256_phased() {
   return !(e && e[0] == '0');
 }
 
+// rows of A per tile for (M, N, splits): 256, or 192 (phased 16x16 form only) where M % 256 != 0
+// or where its grid fills whole rounds of 256 workgroups better; 0 = neither fits
+int gemm256_tile_rows(int M, int N, int K, int splits) {
+  if (N % kBN || splits < 1 || K % splits) return 0;
+  auto fill = [&](int bm) {
+    if (M % bm) return -1.0;
+    const long wg = (long)(M / bm) * (N / kBN) * splits, rounds = (wg + 255) / 256;
+    return (double)wg / (rounds * 256);
+  };
+  const double f256 = fill(256), f192 = gemm256_phased() && gemm256_mfma(K / splits) != 32 ? fill(192) : -1.0;
+  if (f256 < 0 && f192 < 0) return 0;
+  return f192 > f256 + 1e-9 ? 192 : 256;
+}
+
 bool gemm256_ok(const GemmArgs& a) {
   if (a.onehot_ids || !a.A) return false;
-  if (a.M % kBM || a.N % kBN || a.splits < 1 || a.K % a.splits) return false;
+  if (a.N % kBN || a.splits < 1 || a.K % a.splits) return false;
   const int kper = a.K / a.splits;
   if (kper % kBK || a.lda % 8 || a.ldb % 8) return false;
   if (a.splits > 1 && (a.bias || a.accumulate || a.ldc != a.N)) return false;
   if (a.rowsumA && (a.bias || a.accumulate)) return false;
-  return true;
+  return gemm256_tile_rows(a.M, a.N, a.K, a.splits) != 0;
 }
 
 void gemm256(const GemmArgs& a, hipStream_t s) {
   if (!gemm256_ok(a)) throw std::runtime_error("gemm256: unsupported shape");
-  const int ntn = a.N / kBN, ntm = a.M / kBM, kper = a.K / a.splits;
-  const dim3 grid(ntn * ntm * a.splits), block(512);
+  const int kper = a.K / a.splits;
   const int form = gemm256_mfma(kper);
   const bool phased = gemm256_phased();
-#define GK_L(B_, A_, R_)                                                                                   \
-  do {                                                                                                     \
-    if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);           \
+  // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
+  const int bm = (form == 32 || !phased) ? 256 : gemm256_tile_rows(a.M, a.N, a.K, a.splits);
+  if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");
+  const int ntn = a.N / kBN, ntm = a.M / bm;
+  const dim3 grid(ntn * ntm * a.splits), block(512);
+#define GK_L(B_, A_, R_)                                                                                          \
+  do {                                                                                                            \
+    if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);    \
+    else if (phased && bm == 192) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);                  \
   } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate
     if (a.bias || a.accumulate) throw std::runtime_error("gemm256: row sums only without bias / accumulate");

@@ -346,6 +346,8 @@ bool gemm_library(const GemmArgs& a, hipStream_t s);
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
 bool gemm256_ok(const GemmArgs& a);
+// rows of A per gemm256 tile for (M, N, splits): 256 or 192 (the phased kernel), 0 = no fit
+int gemm256_tile_rows(int M, int N, int K, int splits);
 void gemm256(const GemmArgs& a, hipStream_t s);
 // out[m] = sum_k A[m][k] (bf16 A, fp32 sums; the bias gradient beside a GEMM without row sums)
 void rowsum_bf16(const u16* A, int lda, int M, int K, float* out, hipStream_t s);

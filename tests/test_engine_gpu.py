@@ -324,7 +324,7 @@ def test_generator_fp32_probs_match_fp64(precision, persist, atol, rtol):
     torch.testing.assert_close(probs[:N].cpu().double(), want, atol=atol, rtol=rtol)
 
 
-@pytest.mark.parametrize("E,H,group", [(256, 256, 1), (512, 512, 1), (128, 256, 4)])
+@pytest.mark.parametrize("E,H,group", [(256, 256, 1), (512, 512, 1), (256, 256, 4)])
 def test_dp_pipelined_tail_world1(E, H, group):
     """The bucketed, pipelined one-layer data-parallel tail (Trainer::record_dp_tail_l1: AR1 = W_hh0 ..
     dP beside the dW_fc K-slices, AR2 = the FC pair beside the embedding GEMMs and the first Adam
