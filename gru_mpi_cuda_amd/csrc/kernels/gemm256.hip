@@ -334,6 +334,7 @@ template <int BM, bool BIAS, bool ACC, bool RS>
 __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
   constexpr int RT = BM / 32, QR = RT / 2;          // row tiles per wave / per quadrant
   constexpr int NA = BM / 64, NB = 4;                // staging pieces per wave: A, B
+  static_assert(NB == 4, "the counted waits (vmwait256<4>) assume 4 B pieces per wave");
   constexpr int NA1 = (NA + 1) / 2;                  // A pieces in phase 1 (the rest in phase 2)
   constexpr int AOFF = 0, BOFF = BM * 64;            // element offsets inside a buffer
   __shared__ __attribute__((aligned(16))) u16 lds[2][(BM + 256) * 64];   // ONE array (§5 item 4a)
@@ -351,8 +352,11 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
 
   // staging: piece q of wave w covers image rows (NA w + q) * 8 .. + 7 of A, (NB w + q) * 8 .. of B
   const int srow = lane >> 3, sslot = lane & 7;
-  const u16* srcA[NA];
-  const u16* srcB[NB];
+  // (fixed-size arrays: a local array whose bound depends on BM, captured by the staging lambdas,
+  // made ROCm 7.2's host pass drop the kernel's launch stub without a diagnostic)
+  static_assert(NA <= 4, "A pieces per wave");
+  const u16* srcA[4];
+  const u16* srcB[4];
 #pragma unroll
   for (int q = 0; q < NA; ++q) {
     const int r = (NA * w + q) * 8 + srow;
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
   if (nk > 1) {
 #pragma unroll
     for (int q = 0; q < NB; ++q) stB(1, q);
-    vmwait256<NB>();
+    vmwait256<4>();
   } else {
     vmwait256<0>();
   }
@@ -449,7 +453,7 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
     GK_END();
     // phase 4: (A1, B0); the other half, then wait for k-tile kt + 1 (k-tile kt + 2's 4 B pieces
     // stay in flight)
-    if (kt + 2 < nk) { stB(kt + 2, 2); stB(kt + 2, 3); vmwait256<NB>(); } else { vmwait256<0>(); }
+    if (kt + 2 < nk) { stB(kt + 2, 2); stB(kt + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     GK_MMA(1, fb0, 0);
