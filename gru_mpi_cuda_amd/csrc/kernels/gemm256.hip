@@ -317,11 +317,13 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 // set, B0 / B1 16 each).  Buffer c = kt & 1 holds k-tile kt; halves 0/1 = A rows 0-127 / 128-255,
 // 2/3 = B rows 0-127 / 128-255.  A k-tile's B halves are last read in its phase 2, its A halves in
 // phase 3 (each wave retires its reads with lgkmcnt(0) before its MFMAs, and the phase's closing
-// barrier follows), so k-tile kt + 2 is staged into the same buffer as B0h in phase 3, B1h in
-// phase 4, A0h in phase 1 and A1h in phase 2 of k-tile kt + 1; phase 4 of k-tile u waits with
-// vmcnt(4) (k-tile u + 1 landed, u + 2's two B halves in flight) before its first barrier, so every
-// wave's k-tile u + 1 reads (phase 1 of u + 1, after that barrier and phase 4's closing one) see
-// all eight waves' DMA (RAW: wait, then barrier, then read).
+// barrier follows), so the whole of k-tile kt + 2 is staged into that buffer in phase 4, five phases
+// before its first read; phase 4 of k-tile u then waits with vmcnt(one k-tile of pieces) -- k-tile
+// u + 1 landed, u + 2 in flight -- before its first barrier, so every wave's k-tile u + 1 reads
+// (phase 1 of u + 1, after that barrier and phase 4's closing one) see all eight waves' DMA (RAW:
+// wait, then barrier, then read).  (A first form staged a quarter of a k-tile per phase, B halves
+// two k-tiles ahead and A halves one: 1253 TF at 8192^3 against 1292 for gemm256_kernel and 1591
+// for hipBLASLt, profiles/r5_gemm_phased_v1.jsonl -- its A pieces landed two phases before use.)
 template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // BM = 256 or 192 rows of A per tile (192: M = 3H products at 3H % 256 != 0 or whose 256-row grid
@@ -410,50 +412,42 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
                     __builtin_amdgcn_sched_barrier(0); }
 #define GK_END() { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); }
 
-  // prologue: k-tile 0 whole, k-tile 1's B pieces; wait for k-tile 0
+  // prologue: k-tiles 0 and 1 whole; wait for k-tile 0 (k-tile 1 stays in flight)
+  auto stage_all = [&](int kt) {
 #pragma unroll
-  for (int q = 0; q < NB; ++q) stB(0, q);
+    for (int q = 0; q < NB; ++q) stB(kt, q);
 #pragma unroll
-  for (int q = 0; q < NA; ++q) stA(0, q);
-  if (nk > 1) {
-#pragma unroll
-    for (int q = 0; q < NB; ++q) stB(1, q);
-    vmwait256<4>();
-  } else {
-    vmwait256<0>();
-  }
+    for (int q = 0; q < NA; ++q) stA(kt, q);
+  };
+  auto wait_ahead = [&]() {   // all but the NA + NB youngest pieces (one k-tile) landed
+    if constexpr (NA + NB == 8) vmwait256<8>(); else vmwait256<7>();
+  };
+  stage_all(0);
+  if (nk > 1) { stage_all(1); wait_ahead(); } else { vmwait256<0>(); }
   __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
     const int c = kt & 1;
-    // phase 1: (A0, B0); k-tile kt + 1's first A pieces
+    // phase 1: (A0, B0)
     GK_RA(c, 0); GK_RB(fb0, c, 0);
-    if (kt + 1 < nk) {
-#pragma unroll
-      for (int q = 0; q < NA1; ++q) stA(kt + 1, q);
-    }
     GK_SYNC();
     GK_MMA(0, fb0, 0);
     GK_RS(0);
     GK_END();
-    // phase 2: (A0, B1); the rest of k-tile kt + 1's A pieces
+    // phase 2: (A0, B1)
     GK_RB(fb1, c, 1);
-    if (kt + 1 < nk) {
-#pragma unroll
-      for (int q = NA1; q < NA; ++q) stA(kt + 1, q);
-    }
     GK_SYNC();
     GK_MMA(0, fb1, 1);
     GK_END();
-    // phase 3: (A1, B1); this buffer's B rows are free: half of k-tile kt + 2's B pieces
+    // phase 3: (A1, B1) -- the last reads of buffer c
     GK_RA(c, 1);
-    if (kt + 2 < nk) { stB(kt + 2, 0); stB(kt + 2, 1); }
     GK_SYNC();
     GK_MMA(1, fb1, 1);
     GK_RS(1);
     GK_END();
-    // phase 4: (A1, B0); the other half, then wait for k-tile kt + 1 (k-tile kt + 2's 4 B pieces
-    // stay in flight)
-    if (kt + 2 < nk) { stB(kt + 2, 2); stB(kt + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); }
+    // phase 4: (A1, B0); buffer c is free (every wave retired its phase-3 reads before that phase's
+    // closing barrier): all of k-tile kt + 2 goes out, five phases ahead of its first read; then wait
+    // for k-tile kt + 1 with k-tile kt + 2 still in flight
+    if (kt + 2 < nk) { stage_all(kt + 2); wait_ahead(); } else { vmwait256<0>(); }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     GK_MMA(1, fb0, 0);
