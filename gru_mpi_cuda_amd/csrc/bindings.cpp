@@ -254,7 +254,6 @@ PYBIND11_MODULE(_C, m) {
     py::dict d;
     d["fwd64"] = v.fwd64; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["dwfc_group"] = v.dwfc_group;
     d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring;
-    d["fwd_tag"] = v.fwd_tag;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -269,7 +268,6 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd16") v.bwd16 = x;
       else if (k == "bwd_xring") v.bwd_xring = x;
       else if (k == "fwd_xring") v.fwd_xring = x;
-      else if (k == "fwd_tag") v.fwd_tag = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }
   });
@@ -311,7 +309,7 @@ PYBIND11_MODULE(_C, m) {
     a.h0 = GP(const float, d, "h0");
     a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
     a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
-    a.xring = get<int>(d, "xring", 0); a.tag = get<int>(d, "tag", 0);
+    a.xring = get<int>(d, "xring", 0);
     a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
     if (!gru_fwd_seq_supported(a.H, a.Bp)) throw std::runtime_error("fwd_seq: shape not supported");
     gru_fwd_seq(a, S(s));

@@ -113,9 +113,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     }
   }
   size_t o_pP = seq_[0].fuse_p ? R((size_t)seq_[0].nrb * V * 3 * H * 4) : 0;
-  std::vector<size_t> o_fx(L, 0);
-  if (persist_fwd_)
-    for (int l = 0; l < L; ++l) o_fx[l] = R((size_t)kFxSlots * B * H * 2);
   // per-step backward on the split-K LDS kernel: partial tiles + monotonic arrival counters
   // (shared by all layers: their step kernels run one after another on one stream)
   int sk = 0;
@@ -134,9 +131,6 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   cnt_ = arena_.get<unsigned>(o_cnt); err_ = arena_.get<unsigned>(o_err); xbuf_ = arena_.get<u16>(o_x);
   slab_w_ = arena_.get<float>(o_sw); rs_w_ = arena_.get<float>(o_rw);
   slab_fc2_ = arena_.get<float>(o_sfc2); rs_fc2_ = arena_.get<float>(o_rfc2); slab_e_ = arena_.get<float>(o_se);
-  fx_.assign(L, nullptr);
-  if (persist_fwd_)
-    for (int l = 0; l < L; ++l) fx_[l] = arena_.get<u16>(o_fx[l]);
   for (int l = 0; l < L; ++l) {
     seq_[l].dWhh_part = seq_[l].fuse_w ? arena_.get<float>(o_pw[l]) : nullptr;
     seq_[l].HF = o_hf[l] ? arena_.get<u16>(o_hf[l]) : nullptr;   // zero-filled: HF[0] = h_init

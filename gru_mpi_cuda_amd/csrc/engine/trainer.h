@@ -236,10 +236,6 @@ class Trainer {
   // r/z rows from dGh^T, where they are identical (measured: profiles/r2_h2048_dgit_share_ab.jsonl)
   bool dgiT_share_ = false;
   u16* xbuf_ = nullptr;
-  // tagged forward exchange (SeqFwdArgs::tag): per layer a ring of kFxSlots slots of its own
-  static constexpr int kFxSlots = 8;
-  std::vector<u16*> fx_;
-  bool fwd_tag_on(int l) const;
   float *slab_w_ = nullptr, *rs_w_ = nullptr, *dP_part_ = nullptr;
   // dedicated split-K slabs whose reduce is deferred into the final multi-tensor reduce
   float *slab_fc2_ = nullptr, *rs_fc2_ = nullptr, *slab_e_ = nullptr;

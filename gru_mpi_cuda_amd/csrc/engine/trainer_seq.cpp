@@ -124,16 +124,6 @@ void Trainer::slab_job(SlabJobs& j, const float* src, int splits, long n, float*
   t.add(src, splits, n, dst);
 }
 
-// the tagged forward exchange (SeqFwdArgs::tag) for layer l: one-layer persistent forward launches
-// (not the two-layer wavefront) with a ring, whose layer runs the persistent 32- or 16-row backward
-// (it zeroes the ring for the next step's forward; the arena starts zeroed for the first)
-bool Trainer::fwd_tag_on(int l) const {
-  const StepLdsVariants& v = step_lds_variants();
-  const bool wave = fwd_wave_ && (l % 2 == 0 ? l + 1 < d_.L : true);
-  return v.fwd_tag && persist_fwd_ && !wave && v.fwd_xring >= 2 && v.fwd_xring <= kFxSlots &&
-         fx_[l] != nullptr && seq_[l].bwd;
-}
-
 void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
   const int H3 = 3 * H;
@@ -168,7 +158,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     else a.Gi = y.Gi;
     a.cnt = cnt_ + (size_t)l * fw; a.err = err_; a.allow_local = xcd_local_;
     a.xring = step_lds_variants().fwd_xring;
-    if (fwd_tag_on(l)) { a.tag = 1; a.xch = fx_[l]; }
     if (seq_[l].bwd) { a.zero_next = cnt_ + (size_t)(L + l) * fw; a.zero_words = fw; }
     a.T = T; a.Bp = B; a.H = H;
     if (carry_) a.h0 = y.HSf;   // carried state: HS[0] (bf16 copy read as the first MFMA operand)
@@ -286,10 +275,6 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_; a.allow_local = xcd_local_;
       if (persist_fwd_) { a.zero_next = cnt_ + (size_t)l * fw; a.zero_words = fw; }
-      if (fwd_tag_on(l)) {   // the next step's tagged forward ring starts zeroed
-        a.zero2 = reinterpret_cast<unsigned*>(fx_[l]);
-        a.zero2_words = (long)step_lds_variants().fwd_xring * B * H / 2;
-      }
       a.T = T; a.Bp = B; a.H = H;
       if (!persist_fwd_) fill_f32(reinterpret_cast<float*>(a.cnt), fw, 0.f, s);
       a.xring = step_lds_variants().bwd_xring;

@@ -21,7 +21,6 @@
 //     sums per row block are reduced by one small kernel afterwards (no float atomics).
 // Reference mapping: this is the whole per-char hot loop of /root/reference/namegensf.cu:661-872
 // (for all names at once), plus the BPTT half the reference does not have.
-#include <algorithm>
 #include "kernels.h"
 #include "mma_tile.h"
 #include "seq_sync.h"
@@ -37,17 +36,7 @@ namespace gk {
 // (Rejected and removed in round 4, history in docs/DESIGN.md §6.3: a table-free layer 0 computing
 // its P-table columns in every workgroup, layer 0's input projection in the post-publish slack, the
 // FC / softmax-xent pipeline inside the forward, and the saves issued inside the publish drain.)
-// TAG (round 5): the tagged exchange (SeqFwdArgs::tag).  Data h_u (u = 0..T-1) goes to slot u % xr
-// with every bf16 carrying p(u) = (u / xr + 1) & 1 in bit 14, which is 0 in every value |h| < 2
-// (sign, then the exponent's top bit): lap 0 writes 1 over the zeroed ring, lap k writes the
-// opposite of lap k - 1, whose data is what a reader finds before the new store lands.  Each
-// element validates itself (no store atomicity assumed beyond the dword), so the producer stores
-// and moves on -- no vmcnt(0) drain, no flag -- and a consumer wave loads its K-slice, checks every
-// element's bit against p(t - 1), re-loads the k-steps that are not all fresh, and clears the bit.
-// Write-after-read on the ring is safe for xr >= 2 by the argument above (a producer writes step t
-// after reading every producer's step t - 1, each written after its step t - 2 reads).  A
-// non-finite h (the step is garbage anyway) is sent as 0 with error bit 8 set.
-template <int NKW, int RS, bool TAG>
+template <int NKW, int RS>
 __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float part[8][6][256];
   // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
@@ -115,51 +104,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     if (t > 0 || a.h0) {
       // wave w's K-slice [k0, k0 + 32*NKW) is produced by unit tiles k0/16 .. k0/16 + 2*NKW - 1
       bf16x8 af[NKW][NR];
-      if (t > 0 && TAG) {
-        // tagged exchange: load, check every element's lap bit, re-load the stale k-steps
-        const size_t slot = ((size_t)((t - 1) % xr) * nrb + rbk) * nunit;
-        const unsigned want = (((t - 1) / xr + 1) & 1) ? 0x40004000u : 0u;
-        u32x4 raw[NKW][NR];
-        auto issue = [&](int kk) {
-          const int u = k0 + kk * 32 + lk;
-          const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
-#pragma unroll
-          for (int r = 0; r < NR; ++r)
-            raw[kk][r] = __builtin_amdgcn_raw_buffer_load_b128(rX, tb + (unsigned)((rt + r) * 16 * 16 * 2), 0, 16);
-        };
-#pragma unroll
-        for (int kk = 0; kk < NKW; ++kk) issue(kk);
-        unsigned pend = (1u << NKW) - 1u;
-        SpinBudget spin(a.err);
-        for (;;) {
-          unsigned stale = 0;
-#pragma unroll
-          for (int kk = 0; kk < NKW; ++kk) {
-            if (!((pend >> kk) & 1u)) continue;
-            unsigned x = 0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-              const u32x4 v = raw[kk][r] ^ want;
-              x |= v.x | v.y | v.z | v.w;
-            }
-            if (__any((x & 0x40004000u) != 0u)) stale |= 1u << kk;
-          }
-          pend = stale;
-          if (!pend) break;
-          __builtin_amdgcn_s_sleep(1);
-          if (spin.expired()) {
-            if (lane == 0) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-#pragma unroll
-          for (int kk = 0; kk < NKW; ++kk)
-            if ((pend >> kk) & 1u) issue(kk);
-        }
-#pragma unroll
-        for (int kk = 0; kk < NKW; ++kk)
-#pragma unroll
-          for (int r = 0; r < NR; ++r) af[kk][r] = __builtin_bit_cast(bf16x8, raw[kk][r] & 0xBFFFBFFFu);
-      } else if (t > 0) {
+      if (t > 0) {
         // h_t from the producers' exchange tiles (written at step t-1); unit u = k0 + 32kk + lk
         // lives in tile u/16 at column u%16
         const size_t slot = ((size_t)((t - 1) % xr) * nrb + rbk) * nunit;
@@ -211,28 +156,12 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
     const float n = tanhf_(gi[2] + r * gh[2]);
     const float h = n + z * (hp - n);
     hp = h;
-    u16 hb = f2bf(h);
-    if constexpr (TAG) {
-      if (!(fabsf(h) < 2.f)) {   // bit 14 would read as a tag: send 0, flag the step
-        hb = 0;
-        __hip_atomic_fetch_or(a.err, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    const u16 hb = f2bf(h);
     stg[row][col] = hb;
     stgT[col][row] = hb;
     __syncthreads();
     stamp(a.dbg, t, 3);
-    if (w == 0 && TAG) {
-      // publish the tagged tile: the store is the signal (no drain, no flag)
-      const unsigned m = ((t / xr + 1) & 1) ? 0x40004000u : 0u;
-      const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
-      const unsigned xo = (unsigned)((((size_t)(t % xr) * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
-      if (loc) st16_plain(rX, xo, v | m);
-      else st16_sc1(rX, xo, v | m);
-      stamp(a.dbg, t, 4);
-      *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
-      stamp(a.dbg, t, 5);
-    } else if (w == 0) {
+    if (w == 0) {
       // publish: the 32x16 bf16 tile (1 KB, whole lines of its own), 16 B per lane, write-through;
       // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
@@ -607,7 +536,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)(((lk >> 4) * 3 * 512 + lr * 16 + (lk & 15)) * 2);   // exchange lane offset
   zero_next_flags(a.zero_next, a.zero_words);
-  zero_next_flags(a.zero2, a.zero2_words);
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   // the saves of step t-1 are loaded during step t, right after its hand-off: in front of the
   // next poll they would delay it (vmcnt retires in order), and they have a whole step to land
@@ -827,29 +755,22 @@ static int fwd_rs(int H) { return H <= 512 ? 2 : 1; }
 bool gru_fwd_seq_supported(int H, int Bp) {
   if (Bp % 32) return false;
   const int rs = fwd_rs(H);
-  int cap = -1, cap_t = -1;
-#define X(HH, NK, RS)                                                         \
-  if (H == HH && rs == RS) {                                                  \
-    cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, false>);                 \
-    cap_t = resident_blocks(gru_fwd_seq_kernel<NK, RS, true>);                \
-  }
+  int cap = -1;
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS>);
   FWD_VARIANTS(X)
 #undef X
-  return std::min(cap, cap_t) >= (H / 16) * (Bp / 32);
+  return cap >= (H / 16) * (Bp / 32);
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
   if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
-  if (a.tag && a.xring < 2)
-    throw std::runtime_error("gru_fwd_seq: the tagged exchange needs a ring (xring >= 2)");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
-#define X(HH, NK, RS)                                                                           \
-  if (a.H == HH && rs == RS) {                                                                 \
-    if (a.tag) hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, true>), grid, block, 0, s, a);  \
-    else hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, false>), grid, block, 0, s, a);       \
-    return;                                                                                     \
+#define X(HH, NK, RS)                                                          \
+  if (a.H == HH && rs == RS) {                                                \
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS>), grid, block, 0, s, a);   \
+    return;                                                                    \
   }
   FWD_VARIANTS(X)
 #undef X

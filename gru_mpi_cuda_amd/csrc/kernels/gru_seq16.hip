@@ -65,7 +65,6 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
   const rsrc_t rX = make_rsrc(a.xbuf, (unsigned)((size_t)T * Bp * H3 * 2));
   const unsigned xlane = (unsigned)((lr * 32 + lk) * 2);   // fragment lane offset in a 1-KB gate block
   zero_next_flags(a.zero_next, a.zero_words);
-  zero_next_flags(a.zero2, a.zero2_words);
   const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
   float sv[6];
   int svid = 0;

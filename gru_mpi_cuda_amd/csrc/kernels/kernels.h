@@ -86,8 +86,6 @@ struct StepLdsVariants {
                          // slots instead of one per step (0); docs/DESIGN.md §3.1d
   int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
                          // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
-  int fwd_tag = 1;       // one-layer persistent forward: the tagged exchange (SeqFwdArgs::tag) in a
-                         // ring of its own, zeroed by the layer's persistent backward; 0 = epoch flags
 };
 // (Round 5 removed the measured-equal / marginal switches fwd_ns, fwd8, fwd64 = 2, fwd64_fused,
 // fwd64_all, bwd_sk_pf, bwd_sk_map and big_acq with the code only they reached; docs/DESIGN.md §7.)
@@ -129,11 +127,6 @@ struct SeqFwdArgs {
   unsigned long long* dbg = nullptr;   // diagnostic: [2 wgs][T][8] s_memrealtime stamps (nullable)
   int allow_local = 1;             // 0: never the L2-local hand-off (gru_seq.hip row_block_local)
   int xring = 0;                   // h exchange as a ring of xring slots (>= 2; 0 = one per step)
-  // 1: tagged exchange (gru_seq.hip, round 5) -- every bf16 of an exchange tile carries its lap
-  // parity in bit 14 (|h| < 2, so that bit is 0 in every finite h value): the data IS the flag, no
-  // drain + flag store on the producer, no flag round trip on the consumer.  Needs xring >= 2 and
-  // the ring's xring * Bp * H bf16 zeroed before the launch (SeqBwdArgs::zero2 does it).
-  int tag = 0;
   int T = 0, Bp = 0, H = 0;
 };
 // flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
@@ -174,8 +167,6 @@ struct SeqBwdArgs {
   unsigned* cnt = nullptr;
   unsigned* zero_next = nullptr;   // as SeqFwdArgs
   long zero_words = 0;
-  unsigned* zero2 = nullptr;       // a second block zeroed here: the next forward's tagged exchange ring
-  long zero2_words = 0;
   unsigned* err = nullptr;
   unsigned long long* dbg = nullptr;   // diagnostic stamps, as SeqFwdArgs::dbg
   int allow_local = 1;             // as SeqFwdArgs::allow_local
