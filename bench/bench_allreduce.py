@@ -10,12 +10,13 @@ prints one JSON line per size with time, algorithm bandwidth (bytes / time) and 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bench_allreduce.py
     python bench/bench_allreduce.py            # 1 GPU: a 1-rank communicator (plumbing / launch cost)
 
-The headline model's per-step gradient traffic is ~5.25 MB (dP in the W_ih0 slot, W_hh, biases,
-W_fc).  At world > 1 the one-layer step records it as the pipelined tail's two readiness buckets
-(Trainer::record_dp_tail_l1): AR1 = W_hh0, b_hh0, b_ih0, dP (4.6 MB, with the error word) beside
-the dW_fc K-slices, AR2 = the FC pair (0.5 MB) beside the embedding GEMMs and the first Adam launch;
-`--dp-pipeline 0` (bench.py) restores one collective after the backward.  The plan row below prints
-the exact collectives of the captured step at this world size.
+The headline model's per-step gradient traffic is one ~5.25 MB collective (dP in the W_ih0 slot,
+W_hh, biases, W_fc) after the backward.  `bench.py --dp-pipeline 1` records it instead as the
+pipelined tail's two readiness buckets (Trainer::record_dp_tail_l1: AR1 = W_hh0, b_hh0, b_ih0, dP,
+4.6 MB with the error word, beside the dW_fc K-slices; AR2 = the FC pair beside the embedding GEMMs
+and the first Adam launch) -- measured slower on a 1-rank communicator (graph cross-stream edges,
+profiles/r5_rccl_self_dp_pipeline1_timeline.txt), so it is opt-in.  The plan row below prints the
+exact collectives of the captured step at this world size.
 """
 from __future__ import annotations
 

@@ -55,10 +55,11 @@ class GRUConfig:
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
     shard_optim: bool = False   # data-parallel ZeRO-1 step: reduce-scatter the gradient, Adam on the
                                 # owned 1/world slice, all-gather the fp32 masters (Trainer::set_shard_optim)
-    dp_pipeline: int = -1       # one-layer data-parallel step: the bucketed, pipelined tail (three
-                                # readiness buckets, collectives beside the dW_fc / embedding GEMMs and
-                                # Adam; Trainer::record_dp_tail_l1).  -1 auto (on at world > 1), 0 one
-                                # collective after the backward, 1 always
+    dp_pipeline: int = -1       # one-layer data-parallel step: the bucketed, pipelined tail (two
+                                # collectives on a comm stream beside the dW_fc / embedding GEMMs and
+                                # a split Adam; Trainer::record_dp_tail_l1).  1 on; 0 and -1 (auto) one
+                                # collective after the backward -- the pipelined form measured slower
+                                # (graph cross-stream edges, profiles/r5_rccl_self_dp_pipeline1_timeline.txt)
     time_chunks: int = 4        # time-chunked side-stream pipelining inside one step
     overlap: bool = False       # True: chunked side-stream schedule; False: single stream built on
                                 # the persistent sequence kernels (faster on MI355X, profiles/)

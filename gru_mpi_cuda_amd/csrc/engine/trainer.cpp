@@ -710,7 +710,10 @@ bool Trainer::dp_pipe_on() const {
   if (!comm_ || overlap_ || shard_opt_ || d_.L != 1 || o_.clip > 0.f) return false;
   const int V = d_.V, E = d_.E, H = d_.H;
   if (V % 64 || E % 64 || H % 64 || !dP_inplace_) return false;
-  return dp_pipe_ == 1 || (dp_pipe_ == -1 && comm_->world() > 1);
+  // auto (-1) is OFF: on a 1-rank communicator the pipelined tail measured 0.2524 against 0.2215 ms per
+  // step -- every cross-stream edge of the captured graph opened a 5-10 us gap and the dW_fc K-slices
+  // did not start before AR1 had ended (profiles/r5_rccl_self_dp_pipeline{1,0}_timeline.txt)
+  return dp_pipe_ == 1;
 }
 
 long Trainer::group_end(int l) const {

@@ -317,13 +317,15 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 // set, B0 / B1 16 each).  Buffer c = kt & 1 holds k-tile kt; halves 0/1 = A rows 0-127 / 128-255,
 // 2/3 = B rows 0-127 / 128-255.  A k-tile's B halves are last read in its phase 2, its A halves in
 // phase 3 (each wave retires its reads with lgkmcnt(0) before its MFMAs, and the phase's closing
-// barrier follows), so the whole of k-tile kt + 2 is staged into that buffer in phase 4, five phases
-// before its first read; phase 4 of k-tile u then waits with vmcnt(one k-tile of pieces) -- k-tile
-// u + 1 landed, u + 2 in flight -- before its first barrier, so every wave's k-tile u + 1 reads
-// (phase 1 of u + 1, after that barrier and phase 4's closing one) see all eight waves' DMA (RAW:
-// wait, then barrier, then read).  (A first form staged a quarter of a k-tile per phase, B halves
-// two k-tiles ahead and A halves one: 1253 TF at 8192^3 against 1292 for gemm256_kernel and 1591
-// for hipBLASLt, profiles/r5_gemm_phased_v1.jsonl -- its A pieces landed two phases before use.)
+// barrier follows), so k-tile kt + 2's B pieces are staged into that buffer in phases 3 and 4 and
+// its A pieces in phases 1 and 2 of k-tile kt + 1; phase 4 of k-tile u waits with vmcnt(4) --
+// k-tile u + 1 landed, u + 2's B pieces in flight -- before its first barrier, so every wave's
+// k-tile u + 1 reads (phase 4's read of the next first B sub-tile comes after that barrier) see all
+// eight waves' DMA (RAW: wait, then barrier, then read).  Measured (profiles/r5_gemm_phased_v1/v2):
+// this spread staging against gemm256_kernel: h2048 dW_hh 4-way split 1234 vs 1124 TF, h1024 dW_ih
+// 909 vs 879 TF, but 1253 vs 1292 TF at 8192^3; the whole next-next k-tile staged in phase 4
+// instead (v2) lost everywhere (1051 TF at 8192^3).  gemm256() therefore takes the phased kernel for
+// the split-K / 192-row weight-gradient products and keeps gemm256_kernel for unsplit plain ones.
 template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // BM = 256 or 192 rows of A per tile (192: M = 3H products at 3H % 256 != 0 or whose 256-row grid
@@ -412,47 +414,49 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
                     __builtin_amdgcn_sched_barrier(0); }
 #define GK_END() { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); }
 
-  // prologue: k-tiles 0 and 1 whole; wait for k-tile 0 (k-tile 1 stays in flight)
-  auto stage_all = [&](int kt) {
+  // prologue: k-tile 0 whole, k-tile 1's B pieces; wait for k-tile 0, then read its first B sub-tile
 #pragma unroll
-    for (int q = 0; q < NB; ++q) stB(kt, q);
+  for (int q = 0; q < NB; ++q) stB(0, q);
 #pragma unroll
-    for (int q = 0; q < NA; ++q) stA(kt, q);
-  };
-  auto wait_ahead = [&]() {   // all but the NA + NB youngest pieces (one k-tile) landed
-    if constexpr (NA + NB == 8) vmwait256<8>(); else vmwait256<7>();
-  };
-  stage_all(0);
-  if (nk > 1) { stage_all(1); wait_ahead(); } else { vmwait256<0>(); }
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int c = kt & 1;
-    // phase 1: (A0, B0)
-    GK_RA(c, 0); GK_RB(fb0, c, 0);
-    GK_SYNC();
-    GK_MMA(0, fb0, 0);
-    GK_RS(0);
-    GK_END();
-    // phase 2: (A0, B1)
-    GK_RB(fb1, c, 1);
-    GK_SYNC();
-    GK_MMA(0, fb1, 1);
-    GK_END();
-    // phase 3: (A1, B1) -- the last reads of buffer c
-    GK_RA(c, 1);
-    GK_SYNC();
-    GK_MMA(1, fb1, 1);
-    GK_RS(1);
-    GK_END();
-    // phase 4: (A1, B0); buffer c is free (every wave retired its phase-3 reads before that phase's
-    // closing barrier): all of k-tile kt + 2 goes out, five phases ahead of its first read; then wait
-    // for k-tile kt + 1 with k-tile kt + 2 still in flight
-    if (kt + 2 < nk) { stage_all(kt + 2); wait_ahead(); } else { vmwait256<0>(); }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    GK_MMA(1, fb0, 0);
-    GK_END();
+  for (int q = 0; q < NA; ++q) stA(0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) stB(1, q);
+    vmwait256<4>();
+  } else {
+    vmwait256<0>();
   }
+  __builtin_amdgcn_s_barrier();
+  GK_RB(fb0, 0, 0);
+  // one k-tile in buffer C: B sub-tile SF is "first" (read in the previous tile's phase 4, register
+  // set F), SS "second" (set S).  Phases (A0,F) (A0,S) (A1,S) (A1,F): reads A0 8, S 4, A1 8 and, in
+  // phase 4, the NEXT k-tile's first sub-tile (= index SS) into set S, free since phase 3 -- at most
+  // 8 ds_read_b128 per phase.  The sets alternate roles with the k-tile parity (snake order).
+#define GK_TILE(kt_, C, F, SF, S, SS)                                                                     \
+  {                                                                                                      \
+    GK_RA(C, 0);                                                                                         \
+    if ((kt_) + 1 < nk) { _Pragma("unroll") for (int q = 0; q < NA1; ++q) stA((kt_) + 1, q); }          \
+    GK_SYNC(); GK_MMA(0, F, SF); GK_RS(0); GK_END();                                                     \
+    GK_RB(S, C, SS);                                                                                     \
+    if ((kt_) + 1 < nk) { _Pragma("unroll") for (int q = NA1; q < NA; ++q) stA((kt_) + 1, q); }         \
+    GK_SYNC(); GK_MMA(0, S, SS); GK_END();                                                               \
+    GK_RA(C, 1);                                                                                         \
+    if ((kt_) + 2 < nk) { stB((kt_) + 2, 0); stB((kt_) + 2, 1); }                                        \
+    GK_SYNC(); GK_MMA(1, S, SS); GK_RS(1); GK_END();                                                     \
+    if ((kt_) + 2 < nk) { stB((kt_) + 2, 2); stB((kt_) + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); } \
+    __builtin_amdgcn_s_barrier();                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                   \
+    if ((kt_) + 1 < nk) GK_RB(S, (C) ^ 1, SS);                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                                   \
+    GK_MMA(1, F, SF); GK_END();                                                                          \
+  }
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    GK_TILE(kt, 0, fb0, 0, fb1, 1);       // even k-tile: first B sub-tile 0 (in fb0)
+    GK_TILE(kt + 1, 1, fb1, 1, fb0, 0);   // odd k-tile: first B sub-tile 1 (in fb1, read above)
+  }
+  if (kt < nk) GK_TILE(kt, 0, fb0, 0, fb1, 1);
+#undef GK_TILE
 #undef GK_RA
 #undef GK_RB
 #undef GK_MMA
@@ -501,14 +505,17 @@ static int gemm256_mfma(int kper) {
   if (e && e[0]) return std::atoi(e);
   return kper <= 256 ? 32 : 16;
 }
-// 1: the phased pipeline (gemm256p_kernel) for the 16x16x32 form; GK_GEMM256_PHASED=0 keeps gemm256_kernel
-static bool gemm256_phased() {
+// The phased pipeline (gemm256p_kernel) for the 16x16x32 form: GK_GEMM256_PHASED=1 always, =0 never;
+// unset: for the split-K weight-gradient products and wherever 192-row tiles fill better (where it
+// measured faster), gemm256_kernel for unsplit 256-row plain products (where that one did)
+static int gemm256_phased_mode() {
   const char* e = std::getenv("GK_GEMM256_PHASED");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return 0;
+  if (e && e[0] == '1') return 1;
+  return -1;
 }
+static bool gemm256_phased() { return gemm256_phased_mode() != 0; }
 
-// rows of A per tile for (M, N, splits): 256, or 192 (phased 16x16 form only) where M % 256 != 0
-// or where its grid fills whole rounds of 256 workgroups better; 0 = neither fits
 int gemm256_tile_rows(int M, int N, int K, int splits) {
   if (N % kBN || splits < 1 || K % splits) return 0;
   auto fill = [&](int bm) {
@@ -535,9 +542,11 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   if (!gemm256_ok(a)) throw std::runtime_error("gemm256: unsupported shape");
   const int kper = a.K / a.splits;
   const int form = gemm256_mfma(kper);
-  const bool phased = gemm256_phased();
+  const int mode = gemm256_phased_mode();
+  const int bm_best = gemm256_tile_rows(a.M, a.N, a.K, a.splits);
+  const bool phased = mode == 1 || (mode == -1 && (a.splits > 1 || a.rowsumA || bm_best == 192));
   // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
-  const int bm = (form == 32 || !phased) ? 256 : gemm256_tile_rows(a.M, a.N, a.K, a.splits);
+  const int bm = (form == 32 || !phased) ? 256 : bm_best;
   if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");
   const int ntn = a.N / kBN, ntm = a.M / bm;
   const dim3 grid(ntn * ntm * a.splits), block(512);

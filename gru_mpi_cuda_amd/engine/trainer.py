@@ -292,7 +292,7 @@ class CpuTrainer:
         """CPU twin of Trainer::dp_pipe_on (one-layer data-parallel pipelined tail)."""
         c = self.cfg
         return (self.ctx.world > 1 and c.layers == 1 and self.shard is None and c.clip_norm <= 0
-                and c.dp_pipeline in (-1, 1))
+                and c.dp_pipeline == 1)
 
     def allreduce_grads(self) -> None:
         import torch.distributed as dist

@@ -4,6 +4,9 @@ path = sys.argv[1]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 if "--all" in sys.argv:   # whole trace (e.g. generation, no optimiser marker)
     seg = rows
+elif "--prologue" in sys.argv:   # one step = from the next-to-last prologue launch to the last one
+    marks = [i for i, r in enumerate(rows) if "gemm_small_prep" in r["Kernel_Name"]]
+    seg = rows[marks[-2]:marks[-1]]
 else:
     marks = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"] or "tail_kernel" in r["Kernel_Name"]]
     a, b = marks[-2], marks[-1]

@@ -110,7 +110,7 @@ def _pipe_worker(rank, world, port, outdir, steps, pipe):
     ctx = gdist.init(use_gpu=False)
     cfg = GRUConfig(vocab=256, embed=16, hidden=24, layers=1, batch=8, seq=6, lr=1e-2, dp_pipeline=pipe)
     tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1))
-    assert tr._pipelined() == (world > 1 and pipe != 0)
+    assert tr._pipelined() == (world > 1 and pipe == 1)
     ds = NameStream(cfg.batch, cfg.seq, seed=5)
     per = cfg.batch // world
     for _ in range(steps):

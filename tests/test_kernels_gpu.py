@@ -400,7 +400,7 @@ def test_reduce_slabs_cast(ext, R, C, splits):
     (512, 256, 4096, 8, False, False, 64, True), (2304, 1280, 576, 1, True, True, 32, False),
     (1536, 512, 8192, 4, False, False, 0, True), (512, 768, 1024, 1, False, False, 0, True),
     (256, 512, 128, 1, False, False, 0, True), (512, 512, 192, 1, True, False, 0, False)])
-@pytest.mark.parametrize("mfma", ["16", "16legacy", "32"])
+@pytest.mark.parametrize("mfma", ["16", "16auto", "16legacy", "32"])
 def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, rowsum, mfma):
     """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
     operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
@@ -409,7 +409,10 @@ def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, r
     v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32).  K = 64 and odd k-tile counts cover the phased
     pipeline's prologue / drain paths."""
     monkeypatch.setenv("GK_GEMM256_MFMA", mfma[:2])
-    monkeypatch.setenv("GK_GEMM256_PHASED", "0" if mfma == "16legacy" else "1")
+    if mfma == "16auto":
+        monkeypatch.delenv("GK_GEMM256_PHASED", raising=False)
+    else:
+        monkeypatch.setenv("GK_GEMM256_PHASED", "0" if mfma == "16legacy" else "1")
     lda = K + lda_pad
     Af = bf(rnd(M, lda, seed=4))
     A, B = Af[:, :K], bf(rnd(N, K, seed=5) + 0.1 * torch.arange(K, device=DEV) / K)

@@ -154,9 +154,9 @@ def test_dp_h512_on_gpus_equals_one_gpu(tmp_path, n):
 @needs2
 @pytest.mark.parametrize("pipe", [1, 0])
 def test_dp_h512_tail_modes_equal_one_gpu(tmp_path, pipe):
-    """Both one-layer data-parallel tails at world 2: the bucketed, pipelined one (three readiness
-    buckets, the default at world > 1; Trainer::record_dp_tail_l1) and the single collective after
-    the backward, each equal to one GPU on the whole batch."""
+    """Both one-layer data-parallel tails at world 2: the bucketed, pipelined one (readiness buckets on a
+    comm stream, opt-in; Trainer::record_dp_tail_l1) and the single collective after the backward (the
+    default), each equal to one GPU on the whole batch."""
     _compare_dp(tmp_path, 2, dict(H512_CFG, dp_pipeline=pipe), 2e-4)
 
 
