@@ -33,9 +33,13 @@ per_char = np.array([w0[t + 1][0] - w0[t][0] for t in range(1, ML - 1)])
 out = {"N": N, "model": f"L={cfg.layers} H={cfg.hidden}", "us_per_char": round(float(per_char.mean()), 2),
        "phase_us": {f"{names[k - 1]} -> {names[k]}": round(float(diffs[:, k - 1].mean()), 2) for k in range(1, 8)},
        "tail_us (logits published -> next char start)": round(float(np.mean([w0[t + 1][0] - w0[t][7] for t in range(1, ML - 1)])), 2),
-       "sampling_us": {"logits seen -> staged": round(float(np.mean([w0[t][8] - w0[t][1] for t in range(1, ML)])), 2),
-                       "staged -> first name": round(float(np.mean([w0[t][9] - w0[t][8] for t in range(1, ML)])), 2),
-                       "first name -> wave 0 done": round(float(np.mean([w0[t][10] - w0[t][9] for t in range(1, ML)])), 2),
-                       "wave 0 done -> sampled (barrier)": round(float(np.mean([w0[t][2] - w0[t][10] for t in range(1, ML)])), 2)},
+       "sampling_us": ({"logits seen -> staged": round(float(np.mean([w0[t][8] - w0[t][1] for t in range(1, ML)])), 2),
+                        "staged -> first name": round(float(np.mean([w0[t][9] - w0[t][8] for t in range(1, ML)])), 2),
+                        "first name -> wave 0 done": round(float(np.mean([w0[t][10] - w0[t][9] for t in range(1, ML)])), 2),
+                        "wave 0 done -> sampled (barrier)": round(float(np.mean([w0[t][2] - w0[t][10] for t in range(1, ML)])), 2)}
+                       if N <= 16 else   # distributed sampling: workgroup 0 samples name 0, then reads all ids
+                       {"logits seen -> own name sampled": round(float(np.mean([w0[t][9] - w0[t][1] for t in range(1, ML)])), 2),
+                        "own name sampled -> all ids seen": round(float(np.mean([w0[t][10] - w0[t][9] for t in range(1, ML)])), 2),
+                        "ids seen -> sampled (barrier)": round(float(np.mean([w0[t][2] - w0[t][10] for t in range(1, ML)])), 2)}),
        "error_word": int(g.g.read_error())}
 print(json.dumps(out))

@@ -71,11 +71,13 @@ __global__ void __launch_bounds__(512, 1) probe_kernel(Args a) {
     if (tid < 64) {
       // per-producer epoch flags (own 64-B line each), as in the recurrences: lanes 0-31 wait for
       // the 32 workgroups of this XCD, lanes 32-63 for the partner XCD's when remote bytes flow
-      if (tid == 0) __hip_atomic_store(a.flags + (size_t)b * 16, (unsigned)(s + 1), __ATOMIC_RELEASE,
+      // relaxed (sc1) stores and polls after the vmcnt(0) drain above, as the recurrences publish:
+      // release / acquire atomics here would add an L2 writeback and invalidate to every step
+      if (tid == 0) __hip_atomic_store(a.flags + (size_t)b * 16, (unsigned)(s + 1), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
       const unsigned src = (tid < 32 ? xcd : (r.remote_v4 ? (xcd ^ 4u) : xcd)) + 8u * (tid & 31u);
       unsigned spins = 0;
-      while (!__all(__hip_atomic_load(a.flags + (size_t)src * 16, __ATOMIC_ACQUIRE,
+      while (!__all(__hip_atomic_load(a.flags + (size_t)src * 16, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(s + 1))) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 22)) {   // bounded: a non-co-resident grid drains instead of hanging
