@@ -15,15 +15,21 @@
 //     are H/32 contiguous floats per name (float4 loads). The 8 wave partials of a 16 x 16
 //     (rows x names) tile meet in LDS and are summed in wave order.
 //   * Per char t:
-//       - Sample char t-1 from the logits of all 256 workgroups. Every workgroup does this
-//         redundantly and identically; it needs the id for layer 0's input.
+//       - Sample char t-1 from the logits of all 256 workgroups. Up to 16 names every workgroup
+//         does this redundantly and identically (it needs the ids for layer 0's input). Above 16
+//         names workgroup n samples name n alone and publishes id | alive << 16, and every
+//         workgroup reads the N ids back: one more hand-off of a word per name, instead of N / 8
+//         sequential samples per wave in every workgroup (11.5 us per char at 64 names).
 //       - Layer 0: gi = P[id] (the workgroup's slice of the fp32 table, in LDS), then the gates.
 //       - Each layer l >= 1: gi_l = h_{l-1}(t) W_ih_l^T + b_ih_l, then the gates.
-//       - FC: logits = h_{L-1}(t) W_fc^T + b_fc.
+//       - FC: logits = h_{L-1}(t) W_fc^T + b_fc, on the VALU: a workgroup has VR = V / 256 <= 2
+//         rows, which an MFMA tile would compute as 16.
 //     The recurrent products gh_l = h_l(t) W_hh_l^T + b_hh_l are only needed by the next char.
 //     They reuse the x registers of the product that consumes h_l(t) anyway (gi_{l+1}, or the
 //     logits), after that product's publish, so every exchanged state is read once per char and
-//     the gh MFMAs overlap the next hand-off.  Padded names are neither loaded nor sampled.
+//     the gh MFMAs overlap the next hand-off.  Padded names are neither loaded nor sampled.  With
+//     several name tiles the next tile's x loads are issued before the partial-sum barriers
+//     (lds_barrier: no vmcnt drain), so their latency hides behind the cross-wave sums.
 //     That is L + 1 hand-offs per char, each an all-to-all of tiny slices (U or VR floats per
 //     name per producer). A producer's wave 0 publishes them with write-through (sc1) stores,
 //     drains them (vmcnt(0)) and stores its epoch flag. A consumer wave polls only the 32
@@ -53,7 +59,8 @@ constexpr int kG = 256;        // workgroups
 constexpr int kNmax = 64;      // names per launch
 constexpr int kFS = 16;        // flag stride in uints (own 64-B line)
 constexpr int kVmax = 512;     // V = 256 or 512 (the sampler's instances); LDS: sP is V x 3U floats
-constexpr int kLgLds = 64 * 256;   // logits staged through LDS up to names x V = 16 K floats
+constexpr int kDistN = 16;    // more names than this: distributed sampling (workgroup n samples name n)
+constexpr int kLgLds = kDistN * kVmax;   // redundant sampling stages names x V <= 8 K floats in LDS
 constexpr unsigned kSpin = 1u << 21;   // x s_sleep(1) polls: ~0.3 s
 constexpr unsigned kErrBit = 32u;
 }
@@ -118,7 +125,53 @@ DEV f32x4 tile_mm(AVal&& aval, const float (&x)[KJ]) {
   return a0 + a1;
 }
 
+// both products of one name tile from the same x (o0: A values av0, o1: av1 when TWO), and, when
+// pf, the next name tile's x loaded in place b128 by b128 as soon as the MFMAs of the current
+// one have consumed each piece (a rolling prefetch: its latency hides behind the remaining MFMAs
+// with no second x register set)
+template <int KJ, bool TWO, class A0, class A1>
+DEV void tile_mm2(A0&& av0, A1&& av1, float (&x)[KJ], f32x4& o0, f32x4& o1, bool pf, __amdgpu_buffer_rsrc_t r,
+                  unsigned off, bool valid) {
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;   // TWO: a0 accumulates o0, a1 o1 (alternating chains)
+#pragma unroll
+  for (int j = 0; j < KJ; j += 4) {
+    if constexpr (TWO) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0(j + e), x[j + e], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1(j + e), x[j + e], a1, 0, 0, 0);
+      }
+    } else {
+      a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0(j), x[j], a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0(j + 1), x[j + 1], a1, 0, 0, 0);
+      a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0(j + 2), x[j + 2], a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0(j + 3), x[j + 3], a1, 0, 0, 0);
+    }
+    if (pf) {
+      pu32x4 v = {0u, 0u, 0u, 0u};
+      if (valid) v = __builtin_amdgcn_raw_buffer_load_b128(r, off + j * 4, 0, 0);
+      x[j] = __uint_as_float(v.x); x[j + 1] = __uint_as_float(v.y);
+      x[j + 2] = __uint_as_float(v.z); x[j + 3] = __uint_as_float(v.w);
+    }
+  }
+  if constexpr (TWO) { o0 = a0; o1 = a1; }
+  else o0 = a0 + a1;
+}
+
 DEV float sig_ieee(float x) { return 1.f / (1.f + expf(-x)); }
+// a value the compiler cannot hoist out of the char loop: the per-char address math of the sampler
+// otherwise becomes loop-invariant VGPRs that the weight-resident register budget spills to scratch
+// (a scratch reload on the hand-off's critical path)
+DEV int opaque_s(int v) {   // wave-uniform values
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+DEV int lane_now() {   // the lane id, recomputed where it is used
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 
 template <int V_> struct ic { static constexpr int value = V_; };
 template <int B_, int E_, class F> DEV void static_for(F&& f) {
@@ -133,7 +186,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   const int V = a.V, VR = V / kG, N = a.N, Np = (N + 15) & ~15, nnt = Np / 16, ML = a.ML;
 
   __shared__ float sP[kVmax * R3];            // P[v][g H + b U + u] -> sP[v][g U + u]
-  __shared__ float red[2][8][256];            // wave partials of two tiles
+  __shared__ float red[kNmax / 16][2][8][256];   // wave partials of two products, per name tile
   __shared__ float sgh[L][16][kNmax];         // gh rows (incl. b_hh) x names
   __shared__ float sgi[16][kNmax];            // gi rows (incl. b_ih) / logits
   __shared__ float sh[L][kNmax][U];           // own units' hidden states
@@ -144,14 +197,17 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   __shared__ __attribute__((aligned(16))) float sLG[kLgLds];   // staged logits of the last char
   __shared__ float sRf[kNmax];
 
-  // one slot per char (no reuse inside a launch: see load_x), X_l[t][name][H] then LG[t][name][V]
-  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * ML * kNmax * H + (size_t)ML * kNmax * V) * 4));
+  // one slot per char (no reuse inside a launch: see load_x), X_l[t][name][H], LG[t][name][V], then
+  // (distributed sampling) ID[t][name] = id | alive-after << 16
+  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * ML * kNmax * H + (size_t)ML * kNmax * (V + 1)) * 4));
   const unsigned lg0 = (unsigned)((size_t)L * ML * kNmax * H * 4);
+  const unsigned id0 = lg0 + (unsigned)((size_t)ML * kNmax * V * 4);
+  const bool dist = N > kDistN;   // flag kinds: 0..L-1 layer states, L logits, L + 1 sampled ids
   auto xoff = [&](int l, int t, int n, int col) -> unsigned {
     return (unsigned)((((size_t)(l * ML + t) * kNmax + n) * H + col) * 4);
   };
   unsigned* flags = a.sync;
-  unsigned* done = a.sync + (size_t)(L + 1) * kG * kFS;
+  unsigned* done = a.sync + (size_t)(L + 2) * kG * kFS;
   auto publish_flag = [&](int kind, int t) {   // wave 0, after its payload stores
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
@@ -189,23 +245,33 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   }
   for (int i = tid; i < L * kNmax * U; i += 512) (&sh[0][0][0])[i] = 0.f;
   if (tid < kNmax) { sid[tid] = a.sos; sal[tid] = tid < N ? 1 : 0; }
-  if (b == 0)
-    for (int i = tid; i < N * (ML + 1); i += 512) a.out[i] = 0;
+  if (dist ? b < N : b == 0)   // each output row has one writer: its sampler (every row: workgroup 0)
+    for (int i = tid; i < (dist ? ML + 1 : N * (ML + 1)); i += 512) a.out[(dist ? (size_t)b * (ML + 1) : 0) + i] = 0;
   __syncthreads();
 
   // cross-wave sum of tile partials -> dst[row][name tile nt] (+ bias), rows < nrows
-  auto reduce_to = [&](float (*dst)[kNmax], int slot, int nt, const float* bias, int nrows) {
-    if (tid < 256) {
-      const int row = tid >> 4, n = tid & 15;
-      float s = red[slot][0][tid];
+  // (thread i < 256 of the caller's range: element i of the tile)
+  auto reduce_el = [&](float (*dst)[kNmax], int slot, int nt, const float* bias, int nrows, int i) {
+    const int row = i >> 4, n = i & 15;
+    float s = red[nt][slot][0][i];
 #pragma unroll
-      for (int k = 1; k < 8; ++k) s += red[slot][k][tid];
-      if (row < nrows) dst[row][nt * 16 + n] = s + bias[row];
-    }
+    for (int k = 1; k < 8; ++k) s += red[nt][slot][k][i];
+    if (row < nrows) dst[row][nt * 16 + n] = s + bias[row];
   };
-  auto stash = [&](int slot, const f32x4& acc) {
+  // the FC rows' partials: wave w, quarter q4 of its K-slice -> red[0][w][(4 q4 + r) 16 + name]; the
+  // sum runs over the 8 waves and the 4 quarters
+  auto reduce_fc_el = [&](float (*dst)[kNmax], int nt, int i) {   // i < 16 VR
+    const int row = i >> 4, n = i & 15;
+    float s = 0.f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[slot][w][(4 * q4 + r) * 16 + fr] = acc[r];
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += red[nt][0][k][(4 * q + row) * 16 + n];
+    dst[row][nt * 16 + n] = s + sbf[row];
+  };
+  auto stash = [&](int nt, int slot, const f32x4& acc) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[nt][slot][w][(4 * q4 + r) * 16 + fr] = acc[r];
   };
   // gates of layer l for all names -> sh[l], then wave 0 publishes h_l(t) and its flag
   auto gates_publish = [&](int l, int t) {
@@ -259,25 +325,67 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   auto product = [&](auto ta_tag, auto src_tag, int t, float (*dst)[kNmax], const float* bias, int nrows, int sk) {
     constexpr int TA = decltype(ta_tag)::value, SRC = decltype(src_tag)::value;   // TA = NT: the FC rows
     const int kw0 = w * KW + q4 * KJ;
-    auto aval = [&](int j) -> float {
-      if constexpr (TA == NT) return fr < VR ? sWf[fr < VR ? fr : 0][kw0 + j] : 0.f;
-      else return Wr[TA][j];
-    };
+    pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
+    stampk(t, sk);
+    load_x<KJ>(xr, xoff(SRC, t, fr, kw0), fr < N, xk);
+    // several name tiles: gh here from the same x (re-reading it after the publish cost more)
+    const bool gh = nnt > 1 && t + 1 < ML;
+    auto whh = [&](int j) { return Wr[SRC][j]; };
+    // every tile's MFMAs back to back (each tile's partials in their own LDS slots), the next tile's
+    // x rolling in behind them; one barrier pair per product for all tiles
     for (int nt = 0; nt < nnt; ++nt) {
-      if (nt == 0) {
-        pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
-        stampk(t, sk);
+      // (the last tile's x stays for product_gh).  Without the register room for the in-place
+      // prefetch (resident weights NT x KJ > 80 VGPRs: it spilled) the next tile loads after these MFMAs.
+      constexpr bool kRollPF = NT * KJ <= 80;
+      const bool pf = kRollPF && nt + 1 < nnt;
+      const unsigned noff = xoff(SRC, t, (nt + 1) * 16 + fr, kw0);
+      const bool nvalid = (nt + 1) * 16 + fr < N;
+      f32x4 o0, o1;
+      if constexpr (TA == NT) {
+        // the VR <= 2 FC rows on the VALU (an MFMA tile would compute 16 rows for them): KJ fp32
+        // FMAs per row from the LDS copy, the sum over quarters and waves in reduce_fc_el
+        float p0 = 0.f, p1 = 0.f;
+        auto dot = [&](const float* wr, float& p) {
+#pragma unroll
+          for (int j = 0; j < KJ; j += 8) {
+            const float4 u = *reinterpret_cast<const float4*>(wr + j);
+            const float4 v = *reinterpret_cast<const float4*>(wr + j + 4);
+            p = fmaf(u.x, xk[j], p); p = fmaf(u.y, xk[j + 1], p);
+            p = fmaf(u.z, xk[j + 2], p); p = fmaf(u.w, xk[j + 3], p);
+            p = fmaf(v.x, xk[j + 4], p); p = fmaf(v.y, xk[j + 5], p);
+            p = fmaf(v.z, xk[j + 6], p); p = fmaf(v.w, xk[j + 7], p);
+          }
+        };
+        dot(&sWf[0][kw0], p0);
+        if (VR > 1) dot(&sWf[1][kw0], p1);
+        red[nt][0][w][(4 * q4) * 16 + fr] = p0;
+        red[nt][0][w][(4 * q4 + 1) * 16 + fr] = p1;
+        if (gh) {
+          tile_mm2<KJ, false>(whh, whh, xk, o1, o0, pf, xr, noff, nvalid);
+          stash(nt, 1, o1);
+        } else if (pf) {
+          load_x<KJ>(xr, noff, nvalid, xk);
+        }
+      } else {
+        auto wta = [&](int j) { return Wr[TA][j]; };
+        if (gh) tile_mm2<KJ, true>(wta, whh, xk, o0, o1, pf, xr, noff, nvalid);
+        else tile_mm2<KJ, false>(wta, wta, xk, o0, o1, pf, xr, noff, nvalid);
+        stash(nt, 0, o0);
+        if (gh) stash(nt, 1, o1);
       }
-      load_x<KJ>(xr, xoff(SRC, t, nt * 16 + fr, kw0), nt * 16 + fr < N, xk);
-      stash(0, tile_mm<KJ>(aval, xk));
-      // several name tiles: gh here from the same x (re-reading it after the publish cost more)
-      const bool gh = nnt > 1 && t + 1 < ML;
-      if (gh) stash(1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
-      __syncthreads();
-      reduce_to(dst, 0, nt, bias, nrows);
-      if (gh) reduce_to(sgh[SRC], 1, nt, sbh[SRC], R3);
-      __syncthreads();
+      if (!pf && nt + 1 < nnt) {   // (pf: the next tile's x is already in flight)
+        __builtin_amdgcn_sched_barrier(0);   // not hoisted above the MFMAs: one x set live
+        load_x<KJ>(xr, noff, nvalid, xk);
+      }
     }
+    lds_barrier();
+    for (int i = tid; i < nnt * 256; i += 512) {
+      const int nt = i >> 8, e = i & 255;
+      if constexpr (TA == NT) { if (e < 16 * nrows) reduce_fc_el(dst, nt, e); }
+      else reduce_el(dst, 0, nt, bias, nrows, e);
+      if (gh) reduce_el(sgh[SRC], 1, nt, sbh[SRC], R3, e);
+    }
+    lds_barrier();
   };
   // gh_src of the next char from the same h_src(t), after this phase's publish: with one name tile
   // its MFMAs run while the next hand-off is in flight instead of before the publish (x still in
@@ -285,52 +393,62 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   auto product_gh = [&](auto src_tag, int t) {
     constexpr int SRC = decltype(src_tag)::value;
     if (t + 1 >= ML || nnt > 1) return;   // (several name tiles: done inside product)
-    stash(1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
-    __syncthreads();
-    reduce_to(sgh[SRC], 1, 0, sbh[SRC], R3);
-    __syncthreads();
+    stash(0, 1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
+    lds_barrier();
+    if (tid < 256) reduce_el(sgh[SRC], 1, 0, sbh[SRC], R3, tid);
+    lds_barrier();
+  };
+
+  // one name's sample by one wave: logits from LDS (staged) or straight from the exchange
+  auto sample_name = [&](int n, int t, bool staged, float rnd) -> int {
+    const int per = V / 64;
+    const unsigned base = lg0 + (unsigned)(((size_t)(t - 1) * kNmax + n) * V + lane * per) * 4;
+    float* prow = (a.probs && t == ML && (dist || b == 0)) ? a.probs + (size_t)opaque_s(n) * V : nullptr;
+    // the sampler instantiated for exactly V / 64 values per lane: a 16-wide instance runs all 16
+    // IEEE expf / divides as selects (2.9 us per name and wave, probe_gen_persist.py)
+    auto sample = [&](auto per_tag) {
+      constexpr int PER = decltype(per_tag)::value;
+      float xv[PER];
+      if (staged) {
+#pragma unroll
+        for (int e = 0; e < PER; ++e) xv[e] = sLG[n * V + lane * PER + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < PER; e += 4) {
+          const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, base + 4 * e, 0, 0);
+          xv[e] = __uint_as_float(v.x); xv[e + 1] = __uint_as_float(v.y);
+          xv[e + 2] = __uint_as_float(v.z); xv[e + 3] = __uint_as_float(v.w);
+        }
+      }
+      return softmax_sample_wave(xv, PER, V, rnd, prow);
+    };
+    return per == 4 ? sample(ic<4>{}) : sample(ic<8>{});
   };
 
   for (int t = 0; t <= ML; ++t) {
-    if (t == ML && b != 0) break;   // only workgroup 0 samples the last char
+    // the last char is only sampled (workgroup 0 for every name, or each name's own sampler)
+    if (t == ML && (dist ? b >= N : b != 0)) break;
     stampk(t, 0);
     // ---- sample char t-1 from the logits of every workgroup
-    if (t > 0) {
+    if (t > 0 && !dist) {   // every workgroup samples every name, redundantly and identically
       if (w == 0) pwait(flags, L, 0, kG, (unsigned)t, a.err);
       __syncthreads();
       stampk(t, 1);
-      const int per = V / 64;
       const unsigned lgt = lg0 + (unsigned)((size_t)(t - 1) * kNmax * V * 4);
-      const bool staged = N * V <= kLgLds;
       if (tid < N) sRf[tid] = a.rf[(size_t)tid * ML + (t - 1)];   // this char's uniforms, loaded together
-      if (staged) {   // every name's logits into LDS with all loads in flight: one memory round trip
-        for (int i = tid; i < N * V / 4; i += 512) {
-          const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
-          sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
-          sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
-        }
+      // every name's logits into LDS with all loads in flight: one memory round trip
+      for (int i = tid; i < N * V / 4; i += 512) {
+        const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
+        sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
+        sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
       }
       __syncthreads();
       stampk(t, 8);
       for (int n = w; n < N; n += 8) {   // real names only: a padded row keeps sid = sos
-        const float rnd = sRf[n];
-        const unsigned base = lgt + (unsigned)(n * V + lane * per) * 4;
-        float* prow = (b == 0 && a.probs && t == ML) ? a.probs + (size_t)n * V : nullptr;
-        // the sampler instantiated for exactly V / 64 values per lane: a 16-wide instance runs
-        // all 16 IEEE expf / divides as selects (2.9 us per name and wave, probe_gen_persist.py)
-        auto sample = [&](auto per_tag) {
-          constexpr int PER = decltype(per_tag)::value;
-          float xv[PER];
-#pragma unroll
-          for (int e = 0; e < PER; ++e)
-            xv[e] = staged ? sLG[n * V + lane * PER + e]
-                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, base + 4 * e, 0, 0));
-          return softmax_sample_wave(xv, PER, V, rnd, prow);
-        };
-        const int sel = per == 4 ? sample(ic<4>{}) : sample(ic<8>{});
+        const int sel = sample_name(n, t, true, sRf[n]);
         if (lane == 0) {
           if (sal[n]) {
-            if (b == 0) a.out[(size_t)n * (ML + 1) + (t - 1)] = (unsigned char)sel;
+            if (b == 0) a.out[(size_t)opaque_s(n) * (ML + 1) + (t - 1)] = (unsigned char)sel;
             if (sel == a.eos) sal[n] = 0;
           }
           sid[n] = sel;
@@ -339,6 +457,39 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       }
       stampk(t, 10);
       __syncthreads();
+    } else if (t > 0) {
+      // distributed: workgroup n < N samples name n alone (its wave 0), writes its output row and
+      // publishes id | alive-after << 16; every workgroup then reads the N ids -- one more hand-off
+      // of one word per name instead of N / 8 sequential samples per wave in every workgroup
+      if (b < N && w == 0) {
+        pwait(flags, L, 0, kG, (unsigned)t, a.err);
+        stampk(t, 1);
+        const int sel = sample_name(b, t, false, a.rf[(size_t)b * ML + (t - 1)]);
+        stampk(t, 9);
+        const int alive = sal[b] && sel != a.eos;
+        if (lane == 0 && sal[b]) a.out[(size_t)opaque_s(b) * (ML + 1) + (t - 1)] = (unsigned char)sel;
+        if (t < ML) {
+          if (lane == 0) {
+            __builtin_amdgcn_raw_buffer_store_b32((unsigned)(sel | alive << 16), xr,
+                                                  id0 + (unsigned)(((t - 1) * kNmax + b) * 4), 0, 16);
+          }
+          publish_flag(L + 1, t - 1);
+        }
+      }
+      if (t == ML) break;
+      if (w == 0) {
+        pwait(flags, L + 1, 0, N, (unsigned)t, a.err);
+        if (lane < N) {
+          const int ln = lane_now();
+          const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(xr, id0 + (unsigned)(((t - 1) * kNmax + ln) * 4), 0, 0);
+          sid[ln] = (int)(v & 0xFFFFu);
+          sal[ln] = (int)(v >> 16);
+        }
+      }
+      stampk(t, 10);
+      __syncthreads();
+    }
+    if (t > 0) {
       if (t == ML) break;
       if (!a.probs) {   // every name ended: all workgroups see the same ids and stop together
         if (tid == 0) {
@@ -379,7 +530,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   if (tid == 0) s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == kG - 1;
   __syncthreads();
   if (s_last) {
-    for (long i = tid; i < (long)(L + 1) * kG * kFS; i += 512) flags[i] = 0u;
+    for (long i = tid; i < (long)(L + 2) * kG * kFS; i += 512) flags[i] = 0u;
     if (tid == 0) *done = 0u;
   }
 }
@@ -406,8 +557,8 @@ bool gen_persist_supported(int H, int L, int V, int N, int ML) {
   return gp_resident(KJ, L) >= kG;
 }
 
-long gen_persist_ws_floats(int H, int L, int V, int ML) { return ((long)L * kNmax * H + (long)kNmax * V) * ML; }
-long gen_persist_sync_words(int L) { return (long)(L + 1) * kG * kFS + 16; }
+long gen_persist_ws_floats(int H, int L, int V, int ML) { return ((long)L * kNmax * H + (long)kNmax * (V + 1)) * ML; }
+long gen_persist_sync_words(int L) { return (long)(L + 2) * kG * kFS + 16; }
 
 void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
   if (!gen_persist_supported(a.H, a.L, a.V, a.N, a.ML))

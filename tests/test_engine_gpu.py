@@ -214,15 +214,18 @@ def test_generator_fp32_matches_fp64_oracle(L, E, H, precision):
     print(f"identical names vs fp64 oracle: {precision} {same:.4f}, bf16 {(fast == ref).all(1).mean():.4f}")
 
 
-@pytest.mark.parametrize("L,E,H,N", [(2, 512, 1024, 64), (2, 512, 1024, 1), (1, 128, 512, 17),
-                                     (3, 128, 256, 40), (4, 64, 512, 64)])
-def test_generator_persistent_fp32(L, E, H, N):
+@pytest.mark.parametrize("L,E,H,N,V", [(2, 512, 1024, 64, 256), (2, 512, 1024, 1, 256), (1, 128, 512, 17, 256),
+                                       (3, 128, 256, 40, 256), (4, 64, 512, 64, 256), (2, 128, 512, 16, 512),
+                                       (1, 128, 512, 33, 512)])
+def test_generator_persistent_fp32(L, E, H, N, V):
     """Small batches in fp32 run as ONE persistent launch (gen_persist.hip, weights resident in
     VGPRs): same names as the batched fp32 path up to fp32 summation order, and as the fp64 oracle
-    within that; repeated launches identical (self-cleaning flags) with a clean error word."""
+    within that; repeated launches identical (self-cleaning flags) with a clean error word.  Up to 16
+    names every workgroup samples every name; above, each name has its own sampling workgroup
+    (17, 33, 40, 64); V = 512 puts two FC rows on each workgroup's VALU dot."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
-    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=L, max_len=10, sos=0, eos=0, seed=4)
+    cfg = GRUConfig(vocab=V, embed=E, hidden=H, layers=L, max_len=10, sos=0, eos=0, seed=4)
     params = init_params(cfg)
     rf = random_floats(N, cfg.max_len, seed=9)
     gen = HipGenerator(cfg, params, precision="fp32")
