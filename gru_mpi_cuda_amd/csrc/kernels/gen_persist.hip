@@ -75,21 +75,57 @@ DEV unsigned flag_load(const unsigned* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave-level wait: every producer in [lo, lo + cnt) has published epoch `ep` of `kind`.
+// a value the compiler cannot hoist out of the char loop: the per-char address math of the sampler
+// otherwise becomes loop-invariant VGPRs that the weight-resident register budget spills to scratch
+// (a scratch reload on the hand-off's critical path)
+DEV int opaque_s(int v) {   // wave-uniform values
+  v = __builtin_amdgcn_readfirstlane(v);
+  asm volatile("" : "+s"(v));
+  return v;
+}
+DEV int lane_now() {   // the lane id, recomputed where it is used
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+// Wave-level wait: every producer in [lo, lo + cnt) (cnt <= 256) has published epoch `ep` of
+// `kind`.  Lane l polls producers l, l + 64, ..., all of a round's flag loads in flight together.
+// Two rounds in flight (the next issued before the previous is checked) measured slower: per char
+// 12.9 -> 13.3 us at 1 name, 35.9 -> 42.1 at 64 (profiles/r5_gen_persist_v4_probe.jsonl) -- every
+// flag line is polled by a wave of each of the 256 workgroups, and doubling that traffic delays
+// the producers' own flag stores more than it shortens the detection.
 DEV void pwait(const unsigned* flags, int kind, int lo, int cnt, unsigned ep, unsigned* err) {
   const int lane = threadIdx.x & 63;
-  const unsigned* f = flags + (size_t)kind * kG * kFS;
-  unsigned spins = 0;
-  for (;;) {
+  const unsigned* f = flags + ((size_t)kind * kG + lo) * kFS;
+  const int nq = (cnt + 63) >> 6;   // wave-uniform
+  auto issue = [&](unsigned (&v)[4]) {
+    const int ln = lane_now();   // recomputed per poll: hoisted flag addresses cost 8 VGPRs for the launch
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = (q < nq && ln + 64 * q < cnt) ? flag_load(f + (size_t)(ln + 64 * q) * kFS) : ep;
+  };
+  auto seen = [&](const unsigned (&v)[4]) {
     bool ok = true;
-    for (int q = lane; q < cnt; q += 64) ok = ok && flag_load(f + (size_t)(lo + q) * kFS) >= ep;
-    if (__all(ok)) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ok = ok & (v[q] >= ep);
+    return __all(ok);
+  };
+  unsigned spins = 0;
+  auto give_up = [&]() {
     __builtin_amdgcn_s_sleep(1);
-    if ((++spins & 255) == 0 && (flag_load(err) & kErrBit)) break;   // another workgroup gave up
+    ++spins;
+    if ((spins & 255) == 0 && (flag_load(err) & kErrBit)) return true;   // another workgroup gave up
     if (spins > kSpin) {
       if (lane == 0) __hip_atomic_fetch_or(err, kErrBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
+      return true;
     }
+    return false;
+  };
+  unsigned v[4];
+  for (;;) {
+    issue(v);
+    if (seen(v) || give_up()) break;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the payload loads below the poll
 }
@@ -159,20 +195,6 @@ DEV void tile_mm2(A0&& av0, A1&& av1, float (&x)[KJ], f32x4& o0, f32x4& o1, bool
 }
 
 DEV float sig_ieee(float x) { return 1.f / (1.f + expf(-x)); }
-// a value the compiler cannot hoist out of the char loop: the per-char address math of the sampler
-// otherwise becomes loop-invariant VGPRs that the weight-resident register budget spills to scratch
-// (a scratch reload on the hand-off's critical path)
-DEV int opaque_s(int v) {   // wave-uniform values
-  v = __builtin_amdgcn_readfirstlane(v);
-  asm volatile("" : "+s"(v));
-  return v;
-}
-DEV int lane_now() {   // the lane id, recomputed where it is used
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-
 template <int V_> struct ic { static constexpr int value = V_; };
 template <int B_, int E_, class F> DEV void static_for(F&& f) {
   if constexpr (B_ < E_) { f(ic<B_>{}); static_for<B_ + 1, E_>(f); }
@@ -335,7 +357,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     // x rolling in behind them; one barrier pair per product for all tiles
     for (int nt = 0; nt < nnt; ++nt) {
       // (the last tile's x stays for product_gh).  Without the register room for the in-place
-      // prefetch (resident weights NT x KJ > 80 VGPRs: it spilled) the next tile loads after these MFMAs.
+      // prefetch (resident weights NT x KJ > 80 VGPRs: at 96, H = 1024 with L = 2, it fit without spills
+      // but measured slower, 64 names 13.7 -> 15.7 us for layer 1) the next tile loads after these MFMAs.
       constexpr bool kRollPF = NT * KJ <= 80;
       const bool pf = kRollPF && nt + 1 < nnt;
       const unsigned noff = xoff(SRC, t, (nt + 1) * 16 + fr, kw0);
@@ -435,17 +458,25 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       __syncthreads();
       stampk(t, 1);
       const unsigned lgt = lg0 + (unsigned)((size_t)(t - 1) * kNmax * V * 4);
-      if (tid < N) sRf[tid] = a.rf[(size_t)tid * ML + (t - 1)];   // this char's uniforms, loaded together
-      // every name's logits into LDS with all loads in flight: one memory round trip
-      for (int i = tid; i < N * V / 4; i += 512) {
-        const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
-        sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
-        sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
+      const bool direct = N <= 8;   // one name per wave: its logits straight into its registers
+      if (!direct) {
+        if (tid < N) {   // this char's uniforms, loaded together
+          int tt = tid;
+          asm volatile("" : "+v"(tt));   // (address math per char, not a launch-long VGPR pair)
+          sRf[tt] = a.rf[(size_t)tt * ML + (t - 1)];
+        }
+        // every name's logits into LDS with all loads in flight: one memory round trip
+        for (int i = tid; i < N * V / 4; i += 512) {
+          const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
+          sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
+          sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
+        }
+        __syncthreads();
       }
-      __syncthreads();
       stampk(t, 8);
       for (int n = w; n < N; n += 8) {   // real names only: a padded row keeps sid = sos
-        const int sel = sample_name(n, t, true, sRf[n]);
+        const int sel = direct ? sample_name(n, t, false, a.rf[(size_t)n * ML + (t - 1)])
+                               : sample_name(n, t, true, sRf[n]);
         if (lane == 0) {
           if (sal[n]) {
             if (b == 0) a.out[(size_t)opaque_s(n) * (ML + 1) + (t - 1)] = (unsigned char)sel;

@@ -35,6 +35,10 @@ DEV bf16x8 ld8_sc1s(rsrc_t r, unsigned voff, int soff) {
 // the give-up signal: every later wait of the launch (any workgroup) sees it at its next check and
 // returns at once, so a grid that is truly not co-resident drains in one budget, not one per wait.
 static constexpr unsigned long long kSpinTicks = 500000000ull;
+// s_sleep argument between flag polls (x 64 clocks)
+#ifndef GK_POLL_SLEEP
+#define GK_POLL_SLEEP 1
+#endif
 struct SpinBudget {
   const unsigned* err;
   unsigned long long t0 = 0;
@@ -69,7 +73,7 @@ DEV void wait_flags(const unsigned* flags, int nprod, unsigned epoch, unsigned* 
       if (lane < nprod) ok = __hip_atomic_load(flags + lane * kFlagStride, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT) >= epoch;
       if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
       if (spin.expired()) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -90,7 +94,7 @@ DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch,
     if (active) ok = __hip_atomic_load(flags + prod * kFlagStride, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT) >= epoch;
     if (__all(ok)) break;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
     if (spin.expired()) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -98,6 +102,11 @@ DEV void wave_wait(const unsigned* flags, bool active, int prod, unsigned epoch,
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// (Round 5, measured and removed: two flag polls in flight -- the next issued before the previous
+// is examined -- in the one-layer forward: 0.2020-0.2029 -> 0.2051-0.2052 ms/step on the same box,
+// profiles/r5_poll2_ab.txt; in the persistent generator likewise slower.  Each flag line is polled
+// by every consumer workgroup of its row block; doubling that traffic delays the producer's own
+// flag store more than it shortens detection.)
 // Streaming variant: lane p polls producer p; k-step kk reads the columns of producers 2kk and
 // 2kk+1, and its payload loads (loadk(kk): sc1 loads into registers) are issued as soon as BOTH
 // have published -- the early producers' data is in flight while the wave still waits for the
@@ -122,7 +131,7 @@ DEV void wave_wait_load(const unsigned* flags, bool active, int prod, unsigned e
         loaded |= 1u << kk;
       }
     if (loaded == all) break;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
     if (spin.expired()) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -153,7 +162,7 @@ DEV void wave_wait_load1(const unsigned* flags, bool active, int prod, unsigned 
         loaded |= 1u << kk;
       }
     if (loaded == all) break;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
     if (spin.expired()) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -194,7 +203,7 @@ DEV void wave_wait_load2(const unsigned* fa, const unsigned* fb, int prod0, unsi
       }
     }
     if (da == all && db == all) break;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
     if (spin.expired()) {
       if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -263,7 +272,7 @@ DEV bool row_block_local(unsigned* flags /* the row block's producer lines */, i
     for (;;) {
       if (lane < nunit) v = __hip_atomic_load(flags + lane * kFlagStride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__all(v != 0u)) break;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(GK_POLL_SLEEP);
       if (spin.expired()) {
         if (lane == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
