@@ -64,8 +64,8 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
 
 bool Generator::uses_persist(int n) const {
   // bf16 mode: only where the persistent fp32 launch is faster than the bf16 per-char graph (up to
-  // ~24 names: 21.4 vs 31.7 us per char at 16, 29.4 vs 32.2 at 17 on the reference model,
-  // profiles/r2_generate_persistent.jsonl)
+  // 40 names: 29.0 vs 33.2 us per char at 32, 33.7 vs 34.0 at 40, 34.8 vs 34.6 at 48 on the
+  // reference model, launches included, profiles/r5_gen_persist_vs_bf16_graph.jsonl)
   const int cap = d_.fp32 ? persist_max_ : std::min(persist_max_, persist_max_bf16_);
   return persist_ && n <= cap && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
 }

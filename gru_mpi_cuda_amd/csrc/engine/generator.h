@@ -89,7 +89,7 @@ class Generator {
   bool persist_ = true;
   bool inject_ = false;
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
-  int persist_max_bf16_ = 24;   // ... in the bf16 mode (it runs exact fp32, faster up to ~24 names)
+  int persist_max_bf16_ = 40;   // ... in the bf16 mode (it runs exact fp32, faster up to ~40 names)
   unsigned long long* persist_dbg_ = nullptr;
   float* pws_ = nullptr;        // persistent path: exchange buffers
   unsigned* psync_ = nullptr;   // persistent path: flags + done counter (self-cleaning, arena-zeroed)

@@ -270,7 +270,7 @@ def test_generator_persistent_spin_timeout_recovers():
 
 
 def test_generator_bf16_mode_small_batch_runs_persistent_fp32():
-    """bf16 mode up to 24 names takes the persistent launch, which is exact fp32 and faster there:
+    """bf16 mode up to 40 names takes the persistent launch, which is exact fp32 and faster there:
     same names as the fp32 mode; above it stays on the bf16 per-char graph."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
@@ -278,7 +278,7 @@ def test_generator_bf16_mode_small_batch_runs_persistent_fp32():
     params = init_params(cfg)
     fast = HipGenerator(cfg, params, precision="bf16")
     exact = HipGenerator(cfg, params, precision="fp32")
-    assert fast.g.uses_persist(24) and not fast.g.uses_persist(25)
+    assert fast.g.uses_persist(40) and not fast.g.uses_persist(41)
     rf = random_floats(16, cfg.max_len, seed=9)
     assert (fast.generate(rf) == exact.generate(rf)).all()
     assert fast.g.read_error() == 0
