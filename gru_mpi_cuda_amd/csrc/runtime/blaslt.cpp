@@ -107,9 +107,11 @@ void blaslt_init(bool force) {
   init_locked(s);
 }
 
-// Off by default since round 2: the hand-written 256 x 256 GEMM (gemm256.hip) takes the large
-// products (h2048 step 10.44 vs 10.30 ms with the library, h1024_l2 equal; profiles/r2_wgrad_ab.jsonl).
-// GK_BLASLT=1 brings the library back for the shapes gemm_library_wanted() picks.
+// GK_BLASLT=1 sends the plain (non-weight-gradient) GEMMs gemm_library_wanted() picks to the
+// library; off by default (the hand-written gemm256 takes them).  Separately, the weight-gradient
+// engine (trainer_seq.cpp wgrad_engine, GK_WGRAD_GEMM) routes the largest weight-gradient products
+// (>= 8 M outputs and >= 60 GFLOP: dW_hh at H = 2048) to the library by default, where it still beats
+// gemm256p (1.39 vs 1.25 PF, profiles/r5_gemm_phased_v3.jsonl).
 bool blaslt_enabled() {
   const char* e = std::getenv("GK_BLASLT");
   return e && e[0] == '1';
