@@ -60,6 +60,8 @@ constexpr int kNmax = 64;      // names per launch
 constexpr int kFS = 16;        // flag stride in uints (own 64-B line)
 constexpr int kVmax = 512;     // V = 256 or 512 (the sampler's instances); LDS: sP is V x 3U floats
 constexpr int kDistN = 16;    // more names than this: distributed sampling (workgroup n samples name n)
+constexpr int kTagN = 16;     // up to this many names the logits are their own flag (slots pre-filled with kEmpty)
+constexpr unsigned kEmpty = 0xFFFFFFFFu;   // a NaN no arithmetic produces from finite operands
 constexpr int kLgLds = kDistN * kVmax;   // redundant sampling stages names x V <= 8 K floats in LDS
 constexpr unsigned kSpin = 1u << 21;   // x s_sleep(1) polls: ~0.3 s
 constexpr unsigned kErrBit = 32u;
@@ -148,6 +150,40 @@ DEV void load_x(prsrc_t r, unsigned off, bool valid, float (&x)[KJ]) {
     x[j + 2] = __uint_as_float(v.z); x[j + 3] = __uint_as_float(v.w);
   }
 }
+// tagged hand-off (the logits, <= kTagN names): the slots are filled with kEmpty before the launch and
+// the producers store write-through with no drain and no flag; a consumer re-loads (sc1, past the
+// non-coherent L2) the pieces it has not seen yet until none holds kEmpty -- one memory round trip
+// fewer than flag + payload.  Bounded like pwait (err bit 32 on timeout).  Measured: the logits hop
+// + sampling 2.7 -> 1.8 us per char at one name.  The layer-state hand-offs stay on flags: tagged
+// as well (every valid lane re-polling its 8 producers' pieces) they cost 12.9 -> 12.4 us per char at
+// 1 name but 14.5 -> 17.5 at 8 (profiles/r5_gen_persist_tagged_all_probe.jsonl).
+template <int KJ>
+DEV void poll_x(prsrc_t r, unsigned off, bool valid, float (&x)[KJ], unsigned* err) {
+  constexpr int NP = KJ / 4;
+  unsigned need = valid ? (1u << NP) - 1u : 0u;
+  unsigned spins = 0;
+  for (;;) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if ((need >> p) & 1u) {
+        const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + p * 16, 0, 16);
+        x[4 * p] = __uint_as_float(v.x); x[4 * p + 1] = __uint_as_float(v.y);
+        x[4 * p + 2] = __uint_as_float(v.z); x[4 * p + 3] = __uint_as_float(v.w);
+      }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if (((need >> p) & 1u) && __float_as_uint(x[4 * p]) != kEmpty && __float_as_uint(x[4 * p + 1]) != kEmpty &&
+          __float_as_uint(x[4 * p + 2]) != kEmpty && __float_as_uint(x[4 * p + 3]) != kEmpty)
+        need &= ~(1u << p);
+    if (__all(need == 0u)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255) == 0 && (flag_load(err) & kErrBit)) break;
+    if (spins > kSpin) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, kErrBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
 // one wave's partial of a 16 x 16 (rows x names) tile over its K-slice: A values aval(j), B = x;
 // two accumulator chains
 template <int KJ, class AVal>
@@ -225,6 +261,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   const unsigned lg0 = (unsigned)((size_t)L * ML * kNmax * H * 4);
   const unsigned id0 = lg0 + (unsigned)((size_t)ML * kNmax * V * 4);
   const bool dist = N > kDistN;   // flag kinds: 0..L-1 layer states, L logits, L + 1 sampled ids
+  const bool tagged = N <= kTagN;  // the logits hand-off without flags (poll_x)
   auto xoff = [&](int l, int t, int n, int col) -> unsigned {
     return (unsigned)((((size_t)(l * ML + t) * kNmax + n) * H + col) * 4);
   };
@@ -435,6 +472,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       if (staged) {
 #pragma unroll
         for (int e = 0; e < PER; ++e) xv[e] = sLG[n * V + lane * PER + e];
+      } else if (tagged) {   // this name's logits are their own flag (poll_x)
+        poll_x<PER>(xr, base, true, xv, a.err);
       } else {
 #pragma unroll
         for (int e = 0; e < PER; e += 4) {
@@ -454,7 +493,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     stampk(t, 0);
     // ---- sample char t-1 from the logits of every workgroup
     if (t > 0 && !dist) {   // every workgroup samples every name, redundantly and identically
-      if (w == 0) pwait(flags, L, 0, kG, (unsigned)t, a.err);
+      if (w == 0 && !tagged) pwait(flags, L, 0, kG, (unsigned)t, a.err);
       __syncthreads();
       stampk(t, 1);
       const unsigned lgt = lg0 + (unsigned)((size_t)(t - 1) * kNmax * V * 4);
@@ -466,10 +505,36 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
           sRf[tt] = a.rf[(size_t)tt * ML + (t - 1)];
         }
         // every name's logits into LDS with all loads in flight: one memory round trip
-        for (int i = tid; i < N * V / 4; i += 512) {
-          const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
-          sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
-          sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
+        if (tagged) {   // <= 4 pieces per thread, polled two at a time until neither holds kEmpty
+          const int np = N * V / 4;
+          for (int q0 = 0; q0 < 4 && tid + 512 * q0 < np; q0 += 2) {
+            unsigned need = 1u | ((tid + 512 * (q0 + 1) < np) ? 2u : 0u);
+            unsigned spins = 0;
+            for (;;) {
+              pu32x4 v[2];
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                if ((need >> q) & 1u) v[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * (tid + 512 * (q0 + q)), 0, 16);
+#pragma unroll
+              for (int q = 0; q < 2; ++q)
+                if (((need >> q) & 1u) && v[q].x != kEmpty && v[q].y != kEmpty && v[q].z != kEmpty && v[q].w != kEmpty) {
+                  const int i = tid + 512 * (q0 + q);
+                  sLG[4 * i] = __uint_as_float(v[q].x); sLG[4 * i + 1] = __uint_as_float(v[q].y);
+                  sLG[4 * i + 2] = __uint_as_float(v[q].z); sLG[4 * i + 3] = __uint_as_float(v[q].w);
+                  need &= ~(1u << q);
+                }
+              if (need == 0u) break;
+              __builtin_amdgcn_s_sleep(1);
+              if ((++spins & 255) == 0 && (flag_load(a.err) & kErrBit)) break;
+              if (spins > kSpin) { __hip_atomic_fetch_or(a.err, kErrBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+            }
+          }
+        } else {
+          for (int i = tid; i < N * V / 4; i += 512) {
+            const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * i, 0, 0);
+            sLG[4 * i] = __uint_as_float(v.x); sLG[4 * i + 1] = __uint_as_float(v.y);
+            sLG[4 * i + 2] = __uint_as_float(v.z); sLG[4 * i + 3] = __uint_as_float(v.w);
+          }
         }
         __syncthreads();
       }
@@ -550,7 +615,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       if (lane < Np)
         for (int r = 0; r < VR; ++r)
           st_sc1(xr, lg0 + (unsigned)(((size_t)t * kNmax + lane) * V + b * VR + r) * 4, sgi[r][lane]);
-      publish_flag(L, t);
+      if (!tagged) publish_flag(L, t);
     }
     stampk(t, 7 + 2 * (L - 2));
     product_gh(ic<L - 1>{}, t);
@@ -600,6 +665,11 @@ void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
     if (!a.Whh[l] || !a.bhh[l] || (l > 0 && (!a.Wih[l] || !a.bih[l])))
       throw std::runtime_error("gen_persist_f32: missing layer weights");
   const int KJ = a.H / 32;
+  if (a.N <= kTagN) {   // tagged logits: every logits slot starts as kEmpty (poll_x)
+    const size_t lg0 = (size_t)a.L * a.ML * kNmax * a.H, words = (size_t)a.ML * kNmax * a.V;
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws + lg0), (int)kEmpty, words, s) != hipSuccess)
+      throw std::runtime_error("gen_persist_f32: logits fill failed");
+  }
 #define X(K, LL) \
   if (KJ == K && a.L == LL) { hipLaunchKernelGGL((gen_persist_kernel<K, LL>), dim3(kG), dim3(512), 0, s, a); return; }
   GP_VARIANTS(X)

@@ -216,13 +216,14 @@ def test_generator_fp32_matches_fp64_oracle(L, E, H, precision):
 
 @pytest.mark.parametrize("L,E,H,N,V", [(2, 512, 1024, 64, 256), (2, 512, 1024, 1, 256), (1, 128, 512, 17, 256),
                                        (3, 128, 256, 40, 256), (4, 64, 512, 64, 256), (2, 128, 512, 16, 512),
-                                       (1, 128, 512, 33, 512)])
+                                       (1, 128, 512, 33, 512), (2, 512, 1024, 8, 256), (2, 512, 1024, 5, 512)])
 def test_generator_persistent_fp32(L, E, H, N, V):
     """Small batches in fp32 run as ONE persistent launch (gen_persist.hip, weights resident in
     VGPRs): same names as the batched fp32 path up to fp32 summation order, and as the fp64 oracle
     within that; repeated launches identical (self-cleaning flags) with a clean error word.  Up to 16
     names every workgroup samples every name; above, each name has its own sampling workgroup
-    (17, 33, 40, 64); V = 512 puts two FC rows on each workgroup's VALU dot."""
+    (17, 33, 40, 64); up to 8 names the hand-offs are data-tagged (slots pre-filled with an empty
+    marker, no flags: 1, 5, 8); V = 512 puts two FC rows on each workgroup's VALU dot."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
     cfg = GRUConfig(vocab=V, embed=E, hidden=H, layers=L, max_len=10, sos=0, eos=0, seed=4)
@@ -246,25 +247,26 @@ def test_generator_persistent_fp32(L, E, H, N, V):
         assert same_b >= 0.95 and same_r >= 0.95, (same_b, same_r)
 
 
-def test_generator_persistent_spin_timeout_recovers():
+@pytest.mark.parametrize("N", [17, 3])
+def test_generator_persistent_spin_timeout_recovers(N):
     """Fault injection: a persistent launch whose spin-timeout bit is set gives up its
     waits and writes garbage; generate() must see the bit, regenerate the batch on the per-char
     graph (same names as a generator with the persistent path off) and leave a clean error word,
-    and a later call must not inherit the bit."""
+    and a later call must not inherit the bit.  17 names: flag hand-offs; 3: data-tagged polls."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
     cfg = GRUConfig(vocab=256, embed=128, hidden=512, layers=1, max_len=10, sos=0, eos=0, seed=4)
     params = init_params(cfg)
-    rf = random_floats(17, cfg.max_len, seed=9)
+    rf = random_floats(N, cfg.max_len, seed=9)
     ref_gen = HipGenerator(cfg, params, precision="fp32")
     ref_gen.g.set_persist(False)
     want = ref_gen.generate(rf)
     gen = HipGenerator(cfg, params, precision="fp32")
-    assert gen.g.uses_persist(17)
+    assert gen.g.uses_persist(N)
     gen.g.inject_persist_error()
     got = gen.generate(rf)
     assert (got == want).all()
-    assert not gen.g.uses_persist(17)        # the persistent path is off after a timeout
+    assert not gen.g.uses_persist(N)        # the persistent path is off after a timeout
     assert gen.g.read_error() == 0
     assert (gen.generate(rf) == want).all()
 
