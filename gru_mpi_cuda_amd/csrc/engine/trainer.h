@@ -12,6 +12,7 @@
 // side keeps them as torch tensors so RCCL all-reduce and checkpointing work on them directly).
 #pragma once
 #include <map>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "../runtime/runtime.h"
@@ -214,9 +215,10 @@ class Trainer {
   // dp: data-parallel recording (overlapped readiness-ordered all-reduce, dP in place, tail after)
   void record_fb_seq(hipStream_t s0, bool dp = false);
   void record_emb_tail(hipStream_t s, const float* dP_fp32);   // dP_fp32 null: bf16 copies already made
-  // the auto weight-gradient engine's library rule (trainer_seq.cpp wgrad_gemm)
+  // GK_WGRAD_GEMM=lib: the products the library takes (trainer_seq.cpp wgrad_gemm); by default none
   static bool wgrad_prefers_library(int M, int N, long K) {
-    return (double)M * N >= 8e6 && 2.0 * M * N * (double)K >= 60e9;
+    const char* v = std::getenv("GK_WGRAD_GEMM");
+    return v && std::string(v) == "lib" && (double)M * N >= 8e6 && 2.0 * M * N * (double)K >= 60e9;
   }
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);

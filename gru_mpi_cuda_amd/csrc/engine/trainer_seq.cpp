@@ -20,10 +20,13 @@ namespace gk {
 static bool ar_span() { return true; }
 
 // Weight-gradient product engine choice: "256" the 256 x 256 LDS kernel (gemm256.hip) with a
-// split-K depth picked for whole waves of workgroups, "lib" hipBLASLt where it is wanted, "128" the
-// 128 x 128 split-K path only; default (0) "auto": hipBLASLt for the products with >= 8 M outputs and
-// >= 60 GFLOP (dW_hh at H = 2048: one unsplit library GEMM, no slabs; h2048 step 8.93 -> 8.68 ms,
-// profiles/r4_h2048_wgrad_ab.jsonl), gemm256 for the rest.  GK_WGRAD_GEMM overrides it.
+// split-K depth picked for whole waves of workgroups, "lib" hipBLASLt for the products with >= 8 M
+// outputs and >= 60 GFLOP (dW_hh at H = 2048: one unsplit library GEMM), "128" the 128 x 128 split-K
+// path only; default (0) "auto" = gemm256 everywhere.  Round 4 sent dW_hh at H = 2048 to the library
+// by default (1.37 vs 1.12 PF); the staggered phased gemm256p takes that product unsplit on 192-row
+// tiles at 1.35-1.38 PF against the library's 1.33-1.42 on the same boxes, and the h2048 step runs
+// 8.62-8.64 ms against 8.62 with the library (profiles/r5_s24_gemm.jsonl, r5_s24_benches.jsonl), so
+// no library kernel is on the default path.
 static int wgrad_engine() {   // read at record time (tests switch it per trainer)
   const char* v = std::getenv("GK_WGRAD_GEMM");
   if (!v || !*v) return 0;
@@ -52,7 +55,7 @@ static int gemm256_splits(int M, int N, int K) {
 void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* dst,
                          float* rowsum_dst, hipStream_t s) {
   const int eng = wgrad_engine();
-  if (eng == 0 && wgrad_prefers_library(M, N, K)) {
+  if (eng == 1 && wgrad_prefers_library(M, N, K)) {
     GemmArgs w;   // one unsplit library GEMM straight into the gradient (+ a row-sum pass for the bias)
     w.A = A; w.lda = lda; w.B = Bm; w.ldb = ldb; w.C = dst; w.ldc = N; w.rowsumA = rowsum_dst;
     w.M = M; w.N = N; w.K = K;

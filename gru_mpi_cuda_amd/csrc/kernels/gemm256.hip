@@ -303,29 +303,41 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Phased form (round 5, cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4+T5): the same
-// 256 x 256 x 64 tile, 2 (M) x 4 (N) waves of 128 x 64, two 64 KiB k-tile buffers -- but the k-tile is
-// four PHASES, each {this phase's fragment reads + one 16 KiB half-tile of LDS-DMA staging -> raw
-// s_barrier -> lgkmcnt(0) -> setprio(1) 16 MFMAs setprio(0) -> raw s_barrier}, and the staging runs
-// two k-tiles ahead with a COUNTED vmcnt: never vmcnt(0) in the loop, two half-tiles stay in flight
-// across every k-tile boundary (the vmcnt(0) + __syncthreads per k-tile of gemm256_kernel drains the
-// whole pipeline once per k-tile).
+// Phased, staggered form (round 5, cdna_hip_programming.md §5 "The 256² 8-phase template",
+// T3+T4+T5): the same 256 x 256 x 64 tile, 2 (M) x 4 (N) waves of 128 x 64, two 64 KiB k-tile
+// buffers -- but the k-tile is four PHASES, each {fragment reads + LDS-DMA staging (segment R) -> raw
+// s_barrier -> lgkmcnt(0) -> setprio(1) 16 MFMAs setprio(0) (segment M) -> raw s_barrier}, the
+// staging runs ahead with a COUNTED vmcnt (never vmcnt(0) in the loop), and the two wave rows run one
+// barrier apart, so on each SIMD (one wave of each row) one wave's M segment overlaps the other's R
+// segment and the MFMA pipe does not idle while fragments are read.
 //
-// A wave's output is 4 quadrants of 64 x 32 (A sub-tile sa = rows 64 sa.., B sub-tile sb = cols
-// 32 sb..); phase order per k-tile (A0,B0) (A0,B1) (A1,B1) (A1,B0), so the reads are A0+B0 (12
-// ds_read_b128), B1 (4), A1 (8), none -- every fragment is read once per k-tile (A in one 32-VGPR
-// set, B0 / B1 16 each).  Buffer c = kt & 1 holds k-tile kt; halves 0/1 = A rows 0-127 / 128-255,
-// 2/3 = B rows 0-127 / 128-255.  A k-tile's B halves are last read in its phase 2, its A halves in
-// phase 3 (each wave retires its reads with lgkmcnt(0) before its MFMAs, and the phase's closing
-// barrier follows), so k-tile kt + 2's B pieces are staged into that buffer in phases 3 and 4 and
-// its A pieces in phases 1 and 2 of k-tile kt + 1; phase 4 of k-tile u waits with vmcnt(4) --
-// k-tile u + 1 landed, u + 2's B pieces in flight -- before its first barrier, so every wave's
-// k-tile u + 1 reads (phase 4's read of the next first B sub-tile comes after that barrier) see all
-// eight waves' DMA (RAW: wait, then barrier, then read).  Measured (profiles/r5_gemm_phased_v1/v2):
-// this spread staging against gemm256_kernel: h2048 dW_hh 4-way split 1234 vs 1124 TF, h1024 dW_ih
-// 909 vs 879 TF, but 1253 vs 1292 TF at 8192^3; the whole next-next k-tile staged in phase 4
-// instead (v2) lost everywhere (1051 TF at 8192^3).  gemm256() therefore takes the phased kernel for
-// the split-K / 192-row weight-gradient products and keeps gemm256_kernel for unsplit plain ones.
+// A wave's output is 4 quadrants of 64 x 32 (A sub-tile sa = rows 64 sa.. of its row's half, B
+// sub-tile sb = cols 32 sb..); phases (A0,F) (A0,S) (A1,S) (A1,F) with F = B sub-tile 0, S = 1, so
+// every fragment is read once per k-tile (A in one 32-VGPR set, F / S 16 each).  Buffer kt & 1 holds
+// k-tile kt.  Ordering: LDS-DMA data is visible to a ds_read only after the issuing wave's counted
+// vmcnt and then a barrier the reader has passed; a buffer region is restaged only after its readers
+// retired their reads (lgkmcnt(0)) and then a barrier the stager has passed.  With the rows one
+// barrier apart, a program barrier of the lagging row is the NEXT hardware barrier of the leading
+// one, so everything shared by both rows needs one program barrier more: a B half (staged by one row,
+// read by both) is read two barriers after its wait and restaged two barriers after its last read;
+// an A half is staged and read by the same row only and keeps the plain distances.  Per k-tile kt
+// (buffer C):
+//   R1: read F (4) + A0 (8) of C
+//   R2: read S (4) of C; stage B(kt+1) pieces 2, 3 into the other buffer
+//   R3: read A1 (8) of C
+//   R4: stage A(kt+2) (C's A last read in R3 by this row) and B(kt+2) pieces 0, 1 (C's B last read
+//       in R2) into C; vmcnt(NA + 2) -- k-tile kt+1 landed, first read in R1(kt+1) two barriers on
+// so most of a k-tile is in flight for four phases before its wait.
+// Measured (random operands, same box, profiles/r5_gemm_stagger_sched_ab.jsonl, plain form; the
+// unstaggered schedule it replaced and gemm256_kernel -- one vmcnt(0) + __syncthreads per k-tile --
+// in r5_gemm_stagger_v2.jsonl): 8192^3 1449 TF (unstaggered 1230, gemm256_kernel 1278, hipBLASLt
+// 1613), 4096^3 1316 (1088 / 1187, hipBLASLt 1308), h2048 dW_hh (6144 x 2048 x 65536, 192-row tiles,
+// one round) 1384 unsplit (1174 / 975, hipBLASLt 1329), h1024 dW_ih 4-way 1056 (965 / 889).  The R
+// segments set the pace: with B(kt+1) pieces 2, 3 in R1 beside its 12 fragment reads instead of R2,
+// 1357 / 1234 / 1340 / 1004 TF; with all four B(kt+1) pieces in R1 / R2 (R4 only the A pieces)
+// 1456 / 1326 but 1281 on the long-K dW_hh (B then lands two phases after its issue).  The first
+// staggered version staged A(kt+1) in R1 / R2 of k-tile kt: h2048 dW_hh unsplit 1093
+// (r5_gemm_stagger_v1.jsonl) -- the long-K products need the depth.
 template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // BM = 256 or 192 rows of A per tile (192: M = 3H products at 3H % 256 != 0 or whose 256-row grid
@@ -338,8 +350,7 @@ template <int BM, bool BIAS, bool ACC, bool RS>
 __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
   constexpr int RT = BM / 32, QR = RT / 2;          // row tiles per wave / per quadrant
   constexpr int NA = BM / 64, NB = 4;                // staging pieces per wave: A, B
-  static_assert(NB == 4, "the counted waits (vmwait256<4>) assume 4 B pieces per wave");
-  constexpr int NA1 = (NA + 1) / 2;                  // A pieces in phase 1 (the rest in phase 2)
+  static_assert(NB == 4, "the schedule stages B pieces 0, 1 in R4 and 2, 3 in R1");
   constexpr int AOFF = 0, BOFF = BM * 64;            // element offsets inside a buffer
   __shared__ __attribute__((aligned(16))) u16 lds[2][(BM + 256) * 64];   // ONE array (§5 item 4a)
   const int id = xcd_remap256(blockIdx.x, gridDim.x);
@@ -396,7 +407,13 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
     return *reinterpret_cast<const bf16x8*>(&lds[buf][BOFF + r * 64 + ((c ^ ((r >> 1) & 7)) * 8)]);
   };
   bf16x8 fa[2][QR], fb0[2][2], fb1[2][2];   // [k-step][tile]
-  const bool do_rs = RS && tn == 0 && wc == 0;   // wave-uniform
+  // row sums (the workgroups of tile column 0): row tile t of a wave row by its wave column t % 4
+  // (spread over the four SIMDs), four v_dot2 per A fragment after the MFMAs that read it.  Measured
+  // on the single-round grid of 192-row tiles (6144 x 2048 x 65536; plain 1274 TF): 1183 TF this
+  // way, 1092 on the MFMA pipe (A times a fragment of ones), 1047 with the v_dot2 moved into the next
+  // R segment -- the R segments, not the MFMAs, set the pace there (profiles/r5_s20_gemm.jsonl,
+  // r5_s21_gemm.jsonl, r5_s22_gemm.jsonl).
+  const bool do_rs = RS && tn == 0;   // wave-uniform
   float rs[RT];
 #pragma unroll
   for (int i = 0; i < RT; ++i) rs[i] = 0.f;
@@ -409,54 +426,50 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
         acc[(sa) * QR + i][(sb) * 2 + j] = mfma16(fa[ks][i], fb[ks][j], acc[(sa) * QR + i][(sb) * 2 + j]); \
     __builtin_amdgcn_s_setprio(0); }
 #define GK_RS(sa) { if (do_rs) { _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < QR; ++i) \
-      rs[(sa) * QR + i] = add_sum8(fa[ks][i], rs[(sa) * QR + i]); } }
+      if ((((sa) * QR + i) & 3) == wc) rs[(sa) * QR + i] = add_sum8(fa[ks][i], rs[(sa) * QR + i]); } }
 #define GK_SYNC() { __builtin_amdgcn_s_barrier(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
                     __builtin_amdgcn_sched_barrier(0); }
 #define GK_END() { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_barrier(); __builtin_amdgcn_sched_barrier(0); }
 
-  // prologue: k-tile 0 whole, k-tile 1's B pieces; wait for k-tile 0, then read its first B sub-tile
+  // prologue: k-tile 0, then A(1) and B(1) pieces 0, 1; wave row 1 takes one extra barrier
 #pragma unroll
   for (int q = 0; q < NB; ++q) stB(0, q);
 #pragma unroll
   for (int q = 0; q < NA; ++q) stA(0, q);
   if (nk > 1) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q) stB(1, q);
-    vmwait256<4>();
+    for (int q = 0; q < NA; ++q) stA(1, q);
+    stB(1, 0); stB(1, 1);
+    vmwait256<NA + 2>();
   } else {
     vmwait256<0>();
   }
   __builtin_amdgcn_s_barrier();
-  GK_RB(fb0, 0, 0);
-  // one k-tile in buffer C: B sub-tile SF is "first" (read in the previous tile's phase 4, register
-  // set F), SS "second" (set S).  Phases (A0,F) (A0,S) (A1,S) (A1,F): reads A0 8, S 4, A1 8 and, in
-  // phase 4, the NEXT k-tile's first sub-tile (= index SS) into set S, free since phase 3 -- at most
-  // 8 ds_read_b128 per phase.  The sets alternate roles with the k-tile parity (snake order).
-#define GK_TILE(kt_, C, F, SF, S, SS)                                                                     \
-  {                                                                                                      \
-    GK_RA(C, 0);                                                                                         \
-    if ((kt_) + 1 < nk) { _Pragma("unroll") for (int q = 0; q < NA1; ++q) stA((kt_) + 1, q); }          \
-    GK_SYNC(); GK_MMA(0, F, SF); GK_RS(0); GK_END();                                                     \
-    GK_RB(S, C, SS);                                                                                     \
-    if ((kt_) + 1 < nk) { _Pragma("unroll") for (int q = NA1; q < NA; ++q) stA((kt_) + 1, q); }         \
-    GK_SYNC(); GK_MMA(0, S, SS); GK_END();                                                               \
-    GK_RA(C, 1);                                                                                         \
-    if ((kt_) + 2 < nk) { stB((kt_) + 2, 0); stB((kt_) + 2, 1); }                                        \
-    GK_SYNC(); GK_MMA(1, S, SS); GK_RS(1); GK_END();                                                     \
-    if ((kt_) + 2 < nk) { stB((kt_) + 2, 2); stB((kt_) + 2, 3); vmwait256<4>(); } else { vmwait256<0>(); } \
-    __builtin_amdgcn_s_barrier();                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                                                   \
-    if ((kt_) + 1 < nk) GK_RB(S, (C) ^ 1, SS);                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                                                   \
-    GK_MMA(1, F, SF); GK_END();                                                                          \
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int C = kt & 1;
+    GK_RB(fb0, C, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    GK_RA(C, 0);
+    GK_SYNC(); GK_MMA(0, fb0, 0); GK_RS(0); GK_END();
+    GK_RB(fb1, C, 1);
+    if (kt + 1 < nk) { stB(kt + 1, 2); stB(kt + 1, 3); }
+    GK_SYNC(); GK_MMA(0, fb1, 1); GK_END();
+    GK_RA(C, 1);
+    GK_SYNC(); GK_MMA(1, fb1, 1); GK_RS(1); GK_END();
+    if (kt + 2 < nk) {
+#pragma unroll
+      for (int q = 0; q < NA; ++q) stA(kt + 2, q);
+      stB(kt + 2, 0); stB(kt + 2, 1);
+      vmwait256<NA + 2>();
+    } else {
+      vmwait256<0>();
+    }
+    GK_SYNC(); GK_MMA(1, fb0, 0); GK_END();
   }
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    GK_TILE(kt, 0, fb0, 0, fb1, 1);       // even k-tile: first B sub-tile 0 (in fb0)
-    GK_TILE(kt + 1, 1, fb1, 1, fb0, 0);   // odd k-tile: first B sub-tile 1 (in fb1, read above)
-  }
-  if (kt < nk) GK_TILE(kt, 0, fb0, 0, fb1, 1);
-#undef GK_TILE
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
 #undef GK_RA
 #undef GK_RB
 #undef GK_MMA
@@ -467,6 +480,7 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
   if (do_rs) {
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
+      if ((t & 3) != wc) continue;
       float v = rs[t];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
@@ -506,8 +520,10 @@ static int gemm256_mfma(int kper) {
   return kper <= 256 ? 32 : 16;
 }
 // The phased pipeline (gemm256p_kernel) for the 16x16x32 form: GK_GEMM256_PHASED=1 always, =0 never;
-// unset: for the split-K weight-gradient products and wherever 192-row tiles fill better (where it
-// measured faster), gemm256_kernel for unsplit 256-row plain products (where that one did)
+// unset: for the split-K / row-sum weight-gradient products, wherever 192-row tiles fill better and
+// for K-slices >= 4096; gemm256_kernel for the shorter unsplit 256-row plain products, where it
+// measured within a few % either way (profiles/r5_gemm_stagger_sweep.jsonl: h2048 step 270 vs 281 TF,
+// h1024 Gi 784 vs 790)
 static int gemm256_phased_mode() {
   const char* e = std::getenv("GK_GEMM256_PHASED");
   if (e && e[0] == '0') return 0;
@@ -544,7 +560,7 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   const int form = gemm256_mfma(kper);
   const int mode = gemm256_phased_mode();
   const int bm_best = gemm256_tile_rows(a.M, a.N, a.K, a.splits);
-  const bool phased = mode == 1 || (mode == -1 && (a.splits > 1 || a.rowsumA || bm_best == 192));
+  const bool phased = mode == 1 || (mode == -1 && (a.splits > 1 || a.rowsumA || bm_best == 192 || kper >= 4096));
   // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
   const int bm = (form == 32 || !phased) ? 256 : bm_best;
   if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");

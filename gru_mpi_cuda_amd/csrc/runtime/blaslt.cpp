@@ -108,10 +108,9 @@ void blaslt_init(bool force) {
 }
 
 // GK_BLASLT=1 sends the plain (non-weight-gradient) GEMMs gemm_library_wanted() picks to the
-// library; off by default (the hand-written gemm256 takes them).  Separately, the weight-gradient
-// engine (trainer_seq.cpp wgrad_engine, GK_WGRAD_GEMM) routes the largest weight-gradient products
-// (>= 8 M outputs and >= 60 GFLOP: dW_hh at H = 2048) to the library by default, where it still beats
-// gemm256p (1.39 vs 1.25 PF, profiles/r5_gemm_phased_v3.jsonl).
+// library; off by default (the hand-written gemm256 takes them).  Separately, GK_WGRAD_GEMM=lib
+// routes the largest weight-gradient products (>= 8 M outputs and >= 60 GFLOP: dW_hh at H = 2048) to
+// the library (trainer_seq.cpp wgrad_engine); by default gemm256 takes those too.
 bool blaslt_enabled() {
   const char* e = std::getenv("GK_BLASLT");
   return e && e[0] == '1';

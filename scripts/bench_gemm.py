@@ -53,23 +53,28 @@ for name, M, N, K, sp in SHAPES:
     Cs = torch.empty(sp, M, N, device=dev)
     flop = 2.0 * M * N * K
     row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp}
-    ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 34 else None
+    ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 41 else None
     variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
     # algo 3: the one-shot small GEMM at the K-slices it takes (h512 step products)
     variants += [(3, k) for k in (1, 2, 4, 6, 8, 16) if K % k == 0 and (K // k) in (128, 192, 256, 512, 1024, 1536, 2048)]
     # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32); "5o": the
     # one-vmcnt(0)-per-k-tile 16x16 kernel (GK_GEMM256_PHASED=0) against the phased default
-    variants += [("5m", k) for a_, k in variants if a_ == 5] + [("5o", k) for a_, k in variants if a_ == 5]
+    # "5r": the phased kernel with the fused row sums of A (the weight-gradient form)
+    variants += ([("5m", k) for a_, k in variants if a_ == 5] + [("5o", k) for a_, k in variants if a_ == 5]
+                 + [("5r", k) for a_, k in variants if a_ == 5])
     if os.environ.get("GEMM_ONLY256"):
-        variants = [v for v in variants if v[0] in (5, "5m", "5o")]
+        variants = [v for v in variants if v[0] in (5, "5m", "5o", "5r")]
     for algo, ks in variants:
         os.environ["GK_GEMM256_MFMA"] = "32" if algo == "5m" else "16"
         os.environ["GK_GEMM256_PHASED"] = "0" if algo == "5o" else "1"
-        algo_arg = 5 if algo in ("5m", "5o") else algo
+        algo_arg = 5 if algo in ("5m", "5o", "5r") else algo
         if ks > 1 and Cs.shape[0] < ks:
             Cs = torch.empty(ks, M, N, device=dev)
         d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,
                  splits=ks, algo=algo_arg)
+        if algo == "5r":
+            rs = torch.empty(ks, M, device=dev)
+            d["rowsumA"] = rs.data_ptr()
         tag = f"algo{algo}" + (f"s{ks}" if algo_arg in (3, 5) else "")
         try:
             us = timeit(lambda: C.gemm_nt(d, s))

@@ -892,16 +892,16 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
 
 
 def test_wgrad_library_engine_matches_gemm256():
-    """The auto weight-gradient engine sends dW_hh at H = 2048 over >= 2384 tokens (>= 8 M outputs,
-    >= 60 GFLOP) to one unsplit hipBLASLt GEMM, captured in the step graph; it must agree with the
-    gemm256 split-K path (GK_WGRAD_GEMM=256) on every gradient."""
+    """GK_WGRAD_GEMM=lib sends dW_hh at H = 2048 over >= 2384 tokens (>= 8 M outputs, >= 60 GFLOP) to
+    one unsplit hipBLASLt GEMM, captured in the step graph; it must agree with the default engine
+    (the hand-written gemm256p, 192-row tiles, fused row sums) on every gradient."""
     import os
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     cfg = GRUConfig(vocab=256, embed=128, hidden=2048, layers=1, batch=512, seq=8, seed=4)
     params = init_params(cfg)
     x, y = NameStream(cfg.batch, cfg.seq, seed=5).next()
     grads = []
-    for eng in ("", "256"):
+    for eng in ("lib", ""):
         if eng:
             os.environ["GK_WGRAD_GEMM"] = eng
         try:

@@ -407,7 +407,7 @@ def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, r
     bias gradient of a weight-gradient product, one partial per split); on v_mfma_f32_16x16x32_bf16
     (the phased pipeline, and the one-vmcnt(0)-per-k-tile kernel with GK_GEMM256_PHASED=0) and on
     v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32).  K = 64 and odd k-tile counts cover the phased
-    pipeline's prologue / drain paths."""
+    pipeline's prologue / drain paths; BM = 192 tiles (M = 768, 1536, 2304) its 3-piece A staging."""
     monkeypatch.setenv("GK_GEMM256_MFMA", mfma[:2])
     if mfma == "16auto":
         monkeypatch.delenv("GK_GEMM256_PHASED", raising=False)
