@@ -249,7 +249,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
     }
     // (gemm256 on 2048-deep K-slices at h2048 -- 8 tiles x 32 splits -- measured equal: the GEMM
-    // 194 -> 173 us, its 32 slabs given back in the reduce; profiles/r4_h2048_dwfc256_ab.jsonl)
+    // 194 -> 173 us, its 32 slabs given back in the reduce; profiles/r4_h2048_dwfc256_ab.jsonl.  Again
+    // with the staggered gemm256p in round 5: 192 -> 163 us, the reduce 14 -> 27 us, step 8.92 / 8.91
+    // vs 8.93 / 8.90 ms; profiles/r5_dwfc256_ab.jsonl)
     // single GPU, slabs summed inside Adam: nothing reads dW_fc before the optimiser, so its
     // K-slices can join the dW_ih0 / dEmb launch after the backward sweep (one launch fewer; its
     // latency-bound tiles run beside theirs)
