@@ -33,13 +33,21 @@
 //     That is L + 1 hand-offs per char, each an all-to-all of tiny slices (U or VR floats per
 //     name per producer). A producer's wave 0 publishes them with write-through (sc1) stores,
 //     drains them (vmcnt(0)) and stores its epoch flag. A consumer wave polls only the 32
-//     producers of its K-slice (all 256 for the logits), then reads with sc1 loads: the hand-off
-//     protocol of the persistent training kernels (gru_seq.hip). Every char has its own state and
-//     logits slots, so consumers read with plain loads that the 32 workgroups of an XCD share
-//     through its L2.
-//     Data-tagged 8-byte granules (no flag) measured slower here: every waiting lane re-reads its
-//     whole set of granules, 44.6 against 28 us per char at 8 names
+//     producers of its K-slice (all 256 for the logits), then reads with plain loads that the 32
+//     workgroups of an XCD share through its L2 (every char has its own slots).
+//   * Small batches hand off without flags (round 5): every slot is filled with kEmpty (a NaN no
+//     arithmetic produces) before the launch, producers store write-through with no drain, and
+//     consumers re-load (sc1) the pieces they have not seen until none holds kEmpty -- the data is
+//     the signal.  The logits up to 16 names (poll_x); the layer states up to 8 names at U = 4
+//     (poll_xs), each producer's piece on its own 128-B line (one writer per line, the polls spread
+//     over as many lines as flag polls).  Tagged states in the plain [name][H] layout (8 producers
+//     per line) measured slower at 8 names (profiles/r5_gen_persist_tagged_all_probe.jsonl); on
+//     their own lines 13.1 -> 11.8 us per char at 8 names (r5_gen_persist_tagx_probe.jsonl).
+//     Round 2's data-tagged 8-byte granules: 44.6 against 28 us at 8 names
 //     (profiles/r2_generate_persistent.jsonl).
+//   * One name: the products run on the VALU (KJ FMAs per lane against name 0's x, summed over the
+//     K quarters with two shuffles) instead of KJ fp32 MFMAs at 32 cycles of issue each for a
+//     16-name tile with one live column: 11.5 -> 10.0 us per char (r5_gen_persist_final_probe.jsonl).
 //   * Gates use IEEE expf / tanhf, and sampling uses the batched sampler's code (gen_sample.h),
 //     i.e. the same arithmetic as the batched fp32 path. Only the order of the fp32 partial sums
 //     of each dot product differs.
@@ -62,6 +70,9 @@ constexpr int kVmax = 512;     // V = 256 or 512 (the sampler's instances); LDS:
 constexpr int kDistN = 16;    // more names than this: distributed sampling (workgroup n samples name n)
 constexpr int kTagN = 16;     // up to this many names the logits are their own flag (slots pre-filled with kEmpty)
 constexpr unsigned kEmpty = 0xFFFFFFFFu;   // a NaN no arithmetic produces from finite operands
+constexpr int kTagX = 8;      // up to this many names (U = 4) the layer states are tagged too, one line per producer
+constexpr int kXLine = 32;    // floats per producer line of the tagged layer-state layout (128 B)
+constexpr int kStampT = 24;   // chars with diagnostic stamps
 constexpr int kLgLds = kDistN * kVmax;   // redundant sampling stages names x V <= 8 K floats in LDS
 constexpr unsigned kSpin = 1u << 21;   // x s_sleep(1) polls: ~0.3 s
 constexpr unsigned kErrBit = 32u;
@@ -184,6 +195,40 @@ DEV void poll_x(prsrc_t r, unsigned off, bool valid, float (&x)[KJ], unsigned* e
     }
   }
 }
+// the same over KJ / 4 producers' 16-B pieces `stride` bytes apart (the tagged layer states: each
+// producer's piece on its own 128-B line, so a line has one writer and the polls of a consumer wave
+// spread over as many lines as its flag polls would)
+template <int KJ>
+DEV void poll_xs(prsrc_t r, unsigned off, unsigned stride, bool valid, float (&x)[KJ], unsigned* err) {
+  constexpr int NP = KJ / 4;
+  unsigned need = valid ? (1u << NP) - 1u : 0u;
+  if (!valid) {
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) x[j] = 0.f;
+  }
+  unsigned spins = 0;
+  for (;;) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if ((need >> p) & 1u) {
+        const pu32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off + p * stride, 0, 16);
+        x[4 * p] = __uint_as_float(v.x); x[4 * p + 1] = __uint_as_float(v.y);
+        x[4 * p + 2] = __uint_as_float(v.z); x[4 * p + 3] = __uint_as_float(v.w);
+      }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      if (((need >> p) & 1u) && __float_as_uint(x[4 * p]) != kEmpty && __float_as_uint(x[4 * p + 1]) != kEmpty &&
+          __float_as_uint(x[4 * p + 2]) != kEmpty && __float_as_uint(x[4 * p + 3]) != kEmpty)
+        need &= ~(1u << p);
+    if (__all(need == 0u)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255) == 0 && (flag_load(err) & kErrBit)) break;
+    if (spins > kSpin) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(err, kErrBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
 // one wave's partial of a 16 x 16 (rows x names) tile over its K-slice: A values aval(j), B = x;
 // two accumulator chains
 template <int KJ, class AVal>
@@ -254,6 +299,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   __shared__ int s_last, s_live;
   __shared__ __attribute__((aligned(16))) float sLG[kLgLds];   // staged logits of the last char
   __shared__ float sRf[kNmax];
+  __shared__ unsigned long long sStamp[kStampT][16];   // diagnostic phase stamps (a.dbg)
+  __shared__ unsigned long long sClk[kStampT];
 
   // one slot per char (no reuse inside a launch: see load_x), X_l[t][name][H], LG[t][name][V], then
   // (distributed sampling) ID[t][name] = id | alive-after << 16
@@ -264,6 +311,11 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   const bool tagged = N <= kTagN;  // the logits hand-off without flags (poll_x)
   auto xoff = [&](int l, int t, int n, int col) -> unsigned {
     return (unsigned)((((size_t)(l * ML + t) * kNmax + n) * H + col) * 4);
+  };
+  // tagged layer states (N <= kTagX, U = 4): X_l[t][producer][kXLine], name n's U floats at n U
+  const bool tagx = U == 4 && N <= kTagX;
+  auto xoffp = [&](int l, int t, int p, int n) -> unsigned {
+    return (unsigned)((((size_t)(l * ML + t) * kG + p) * kXLine + n * U) * 4);
   };
   unsigned* flags = a.sync;
   unsigned* done = a.sync + (size_t)(L + 2) * kG * kFS;
@@ -303,6 +355,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     sbf[tid] = tid < VR ? a.bfc[b * VR + tid] : 0.f;
   }
   for (int i = tid; i < L * kNmax * U; i += 512) (&sh[0][0][0])[i] = 0.f;
+  if (a.dbg)
+    for (int i = tid; i < kStampT * 16; i += 512) (&sStamp[0][0])[i] = 0ull;
   if (tid < kNmax) { sid[tid] = a.sos; sal[tid] = tid < N ? 1 : 0; }
   if (dist ? b < N : b == 0)   // each output row has one writer: its sampler (every row: workgroup 0)
     for (int i = tid; i < (dist ? ML + 1 : N * (ML + 1)); i += 512) a.out[(dist ? (size_t)b * (ML + 1) : 0) + i] = 0;
@@ -332,6 +386,18 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[nt][slot][w][(4 * q4 + r) * 16 + fr] = acc[r];
   };
+  // diagnostic phase stamps (100 MHz wall clock), first and last workgroup, thread 0 only:
+  // 0 char start, 1 logits seen, 2 sampled, 3 layer 0 published, 4 + 2(l-1) layer l input seen,
+  // 5 + 2(l-1) layer l published, 6 + 2(L-2) logits input seen, 7 + 2(L-2) logits published;
+  // sampling internals: 8 logits staged, 9 wave 0's first name sampled, 10 wave 0's names done;
+  // layer 1's phase: 11 x in, 12 MFMAs stashed, 13 reduced, 14 gates, 15 gate barrier
+  // Kept in LDS and copied out after the char loop: a global store per stamp put its write
+  // acknowledgement inside the next vmcnt(0) of the timed phase (1 us of phantom time).
+  auto stampk = [&](int t, int k) {
+    if (!a.dbg || tid != 0 || (b != 0 && b != kG - 1) || k > 15 || t >= kStampT) return;
+    sStamp[t][k] = __builtin_amdgcn_s_memrealtime();
+    if (k == 0) sClk[t] = __builtin_amdgcn_s_memtime();   // shader clock at char start: the probe's SCLK
+  };
   // gates of layer l for all names -> sh[l], then wave 0 publishes h_l(t) and its flag
   auto gates_publish = [&](int l, int t) {
     for (int i = tid; i < Np * U; i += 512) {
@@ -347,29 +413,31 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       const float nn = tanhf(gi[2] + r * gh[2]);
       sh[l][n][u] = (1.f - z) * nn + z * sh[l][n][u];
     }
+    if (l == 1) stampk(t, 14);   // (probe: gates)
     __syncthreads();
+    if (l == 1) stampk(t, 15);   // (probe: barrier)
+    // (wave 0 publishes every exchange; hipcc waits for a store's completion -- vmcnt(0) -- before
+    // it reuses the store's data registers, so each publish waits for the previous one's
+    // write-through.  A different wave per exchange shortens the publishes and lengthens the
+    // consumers' wait by as much: 10.03 -> 10.19 us per char at 1 name, r5_gen_publish_wave_ab.txt)
     if (w == 0) {
       if (lane < Np) {
         if constexpr (U == 4) {
           const pu32x4 v = {__float_as_uint(sh[l][lane][0]), __float_as_uint(sh[l][lane][1]),
                             __float_as_uint(sh[l][lane][2]), __float_as_uint(sh[l][lane][3])};
-          __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoff(l, t, lane, b * U), 0, 16);
+          if (tagx) {   // its own line, no drain, no flag: the data is the signal
+            if (lane < N) __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoffp(l, t, b, lane), 0, 16);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(v, xr, xoff(l, t, lane, b * U), 0, 16);
+          }
         } else {
           for (int u = 0; u < U; ++u) st_sc1(xr, xoff(l, t, lane, b * U + u), sh[l][lane][u]);
         }
       }
-      publish_flag(l, t);
+      if (!tagx) publish_flag(l, t);
     }
   };
 
-  // diagnostic phase stamps (100 MHz wall clock), first and last workgroup, thread 0 only:
-  // 0 char start, 1 logits seen, 2 sampled, 3 layer 0 published, 4 + 2(l-1) layer l input seen,
-  // 5 + 2(l-1) layer l published, 6 + 2(L-2) logits input seen, 7 + 2(L-2) logits published;
-  // sampling internals: 8 logits staged, 9 wave 0's first name sampled, 10 wave 0's names done
-  auto stampk = [&](int t, int k) {
-    if (!a.dbg || tid != 0 || (b != 0 && b != kG - 1) || k > 15) return;
-    a.dbg[((size_t)(b == 0 ? 0 : 1) * (ML + 1) + t) * 16 + k] = __builtin_amdgcn_s_memrealtime();
-  };
   // gh_l = h_l W_hh_l^T + b_hh_l is only needed by the next char's gates: it is computed beside the
   // product that consumes h_l(t) anyway (gi_{l+1}, or the logits for the top layer), so each
   // exchanged state is read once per char.  At t = 0 (h = 0) it is the bias.
@@ -381,12 +449,36 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   // x = h_src(t) (this wave's K-slice, name tile nt) times W tile TA (-> dst rows < nrows, + bias)
   // and, unless this is the last char, times W_hh_src (-> sgh[src] for the next char)
   float xk[KJ];   // this wave's x of the last name tile, kept for the gh pass after the publish
+  // one name (N = 1): lane (row fr, quarter q4) dots its KJ resident weights of tile ti with name
+  // 0's x; the quarters' sum lands in name column 0 of the tile's partial slot
+  const bool one = N == 1;
+  auto vdot_q = [&](auto ti_tag) -> float {
+    constexpr int TI = decltype(ti_tag)::value;
+    float p = 0.f;
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) p = fmaf(Wr[TI][j], xk[j], p);
+    p += __shfl_xor(p, 16, 64);
+    p += __shfl_xor(p, 32, 64);
+    return p;
+  };
+  auto stash_one = [&](int slot, float p) {
+    if (q4 == 0) red[0][slot][w][fr * 16] = p;
+  };
   auto product = [&](auto ta_tag, auto src_tag, int t, float (*dst)[kNmax], const float* bias, int nrows, int sk) {
     constexpr int TA = decltype(ta_tag)::value, SRC = decltype(src_tag)::value;   // TA = NT: the FC rows
     const int kw0 = w * KW + q4 * KJ;
-    pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
-    stampk(t, sk);
-    load_x<KJ>(xr, xoff(SRC, t, fr, kw0), fr < N, xk);
+    // one name: every lane takes name 0's x (the VALU products below need it in all 16 rows)
+    const int xn = one ? 0 : fr;
+    const bool xv = one || fr < N;
+    if (tagx) {
+      stampk(t, sk);
+      poll_xs<KJ>(xr, xoffp(SRC, t, kw0 / U, xn), kXLine * 4, xv, xk, a.err);
+    } else {
+      pwait(flags, SRC, w * 32, 32, (unsigned)(t + 1), a.err);
+      stampk(t, sk);
+      load_x<KJ>(xr, xoff(SRC, t, xn, kw0), xv, xk);
+    }
+    if (sk == 4 && a.dbg) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); stampk(t, 11); }   // (probe: x in)
     // several name tiles: gh here from the same x (re-reading it after the publish cost more)
     const bool gh = nnt > 1 && t + 1 < ML;
     auto whh = [&](int j) { return Wr[SRC][j]; };
@@ -426,6 +518,10 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
         } else if (pf) {
           load_x<KJ>(xr, noff, nvalid, xk);
         }
+      } else if (one) {
+        // one name: KJ VALU FMAs per lane (row fr, quarter q4 of the K-slice), summed over the
+        // quarters, instead of KJ MFMAs (32 cycles of issue each) for a 16-name tile of one column
+        stash_one(0, vdot_q(ic<TA>{}));
       } else {
         auto wta = [&](int j) { return Wr[TA][j]; };
         if (gh) tile_mm2<KJ, true>(wta, whh, xk, o0, o1, pf, xr, noff, nvalid);
@@ -438,6 +534,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
         load_x<KJ>(xr, noff, nvalid, xk);
       }
     }
+    if (sk == 4) stampk(t, 12);   // (probe: MFMAs issued, partials stashed)
     lds_barrier();
     for (int i = tid; i < nnt * 256; i += 512) {
       const int nt = i >> 8, e = i & 255;
@@ -446,6 +543,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
       if (gh) reduce_el(sgh[SRC], 1, nt, sbh[SRC], R3, e);
     }
     lds_barrier();
+    if (sk == 4) stampk(t, 13);   // (probe: partial sums reduced)
   };
   // gh_src of the next char from the same h_src(t), after this phase's publish: with one name tile
   // its MFMAs run while the next hand-off is in flight instead of before the publish (x still in
@@ -453,7 +551,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   auto product_gh = [&](auto src_tag, int t) {
     constexpr int SRC = decltype(src_tag)::value;
     if (t + 1 >= ML || nnt > 1) return;   // (several name tiles: done inside product)
-    stash(0, 1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
+    if (one) stash_one(1, vdot_q(ic<SRC>{}));
+    else stash(0, 1, tile_mm<KJ>([&](int j) { return Wr[SRC][j]; }, xk));
     lds_barrier();
     if (tid < 256) reduce_el(sgh[SRC], 1, 0, sbh[SRC], R3, tid);
     lds_barrier();
@@ -507,18 +606,20 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
         // every name's logits into LDS with all loads in flight: one memory round trip
         if (tagged) {   // <= 4 pieces per thread, polled two at a time until neither holds kEmpty
           const int np = N * V / 4;
-          for (int q0 = 0; q0 < 4 && tid + 512 * q0 < np; q0 += 2) {
-            unsigned need = 1u | ((tid + 512 * (q0 + 1) < np) ? 2u : 0u);
+          int ti = tid;
+          asm volatile("" : "+v"(ti));   // (per char, not a launch-long VGPR: see opaque_s)
+          for (int q0 = 0; q0 < 4 && ti + 512 * q0 < np; q0 += 2) {
+            unsigned need = 1u | ((ti + 512 * (q0 + 1) < np) ? 2u : 0u);
             unsigned spins = 0;
             for (;;) {
               pu32x4 v[2];
 #pragma unroll
               for (int q = 0; q < 2; ++q)
-                if ((need >> q) & 1u) v[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * (tid + 512 * (q0 + q)), 0, 16);
+                if ((need >> q) & 1u) v[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, lgt + 16u * (ti + 512 * (q0 + q)), 0, 16);
 #pragma unroll
               for (int q = 0; q < 2; ++q)
                 if (((need >> q) & 1u) && v[q].x != kEmpty && v[q].y != kEmpty && v[q].z != kEmpty && v[q].w != kEmpty) {
-                  const int i = tid + 512 * (q0 + q);
+                  const int i = ti + 512 * (q0 + q);
                   sLG[4 * i] = __uint_as_float(v[q].x); sLG[4 * i + 1] = __uint_as_float(v[q].y);
                   sLG[4 * i + 2] = __uint_as_float(v[q].z); sLG[4 * i + 3] = __uint_as_float(v[q].w);
                   need &= ~(1u << q);
@@ -621,6 +722,10 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     product_gh(ic<L - 1>{}, t);
   }
 
+  if (a.dbg && tid == 0 && (b == 0 || b == kG - 1))
+    for (int t = 0; t <= ML && t < kStampT; ++t)
+      for (int k = 0; k < 16; ++k)   // slot 15 of the last workgroup's rows: its shader clock at char start
+        a.dbg[((size_t)(b == 0 ? 0 : 1) * (ML + 1) + t) * 16 + k] = (b != 0 && k == 15) ? sClk[t] : sStamp[t][k];
   // ---- the last workgroup out zeroes the flags for the next launch (nobody polls them any more)
   __syncthreads();
   if (tid == 0) s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == kG - 1;
@@ -669,6 +774,12 @@ void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
     const size_t lg0 = (size_t)a.L * a.ML * kNmax * a.H, words = (size_t)a.ML * kNmax * a.V;
     if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws + lg0), (int)kEmpty, words, s) != hipSuccess)
       throw std::runtime_error("gen_persist_f32: logits fill failed");
+  }
+  if (a.H == 1024 && a.N <= kTagX) {   // tagged layer states (poll_xs): their lines start as kEmpty
+    const size_t words = (size_t)a.L * a.ML * kG * kXLine;
+    static_assert((size_t)kG * kXLine <= (size_t)kNmax * 1024, "tagged layout inside the state slots");
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws), (int)kEmpty, words, s) != hipSuccess)
+      throw std::runtime_error("gen_persist_f32: state fill failed");
   }
 #define X(K, LL) \
   if (KJ == K && a.L == LL) { hipLaunchKernelGGL((gen_persist_kernel<K, LL>), dim3(kG), dim3(512), 0, s, a); return; }

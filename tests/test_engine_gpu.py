@@ -247,15 +247,16 @@ def test_generator_persistent_fp32(L, E, H, N, V):
         assert same_b >= 0.95 and same_r >= 0.95, (same_b, same_r)
 
 
-@pytest.mark.parametrize("N", [17, 3])
-def test_generator_persistent_spin_timeout_recovers(N):
+@pytest.mark.parametrize("N,H", [(17, 512), (3, 512), (3, 1024)])
+def test_generator_persistent_spin_timeout_recovers(N, H):
     """Fault injection: a persistent launch whose spin-timeout bit is set gives up its
     waits and writes garbage; generate() must see the bit, regenerate the batch on the per-char
     graph (same names as a generator with the persistent path off) and leave a clean error word,
-    and a later call must not inherit the bit.  17 names: flag hand-offs; 3: data-tagged polls."""
+    and a later call must not inherit the bit.  17 names: flag hand-offs; 3: data-tagged logits (and,
+    at H = 1024, data-tagged layer states)."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
-    cfg = GRUConfig(vocab=256, embed=128, hidden=512, layers=1, max_len=10, sos=0, eos=0, seed=4)
+    cfg = GRUConfig(vocab=256, embed=128, hidden=H, layers=1, max_len=10, sos=0, eos=0, seed=4)
     params = init_params(cfg)
     rf = random_floats(N, cfg.max_len, seed=9)
     ref_gen = HipGenerator(cfg, params, precision="fp32")
