@@ -47,7 +47,12 @@
 //     (profiles/r2_generate_persistent.jsonl).
 //   * One name: the products run on the VALU (KJ FMAs per lane against name 0's x, summed over the
 //     K quarters with two shuffles) instead of KJ fp32 MFMAs at 32 cycles of issue each for a
-//     16-name tile with one live column: 11.5 -> 10.0 us per char (r5_gen_persist_final_probe.jsonl).
+//     16-name tile with one live column: 11.5 -> 10.0 us per char.
+//   * Up to 16 names every (name, unit) gate of a workgroup is one lane of wave 0: it sums layer
+//     l >= 1's gi from the wave partials itself, computes the gate and stores it at once, and the
+//     barrier that protects the partials follows the store (one barrier, a reduce pass and an LDS
+//     round trip fewer before each publish); the logits likewise from the FC reduce.  1 name 10.0
+//     -> 9.7 us per char, 8 names 12.3 -> 11.7 (profiles/r5_gen_persist_final_probe.jsonl).
 //   * Gates use IEEE expf / tanhf, and sampling uses the batched sampler's code (gen_sample.h),
 //     i.e. the same arithmetic as the batched fp32 path. Only the order of the fp32 partial sums
 //     of each dot product differs.
@@ -309,6 +314,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   const unsigned id0 = lg0 + (unsigned)((size_t)ML * kNmax * V * 4);
   const bool dist = N > kDistN;   // flag kinds: 0..L-1 layer states, L logits, L + 1 sampled ids
   const bool tagged = N <= kTagN;  // the logits hand-off without flags (poll_x)
+  const bool fastg = N <= 16;      // one name tile, Np U <= 64: gates and publishes by wave 0 alone
   auto xoff = [&](int l, int t, int n, int col) -> unsigned {
     return (unsigned)((((size_t)(l * ML + t) * kNmax + n) * H + col) * 4);
   };
@@ -390,7 +396,8 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   // 0 char start, 1 logits seen, 2 sampled, 3 layer 0 published, 4 + 2(l-1) layer l input seen,
   // 5 + 2(l-1) layer l published, 6 + 2(L-2) logits input seen, 7 + 2(L-2) logits published;
   // sampling internals: 8 logits staged, 9 wave 0's first name sampled, 10 wave 0's names done;
-  // layer 1's phase: 11 x in, 12 MFMAs stashed, 13 reduced, 14 gates, 15 gate barrier
+  // layer 1's phase: 11 x in, 12 MFMAs stashed, 13 reduced (<= 16 names: partials barrier), 14 gates,
+  // 15 gate barrier (<= 16 names: stored)
   // Kept in LDS and copied out after the char loop: a global store per stamp put its write
   // acknowledgement inside the next vmcnt(0) of the timed phase (1 us of phantom time).
   auto stampk = [&](int t, int k) {
@@ -400,6 +407,46 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   };
   // gates of layer l for all names -> sh[l], then wave 0 publishes h_l(t) and its flag
   auto gates_publish = [&](int l, int t) {
+    if (fastg) {
+      // <= 16 names: every (name, unit) of the workgroup is one lane of wave 0, which computes its
+      // gate (layers >= 1: gi summed straight from the product's wave partials, in reduce_el's
+      // order) and stores it at once; the barrier that protects red / sgi / sh comes after the
+      // store instead of two barriers and an LDS round trip before it
+      if (w == 0) {
+        const int ln = lane_now();   // (per use: hoisted lane addresses spill at the weight-resident budget)
+        const int n = ln / U, u = ln % U;
+        if (ln < Np * U) {
+          float gi[3], gh[3];
+#pragma unroll
+          for (int g = 0; g < 3; ++g) {
+            gh[g] = sgh[l][g * U + u][n];
+            if (l == 0) {
+              gi[g] = sP[sid[n] * R3 + g * U + u];
+            } else {
+              const int e = (g * U + u) * 16 + n;
+              float sum = red[0][0][0][e];
+#pragma unroll
+              for (int k = 1; k < 8; ++k) sum += red[0][0][k][e];
+              gi[g] = sum + sbi[l][g * U + u];
+            }
+          }
+          const float r = sig_ieee(gi[0] + gh[0]);
+          const float z = sig_ieee(gi[1] + gh[1]);
+          const float nn = tanhf(gi[2] + r * gh[2]);
+          const float hv = (1.f - z) * nn + z * sh[l][n][u];
+          sh[l][n][u] = hv;
+          if (l == 1) stampk(t, 14);   // (probe: gates)
+          if (n < N) {
+            if (tagx) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(hv), xr, xoffp(l, t, b, n) + 4u * u, 0, 16);
+            else st_sc1(xr, xoff(l, t, n, b * U + u), hv);
+          }
+          if (l == 1) stampk(t, 15);   // (probe: stored)
+        }
+        if (!tagx) publish_flag(l, t);
+      }
+      __syncthreads();
+      return;
+    }
     for (int i = tid; i < Np * U; i += 512) {
       const int n = i / U, u = i % U;
       float gi[3], gh[3];
@@ -536,10 +583,23 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     }
     if (sk == 4) stampk(t, 12);   // (probe: MFMAs issued, partials stashed)
     lds_barrier();
+    if (fastg && TA != NT) {   // the gates read the partials themselves (gates_publish)
+      if (sk == 4) stampk(t, 13);
+      return;
+    }
     for (int i = tid; i < nnt * 256; i += 512) {
       const int nt = i >> 8, e = i & 255;
-      if constexpr (TA == NT) { if (e < 16 * nrows) reduce_fc_el(dst, nt, e); }
-      else reduce_el(dst, 0, nt, bias, nrows, e);
+      if constexpr (TA == NT) {
+        if (e < 16 * nrows) {
+          reduce_fc_el(dst, nt, e);
+          if (fastg) {   // wave 0 lanes store their logit at once
+            const int ln = lane_now(), row = ln >> 4, n = ln & 15;
+            if (n < N) st_sc1(xr, lg0 + (unsigned)(((size_t)t * kNmax + n) * V + b * VR + row) * 4, dst[row][n]);
+          }
+        }
+      } else {
+        reduce_el(dst, 0, nt, bias, nrows, e);
+      }
       if (gh) reduce_el(sgh[SRC], 1, nt, sbh[SRC], R3, e);
     }
     lds_barrier();
@@ -713,7 +773,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     // ---- FC: logits rows b VR .. b VR + VR  (+ gh_{L-1} of the next char)
     product(ic<NT>{}, ic<L - 1>{}, t, sgi, sbf, VR, 6 + 2 * (L - 2));
     if (w == 0) {
-      if (lane < Np)
+      if (lane < Np && !fastg)   // (fastg: stored inside the product's reduce)
         for (int r = 0; r < VR; ++r)
           st_sc1(xr, lg0 + (unsigned)(((size_t)t * kNmax + lane) * V + b * VR + r) * 4, sgi[r][lane]);
       if (!tagged) publish_flag(L, t);

@@ -45,8 +45,8 @@ out = {"N": N, "model": f"L={cfg.layers} H={cfg.hidden}", "us_per_char": round(f
                        "x in -> MFMAs stashed": round(float(np.mean([w0[t][12] - w0[t][11] for t in range(1, ML)])), 2),
                        "stashed -> reduced": round(float(np.mean([w0[t][13] - w0[t][12] for t in range(1, ML)])), 2),
                        "reduced -> gates": round(float(np.mean([w0[t][14] - w0[t][13] for t in range(1, ML)])), 2),
-                       "gates -> barrier": round(float(np.mean([w0[t][15] - w0[t][14] for t in range(1, ML)])), 2),
-                       "barrier -> published": round(float(np.mean([w0[t][5] - w0[t][15] for t in range(1, ML)])), 2)}
+                       "gates -> barrier (<= 16 names: stored)": round(float(np.mean([w0[t][15] - w0[t][14] for t in range(1, ML)])), 2),
+                       "barrier (stored) -> published": round(float(np.mean([w0[t][5] - w0[t][15] for t in range(1, ML)])), 2)}
        if cfg.layers >= 2 else {},
        "sclk_ghz": round(float(np.mean([(dbg.view(2, ML + 1, 16)[1, t + 1, 15] - dbg.view(2, ML + 1, 16)[1, t, 15]).item()
                                          / ((d[1][t + 1][0] - d[1][t][0]) * 1e3) for t in range(1, ML - 1)])), 3),
