@@ -325,8 +325,9 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 //   R1: read F (4) + A0 (8) of C
 //   R2: read S (4) of C; stage B(kt+1) pieces 2, 3 into the other buffer
 //   R3: read A1 (8) of C
-//   R4: stage A(kt+2) (C's A last read in R3 by this row) and B(kt+2) pieces 0, 1 (C's B last read
-//       in R2) into C; vmcnt(NA + 2) -- k-tile kt+1 landed, first read in R1(kt+1) two barriers on
+//   R4: stage A(kt+2) (C's A last read in R3 by this row; SC 1: pieces 0, 1 here, the rest in
+//       R1(kt+1)) and B(kt+2) pieces 0, 1 (C's B last read in R2) into C; counted vmcnt -- k-tile
+//       kt+1 landed, first read in R1(kt+1) two barriers on
 // so most of a k-tile is in flight for four phases before its wait.
 // Measured (random operands, same box, profiles/r5_gemm_stagger_sched_ab.jsonl, plain form; the
 // unstaggered schedule it replaced and gemm256_kernel -- one vmcnt(0) + __syncthreads per k-tile --
@@ -337,7 +338,10 @@ __global__ void __launch_bounds__(512, 1) gemm256m32_kernel(GemmArgs a, int ntn,
 // 1357 / 1234 / 1340 / 1004 TF; with all four B(kt+1) pieces in R1 / R2 (R4 only the A pieces)
 // 1456 / 1326 but 1281 on the long-K dW_hh (B then lands two phases after its issue).  The first
 // staggered version staged A(kt+1) in R1 / R2 of k-tile kt: h2048 dW_hh unsplit 1093
-// (r5_gemm_stagger_v1.jsonl) -- the long-K products need the depth.
+// (r5_gemm_stagger_v1.jsonl) -- the long-K products need the depth.  Issuing A pieces 2.. of k-tile
+// kt+2 in R1(kt+1) instead (at most 4 LDS-DMA pieces in any R segment, three phases of slack for
+// them): 8192^3 1398 -> 1475, 4096^3 1241 -> 1291, h1024 dW_ih 4-way 995 -> 1063, but h2048 dW_hh
+// unsplit 1336 -> 1307 (r5_gemm_stagger_sc_ab.jsonl), so it is taken up to 128 k-tiles per workgroup.
 template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // BM = 256 or 192 rows of A per tile (192: M = 3H products at 3H % 256 != 0 or whose 256-row grid
@@ -346,7 +350,7 @@ template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"
 // (BM / 2) x 64 output: RT = BM / 32 row tiles of 16, a quadrant is RT / 2 of them x 2 column tiles.
 // LDS per buffer: A [BM][64] + B [256][64] bf16, staged in 1-KiB pieces of 8 rows (one wave
 // instruction each): A BM / 64 pieces per wave, B 4.
-template <int BM, bool BIAS, bool ACC, bool RS>
+template <int BM, bool BIAS, bool ACC, bool RS, int SC>
 __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
   constexpr int RT = BM / 32, QR = RT / 2;          // row tiles per wave / per quadrant
   constexpr int NA = BM / 64, NB = 4;                // staging pieces per wave: A, B
@@ -436,6 +440,8 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
   for (int q = 0; q < NB; ++q) stB(0, q);
 #pragma unroll
   for (int q = 0; q < NA; ++q) stA(0, q);
+  // SC 1: A pieces 2.. of k-tile kt+2 are issued in R1(kt+1) instead of R4(kt) (see gemm256())
+  constexpr int NAE = SC == 1 ? 2 : NA;   // A pieces staged in R4
   if (nk > 1) {
 #pragma unroll
     for (int q = 0; q < NA; ++q) stA(1, q);
@@ -452,6 +458,12 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
     GK_RB(fb0, C, 0);
     __builtin_amdgcn_sched_barrier(0);
     GK_RA(C, 0);
+    if constexpr (SC == 1) {
+      if (kt >= 1 && kt + 1 < nk) {
+#pragma unroll
+        for (int q = NAE; q < NA; ++q) stA(kt + 1, q);
+      }
+    }
     GK_SYNC(); GK_MMA(0, fb0, 0); GK_RS(0); GK_END();
     GK_RB(fb1, C, 1);
     if (kt + 1 < nk) { stB(kt + 1, 2); stB(kt + 1, 3); }
@@ -460,9 +472,9 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
     GK_SYNC(); GK_MMA(1, fb1, 1); GK_RS(1); GK_END();
     if (kt + 2 < nk) {
 #pragma unroll
-      for (int q = 0; q < NA; ++q) stA(kt + 2, q);
+      for (int q = 0; q < NAE; ++q) stA(kt + 2, q);
       stB(kt + 2, 0); stB(kt + 2, 1);
-      vmwait256<NA + 2>();
+      vmwait256<NAE + 2>();
     } else {
       vmwait256<0>();
     }
@@ -561,6 +573,12 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   const int mode = gemm256_phased_mode();
   const int bm_best = gemm256_tile_rows(a.M, a.N, a.K, a.splits);
   const bool phased = mode == 1 || (mode == -1 && (a.splits > 1 || a.rowsumA || bm_best == 192 || kper >= 4096));
+  // where the A pieces of k-tile kt+2 are issued: SC 1 (two in R4(kt), the rest in R1(kt+1), no
+  // segment with more than 4 LDS-DMA pieces) up to 128 k-tiles per workgroup, SC 0 (all in R4(kt),
+  // four phases of slack) for the long-K products that stream their operands from memory
+  // (profiles/r5_gemm_stagger_sc_ab.jsonl); GK_GEMM256_SCHED=0 / 1 forces one
+  const char* sce = std::getenv("GK_GEMM256_SCHED");
+  const int sc = sce && sce[0] ? (sce[0] == '1' ? 1 : 0) : (kper / kBK <= 128 ? 1 : 0);
   // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
   const int bm = (form == 32 || !phased) ? 256 : bm_best;
   if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");
@@ -569,8 +587,10 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
 #define GK_L(B_, A_, R_)                                                                                          \
   do {                                                                                                            \
     if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);    \
-    else if (phased && bm == 192) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased && bm == 192 && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased && bm == 192) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper); \
     else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);                  \
   } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate

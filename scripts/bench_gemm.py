@@ -67,6 +67,7 @@ for name, M, N, K, sp in SHAPES:
     for algo, ks in variants:
         os.environ["GK_GEMM256_MFMA"] = "32" if algo == "5m" else "16"
         os.environ["GK_GEMM256_PHASED"] = "0" if algo == "5o" else "1"
+        os.environ.pop("GK_GEMM256_SCHED", None)   # the staggered schedule picked per shape
         algo_arg = 5 if algo in ("5m", "5o", "5r") else algo
         if ks > 1 and Cs.shape[0] < ks:
             Cs = torch.empty(ks, M, N, device=dev)

@@ -400,15 +400,20 @@ def test_reduce_slabs_cast(ext, R, C, splits):
     (512, 256, 4096, 8, False, False, 64, True), (2304, 1280, 576, 1, True, True, 32, False),
     (1536, 512, 8192, 4, False, False, 0, True), (512, 768, 1024, 1, False, False, 0, True),
     (256, 512, 128, 1, False, False, 0, True), (512, 512, 192, 1, True, False, 0, False)])
-@pytest.mark.parametrize("mfma", ["16", "16auto", "16legacy", "32"])
+@pytest.mark.parametrize("mfma", ["16", "16auto", "16legacy", "16sc0", "32"])
 def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, rowsum, mfma):
     """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
     operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
     bias gradient of a weight-gradient product, one partial per split); on v_mfma_f32_16x16x32_bf16
     (the phased pipeline, and the one-vmcnt(0)-per-k-tile kernel with GK_GEMM256_PHASED=0) and on
     v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32).  K = 64 and odd k-tile counts cover the phased
-    pipeline's prologue / drain paths; BM = 192 tiles (M = 768, 1536, 2304) its 3-piece A staging."""
+    pipeline's prologue / drain paths; BM = 192 tiles (M = 768, 1536, 2304) its 3-piece A staging;
+    16sc0 the staging schedule of the long-K products (GK_GEMM256_SCHED=0, all A pieces in R4)."""
     monkeypatch.setenv("GK_GEMM256_MFMA", mfma[:2])
+    if mfma == "16sc0":
+        monkeypatch.setenv("GK_GEMM256_SCHED", "0")
+    else:
+        monkeypatch.delenv("GK_GEMM256_SCHED", raising=False)
     if mfma == "16auto":
         monkeypatch.delenv("GK_GEMM256_PHASED", raising=False)
     else:
