@@ -1,0 +1,17 @@
+#!/bin/bash
+# session 40: large-H backward with non-temporal stores of the weight-gradient operands (GK_BIG_NTST)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread -k "big or h2048 or wgrad or exchange_ring" > gpurun_out/s40_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/s40_tests.log; [ $rc -ne 0 ] && exit $rc
+out=gpurun_out/s40_benches.jsonl; : > $out
+run() { tag=$1; shift; line=$(timeout -k 10 300 "$@" 2>/dev/null | grep '^{') || { echo "fail $tag"; exit 1; }; echo "{\"tag\": \"$tag\", \"b\": $line}" >> $out; echo "$tag $(echo $line | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["ms_per_step"], d.get("final_loss"))')"; }
+for i in 1 2; do
+  GK_BIG_NTST=1 run c5_ntst python bench.py --preset h2048 --per-gpu-batch 512 --steps 6 --warmup 2
+  GK_BIG_NTST=0 run c5_plain python bench.py --preset h2048 --per-gpu-batch 512 --steps 6 --warmup 2
+done
+GK_BIG_NTST=1 run h1024x1024_ntst python bench.py --preset h1024_l2 --per-gpu-batch 1024 --steps 6 --warmup 2
+GK_BIG_NTST=0 run h1024x1024_plain python bench.py --preset h1024_l2 --per-gpu-batch 1024 --steps 6 --warmup 2
+for m in 1 0; do
+  GK_BIG_NTST=$m timeout -k 10 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/pmc_c5_ntst$m/g1 -o run -- python3 bench.py --preset h2048 --per-gpu-batch 512 --steps 3 --warmup 2 --min-warmup 0 > gpurun_out/pmc_c5_ntst$m.log 2>&1 || exit 1
+  python3 scripts/analyze_pmc.py gpurun_out/pmc_c5_ntst$m 2>/dev/null | grep -i "big\|kernel " | head -3
+done
