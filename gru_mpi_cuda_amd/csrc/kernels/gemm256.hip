@@ -531,11 +531,13 @@ static int gemm256_mfma(int kper) {
   if (e && e[0]) return std::atoi(e);
   return kper <= 256 ? 32 : 16;
 }
-// The phased, staggered pipeline (gemm256p_kernel) takes every 16x16x32-form product;
-// GK_GEMM256_PHASED=0 selects gemm256_kernel (one vmcnt(0) + barrier per k-tile) for A/B.  The
-// staggered kernel measured ahead of it on every engine shape but the smallest
-// (profiles/r5_gemm_stagger_sweep.jsonl, r5_gemm_plain_shapes_ab.jsonl: h1024 Gi 795 vs 755 TF,
-// h2048 logits 770 vs 758, h2048 step 281 vs 270; h512 dW_ih0 36 vs 32)
+// The phased, staggered pipeline (gemm256p_kernel) for the 16x16x32 form: GK_GEMM256_PHASED=1
+// always, =0 never; unset: the split-K / row-sum weight-gradient products, the 192-row shapes and
+// K-slices >= 4096, gemm256_kernel (one vmcnt(0) + barrier per k-tile) for the shorter unsplit plain
+// products.  In microbenchmarks the staggered kernel led there too (h1024 Gi 795 vs 755 TF, h2048
+// logits 770 vs 758, profiles/r5_gemm_plain_shapes_ab.jsonl), but in the h2048 step the logits GEMM
+// (with its bias) took 140.7 us on it against 122.6 on gemm256_kernel (r5_c5_step_summary_final.txt,
+// r5_c5_step_summary_dp256.txt), so the plain products stay where they were
 static int gemm256_phased_mode() {
   const char* e = std::getenv("GK_GEMM256_PHASED");
   if (e && e[0] == '0') return 0;
@@ -572,7 +574,7 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   const int form = gemm256_mfma(kper);
   const int mode = gemm256_phased_mode();
   const int bm_best = gemm256_tile_rows(a.M, a.N, a.K, a.splits);
-  const bool phased = mode != 0;
+  const bool phased = mode == 1 || (mode == -1 && (a.splits > 1 || a.rowsumA || bm_best == 192 || kper >= 4096));
   // where the A pieces of k-tile kt+2 are issued: SC 1 (two in R4(kt), the rest in R1(kt+1), no
   // segment with more than 4 LDS-DMA pieces) up to 128 k-tiles per workgroup, SC 0 (all in R4(kt),
   // four phases of slack) for the long-K products that stream their operands from memory
