@@ -72,7 +72,8 @@ def main() -> int:
                          "to time the data-parallel step structure")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--dp-pipeline", type=int, choices=[-1, 0, 1], default=None,
-                    help="one-layer data-parallel tail: -1 auto (pipelined at world > 1), 0 one collective, 1 pipelined")
+                    help="one-layer data-parallel tail: -1 auto (= one collective; the pipelined form measured "
+                         "slower), 0 one collective, 1 pipelined")
     ap.add_argument("--shard-optim", action="store_true",
                     help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
     ap.add_argument("--min-warmup", type=int, default=300,

@@ -144,7 +144,8 @@ class Trainer {
   //   | beside it: dW_fc K-slices -> reduce -> AR2 (FC pair) on the comm stream
   //   join AR1 -> dW_ih0 / dEmb from the averaged dP -> Adam (all but FC) | beside it: AR2
   //   join AR2 -> Adam (FC pair).
-  // dp_pipe_: -1 auto (on at world > 1), 0 one collective (the single-bucket step), 1 on.
+  // dp_pipe_: -1 auto (= off: measured slower, dp_pipe_on), 0 one collective (the single-bucket
+  // step), 1 on.
   int dp_pipe_ = -1;
   bool dp_pipe_on() const;
   bool opt_in_fb_ = false;   // record_fb_seq recorded the optimiser itself (pipelined tail)
