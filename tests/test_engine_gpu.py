@@ -216,14 +216,17 @@ def test_generator_fp32_matches_fp64_oracle(L, E, H, precision):
 
 @pytest.mark.parametrize("L,E,H,N,V", [(2, 512, 1024, 64, 256), (2, 512, 1024, 1, 256), (1, 128, 512, 17, 256),
                                        (3, 128, 256, 40, 256), (4, 64, 512, 64, 256), (2, 128, 512, 16, 512),
-                                       (1, 128, 512, 33, 512), (2, 512, 1024, 8, 256), (2, 512, 1024, 5, 512)])
+                                       (1, 128, 512, 33, 512), (2, 512, 1024, 8, 256), (2, 512, 1024, 5, 512),
+                                       (1, 128, 512, 1, 256), (3, 128, 256, 1, 512), (2, 128, 512, 12, 256)])
 def test_generator_persistent_fp32(L, E, H, N, V):
     """Small batches in fp32 run as ONE persistent launch (gen_persist.hip, weights resident in
     VGPRs): same names as the batched fp32 path up to fp32 summation order, and as the fp64 oracle
     within that; repeated launches identical (self-cleaning flags) with a clean error word.  Up to 16
     names every workgroup samples every name; above, each name has its own sampling workgroup
-    (17, 33, 40, 64); up to 8 names the hand-offs are data-tagged (slots pre-filled with an empty
-    marker, no flags: 1, 5, 8); V = 512 puts two FC rows on each workgroup's VALU dot."""
+    (17, 33, 40, 64); up to 16 names the logits and, at H = 1024 up to 8 names, the layer states are
+    data-tagged (slots pre-filled with an empty marker, no flags: 1, 5, 8, 12); one name runs the
+    products on the VALU (H = 256, 512, 1024); up to 16 names wave 0 computes and publishes every gate;
+    V = 512 puts two FC rows on each workgroup's VALU dot."""
     from gru_mpi_cuda_amd.engine.generator import HipGenerator
     from gru_mpi_cuda_amd.utils.data import random_floats
     cfg = GRUConfig(vocab=V, embed=E, hidden=H, layers=L, max_len=10, sos=0, eos=0, seed=4)
