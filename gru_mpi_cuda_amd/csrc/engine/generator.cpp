@@ -265,7 +265,6 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
   HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);
-    HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
     bool persist_done = false;
     if (uses_persist(n)) {   // one launch for the whole batch: no graph needed
       GenPersistArgs a;
@@ -274,8 +273,17 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
         a.Whh[l] = P("weight_hh_l" + k); a.bhh[l] = P("bias_hh_l" + k);
         if (l > 0) { a.Wih[l] = P("weight_ih_l" + k); a.bih[l] = P("bias_ih_l" + k); }
       }
-      a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab32_; a.rf = rf_; a.out = out_; a.probs = probe_;
+      // the caller's uniforms and output rows directly (no staging copies: two fewer stream
+      // operations per call on the latency-bound small-batch path)
+      a.Wfc = P("fc.weight"); a.bfc = P("fc.bias"); a.P = Ptab32_; a.probs = probe_;
+      a.rf = rf + (size_t)start * ML; a.out = out + (size_t)start * (ML + 1);
       a.ws = pws_; a.sync = psync_; a.err = err_; a.dbg = persist_dbg_;
+      if (ppar_ < 0) {   // first launch: both sets' tagged slots -> kEmpty; later launches refill in-kernel
+        gen_persist_fill_ws(pws_, d_.H, d_.L, d_.V, ML, s);
+        ppar_ = 0;
+      }
+      a.par = ppar_;
+      ppar_ ^= 1;
       a.N = n; a.H = d_.H; a.L = d_.L; a.V = d_.V; a.ML = ML; a.sos = d_.sos; a.eos = d_.eos;
       if (inject_) {   // test hook: OR the spin-limit bit into the word (earlier batches' bits stay)
         unsigned cur = 0;
@@ -302,8 +310,9 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
         HIP_CHECK(hipMemcpy(err_, &keep, 4, hipMemcpyHostToDevice));
       }
     }
-    if (persist_done) {
-    } else if (use_graph_) {
+    if (persist_done) continue;   // rows already in `out`
+    HIP_CHECK(hipMemcpyAsync(rf_, rf + (size_t)start * ML, (size_t)n * ML * 4, hipMemcpyDeviceToDevice, s));
+    if (use_graph_) {
       auto& g = graphs_[n];
       if (!g) {
         g.reset(new Graph());

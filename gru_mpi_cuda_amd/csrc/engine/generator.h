@@ -91,7 +91,8 @@ class Generator {
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
   int persist_max_bf16_ = 40;   // ... in the bf16 mode (it runs exact fp32, faster up to ~40 names)
   unsigned long long* persist_dbg_ = nullptr;
-  float* pws_ = nullptr;        // persistent path: exchange buffers
+  float* pws_ = nullptr;        // persistent path: exchange buffers (two sets, by launch parity)
+  int ppar_ = -1;               // the next persistent launch's set; -1: workspace not filled yet
   unsigned* psync_ = nullptr;   // persistent path: flags + done counter (self-cleaning, arena-zeroed)
   static constexpr int kF32SlabRows = 2048;   // fp32 split-K slab capacity (rows x 3H)
 };

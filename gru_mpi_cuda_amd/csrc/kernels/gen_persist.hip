@@ -309,7 +309,11 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
 
   // one slot per char (no reuse inside a launch: see load_x), X_l[t][name][H], LG[t][name][V], then
   // (distributed sampling) ID[t][name] = id | alive-after << 16
-  const prsrc_t xr = prsrc(a.ws, (unsigned)(((size_t)L * ML * kNmax * H + (size_t)ML * kNmax * (V + 1)) * 4));
+  // two sets of exchange buffers, by launch parity: this launch uses set a.par and, after its char loop,
+  // refills the other set's tagged slots with kEmpty for the next launch (no fill operations on the
+  // stream: two fewer per call, docs/DESIGN.md §4)
+  const size_t set_floats = (size_t)L * ML * kNmax * H + (size_t)ML * kNmax * (V + 1);
+  const prsrc_t xr = prsrc(a.ws + (size_t)a.par * set_floats, (unsigned)(set_floats * 4));
   const unsigned lg0 = (unsigned)((size_t)L * ML * kNmax * H * 4);
   const unsigned id0 = lg0 + (unsigned)((size_t)ML * kNmax * V * 4);
   const bool dist = N > kDistN;   // flag kinds: 0..L-1 layer states, L logits, L + 1 sampled ids
@@ -332,6 +336,9 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
                          __HIP_MEMORY_SCOPE_AGENT);
   };
 
+  // (probe: the launch's entry time, before the weights load; kept in a register until the stamps
+  // are zeroed)
+  const unsigned long long t_entry = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // ---- resident weights: tile ti < L: W_hh_ti; L <= ti < 2L-1: W_ih_(ti-L+1).  The FC rows (VR of
   // the 16 rows of its tile) live in LDS.
   float Wr[NT][KJ];
@@ -361,8 +368,11 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     sbf[tid] = tid < VR ? a.bfc[b * VR + tid] : 0.f;
   }
   for (int i = tid; i < L * kNmax * U; i += 512) (&sh[0][0][0])[i] = 0.f;
-  if (a.dbg)
+  if (a.dbg) {
     for (int i = tid; i < kStampT * 16; i += 512) (&sStamp[0][0])[i] = 0ull;
+    __syncthreads();
+    if (tid == 0 && ML < kStampT) sStamp[ML][14] = t_entry;   // (row ML has no layer phases)
+  }
   if (tid < kNmax) { sid[tid] = a.sos; sal[tid] = tid < N ? 1 : 0; }
   if (dist ? b < N : b == 0)   // each output row has one writer: its sampler (every row: workgroup 0)
     for (int i = tid; i < (dist ? ML + 1 : N * (ML + 1)); i += 512) a.out[(dist ? (size_t)b * (ML + 1) : 0) + i] = 0;
@@ -397,7 +407,7 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
   // 5 + 2(l-1) layer l published, 6 + 2(L-2) logits input seen, 7 + 2(L-2) logits published;
   // sampling internals: 8 logits staged, 9 wave 0's first name sampled, 10 wave 0's names done;
   // layer 1's phase: 11 x in, 12 MFMAs stashed, 13 reduced (<= 16 names: partials barrier), 14 gates,
-  // 15 gate barrier (<= 16 names: stored)
+  // 15 gate barrier (<= 16 names: stored); row ML: 14 the launch's entry, 13 the end of the char loop
   // Kept in LDS and copied out after the char loop: a global store per stamp put its write
   // acknowledgement inside the next vmcnt(0) of the timed phase (1 us of phantom time).
   auto stampk = [&](int t, int k) {
@@ -782,6 +792,17 @@ __global__ void __launch_bounds__(512, 1) gen_persist_kernel(GenPersistArgs a) {
     product_gh(ic<L - 1>{}, t);
   }
 
+  if (a.dbg && tid == 0 && ML < kStampT) sStamp[ML][13] = __builtin_amdgcn_s_memrealtime();   // (probe: loop end)
+  {   // the other set's tagged slots -> kEmpty (nobody reads that set in this launch; the next one does
+      // after the kernel boundary): the layer-state lines and the logits, 1/kG of each per workgroup
+    float* other = a.ws + (size_t)(1 - a.par) * set_floats;
+    const size_t nst = (size_t)L * ML * kG * kXLine / 4, nlg = (size_t)ML * kNmax * V / 4;
+    const pu32x4 e4 = {kEmpty, kEmpty, kEmpty, kEmpty};
+    pu32x4* st4 = reinterpret_cast<pu32x4*>(other);
+    pu32x4* lg4 = reinterpret_cast<pu32x4*>(other + (size_t)L * ML * kNmax * H);
+    for (size_t i = (size_t)b * 512 + tid; i < nst; i += (size_t)kG * 512) st4[i] = e4;
+    for (size_t i = (size_t)b * 512 + tid; i < nlg; i += (size_t)kG * 512) lg4[i] = e4;
+  }
   if (a.dbg && tid == 0 && (b == 0 || b == kG - 1))
     for (int t = 0; t <= ML && t < kStampT; ++t)
       for (int k = 0; k < 16; ++k)   // slot 15 of the last workgroup's rows: its shader clock at char start
@@ -818,8 +839,13 @@ bool gen_persist_supported(int H, int L, int V, int N, int ML) {
   return gp_resident(KJ, L) >= kG;
 }
 
-long gen_persist_ws_floats(int H, int L, int V, int ML) { return ((long)L * kNmax * H + (long)kNmax * (V + 1)) * ML; }
+long gen_persist_ws_floats(int H, int L, int V, int ML) { return 2 * ((long)L * kNmax * H + (long)kNmax * (V + 1)) * ML; }
 long gen_persist_sync_words(int L) { return (long)(L + 2) * kG * kFS + 16; }
+
+void gen_persist_fill_ws(float* ws, int H, int L, int V, int ML, hipStream_t s) {
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ws), (int)kEmpty, (size_t)gen_persist_ws_floats(H, L, V, ML), s) != hipSuccess)
+    throw std::runtime_error("gen_persist_fill_ws: fill failed");
+}
 
 void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
   if (!gen_persist_supported(a.H, a.L, a.V, a.N, a.ML))
@@ -830,17 +856,10 @@ void gen_persist_f32(const GenPersistArgs& a, hipStream_t s) {
     if (!a.Whh[l] || !a.bhh[l] || (l > 0 && (!a.Wih[l] || !a.bih[l])))
       throw std::runtime_error("gen_persist_f32: missing layer weights");
   const int KJ = a.H / 32;
-  if (a.N <= kTagN) {   // tagged logits: every logits slot starts as kEmpty (poll_x)
-    const size_t lg0 = (size_t)a.L * a.ML * kNmax * a.H, words = (size_t)a.ML * kNmax * a.V;
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws + lg0), (int)kEmpty, words, s) != hipSuccess)
-      throw std::runtime_error("gen_persist_f32: logits fill failed");
-  }
-  if (a.H == 1024 && a.N <= kTagX) {   // tagged layer states (poll_xs): their lines start as kEmpty
-    const size_t words = (size_t)a.L * a.ML * kG * kXLine;
-    static_assert((size_t)kG * kXLine <= (size_t)kNmax * 1024, "tagged layout inside the state slots");
-    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws), (int)kEmpty, words, s) != hipSuccess)
-      throw std::runtime_error("gen_persist_f32: state fill failed");
-  }
+  // tagged slots (poll_x / poll_xs) start as kEmpty: set a.par was refilled by the previous launch;
+  // before the first launch the caller fills the whole workspace (gen_persist_fill_ws)
+  static_assert((size_t)kG * kXLine <= (size_t)kNmax * 1024, "tagged layout inside the state slots");
+  if (a.par != 0 && a.par != 1) throw std::runtime_error("gen_persist_f32: launch parity must be 0 or 1");
 #define X(K, LL) \
   if (KJ == K && a.L == LL) { hipLaunchKernelGGL((gen_persist_kernel<K, LL>), dim3(kG), dim3(512), 0, s, a); return; }
   GP_VARIANTS(X)

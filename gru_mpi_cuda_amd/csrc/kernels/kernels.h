@@ -294,7 +294,8 @@ struct GenPersistArgs {
   const float* rf = nullptr;       // [N][ML] uniforms
   unsigned char* out = nullptr;    // [N][ML + 1]
   float* probs = nullptr;          // nullable [Npad][V]: softmax of the last step (tests)
-  float* ws = nullptr;             // gen_persist_ws_floats(): exchange buffers
+  float* ws = nullptr;             // gen_persist_ws_floats(): two exchange-buffer sets (launch parity)
+  int par = 0;                     // this launch's set; it refills the other set's tagged slots
   unsigned* sync = nullptr;        // gen_persist_sync_words(): epoch flags + arrival count (zeroed once, self-cleaning)
   unsigned* err = nullptr;         // bit 32: a cross-workgroup wait hit its spin limit
   unsigned long long* dbg = nullptr;   // diagnostic (nullable): [2 wgs][ML + 1][16] s_memrealtime stamps
@@ -302,6 +303,7 @@ struct GenPersistArgs {
 };
 bool gen_persist_supported(int H, int L, int V, int N, int ML);
 long gen_persist_ws_floats(int H, int L, int V, int ML);
+void gen_persist_fill_ws(float* ws, int H, int L, int V, int ML, hipStream_t s);   // both sets -> kEmpty
 long gen_persist_sync_words(int L);
 void gen_persist_f32(const GenPersistArgs& a, hipStream_t s);
 

@@ -76,7 +76,7 @@ class HipGenerator:
 
     def generate_device(self, rf_dev: torch.Tensor, n: int) -> torch.Tensor:
         ML = self.cfg.max_len
-        out = torch.zeros(max(n, 1), ML + 1, dtype=torch.uint8, device=self.dev)
+        out = torch.empty(max(n, 1), ML + 1, dtype=torch.uint8, device=self.dev)   # every row written
         if n > 0:
             self.g.generate(rf_dev.data_ptr(), n, out.data_ptr(), self._s())
         return out[:n]

@@ -20,6 +20,14 @@ dbg = torch.zeros(2 * (ML + 1) * 16, dtype=torch.int64, device="cuda")
 rf = torch.from_numpy(random_floats(N, ML, seed=3).reshape(N, ML)).cuda()
 g.generate_device(rf, N)
 torch.cuda.synchronize()
+# end to end (no stamps): one generate_device per batch, launch and slot fills included
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+for _ in range(20):
+    g.generate_device(rf, N)
+ev1.record()
+torch.cuda.synchronize()
+e2e = ev0.elapsed_time(ev1) * 1e3 / 20
 g.g.set_persist_dbg(dbg.data_ptr())
 g.generate_device(rf, N)
 torch.cuda.synchronize()
@@ -50,5 +58,10 @@ out = {"N": N, "model": f"L={cfg.layers} H={cfg.hidden}", "us_per_char": round(f
        if cfg.layers >= 2 else {},
        "sclk_ghz": round(float(np.mean([(dbg.view(2, ML + 1, 16)[1, t + 1, 15] - dbg.view(2, ML + 1, 16)[1, t, 15]).item()
                                          / ((d[1][t + 1][0] - d[1][t][0]) * 1e3) for t in range(1, ML - 1)])), 3),
+       "launch_us": {"entry -> char 0 start (weights to VGPRs / LDS)": round(float(w0[0][0] - w0[ML][14]), 2),
+                     "char 0 (no sampling)": round(float(w0[1][0] - w0[0][0]), 2),
+                     "char ML start -> loop end (last sampling)": round(float(w0[ML][13] - w0[ML][0]), 2),
+                     "entry -> loop end": round(float(w0[ML][13] - w0[ML][14]), 2)},
+       "end_to_end_us_per_generate": round(e2e, 2), "end_to_end_us_per_char": round(e2e / ML, 2),
        "error_word": int(g.g.read_error())}
 print(json.dumps(out))
