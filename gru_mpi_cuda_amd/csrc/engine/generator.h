@@ -89,7 +89,8 @@ class Generator {
   bool persist_ = true;
   bool inject_ = false;
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
-  int persist_max_bf16_ = 40;   // ... in the bf16 mode (it runs exact fp32, faster up to ~40 names)
+  int persist_max_bf16_ = 40;   // ... in the bf16 mode (it runs exact fp32, faster up to ~40 names:
+                                // profiles/r5_gen_persist_vs_bf16_graph_final.jsonl)
   unsigned long long* persist_dbg_ = nullptr;
   float* pws_ = nullptr;        // persistent path: exchange buffers (two sets, by launch parity)
   int ppar_ = -1;               // the next persistent launch's set; -1: workspace not filled yet
