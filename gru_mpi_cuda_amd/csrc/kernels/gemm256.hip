@@ -19,6 +19,7 @@
 //     XCD's resident workgroups share A and B panels in its L2.
 // Measured (scripts/bench_gemm.py, random operands, profiles/r2_gemm256.jsonl): 4096^3 1172 TF,
 // 8192^3 1287 TF (hipBLASLt on the same box 1190 / 1441); the 128^2 kernel 906 / 893.
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -351,14 +352,13 @@ template <int N> DEV void vmwait256() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"
 // LDS per buffer: A [BM][64] + B [256][64] bf16, staged in 1-KiB pieces of 8 rows (one wave
 // instruction each): A BM / 64 pieces per wave, B 4.
 template <int BM, bool BIAS, bool ACC, bool RS, int SC>
-__global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper) {
+__global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, int ntm, int kper, int kGroupM) {
   constexpr int RT = BM / 32, QR = RT / 2;          // row tiles per wave / per quadrant
   constexpr int NA = BM / 64, NB = 4;                // staging pieces per wave: A, B
   static_assert(NB == 4, "the schedule stages B pieces 0, 1 in R4 and 2, 3 in R1");
   constexpr int AOFF = 0, BOFF = BM * 64;            // element offsets inside a buffer
   __shared__ __attribute__((aligned(16))) u16 lds[2][(BM + 256) * 64];   // ONE array (§5 item 4a)
   const int id = xcd_remap256(blockIdx.x, gridDim.x);
-  constexpr int kGroupM = 4;
   const int sp = id / (ntn * ntm), pid = id % (ntn * ntm);
   const int per_group = kGroupM * ntn, first_m = (pid / per_group) * kGroupM;
   const int gm = min(ntm - first_m, kGroupM);
@@ -581,6 +581,10 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   // (profiles/r5_gemm_stagger_sc_ab.jsonl); GK_GEMM256_SCHED=0 / 1 forces one
   const char* sce = std::getenv("GK_GEMM256_SCHED");
   const int sc = sce && sce[0] ? (sce[0] == '1' ? 1 : 0) : (kper / kBK <= 128 ? 1 : 0);
+  // raster run length of the staggered kernel: 4 tile-rows; 2 / 8 / 16 measured, none better across
+  // shapes (profiles/r5_gemm_groupm_ab.jsonl), GK_GEMM256_GROUPM=n overrides
+  const char* gme = std::getenv("GK_GEMM256_GROUPM");
+  const int gmr = gme && gme[0] ? std::max(1, std::atoi(gme)) : 4;
   // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
   const int bm = (form == 32 || !phased) ? 256 : bm_best;
   if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");
@@ -589,10 +593,10 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
 #define GK_L(B_, A_, R_)                                                                                          \
   do {                                                                                                            \
     if (form == 32) hipLaunchKernelGGL((gemm256m32_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);    \
-    else if (phased && bm == 192 && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (phased && bm == 192) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (phased && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper); \
-    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper); \
+    else if (phased && bm == 192 && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper, gmr); \
+    else if (phased && bm == 192) hipLaunchKernelGGL((gemm256p_kernel<192, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper, gmr); \
+    else if (phased && sc == 1) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 1>), grid, block, 0, s, a, ntn, ntm, kper, gmr); \
+    else if (phased) hipLaunchKernelGGL((gemm256p_kernel<256, B_, A_, R_, 0>), grid, block, 0, s, a, ntn, ntm, kper, gmr); \
     else hipLaunchKernelGGL((gemm256_kernel<B_, A_, R_>), grid, block, 0, s, a, ntn, ntm, kper);                  \
   } while (0)
   if (a.rowsumA) {   // weight-gradient form: no bias, no accumulate

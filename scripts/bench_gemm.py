@@ -63,14 +63,16 @@ for name, M, N, K, sp in SHAPES:
     # one-vmcnt(0)-per-k-tile 16x16 kernel (GK_GEMM256_PHASED=0) against the phased default
     # "5r": the phased kernel with the fused row sums of A (the weight-gradient form)
     variants += ([("5m", k) for a_, k in variants if a_ == 5] + [("5o", k) for a_, k in variants if a_ == 5]
-                 + [("5r", k) for a_, k in variants if a_ == 5])
+                 + [("5r", k) for a_, k in variants if a_ == 5]
+                 + [(x, k) for a_, k in variants if a_ == 5 for x in ("5g", "5h", "5i", "5")])
     if os.environ.get("GEMM_ONLY256"):
-        variants = [v for v in variants if v[0] in (5, "5m", "5o", "5r")]
+        variants = [v for v in variants if v[0] in (5, "5", "5g", "5h", "5i")]
     for algo, ks in variants:
         os.environ["GK_GEMM256_MFMA"] = "32" if algo == "5m" else "16"
         os.environ["GK_GEMM256_PHASED"] = "0" if algo == "5o" else "1"
         os.environ.pop("GK_GEMM256_SCHED", None)   # the staggered schedule picked per shape
-        algo_arg = 5 if algo in ("5m", "5o", "5r") else algo
+        os.environ["GK_GEMM256_GROUPM"] = {"5g": "8", "5h": "16", "5i": "2"}.get(algo, "4")
+        algo_arg = 5 if algo in ("5m", "5o", "5r", "5", "5g", "5h", "5i") else algo
         if ks > 1 and Cs.shape[0] < ks:
             Cs = torch.empty(ks, M, N, device=dev)
         d = dict(A=A.data_ptr(), lda=K, B=B.data_ptr(), ldb=K, C=Cs.data_ptr(), ldc=N, M=M, N=N, K=K,
@@ -79,6 +81,8 @@ for name, M, N, K, sp in SHAPES:
             rs = torch.empty(ks, M, device=dev)
             d["rowsumA"] = rs.data_ptr()
         tag = f"algo{algo}" + (f"s{ks}" if algo_arg in (3, 5) else "")
+        if tag in row or f"{tag}_us" in row:
+            tag += "b"   # a repeated variant (order check)
         try:
             us = timeit(lambda: C.gemm_nt(d, s))
         except RuntimeError as e:
