@@ -55,6 +55,7 @@ Generator::Generator(const GenDims& d, const float* params, const std::map<std::
   rf_ = arena_.get<float>(orf); ids_ = arena_.get<int>(oids); alive_ = arena_.get<int>(oal);
   out_ = arena_.get<unsigned char>(oout);
   HIP_CHECK(hipStreamCreateWithFlags(&cap_, hipStreamNonBlocking));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&err_pin_), 64, hipHostMallocDefault));
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
   if (const char* sa = std::getenv("GK_STEP_ALGO")) step_algo_ = std::atoi(sa);   // 0 auto, 1 reg, 2 LDS
@@ -73,6 +74,7 @@ bool Generator::uses_persist(int n) const {
 Generator::~Generator() {
   graphs_.clear();
   if (cap_) (void)hipStreamDestroy(cap_);
+  if (err_pin_) (void)hipHostFree(err_pin_);
 }
 
 void Generator::refresh_weights(hipStream_t s) {
@@ -262,7 +264,8 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
   const int ML = d_.max_len;
   // the error word covers the whole call: every batch ORs its bits in, read_error() reports them all
   // (a persistent launch's spin-limit bit 32 is taken out again below once its batch is regenerated)
-  HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
+  if (!err_clean_) HIP_CHECK(hipMemsetAsync(err_, 0, 16, s));
+  err_clean_ = false;
   for (int start = 0; start < N; start += Bmax_) {
     const int n = std::min(Bmax_, N - start);
     bool persist_done = false;
@@ -298,9 +301,12 @@ void Generator::generate(const float* rf, int N, unsigned char* out, hipStream_t
       // small batch, latency-bound launch: check its error word now.  A spin timeout means the
       // workgroups were not co-resident (something else held CUs): the batch's output is garbage,
       // so say so, stop using the persistent path and regenerate the batch on the per-char graph.
-      unsigned e = 0;
-      HIP_CHECK(hipMemcpyAsync(&e, err_, 4, hipMemcpyDeviceToHost, s));
+      // (pinned host word: 138 vs 146-150 us per 1-name call against a pageable one; skipping the
+      // next call's memset after a clean call another ~2 us: profiles/r5_gen_err_readback_ab.txt)
+      HIP_CHECK(hipMemcpyAsync(err_pin_, err_, 4, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
+      const unsigned e = *reinterpret_cast<volatile unsigned*>(err_pin_);
+      if (e == 0 && start + n >= N) err_clean_ = true;   // the call ends here, word still 0
       persist_done = !(e & 32u);
       if (!persist_done) {
         std::fprintf(stderr, "[generator] persistent launch hit its spin limit (error word %u): "

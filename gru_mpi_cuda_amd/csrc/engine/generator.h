@@ -86,6 +86,10 @@ class Generator {
   unsigned char* out_;
   float *gh_ = nullptr, *gi_ = nullptr, *logits_ = nullptr;   // fp32 mode: [Bmax][3H] x2, [Bmax][V]
   unsigned* err_ = nullptr;
+  unsigned* err_pin_ = nullptr;   // pinned host word: the persistent launch's error-word read-back
+  // the device error word is known to be zero (the last call ended on a persistent launch that read
+  // it back as 0, nothing queued since): the next call skips its clearing memset
+  bool err_clean_ = false;
   bool persist_ = true;
   bool inject_ = false;
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
