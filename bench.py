@@ -216,7 +216,7 @@ def main() -> int:
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
                        "overlap": cfg.overlap, "plan": plan, "shard_optim": cfg.shard_optim,
-                       "dp_pipeline": (tr.t.dp_pipeline() if args.impl == "hip" and hasattr(tr, "t") else 0),
+                       "dp_pipeline": (int(tr.t.dp_tail_recorded()) if args.impl == "hip" and hasattr(tr, "t") else 0),
                        "collectives": (len(tr.t.allreduce_log()) if args.impl == "hip" and comm is not None
                                        and hasattr(tr, "t") else 0)},
             "rccl_ranks": comm.count() if comm is not None else (world if ctx.backend != "none" else 1),

@@ -165,6 +165,10 @@ def build_host_tools(force: bool = False) -> list:
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.join(HERE, "bin"), exist_ok=True)
+    # the sidecar must describe the bytes the objects are compiled FROM: hash before compiling, and
+    # refuse to stamp a build whose sources changed while it ran (an edit mid-build would otherwise
+    # label an old-source binary with the new tree's hash and defeat the stale-binary guard)
+    src_hash = source_hash()
     hdr = _headers_digest()
     srcs = KERNELS + ENGINE + PYBIND + [s for s in CAPI + DRIVER if os.path.exists(os.path.join(CSRC, s))]
     jobs = jobs or min(8, os.cpu_count() or 4, 16)
@@ -182,9 +186,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
                   libs=[f"-L{os.path.join(HERE, 'bin')}", "-lnamegen", "-lrccl", "-lhipblaslt", "-lrocprofiler-sdk-roctx",
                         f"-Wl,-rpath,{os.path.join(HERE, 'bin')}", "-Wl,-rpath,$ORIGIN"])
     build_host_tools(force)
+    if source_hash() != src_hash:
+        raise RuntimeError("build_ext: csrc/ changed while building; run the build again")
     tmp = hash_path() + ".tmp"
     with open(tmp, "w") as fh:
-        fh.write(source_hash() + "\n")
+        fh.write(src_hash + "\n")
     os.replace(tmp, hash_path())
     if verbose:
         print(f"[build_ext] {ext_path()} ({len(srcs)} sources, arch {ARCH}, src {built_hash()[:16]})")

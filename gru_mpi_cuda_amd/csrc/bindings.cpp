@@ -128,6 +128,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_shard_optim", &Trainer::set_shard_optim)
       .def("set_dp_pipeline", &Trainer::set_dp_pipeline)
       .def("dp_pipeline", &Trainer::dp_pipeline)
+      .def("dp_tail_recorded", &Trainer::dp_tail_recorded)
       .def("shard_optim", &Trainer::shard_optim)
       .def("shard_chunk", &Trainer::shard_chunk)
       .def("gather_opt_state", [](Trainer& t, uintptr_t s) { t.gather_opt_state(S(s)); })
@@ -156,6 +157,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_persist_max", &Generator::set_persist_max)
       .def("set_persist_dbg", [](Generator& g, uintptr_t p) { g.set_persist_dbg(reinterpret_cast<unsigned long long*>(p)); })
       .def("uses_persist", &Generator::uses_persist)
+      .def("set_global_names", &Generator::set_global_names)
       .def("inject_persist_error", &Generator::inject_persist_error)
       .def("dump_graph", &Generator::dump_graph);
 
@@ -253,7 +255,7 @@ PYBIND11_MODULE(_C, m) {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
     d["fwd64"] = v.fwd64; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["dwfc_group"] = v.dwfc_group;
-    d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring;
+    d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring; d["fwd_fc"] = v.fwd_fc;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -268,7 +270,26 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "bwd16") v.bwd16 = x;
       else if (k == "bwd_xring") v.bwd_xring = x;
       else if (k == "fwd_xring") v.fwd_xring = x;
+      else if (k == "fwd_fc") v.fwd_fc = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
+    }
+  });
+  m.def("gemm_variants", []() {
+    const GemmVariants& v = gemm_variants();
+    py::dict d;
+    d["mfma"] = v.mfma; d["phased"] = v.phased; d["sched"] = v.sched; d["groupm"] = v.groupm;
+    return d;
+  });
+  m.def("set_gemm_variants", [](py::dict d) {
+    GemmVariants& v = gemm_variants();
+    for (auto kv : d) {
+      const std::string k = py::str(kv.first);
+      const int x = kv.second.cast<int>();
+      if (k == "mfma") v.mfma = x;
+      else if (k == "phased") v.phased = x;
+      else if (k == "sched") v.sched = x;
+      else if (k == "groupm") v.groupm = x;
+      else throw std::runtime_error("set_gemm_variants: unknown field " + k);
     }
   });
   m.def("bwd_seq_supported", &gru_bwd_seq_supported);
@@ -297,6 +318,30 @@ PYBIND11_MODULE(_C, m) {
     HIP_LAUNCH_CHECK();
   });
   m.def("fwd_seq2_supported", &gru_fwd_seq2_supported);
+  m.def("fwd_seq_fc_supported", &gru_fwd_seq_fc_supported);
+  m.def("fwd_seq_fc", [](py::dict d, py::dict fd, uintptr_t s) {
+    SeqFwdArgs a;
+    a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);
+    a.HF = GP(u16, d, "HF"); a.xch = GP(u16, d, "xch");
+    a.sr = GP(float, d, "sr"); a.sz = GP(float, d, "sz"); a.sn = GP(float, d, "sn"); a.sghn = GP(float, d, "sghn");
+    a.Whh = GP(const u16, d, "Whh"); a.bhh = GP(const float, d, "bhh");
+    a.P = GP(const float, d, "P"); a.ids = GP(const int, d, "ids"); a.Gi = GP(const float, d, "Gi");
+    a.h0 = GP(const float, d, "h0");
+    a.cnt = GP(unsigned, d, "cnt"); a.err = GP(unsigned, d, "err");
+    a.dbg = GP(unsigned long long, d, "dbg"); a.allow_local = get<int>(d, "allow_local", 1);
+    a.xring = get<int>(d, "xring", 0);
+    a.T = get<int>(d, "T", 0); a.Bp = get<int>(d, "Bp", 0); a.H = get<int>(d, "H", 0);
+    SeqFcArgs f;
+    f.Wf = GP(const u16, fd, "Wf"); f.WTf = GP(const u16, fd, "WTf"); f.b = GP(const float, fd, "b");
+    f.labels = GP(const int, fd, "labels"); f.inv_count = GP(const float, fd, "inv_count");
+    f.dy = GP(float, fd, "dy"); f.dlF = GP(u16, fd, "dlF"); f.loss_part = GP(float, fd, "loss_part");
+    f.dW = GP(float, fd, "dW"); f.db = GP(float, fd, "db"); f.V = get<int>(fd, "V", 0);
+    f.probe = get<int>(fd, "probe", 0);
+    if (!a.xch || !a.cnt || !a.HSb || !a.HSf || !a.Whh || !a.bhh) throw std::runtime_error("fwd_seq_fc: HSb/HSf/xch/cnt/Whh/bhh required");
+    if (!gru_fwd_seq_fc_supported(a.H, a.Bp, f.V)) throw std::runtime_error("fwd_seq_fc: shape not supported");
+    gru_fwd_seq_fc(a, f, S(s));
+    HIP_LAUNCH_CHECK();
+  });
   m.def("fwd_seq", [](py::dict d, uintptr_t s) {
     SeqFwdArgs a;
     a.HSb = GP(u16, d, "HSb"); a.HSf = GP(float, d, "HSf"); a.HT = GP(u16, d, "HT"); a.ldT = get<int>(d, "ldT", 0);

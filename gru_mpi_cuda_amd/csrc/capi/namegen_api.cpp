@@ -158,6 +158,7 @@ static void namegen_impl(int N, float* random_floats, char* output) {
   if (st.comm) st.comm->scatterv_f32(rf, cnt.data(), dsp.data(), rf, 0, st.s);
   // the root's slice sits at its displacement of the full buffer; another rank's at offset 0
   const size_t in_off = root ? (size_t)dsp[me] : 0, out_off = root ? (size_t)odsp[me] : 0;
+  st.gen->set_global_names(N);   // the same precision path at every world size
   if (my_names > 0) st.gen->generate(rf + in_off, (int)my_names, out + out_off, st.s);
   if (st.comm) st.comm->gatherv_u8(out, ocnt.data(), odsp.data(), out, 0, st.s);
   if (root && N > 0) HIP_CHECK(hipMemcpyAsync(output, out, (size_t)N * (ML + 1), hipMemcpyDeviceToHost, st.s));

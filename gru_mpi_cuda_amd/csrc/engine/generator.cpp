@@ -67,8 +67,11 @@ bool Generator::uses_persist(int n) const {
   // bf16 mode: only where the persistent fp32 launch is faster than the bf16 per-char graph (up to
   // 40 names: 29.0 vs 33.2 us per char at 32, 33.7 vs 34.0 at 40, 34.8 vs 34.6 at 48 on the
   // reference model, launches included, profiles/r5_gen_persist_vs_bf16_graph.jsonl)
-  const int cap = d_.fp32 ? persist_max_ : std::min(persist_max_, persist_max_bf16_);
-  return persist_ && n <= cap && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
+  // The bf16 mode's choice is PRECISION-visible (the persistent launch runs exact fp32), so it follows
+  // the job's global name count when the caller gave one (set_global_names): a data-parallel call
+  // then picks the same arithmetic on every world size.  fp32 mode: both paths are fp32.
+  if (!d_.fp32 && std::max(n, global_n_) > persist_max_bf16_) return false;
+  return persist_ && n <= persist_max_ && gen_persist_supported(d_.H, d_.L, d_.V, n, d_.max_len);
 }
 
 Generator::~Generator() {

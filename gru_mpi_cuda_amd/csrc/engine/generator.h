@@ -42,6 +42,8 @@ class Generator {
   void set_persist_max(int n) { persist_max_ = n; }
   void set_persist_dbg(unsigned long long* p) { persist_dbg_ = p; }   // diagnostic stamps (nullable)
   bool uses_persist(int n) const;
+  // names in the whole (data-parallel) job; 0 = unknown (then the per-call count decides)
+  void set_global_names(int n) { global_n_ = n > 0 ? n : 0; }
   unsigned read_error();   // blocking: device error word (fp32 path: bit 4 = char id out of range)
   // fault injection (tests): the next persistent launch starts with its spin-timeout bit set, as if
   // an earlier wait had given up -- generate() must notice and regenerate the batch
@@ -92,6 +94,7 @@ class Generator {
   bool err_clean_ = false;
   bool persist_ = true;
   bool inject_ = false;
+  int global_n_ = 0;            // set_global_names
   int persist_max_ = 64;        // names per batch up to which the persistent launch is used
   int persist_max_bf16_ = 40;   // ... in the bf16 mode (it runs exact fp32, faster up to ~40 names:
                                 // profiles/r5_gen_persist_vs_bf16_graph_final.jsonl)

@@ -147,6 +147,7 @@ class Trainer {
   // dp_pipe_: -1 auto (= off: measured slower, dp_pipe_on), 0 one collective (the single-bucket
   // step), 1 on.
   int dp_pipe_ = -1;
+  bool dp_tail_rec_ = false;
   bool dp_pipe_on() const;
   bool opt_in_fb_ = false;   // record_fb_seq recorded the optimiser itself (pipelined tail)
   void record_dp_tail_l1(hipStream_t s, SlabJobs& j, const SlabJobs& fc_tail);
@@ -168,6 +169,9 @@ class Trainer {
   // pipelined data-parallel tail (see dp_pipe_): -1 auto, 0 off, 1 on; takes effect at the next capture
   void set_dp_pipeline(int mode);
   int dp_pipeline() const { return dp_pipe_on() ? 1 : 0; }
+  // whether the last recorded step actually contains the pipelined tail (a capture fallback or an
+  // eager step records the single-collective structure whatever dp_pipeline() says)
+  bool dp_tail_recorded() const { return dp_tail_rec_; }
   // Sharded optimiser step (ZeRO-1 style, data-parallel only; call after set_comm).  The step graph
   // reduce-scatters the flat fp32 gradient in place (rank r owns floats [r*c, (r+1)*c), c a multiple
   // of 4; the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the masters and
@@ -224,6 +228,9 @@ class Trainer {
   void wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, int N, int K, float* slab,
                   float* rowsum, hipStream_t s);
   bool persist_fwd_ = false;
+  // one-layer H = 512, V = 256: the FC head runs as consumer workgroups of the persistent forward
+  // (gru_fwd_seq_fc): no fc_xent launch, no dW_fc GEMM; decided per trainer (StepLdsVariants::fwd_fc)
+  bool fc_in_fwd_ = false;
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)

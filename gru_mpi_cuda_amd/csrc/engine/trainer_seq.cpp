@@ -135,6 +135,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   ev_next_ = 0;
   fc_held_on_ = false;
   if (dp) { ar_ready_ = ar_launched_ = 0; ar_busy_ = false; ar_log_.clear(); }
+  dp_tail_rec_ = false;
   // Flag blocks: forward(l) at cnt_ + l*fw, backward(l) at cnt_ + (L+l)*fw.  Each persistent
   // kernel zeroes the block of the kernel that follows it (forward(l) -> backward(l) ->
   // next step's forward(l)), so no memset node is needed; a block whose partner runs per-step
@@ -189,6 +190,14 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       w2.Wih = Ls_[l + 1].Wih; w2.bih = P("bias_ih_l" + std::to_string(l + 1));
       gru_fwd_seq2(w2, s);
       ++l;
+    } else if (persist_fwd_ && fc_in_fwd_) {
+      // the FC head's consumer workgroups in the same launch (fc_xent + dW_fc K-slices' work)
+      SeqFwdArgs a = fwd_args(l);
+      a.HT = nullptr;   // its only reader at L = 1 was the dW_fc GEMM
+      SeqFcArgs f;
+      f.Wf = WfcF; f.WTf = WfcTF; f.b = P("fc.bias"); f.labels = labels_; f.inv_count = inv_count_;
+      f.dy = y.dy; f.dlF = dlT_; f.loss_part = loss_part_; f.dW = slab_fc2_; f.db = rs_fc2_; f.V = V;
+      gru_fwd_seq_fc(a, f, s);
     } else if (persist_fwd_) {
       gru_fwd_seq(fwd_args(l), s);
     } else {
@@ -198,7 +207,11 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
   // ------------------------------------------------------------------ FC + loss + dH
   Layer& top = Ls_[L - 1];
   SlabJobs tail;   // reductions deferred to the last multi-tensor reduce (layer 0's)
-  {
+  if (fc_in_fwd_) {
+    // done inside the forward launch: loss partials, dy, and one dW_fc / db_fc partial per row block
+    tail.add(slab_fc2_, B / 32, (long)V * H, G("fc.weight"));
+    tail.add(rs_fc2_, B / 32, V, G("fc.bias"));
+  } else {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
     f.labels = labels_; f.inv_count = inv_count_;
@@ -429,8 +442,8 @@ void Trainer::record_dp_tail_l1(hipStream_t s, SlabJobs& j, const SlabJobs& fc_t
   hipEvent_t ar1 = ev();
   HIP_CHECK(hipEventRecord(ar1, sc_));
   // beside AR1: the dW_fc K-slices (held back from before the backward) and their slab reduce
-  if (!fc_held_on_) throw std::runtime_error("pipelined data-parallel tail: the dW_fc GEMM was not held");
-  gemm_nt(fc_held_, s);
+  if (fc_held_on_) gemm_nt(fc_held_, s);
+  else if (!fc_in_fwd_) throw std::runtime_error("pipelined data-parallel tail: the dW_fc GEMM was not held");
   fc_held_on_ = false;
   if (fc_tail.n) {
     SlabJobs f;
@@ -455,6 +468,7 @@ void Trainer::record_dp_tail_l1(hipStream_t s, SlabJobs& j, const SlabJobs& fc_t
   record_opt(s, 2);
   ar_busy_ = false;
   opt_in_fb_ = true;
+  dp_tail_rec_ = true;
 }
 
 // dEmb = dP · W_ih0 and dW_ih0 = dP^T · Emb from the layer-0 table gradient dP.  dP_fp32 may
@@ -533,7 +547,7 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
 
 std::string Trainer::plan() const {
   std::string p = std::string("fwd=") +
-                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : "persistent") : "per-step");
+                  (persist_fwd_ ? (fwd_wave_ ? "persistent+wave" : fc_in_fwd_ ? "persistent+fc" : "persistent") : "per-step");
   for (size_t l = 0; l < seq_.size(); ++l) {
     p += " bwd" + std::to_string(l) + "=" +
          (seq_[l].bwd ? (seq_[l].rows16 ? "persistent16" : "persistent") : seq_[l].big ? "persistent-big" : "per-step");

@@ -526,9 +526,13 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
 // in-process).  Default: 32x32x16 only for short K-slices (<= 256), where it measured faster --
 // h2048 dH 65536 x 2048 x 256: 438 vs 360 TF -- and 16x16x32 elsewhere (sq8192 1284 vs 1203 TF,
 // h2048 dW_hh 4-way split 1139 vs 1073 TF; profiles/r3_gemm256_m32.jsonl)
+GemmVariants& gemm_variants() {
+  static GemmVariants v;
+  return v;
+}
 static int gemm256_mfma(int kper) {
-  const char* e = std::getenv("GK_GEMM256_MFMA");
-  if (e && e[0]) return std::atoi(e);
+  const int m = gemm_variants().mfma;
+  if (m == 16 || m == 32) return m;
   return kper <= 256 ? 32 : 16;
 }
 // The phased, staggered pipeline (gemm256p_kernel) for the 16x16x32 form: GK_GEMM256_PHASED=1
@@ -539,10 +543,8 @@ static int gemm256_mfma(int kper) {
 // (with its bias) took 140.7 us on it against 122.6 on gemm256_kernel (r5_c5_step_summary_final.txt,
 // r5_c5_step_summary_dp256.txt), so the plain products stay where they were
 static int gemm256_phased_mode() {
-  const char* e = std::getenv("GK_GEMM256_PHASED");
-  if (e && e[0] == '0') return 0;
-  if (e && e[0] == '1') return 1;
-  return -1;
+  const int p = gemm_variants().phased;
+  return p == 0 || p == 1 ? p : -1;
 }
 static bool gemm256_phased() { return gemm256_phased_mode() != 0; }
 
@@ -578,13 +580,12 @@ void gemm256(const GemmArgs& a, hipStream_t s) {
   // where the A pieces of k-tile kt+2 are issued: SC 1 (two in R4(kt), the rest in R1(kt+1), no
   // segment with more than 4 LDS-DMA pieces) up to 128 k-tiles per workgroup, SC 0 (all in R4(kt),
   // four phases of slack) for the long-K products that stream their operands from memory
-  // (profiles/r5_gemm_stagger_sc_ab.jsonl); GK_GEMM256_SCHED=0 / 1 forces one
-  const char* sce = std::getenv("GK_GEMM256_SCHED");
-  const int sc = sce && sce[0] ? (sce[0] == '1' ? 1 : 0) : (kper / kBK <= 128 ? 1 : 0);
+  // (profiles/r5_gemm_stagger_sc_ab.jsonl); GemmVariants::sched = 0 / 1 forces one
+  const int scv = gemm_variants().sched;
+  const int sc = scv == 0 || scv == 1 ? scv : (kper / kBK <= 128 ? 1 : 0);
   // raster run length of the staggered kernel: 4 tile-rows; 2 / 8 / 16 measured, none better across
-  // shapes (profiles/r5_gemm_groupm_ab.jsonl), GK_GEMM256_GROUPM=n overrides
-  const char* gme = std::getenv("GK_GEMM256_GROUPM");
-  const int gmr = gme && gme[0] ? std::max(1, std::atoi(gme)) : 4;
+  // shapes (profiles/r5_gemm_groupm_ab.jsonl); GemmVariants::groupm for A/B runs only
+  const int gmr = std::max(1, gemm_variants().groupm);
   // the 32x32 form and the unphased 16x16 kernel have 256-row tiles only
   const int bm = (form == 32 || !phased) ? 256 : bm_best;
   if (a.M % bm) throw std::runtime_error("gemm256: M not a multiple of the tile rows");

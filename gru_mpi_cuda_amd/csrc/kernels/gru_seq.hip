@@ -36,22 +36,368 @@ namespace gk {
 // (Rejected and removed in round 4, history in docs/DESIGN.md §6.3: a table-free layer 0 computing
 // its P-table columns in every workgroup, layer 0's input projection in the post-publish slack, the
 // FC / softmax-xent pipeline inside the forward, and the saves issued inside the publish drain.)
-template <int NKW, int RS>
-__global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float part[8][6][256];
+// FC = true (gru_fwd_seq_fc): the same recurrence in blocks [0, H/16 * Bp/32), plus kFcCons FC
+// consumer workgroups per row block behind them in the same grid (fwd_fc_consumer below); the
+// recurrence then also drains its h copies before each step's first barrier and signals T + 1
+// after the last step, so a consumer that saw epoch t + 2 may read HSb / HF of step t.
+static constexpr size_t kFwdRecLds = sizeof(float) * 8 * 6 * 256 + sizeof(u16) * 32 * 24 + sizeof(u16) * 16 * 40;
+static constexpr size_t kFwdFcLds = sizeof(u16) * 32 * (512 + 8) + sizeof(u16) * 32 * (256 + 8) +
+                                    sizeof(float) * (2 * 8 * 32 + 3 * 32);
+
+// ---------------------------------------------------------------------------- FC consumers
+// Workgroup ci of the consumer part of gru_fwd_seq_fc's grid serves row block rbk = ci % nrb as its
+// consumer c = ci / nrb (placed on rbk's XCD by the dispatcher's round-robin; the placement census
+// covers producers and consumers, so a row block whose members are not all on one XCD takes the
+// write-through protocol for every hand-off).  Two phases, both behind the recurrence:
+//  1. items: step t = c, c + kFcCons, ... of the row block -- the 32 x V logits of h_t (X tile read
+//     from HSb once the row block's producers signalled t + 2, W_fc fragments already in flight),
+//     softmax-xent, the loss partial, dl as bf16 fragment blocks (dlF), dy_t = dl · W_fc (fp32); then
+//     the consumer's own flag line carries "items done".
+//  2. dW_fc: consumer c owns the 64 x 64 tile c of the row block's V x H partial and accumulates
+//     dl_t^T h_t over t = 0 .. T-1 in order (one flag check per step: the item of step t done), from
+//     dlF and the backward's fragment-tiled HF copy -- K = 32 rows per step, one MFMA per 16 x 16
+//     tile; the tiles of unit column 0 also take db_fc (row sums of dl^T, an MFMA against ones).
+//     The row block's partial lands in slab rbk (the trainer's dW_fc / db_fc slabs, summed in Adam).
+// The recurrence never waits on a consumer.  This is the FC / softmax-xent / dH work of fc_xent and
+// the dW_fc K-slices of the post-backward group, off the step's serial tail (VERDICT r5 item 1;
+// reference: the per-char FC + softmax of /root/reference/namegensf.cu:856-873).
+template <int H>
+DEV void fwd_fc_consumer(const SeqFwdArgs& a, const SeqFcArgs& f, unsigned char* smem, int ci) {
+  constexpr int V = 256, NW = 8, LDX = H + 8, LDR = V + 8, NKS = H / 32, NKC = 4;
+  static_assert((V / 64) * (H / 64) == kFcCons, "one 64 x 64 dW_fc tile per consumer");
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: fragment offsets go to soffset
+  const int T = a.T, Bp = a.Bp, nrb = Bp / 32;
+  constexpr int nunit = H / 16;
+  const int rbk = ci % nrb, c = ci / nrb, b0 = rbk * 32;
+  unsigned* const fl = a.cnt + (size_t)rbk * (nunit + kFcCons) * kFlagStride;   // producers' lines
+  unsigned* const cfl = fl + (size_t)nunit * kFlagStride;                       // consumers' lines
+  const int probe = f.probe & 7;
+  if (probe == 3) return;
+  const bool loc = a.allow_local && row_block_local(fl, nunit + c, nunit + kFcCons, a.err);
+  if (probe == 1) return;
+  u16* xs = reinterpret_cast<u16*>(smem);              // [32][H + 8] X tile
+  u16* dlr = xs + 32 * LDX;                            // [32][V + 8] dl row-major (dH A operand)
+  float* red = reinterpret_cast<float*>(dlr + 32 * LDR);   // [2][8][32] row max / sum-exp partials
+  float* lab = red + 2 * NW * 32;                      // [32] label logit
+  float* lrow = lab + 32;                              // [32] row loss
+  int* ys = reinterpret_cast<int*>(lrow + 32);         // [32] labels
+  const rsrc_t rH = make_rsrc(a.HSb, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+  const rsrc_t rD = make_rsrc(f.dlF, (unsigned)((size_t)T * Bp * V * 2));
+  const int v0 = w * 32;
+  float bias[2];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) bias[cc] = f.b[v0 + cc * 16 + lr];
+  // W_fc fragments (FT layout, 1 KB per load instruction): wave w's 2 vocab tiles, k-steps ks..ks+NKC;
+  // buffer loads with the lane's 16 B in the VGPR offset and the block in the scalar offset (64-bit
+  // VGPR addresses per fragment pushed the consumer past its 128-register budget)
+  const rsrc_t rWf = make_rsrc(f.Wf, (unsigned)(V * H * 2)), rWt = make_rsrc(f.WTf, (unsigned)(V * H * 2));
+  const unsigned l16 = (unsigned)lane * 16u;
+  auto load_w = [&](bf16x8 (&b)[NKC][2], int ks) {
+    if (probe == 4) {   // diagnostic: the items without their weight stream
+#pragma unroll
+      for (int kk = 0; kk < NKC; ++kk) b[kk][0] = b[kk][1] = zero8();
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < NKC; ++kk)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) b[kk][cc] = ld8_plain_s(rWf, l16, ((v0 / 16 + cc) * NKS + ks + kk) * 1024);
+  };
+  auto mma_w = [&](f32x4 (&acc)[2][2], const bf16x8 (&b)[NKC][2], int ks) {
+#pragma unroll
+    for (int kk = 0; kk < NKC; ++kk) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(xs + (r * 16 + lr) * LDX + (ks + kk) * 32 + 8 * lq);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) acc[r][cc] = mfma16(af[r], b[kk][cc], acc[r][cc]);
+    }
+  };
+  // W_fc^T fragments of wave w's 64 dH columns, two k-steps of V
+  auto load_wt = [&](bf16x8 (&b)[2][4], int kk0) {
+    if (probe == 4) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) b[kk][cc] = zero8();
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) b[kk][cc] = ld8_plain_s(rWt, l16, ((w * 4 + cc) * (V / 32) + kk0 + kk) * 1024);
+  };
+  auto mma_t = [&](f32x4 (&acc)[2][4], const bf16x8 (&b)[2][4], int kk0) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) af[r] = *reinterpret_cast<const bf16x8*>(dlr + (r * 16 + lr) * LDR + (kk0 + kk) * 32 + 8 * lq);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) acc[r][cc] = mfma16(af[r], b[kk][cc], acc[r][cc]);
+    }
+  };
+
+  // ---- phase 1: the FC items of this consumer
+  for (int t = c; t < T; t += kFcCons) {
+    const int m0 = t * Bp + b0;
+    bf16x8 wa[NKC][2], wb[NKC][2];
+    load_w(wa, 0);
+    load_w(wb, NKC);
+    const int ylab = tid < 32 ? f.labels[m0 + tid] : 0;
+    const float inv = f.inv_count[0];
+    // h_t of the whole row block is in HSb once every producer signalled t + 2 (T + 1: the final signal).
+    // The producers' flag lines are the recurrence's own hot lines: until this item is near, one lane
+    // polls one of them with a long back-off (a full 32-lane sweep every ~100 clocks by each waiting
+    // consumer measured +0.7 us per recurrence step), then the sweep of all producers.
+    if (tid < 64) {
+      SpinBudget spin(a.err);
+      for (;;) {
+        unsigned v = 0;
+        if (lane == 0) v = __hip_atomic_load(fl + (size_t)(c % nunit) * kFlagStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __builtin_amdgcn_readfirstlane(v);
+        if (v + 1u >= (unsigned)(t + 2)) break;
+        __builtin_amdgcn_s_sleep(16);
+        if (spin.expired()) break;   // the full wait below reports it
+      }
+    }
+    wait_flags(fl, nunit, (unsigned)(t + 2), a.err);
+    stamp(a.dbg, t, 0);
+    constexpr int NXP = 32 * H / 8 / 512;
+    u32x4 xv[NXP];
+#pragma unroll
+    for (int e = 0; e < NXP; ++e) {
+      const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+      xv[e] = __builtin_amdgcn_raw_buffer_load_b128(rH, (unsigned)((((size_t)(t + 1) * Bp + b0 + row) * H + c8 * 8) * 2), 0, 16);
+    }
+#pragma unroll
+    for (int e = 0; e < NXP; ++e) {
+      const int q = tid + e * 512, row = q / (H / 8), c8 = q % (H / 8);
+      *reinterpret_cast<u32x4*>(xs + row * LDX + c8 * 8) = xv[e];
+    }
+    if (tid < 32) ys[tid] = ylab;
+    lds_barrier();
+    stamp(a.dbg, t, 1);
+    f32x4 acc[2][2];
+    zero_acc(acc);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ks += 2 * NKC) {
+      mma_w(acc, wa, ks);
+      if (ks + 2 * NKC < NKS) load_w(wa, ks + 2 * NKC);
+      mma_w(acc, wb, ks + NKC);
+      if (ks + 3 * NKC < NKS) load_w(wb, ks + 3 * NKC);
+    }
+    bf16x8 ta[2][4], tb[2][4];   // the dH pass's first W_fc^T fragments, under the softmax
+    load_wt(ta, 0);
+    load_wt(tb, 2);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[r][cc][i] += bias[cc];
+    // softmax statistics across the 8 waves' columns
+    float mx[2][4];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float m = max16(fmaxf(acc[r][0][i], acc[r][1][i]));
+        if (lr == 0) red[w * 32 + r * 16 + lq * 4 + i] = m;
+      }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r * 16 + lq * 4 + i;
+        float m = red[row];
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+        mx[r][i] = m;
+        const float e = sum16(__expf(acc[r][0][i] - m) + __expf(acc[r][1][i] - m));
+        if (lr == 0) red[NW * 32 + w * 32 + row] = e;
+      }
+    lds_barrier();
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      u16 dv[2][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r * 16 + lq * 4 + i;
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
+        const int y = ys[row];
+        const float scale = (y >= 0) ? inv : 0.f;
+        const float rs = __builtin_amdgcn_rcpf(sum);
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+          const int col = v0 + cc * 16 + lr;
+          const float x = acc[r][cc][i];
+          if (col == y) lab[row] = x;
+          const float d = (__expf(x - mx[r][i]) * rs - (col == y ? 1.f : 0.f)) * scale;
+          dv[cc][i] = f2bf(d);
+          dlr[row * LDR + col] = dv[cc][i];
+        }
+      }
+      // dlF block (t, rbk, vocab tile): lane L holds rows 8(L >> 4) .. +8 of vocab column L & 15; this
+      // lane's 4 rows r*16 + 4lq .. +4 are half of lane (2r + lq/2)*16 + lr's slot
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const unsigned lo = (unsigned)dv[cc][0] | ((unsigned)dv[cc][1] << 16);
+        const unsigned hi = (unsigned)dv[cc][2] | ((unsigned)dv[cc][3] << 16);
+        const unsigned off = (unsigned)(((((size_t)(t * nrb + rbk) * (V / 16) + v0 / 16 + cc) * 64 +
+                                          (2 * r + (lq >> 1)) * 16 + lr) * 8 + (lq & 1) * 4) * 2);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 pv = {lo, hi};
+        if (loc) __builtin_amdgcn_raw_buffer_store_b64(pv, rD, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(pv, rD, off, 0, 16);
+      }
+    }
+    lds_barrier();   // dl row-major and the label logits in LDS
+    stamp(a.dbg, t, 2);
+    if (tid < 32) {
+      const int row = tid, y = ys[row];
+      float m = red[row], sum = 0.f;
+      for (int ww = 1; ww < NW; ++ww) m = fmaxf(m, red[ww * 32 + row]);
+      for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
+      lrow[row] = (y >= 0) ? (logf(sum) + m - lab[row]) * inv : 0.f;
+    }
+    // dy_t = dl · W_fc: wave w's 64 columns, K = V
+    f32x4 dacc[2][4];
+    zero_acc(dacc);
+#pragma unroll
+    for (int kk0 = 0; kk0 < V / 32; kk0 += 4) {
+      mma_t(dacc, ta, kk0);
+      if (kk0 + 4 < V / 32) load_wt(ta, kk0 + 4);
+      mma_t(dacc, tb, kk0 + 2);
+      if (kk0 + 6 < V / 32) load_wt(tb, kk0 + 6);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          f.dy[(size_t)(m0 + r * 16 + lq * 4 + i) * H + w * 64 + cc * 16 + lr] = dacc[r][cc][i];
+    lds_barrier();   // lrow complete
+    if (tid == 0) {
+      float s = 0.f;
+      for (int i = 0; i < 32; ++i) s += lrow[i];
+      f.loss_part[m0 / 32] = s;
+    }
+    // item done: every wave's dlF stores complete, then one flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(a.dbg, t, 3);
+    if (tid == 0) {
+      if (loc) signal_flag_local(cfl + (size_t)c * kFlagStride, (unsigned)(t / kFcCons + 1));
+      else signal_flag(cfl + (size_t)c * kFlagStride, (unsigned)(t / kFcCons + 1));
+    }
+  }
+
+  if (probe == 2 || probe == 4) return;
+  // ---- phase 2: this consumer's 64 x 64 tile of the row block's dW_fc partial, t = 0 .. T-1 in order
+  constexpr int TPH = H / 64;
+  const int tv = (c / TPH) * 4 + (w >> 1);          // 16-row vocab tile
+  const int th = (c % TPH) * 4 + 2 * (w & 1);       // first of two 16-column unit tiles
+  const bool rs_on = (c % TPH) == 0 && (w & 1) == 0;
+  const rsrc_t rF = make_rsrc(a.HF, (unsigned)((size_t)(T + 1) * Bp * H * 2));
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  f32x4 aw[2], ab;
+  aw[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  aw[1] = aw[0];
+  ab = aw[0];
+  // steps in groups of DG: one poll covers the group's items (lane i: step t0 + i), then all of its
+  // fragments are loaded at once and accumulated in step order (deterministic)
+  constexpr int DG = 4;
+  for (int t0 = 0; t0 < T; t0 += DG) {
+    const int n = T - t0 < DG ? T - t0 : DG;
+    {
+      SpinBudget spin(a.err);
+      for (;;) {
+        bool ok = true;
+        if (lane < n)
+          ok = __hip_atomic_load(cfl + (size_t)((t0 + lane) % kFcCons) * kFlagStride, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)((t0 + lane) / kFcCons + 1);
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(8);
+        if (spin.expired()) {
+          if (lane == 0) __hip_atomic_fetch_or(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    bf16x8 A[DG], Bf[DG][2];
+#pragma unroll
+    for (int i = 0; i < DG; ++i) {
+      if (i < n) {
+        const int t = t0 + i;
+        A[i] = ld8_sc1(rD, (unsigned)((((size_t)(t * nrb + rbk) * (V / 16) + tv) * 512 + lane * 8) * 2));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          Bf[i][j] = ld8_sc1(rF, (unsigned)(((((size_t)(t + 1) * nunit + th + j) * nrb + rbk) * 512 + lane * 8) * 2));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DG; ++i) {
+      if (i < n) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) aw[j] = mfma16(A[i], Bf[i][j], aw[j]);
+        if (rs_on) ab = mfma16(A[i], ones, ab);
+      }
+    }
+  }
+  float* W = f.dW + (size_t)rbk * V * H;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) W[(size_t)(tv * 16 + lq * 4 + i) * H + (th + j) * 16 + lr] = aw[j][i];
+  if (rs_on && lr == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.db[(size_t)rbk * V + tv * 16 + lq * 4 + i] = ab[i];
+  }
+}
+
+
+template <int NKW, int RS, bool FC, int WPE = FC ? 4 : 1>
+__global__ void __launch_bounds__(512, WPE) gru_fwd_seq_kernel(SeqFwdArgs a, SeqFcArgs fc) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[FC ? (kFwdFcLds > kFwdRecLds ? kFwdFcLds : kFwdRecLds) : kFwdRecLds];
+  auto& part = *reinterpret_cast<float(*)[8][6][256]>(smem);
   // padded rows (48 B / 80 B, still 16-B aligned for the vector reads): the epilogue's per-item
   // u16 writes -- rows 4 apart within a wave -- land in distinct banks (unpadded: 2-way / 4-way)
-  __shared__ __attribute__((aligned(16))) u16 stg[32][24];
-  __shared__ __attribute__((aligned(16))) u16 stgT[16][40];
+  auto& stg = *reinterpret_cast<u16(*)[32][24]>(smem + sizeof(float) * 8 * 6 * 256);
+  auto& stgT = *reinterpret_cast<u16(*)[16][40]>(smem + sizeof(float) * 8 * 6 * 256 + sizeof(u16) * 32 * 24);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int H = a.H, Bp = a.Bp, T = a.T;
-  const int nrb = Bp / 32, ut = seq_unit_tile(nrb);
-  const int j0 = ut * 16, rbk = seq_row_block(nrb), b0 = rbk * 32;
+  const int nrb = Bp / 32;
+  const unsigned nunit = (unsigned)(H / 16);
+  if constexpr (FC) {
+    const int nrec = (int)nunit * nrb;
+    if ((int)blockIdx.x >= nrec) {
+      zero_next_flags(a.zero_next, a.zero_words);
+      if constexpr (NKW * 128 == 512 && RS == 2) fwd_fc_consumer<512>(a, fc, smem, (int)blockIdx.x - nrec);
+      return;
+    }
+  }
+  // flag lines per row block: its H/16 producers (+ its FC consumers)
+  const size_t rb_lines = nunit + (FC ? kFcCons : 0);
+  // (FC: the grid also holds the consumers, so the block -> tile map takes the recurrence's own count)
+  const int ut = FC ? seq_unit_tile_n(nrb, (int)nunit * nrb) : seq_unit_tile(nrb);
+  const int j0 = ut * 16, rbk = FC ? seq_row_block_n(nrb, (int)nunit * nrb) : seq_row_block(nrb), b0 = rbk * 32;
   const int lr = lane & 15, lk = 8 * (lane >> 4);
   constexpr int NR = RS == 2 ? 1 : 2;           // row tiles per wave
   const int rt = RS == 2 ? (w >> 2) : 0;        // first row tile of this wave
   const int k0 = (RS == 2 ? (w & 3) : w) * NKW * 32;
-  const unsigned nunit = (unsigned)(H / 16);
 
   bf16x8 bw[NKW][3];   // this wave's K-slice of W_h{r,z,n} for the 16 units, resident all sequence
 #pragma unroll
@@ -80,7 +426,10 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
   const unsigned sv_lane = (unsigned)((b * H + j) * 4);
   stamp(a.dbg, T + 1, 0);   // prologue stamps in the (unused) step slot T + 1
   zero_next_flags(a.zero_next, a.zero_words);
-  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * nunit * kFlagStride, ut, (int)nunit, a.err);
+  // (probe 3: consumers leave before the census, which then covers the producers only)
+  const int cens = FC && (fc.probe & 7) == 3 ? (int)nunit : (int)rb_lines;
+  if (FC && (fc.probe & 8)) __builtin_amdgcn_s_setprio(2);
+  const bool loc = a.allow_local && row_block_local(a.cnt + (size_t)rbk * rb_lines * kFlagStride, ut, cens, a.err);
   stamp(a.dbg, T + 1, 4);
 
   // the input projection of step t, gathered one step ahead, after the publish (its latency off
@@ -108,7 +457,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
         // h_t from the producers' exchange tiles (written at step t-1); unit u = k0 + 32kk + lk
         // lives in tile u/16 at column u%16
         const size_t slot = ((size_t)((t - 1) % xr) * nrb + rbk) * nunit;
-        wave_wait_load<NKW>(a.cnt + (size_t)rbk * nunit * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
+        wave_wait_load<NKW>(a.cnt + (size_t)rbk * rb_lines * kFlagStride, lane < 2 * NKW, k0 / 16 + lane,
                             (unsigned)t, a.err, [&](int kk) {
           const int u = k0 + kk * 32 + lk;
           const unsigned tb = (unsigned)(((slot + u / 16) * 32 + lr) * 16 + (u & 15)) * 2;
@@ -136,6 +485,11 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       for (int g = 0; g < 3; ++g)
 #pragma unroll
         for (int i = 0; i < 4; ++i) part[w][r * 3 + g][i * 64 + lane] = acc[r][g][i];
+    // FC consumers read wave 2's HF block of step t - 1 once wave 0 signals t + 1: drain it before
+    // the barrier wave 0 passes first (its exchange loads retired, so this waits on nothing else)
+    if constexpr (FC) {
+      if (w == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     stamp(a.dbg, t, 2);
     float gh[3];
@@ -166,7 +520,7 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       // drain; one signal.  Then the row-major copy for the GEMMs that read HS later.
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stg[lane >> 1][(lane & 1) * 8]);
       const unsigned xo = (unsigned)((((size_t)(t % xr) * nrb + rbk) * nunit + ut) * 512 + lane * 8) * 2;
-      unsigned* fl = a.cnt + ((size_t)rbk * nunit + ut) * kFlagStride;
+      unsigned* fl = a.cnt + ((size_t)rbk * rb_lines + ut) * kFlagStride;
       if (loc) {
         st16_plain(rX, xo, v);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -177,14 +531,18 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
         if (lane == 0) signal_flag(fl, (unsigned)(t + 1));
       }
       stamp(a.dbg, t, 4);
-      *reinterpret_cast<u32x4*>(a.HSb + ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8) = v;
+      const size_t hs = ((size_t)(t + 1) * Bp + b0 + (lane >> 1)) * H + j0 + (lane & 1) * 8;
+      if (FC && !loc) st16_sc1(rH, (unsigned)(hs * 2), v);   // write-through: FC consumers on other XCDs
+      else *reinterpret_cast<u32x4*>(a.HSb + hs) = v;
       stamp(a.dbg, t, 5);
     } else if (w == 1 && a.HT) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane >> 2][(lane & 3) * 8]);
       *reinterpret_cast<u32x4*>(a.HT + (size_t)(j0 + (lane >> 2)) * a.ldT + (size_t)(t + 1) * Bp + b0 + (lane & 3) * 8) = v;
     } else if (w == 2 && a.HF) {   // the backward's dW_hh operand: one whole 1-KB block
       const u32x4 v = *reinterpret_cast<const u32x4*>(&stgT[lane & 15][8 * (lane >> 4)]);
-      *reinterpret_cast<u32x4*>(a.HF + (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8) = v;
+      const size_t hf = (((size_t)(t + 1) * nunit + ut) * nrb + rbk) * 512 + lane * 8;
+      if (FC && !loc) st16_sc1(make_rsrc(a.HF, (unsigned)((size_t)(T + 1) * Bp * H * 2)), (unsigned)(hf * 2), v);
+      else *reinterpret_cast<u32x4*>(a.HF + hf) = v;
     }
     // the next gather, then the saves for the backward pass, AFTER the publish (not part of wave
     // 0's drain).  Saves as buffer stores: one per-lane offset for the launch, the step in the
@@ -200,6 +558,15 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq_kernel(SeqFwdArgs a) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gh[2]), rSg, sv_lane, sstep, 0);
     }
     stamp(a.dbg, t, 6);
+  }
+  if constexpr (FC) {   // h of the last step complete in HSb / HF -> epoch T + 1 for the consumers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      unsigned* fl = a.cnt + ((size_t)rbk * rb_lines + ut) * kFlagStride;
+      if (loc) signal_flag_local(fl, (unsigned)(T + 1));
+      else signal_flag(fl, (unsigned)(T + 1));
+    }
   }
 }
 
@@ -756,7 +1123,7 @@ bool gru_fwd_seq_supported(int H, int Bp) {
   if (Bp % 32) return false;
   const int rs = fwd_rs(H);
   int cap = -1;
-#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS>);
+#define X(HH, NK, RS) if (H == HH && rs == RS) cap = resident_blocks(gru_fwd_seq_kernel<NK, RS, false>);
   FWD_VARIANTS(X)
 #undef X
   return cap >= (H / 16) * (Bp / 32);
@@ -769,12 +1136,36 @@ void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
   const int rs = fwd_rs(a.H);
 #define X(HH, NK, RS)                                                          \
   if (a.H == HH && rs == RS) {                                                \
-    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS>), grid, block, 0, s, a);   \
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<NK, RS, false>), grid, block, 0, s, a, SeqFcArgs{});   \
     return;                                                                    \
   }
   FWD_VARIANTS(X)
 #undef X
   throw std::runtime_error("gru_fwd_seq: no kernel variant for this shape");
+}
+
+// The one-layer forward with the FC consumers in the same grid (H = 512, V = 256): co-residency of
+// the H/16 x Bp/32 recurrence blocks AND nrb x kFcCons consumers (two 512-thread workgroups per CU at
+// <= 128 VGPRs and ~52 KB of LDS each), and room for both in one 64-lane placement census.
+bool gru_fwd_seq_fc_supported(int H, int Bp, int V) {
+  if (H != 512 || V != 256 || Bp % 32 || fwd_rs(H) != 2) return false;
+  if (H / 16 + kFcCons > 64) return false;
+  const int cap = resident_blocks(gru_fwd_seq_kernel<4, 2, true>);
+  return cap >= (H / 16 + kFcCons) * (Bp / 32);
+}
+
+void gru_fwd_seq_fc(const SeqFwdArgs& a, const SeqFcArgs& f, hipStream_t s) {
+  if (a.H != 512 || f.V != 256 || !a.HF || !f.Wf || !f.WTf || !f.dlF || !f.dy || !f.dW || !f.db || !f.loss_part ||
+      !f.labels || !f.inv_count || !f.b)
+    throw std::runtime_error("gru_fwd_seq_fc: needs H = 512, V = 256, the HF copy and every FC buffer");
+  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
+    throw std::runtime_error("gru_fwd_seq_fc: saves exceed the 2 GB buffer-offset range");
+  const int nrb = a.Bp / 32;
+  dim3 grid((a.H / 16) * nrb + kFcCons * nrb), block(512);
+  if (f.probe & 16)   // diagnostic: the FC build without the 128-VGPR cap (cannot host consumers)
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<4, 2, true, 1>), grid, block, 0, s, a, f);
+  else
+    hipLaunchKernelGGL((gru_fwd_seq_kernel<4, 2, true>), grid, block, 0, s, a, f);
 }
 
 #define FWD2_VARIANTS(X) X(256, 1) X(512, 2) X(1024, 4)

@@ -86,10 +86,21 @@ struct StepLdsVariants {
                          // slots instead of one per step (0); docs/DESIGN.md §3.1d
   int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
                          // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
+  int fwd_fc = 0;        // one-layer H = 512, V = 256: the FC head (fc_xent + dW_fc) as consumer
+                         // workgroups inside the persistent forward launch (gru_fwd_seq_fc); 0: after it
 };
 // (Round 5 removed the measured-equal / marginal switches fwd_ns, fwd8, fwd64 = 2, fwd64_fused,
 // fwd64_all, bwd_sk_pf, bwd_sk_map and big_acq with the code only they reached; docs/DESIGN.md §7.)
 StepLdsVariants& step_lds_variants();
+// gemm256 (algo 5) forms for A/B runs and tests, set at run time (bindings set_gemm_variants); every
+// default is the measured-best rule of gemm256.hip
+struct GemmVariants {
+  int mfma = 0;     // 16 / 32: force v_mfma_f32_16x16x32 / 32x32x16; 0: by K-slice (32 up to 256 deep)
+  int phased = -1;  // 1 / 0: always / never the staggered phased pipeline; -1: by shape
+  int sched = -1;   // staggered pipeline staging schedule 0 / 1; -1: by k-tiles per workgroup
+  int groupm = 4;   // grouped raster run length (tile-rows)
+};
+GemmVariants& gemm_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
 bool gru_step_lds_ok(int H, int Bp);
 // which per-step kernel gru_fwd_step/gru_bwd_step pick for (algo, H, Bp) without fused input
@@ -129,10 +140,34 @@ struct SeqFwdArgs {
   int xring = 0;                   // h exchange as a ring of xring slots (>= 2; 0 = one per step)
   int T = 0, Bp = 0, H = 0;
 };
-// flag words a sequence kernel needs in `cnt` ([Bp/32][H/16] producers x 16-word lines); zero per launch
-inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16) * 16; }
+// FC consumer workgroups per row block of the one-layer forward with the FC head inside (gru_fwd_seq_fc)
+static constexpr int kFcCons = 32;
+// flag words a sequence kernel needs in `cnt` ([Bp/32] row blocks x (H/16 producers + kFcCons FC
+// consumers) x 16-word lines; the consumer lines are used by gru_fwd_seq_fc only); zero per launch
+inline long seq_flag_words(int H, int Bp) { return (long)(Bp / 32) * (H / 16 + kFcCons) * 16; }
 bool gru_fwd_seq_supported(int H, int Bp);
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s);
+// The FC head inside the one-layer persistent forward (gru_seq.hip fwd_fc_consumer): kFcCons extra
+// workgroups per row block, co-resident with the recurrence, compute each finished step's logits,
+// softmax-xent, loss partial, dl and dy = dl · W_fc (fc_xent's work), then the row block's dW_fc /
+// db_fc partial (the dW_fc K-slices' work) -- nothing of the FC head is left for after the forward.
+struct SeqFcArgs {
+  const u16* Wf = nullptr;          // W_fc [V][H] in the FT fragment layout (ft_offset)
+  const u16* WTf = nullptr;         // W_fc^T [H][V] in the FT fragment layout
+  const float* b = nullptr;         // b_fc [V]
+  const int* labels = nullptr;      // [T][Bp], -1 = ignore
+  const float* inv_count = nullptr; // device scalar 1 / #valid tokens
+  float* dy = nullptr;              // [T*Bp][H] fp32 dL/dh of the top layer
+  u16* dlF = nullptr;               // [T][Bp/32][V/16] 1-KB blocks of dl^T fragments (T*Bp*V bf16)
+  float* loss_part = nullptr;       // [T*Bp/32] per-32-row loss partials (fc_xent's order)
+  float* dW = nullptr;              // [Bp/32][V][H] dW_fc partial per row block
+  float* db = nullptr;              // [Bp/32][V] db_fc partial per row block
+  int V = 0;
+  int probe = 0;                    // diagnostic (scripts/probe_fwd_fc.py): 1 consumers stop after the
+                                    // census, 2 after their items (no dW_fc); 0 = everything
+};
+bool gru_fwd_seq_fc_supported(int H, int Bp, int V);
+void gru_fwd_seq_fc(const SeqFwdArgs& a, const SeqFcArgs& f, hipStream_t s);
 
 
 // Two-layer wavefront forward (gru_seq.hip gru_fwd_seq2_kernel): ONE persistent launch runs layer

@@ -27,6 +27,12 @@ DEV bf16x8 ld8_sc1s(rsrc_t r, unsigned voff, int soff) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// plain (cached) buffer load, per-lane VGPR offset + wave-uniform scalar offset: read-only operands
+DEV bf16x8 ld8_plain_s(rsrc_t r, unsigned voff, int soff) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // Every cross-workgroup wait is bounded by WALL CLOCK, not by a poll count: workgroups that start
 // late because something else holds their CUs (an RCCL kernel of a data-parallel step waiting for a
 // slow peer, another process's kernel) delay the wait without tripping it.  5 s of the 100 MHz
@@ -249,6 +255,13 @@ DEV int seq_unit_tile(int nrb) {
 }
 DEV int seq_row_block(int nrb) {
   return seq_rb_fast(nrb) ? (int)(blockIdx.x % nrb) : (int)(blockIdx.x / (gridDim.x / nrb));
+}
+// the same map over the first nblk blocks of a larger grid (the recurrence part of gru_fwd_seq_fc)
+DEV int seq_unit_tile_n(int nrb, int nblk) {
+  return seq_rb_fast(nrb) ? (int)(blockIdx.x / nrb) : (int)(blockIdx.x % (nblk / nrb));
+}
+DEV int seq_row_block_n(int nrb, int nblk) {
+  return seq_rb_fast(nrb) ? (int)(blockIdx.x % nrb) : (int)(blockIdx.x / (nblk / nrb));
 }
 
 // Exchange protocol per row block, decided once per launch from where its workgroups actually

@@ -149,6 +149,7 @@ def namegen(N: int, random_floats: np.ndarray, output: np.ndarray) -> None:
     start, count = shard(N, ctx.rank, ctx.world)
     per = -(-N // ctx.world)          # ceil: fixed slab size for the all-gather
     if _S.gen is not None:
+        _S.gen.g.set_global_names(N)   # bf16 mode: the same arithmetic path at every world size
         mine = _S.gen.generate(random_floats, start, count)
         if ctx.world > 1:
             dev = ctx.device

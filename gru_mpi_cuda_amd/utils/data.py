@@ -96,8 +96,11 @@ def make_stream(batch: int, seq: int, sos: int = 0, eos: int = 0, seed: int = 0,
     """The training loop's data source: the native prefetching loader when the extension is
     built, else the Python generator (files need the native loader)."""
     if native:
+        from ..ops._ext import StaleExtensionError
         try:
             return NativeNameStream(batch, seq, sos, eos, seed, max_len, path)
+        except StaleExtensionError:
+            raise   # a stale build must fail loudly here too, not fall back to the Python stream
         except (ImportError, OSError, AttributeError):
             if path:
                 raise

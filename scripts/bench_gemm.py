@@ -59,8 +59,8 @@ for name, M, N, K, sp in SHAPES:
     variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
     # algo 3: the one-shot small GEMM at the K-slices it takes (h512 step products)
     variants += [(3, k) for k in (1, 2, 4, 6, 8, 16) if K % k == 0 and (K // k) in (128, 192, 256, 512, 1024, 1536, 2048)]
-    # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32); "5o": the
-    # one-vmcnt(0)-per-k-tile 16x16 kernel (GK_GEMM256_PHASED=0) against the phased default
+    # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GemmVariants mfma = 32); "5o": the
+    # one-vmcnt(0)-per-k-tile 16x16 kernel (phased = 0) against the phased default
     # "5r": the phased kernel with the fused row sums of A (the weight-gradient form)
     variants += ([("5m", k) for a_, k in variants if a_ == 5] + [("5o", k) for a_, k in variants if a_ == 5]
                  + [("5r", k) for a_, k in variants if a_ == 5]
@@ -68,10 +68,9 @@ for name, M, N, K, sp in SHAPES:
     if os.environ.get("GEMM_ONLY256"):
         variants = [v for v in variants if v[0] in (5, "5", "5g", "5h", "5i")]
     for algo, ks in variants:
-        os.environ["GK_GEMM256_MFMA"] = "32" if algo == "5m" else "16"
-        os.environ["GK_GEMM256_PHASED"] = "0" if algo == "5o" else "1"
-        os.environ.pop("GK_GEMM256_SCHED", None)   # the staggered schedule picked per shape
-        os.environ["GK_GEMM256_GROUPM"] = {"5g": "8", "5h": "16", "5i": "2"}.get(algo, "4")
+        C.set_gemm_variants(dict(mfma=32 if algo == "5m" else 16, phased=0 if algo == "5o" else 1,
+                                 sched=-1,   # the staggered schedule picked per shape
+                                 groupm={"5g": 8, "5h": 16, "5i": 2}.get(algo, 4)))
         algo_arg = 5 if algo in ("5m", "5o", "5r", "5", "5g", "5h", "5i") else algo
         if ks > 1 and Cs.shape[0] < ks:
             Cs = torch.empty(ks, M, N, device=dev)

@@ -895,6 +895,50 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
         assert torch.equal(out[0][0], o[0]) and out[0][1] == o[1]
 
 
+@pytest.mark.parametrize("B,T,xcd", [(256, 32, "1"), (256, 40, "1"), (256, 12, "1"), (128, 32, "1"), (256, 32, "0")])
+def test_fc_in_forward_matches_fc_xent(B, T, xcd, monkeypatch):
+    """StepLdsVariants.fwd_fc: the FC head as consumer workgroups of the persistent forward launch
+    (gru_fwd_seq_fc) against fc_xent + the dW_fc K-slice GEMM after it (fwd_fc = 0).  The logits,
+    softmax-xent and dH run the same MFMA k order, so the loss and every gradient except dW_fc / db_fc
+    are bitwise equal; dW_fc / db_fc sum the same products per row block instead of per K-slice.
+    T = 40: consumers with two items; T = 12: consumers without items; B = 128: 4 row blocks whose
+    consumers sit on other XCDs (write-through protocol); GK_XCD_LOCAL=0 forces it everywhere."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    monkeypatch.setenv("GK_XCD_LOCAL", xcd)
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=512, hidden=512, layers=1, batch=B, seq=T, seed=11)
+    params = init_params(cfg)
+    ds = NameStream(B, T, seed=12)
+    batches = [ds.next() for _ in range(3)]
+    out = []
+    try:
+        for v in (0, 1):
+            C.set_step_lds_variants(dict(fwd_fc=v))
+            tr = HipTrainer(cfg, params=params)
+            plan = tr.t.plan()
+            assert ("fwd=persistent+fc" in plan) == (v == 1), plan
+            tr.forward_backward(*batches[0])
+            g = {k: t.clone() for k, t in tr.grad_dict().items()}
+            loss = tr.loss()
+            for x, y in batches:
+                tr.step(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((g, loss, tr.params.clone(), tr.loss()))
+    finally:
+        C.set_step_lds_variants(saved)
+    (g0, l0, p0, s0), (g1, l1, p1, s1) = out
+    assert l0 == l1
+    for k in g0:
+        if k.startswith("fc."):
+            assert rel(g1[k], g0[k]) < 1e-5, k
+        else:
+            assert torch.equal(g0[k], g1[k]), k
+    assert rel(p1, p0) < 1e-4 and abs(s1 - s0) < 1e-4 * abs(s0)
+
+
 def test_wgrad_library_engine_matches_gemm256():
     """GK_WGRAD_GEMM=lib sends dW_hh at H = 2048 over >= 2384 tokens (>= 8 M outputs, >= 60 GFLOP) to
     one unsplit hipBLASLt GEMM, captured in the step graph; it must agree with the default engine

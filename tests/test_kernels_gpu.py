@@ -405,19 +405,20 @@ def test_gemm256(ext, monkeypatch, M, N, K, splits, bias, accumulate, lda_pad, r
     """algo 5: 256 x 256 x 64 LDS-staged MFMA GEMM (gemm256.hip) against fp32 torch on bf16-rounded
     operands -- bias, accumulate, split-K slabs, a strided A view and the fused row sums of A (the
     bias gradient of a weight-gradient product, one partial per split); on v_mfma_f32_16x16x32_bf16
-    (the phased pipeline, and the one-vmcnt(0)-per-k-tile kernel with GK_GEMM256_PHASED=0) and on
-    v_mfma_f32_32x32x16_bf16 (GK_GEMM256_MFMA=32).  K = 64 and odd k-tile counts cover the phased
+    (the phased pipeline, and the one-vmcnt(0)-per-k-tile kernel with GemmVariants phased = 0) and on
+    v_mfma_f32_32x32x16_bf16 (mfma = 32).  K = 64 and odd k-tile counts cover the phased
     pipeline's prologue / drain paths; BM = 192 tiles (M = 768, 1536, 2304) its 3-piece A staging;
-    16sc0 the staging schedule of the long-K products (GK_GEMM256_SCHED=0, all A pieces in R4)."""
-    monkeypatch.setenv("GK_GEMM256_MFMA", mfma[:2])
-    if mfma == "16sc0":
-        monkeypatch.setenv("GK_GEMM256_SCHED", "0")
-    else:
-        monkeypatch.delenv("GK_GEMM256_SCHED", raising=False)
-    if mfma == "16auto":
-        monkeypatch.delenv("GK_GEMM256_PHASED", raising=False)
-    else:
-        monkeypatch.setenv("GK_GEMM256_PHASED", "0" if mfma == "16legacy" else "1")
+    16sc0 the staging schedule of the long-K products (sched = 0, all A pieces in R4)."""
+    saved = ext.gemm_variants()
+    ext.set_gemm_variants(dict(mfma=int(mfma[:2]), sched=0 if mfma == "16sc0" else -1,
+                               phased=-1 if mfma == "16auto" else (0 if mfma == "16legacy" else 1)))
+    try:
+        _gemm256_case(ext, M, N, K, splits, bias, accumulate, lda_pad, rowsum)
+    finally:
+        ext.set_gemm_variants(saved)
+
+
+def _gemm256_case(ext, M, N, K, splits, bias, accumulate, lda_pad, rowsum):
     lda = K + lda_pad
     Af = bf(rnd(M, lda, seed=4))
     A, B = Af[:, :K], bf(rnd(N, K, seed=5) + 0.1 * torch.arange(K, device=DEV) / K)
