@@ -93,6 +93,13 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     q.nrb = q.rows16 ? B / 16 : B / 32;
     any_bwd |= q.bwd;
   }
+  // packed bf16 saves where the layer's forward (LDS-staged step kernels, or the two-layer wavefront)
+  // and backward (large-H or 16-row persistent) kernels both read / write them
+  for (int l = 0; l < L; ++l) {
+    SeqPlan& q = seq_[l];
+    const bool fwd16 = persist_fwd_ ? (fwd_wave_ && (l % 2 == 1 || l + 1 < L)) : gru_step_picks_lds(step_algo_, H, B);
+    q.s16 = step_lds_variants().save16 && d_.overlap == 0 && (q.big || q.rows16) && fwd16;
+  }
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);
   // split-K slab: large enough for every weight-gradient product it serves
@@ -103,8 +110,9 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_rw = R((size_t)splits_ * std::max(V, 3 * H) * 4);
   size_t o_sfc2 = R((size_t)kFcSplitsMax * V * H * 4), o_rfc2 = R((size_t)kFcSplitsMax * V * 4);
   size_t o_se = R((size_t)splits_ * V * E * 4);
-  std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0), o_hf(L, 0);
+  std::vector<size_t> o_pw(L, 0), o_pbh(L, 0), o_pbi(L, 0), o_hf(L, 0), o_s16(L, 0);
   for (int l = 0; l < L; ++l) {
+    if (seq_[l].s16) o_s16[l] = R(tok * H * 8);
     if (seq_[l].fuse_w) o_pw[l] = R((size_t)seq_[l].nrb * 3 * H * H * 4);
     if (seq_[l].fuse_w && persist_fwd_) o_hf[l] = R((tok + B) * H * 2);
     if (seq_[l].bwd || seq_[l].big) {
@@ -167,6 +175,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     y.Wih = arena_.get<u16>(x.Wih); y.WihT = arena_.get<u16>(x.WihT);
     y.slab_hh = arena_.get<float>(x.shh); y.rs_hh = arena_.get<float>(x.rhh);
     y.slab_ih = l > 0 ? arena_.get<float>(x.sih) : nullptr; y.rs_ih = l > 0 ? arena_.get<float>(x.rih) : nullptr;
+    y.s16 = o_s16[l] ? arena_.get<u16>(o_s16[l]) : nullptr;
   }
 
   HIP_CHECK(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
@@ -354,7 +363,8 @@ void Trainer::fwd_step(int l, int t, hipStream_t s) {
   a.h_bf = y.HSb + (size_t)(t + 1) * B * H;
   a.hT = y.HT; a.ldT = (d_.T + 1) * B; a.colT = (t + 1) * B;
   const size_t so = (size_t)t * B * H;
-  a.sr = y.sr + so; a.sz = y.sz + so; a.sn = y.sn + so; a.sghn = y.sghn + so;
+  if (y.s16 && !overlap_) a.s16 = y.s16 + so * 4;
+  else { a.sr = y.sr + so; a.sz = y.sz + so; a.sn = y.sn + so; a.sghn = y.sghn + so; }
   a.Bp = B; a.H = H; a.algo = step_algo_;
   gru_fwd_step(a, s);
 }

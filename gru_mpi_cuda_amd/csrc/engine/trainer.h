@@ -203,6 +203,7 @@ class Trainer {
 
   struct Layer {
     float *HSf, *sr, *sz, *sn, *sghn, *dy, *Gi, *carry[2];
+    u16* s16 = nullptr;   // packed bf16 saves [T][Bp][H][4] when SeqPlan::s16 (then sr..sghn are unused)
     u16 *HSb, *HT, *dgh[2], *dghT, *dgiT, *dgi;
     u16 *Whh, *WhhT, *Wih, *WihT;
     float *slab_hh, *rs_hh, *slab_ih, *rs_ih;
@@ -213,6 +214,7 @@ class Trainer {
     bool bwd = false, fuse_w = false, fuse_p = false;
     bool big = false;    // large H: the persistent split-K backward (gru_seq_big.hip) instead of T step kernels
     bool rows16 = false; // the persistent backward on 16-row blocks (gru_seq16.hip)
+    bool s16 = false;    // packed bf16 (r, z, n, gh_n) saves: its forward and backward kernels both take them
     int nrb = 0;         // row blocks of the backward's bias / dP / dW_hh partials
     float *dWhh_part = nullptr, *dbhh_part = nullptr, *dbih_part = nullptr;
     u16* HF = nullptr;   // fragment-tiled h for the fused dW_hh (SeqFwdArgs::HF)

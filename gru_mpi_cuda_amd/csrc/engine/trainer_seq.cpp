@@ -156,7 +156,8 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     SeqFwdArgs a;
     a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = seq_[l].HF;
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
-    a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+    if (y.s16) a.s16 = y.s16;   // (the wavefront only: SeqPlan::s16)
+    else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
     if (l == 0) { a.P = Ptab_; a.ids = ids_; }
     else a.Gi = y.Gi;
@@ -284,7 +285,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     const std::string k = std::to_string(l);
     if (q.bwd) {
       SeqBwdArgs a;
-      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn;
+      a.dy = y.dy;
+      if (q.s16) a.s16 = y.s16;   // (the 16-row kernel only: SeqPlan::s16)
+      else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
       a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;
@@ -299,7 +302,9 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (q.rows16) gru_bwd_seq16(a, s); else gru_bwd_seq(a, s);
     } else if (q.big) {
       SeqBwdArgs a;
-      a.dy = y.dy; a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; a.HSf = y.HSf;
+      a.dy = y.dy; a.HSf = y.HSf;
+      if (q.s16) a.s16 = y.s16;
+      else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
       a.WhhT = y.WhhT; a.xbuf = xbuf_; a.part = bpart_;
       a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)tok; a.dgi = y.dgi;
       a.dgiT_n_only = l == 0 && dgiT_share_;

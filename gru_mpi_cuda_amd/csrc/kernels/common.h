@@ -103,6 +103,35 @@ DEV void prep_batch_body(const PrepJob& j, int blk, int nblk) {
   if (blk == 0 && threadIdx.x == 0) j.inv_count[0] = __int_as_float(j.in[1]);
 }
 
+// Packed bf16 saves of the large-H / wavefront kernels (a layer's SeqPlan::s16): (r, z, n, gh_n) of one
+// (row, unit) item as 4 bf16 in 8 bytes -- one store in the forward, one load in the backward, half the
+// bytes of the four fp32 arrays.  h itself stays fp32 (HSf).
+DEV void st_save16(u16* p, float r, float z, float n, float g) {
+  typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+  const u32x2_ v = {(unsigned)f2bf(r) | ((unsigned)f2bf(z) << 16), (unsigned)f2bf(n) | ((unsigned)f2bf(g) << 16)};
+  *reinterpret_cast<u32x2_*>(p) = v;
+}
+// raw load (the packed words parked in two float registers) and the unpack at the point of use: unpacking
+// right after the load made the compiler wait for it there, exposing the latency the early issue hides
+// (large-H backward 3.61 -> 3.90 ms at H = 2048)
+DEV void ld_save16_raw(const u16* p, float& w0, float& w1) {
+  typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+  const u32x2_ v = *reinterpret_cast<const u32x2_*>(p);
+  w0 = __uint_as_float(v.x);
+  w1 = __uint_as_float(v.y);
+}
+DEV void unpack_save16(float w0, float w1, float& r, float& z, float& n, float& g) {
+  const unsigned x = __float_as_uint(w0), y = __float_as_uint(w1);
+  r = __uint_as_float(x << 16); z = __uint_as_float(x & 0xffff0000u);
+  n = __uint_as_float(y << 16); g = __uint_as_float(y & 0xffff0000u);
+}
+DEV void ld_save16(const u16* p, float& r, float& z, float& n, float& g) {
+  typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+  const u32x2_ v = *reinterpret_cast<const u32x2_*>(p);
+  r = __uint_as_float(v.x << 16); z = __uint_as_float(v.x & 0xffff0000u);
+  n = __uint_as_float(v.y << 16); g = __uint_as_float(v.y & 0xffff0000u);
+}
+
 // Workgroup barrier WITHOUT the release fence __syncthreads() carries (that fence is an
 // s_waitcnt vmcnt(0), which drains every global load in flight, prefetches included): own LDS
 // operations retired, then s_barrier.  For LDS hand-offs between the waves of a workgroup only.

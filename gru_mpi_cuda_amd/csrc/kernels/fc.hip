@@ -411,6 +411,244 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
   STAMP();
 }
 
+// ---------------------------------------------------------------------------------------------
+// fc_xent_fl: the V = 256, H = 512 training FC head with W_fc read ONCE per 32-row block (the 8-wave
+// kernel above streams it twice, 512 KB per CU: W_fc for the logits, W_fc^T for dH -- the arrival of
+// those fragments is most of its 15 us, docs/DESIGN.md §3.4).  The vocabulary is walked in 4 chunks
+// of 64 columns; chunk c's 64 x 512 slab of W_fc lands in LDS by DMA (double-buffered, chunk c + 1 in
+// flight) and is read twice from the one image:
+//   * row reads (ds_read_b128) as the B operand of the chunk's logits  S_c = X · W_c^T  (K = H), X's
+//     fragments held in VGPRs for the whole launch;
+//   * transposed reads (ds_read_b64_tr_b16) as the B operand of  U = alpha U + e_c · W_c  (K = the
+//     chunk's 64 vocabulary columns),
+// with an online softmax across chunks (running row max m, alpha = exp(m_old - m_new), e_c = exp(S_c -
+// m_new) in bf16).  At the end  dy = scale (U / s - W_fc[y])  = scale (softmax - onehot) · W_fc, the same
+// quantity fc_xent computes as dl · W_fc; dl itself (for dW_fc) comes from the logits kept in
+// registers, exactly as fc_xent forms it.  W_fc is read from its FT copy (the LDS-DMA source address
+// of each lane is the FT position of the 8 elements it places).
+// LDS image of a chunk: 4 quarters (128 columns each) of [64 rows][256 B], chunk ch of row r at
+// 16 (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))): the row reads of the 16x16x32 operand are 2-way, the
+// transposed reads conflict-free (cdna_hip_programming.md T10, image (b)).
+namespace {
+constexpr int kFlVC = 64;                 // vocabulary columns per chunk
+constexpr int kFlQB = 64 * 256;           // one quarter image [64 rows][256 B]
+constexpr int kFlCB = 4 * kFlQB;          // one chunk buffer (64 KB)
+constexpr int kFlELD = 72;                // e tile row pitch (u16)
+}
+DEV int fl_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+typedef short fl_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) fl_v4s fl_lds_v4s;
+typedef __attribute__((address_space(3))) void fl_lds_void;
+
+__global__ void __launch_bounds__(512, 1) fc_xent_fl_kernel(FcXentArgs a) {
+  constexpr int H = 512, V = 256, NKS = H / 32, NCH = V / kFlVC;
+  // Separate LDS objects on purpose: the compiler's wait insertion treats an LDS-DMA in flight as a
+  // possible writer of every LDS read of the SAME object, so one shared buffer would put a vmcnt(0)
+  // (the next chunk's DMA) in front of every read of the current chunk
+  __shared__ __attribute__((aligned(16))) unsigned char wb0[kFlCB];   // chunk buffers: [4][64][256 B]
+  __shared__ __attribute__((aligned(16))) unsigned char wb1[kFlCB];
+  __shared__ __attribute__((aligned(16))) u16 et[32 * kFlELD];        // e tile (bf16)
+  __shared__ __attribute__((aligned(16))) float red[8 * 32];          // [4][32] max | [4][32] sum partials
+  __shared__ float mrow[2 * 32];                                      // running max (by chunk parity)
+  __shared__ float alpha[32], srow[32];                               // rescale factors, final sums
+  __shared__ int ys[32];                                              // labels
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * FROWS;
+  const int r = w & 1, vt = w >> 1;   // this wave's logits tile of a chunk: row tile r, vocab tile vt
+  int nst = 0;   // diagnostic phase stamps of workgroup 0 (scripts/probe_fc.py)
+  auto STAMP = [&]() {
+    if (a.dbg && blockIdx.x == 0 && tid == 0) a.dbg[nst] = __builtin_amdgcn_s_memrealtime();
+    ++nst;
+  };
+  STAMP();
+  const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(a.Wf), (short)0, V * H * 2, 0x00020000);
+  // chunk c -> buffer b: wave w places 1-KB pieces n = 8w .. 8w+7 (quarter n / 16, rows 4 (n % 16) .. +3;
+  // lane L: row + L / 16, physical 16-B chunk L % 16, i.e. logical chunk (L % 16) ^ swz(row))
+  auto dma = [&](int c, int b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = w * 8 + i, hq = n >> 4, vr = 4 * (n & 15) + (lane >> 4);
+      const int h0 = hq * 128 + (((lane & 15) ^ fl_swz(vr)) << 3), v = c * kFlVC + vr;
+      const unsigned src = (unsigned)(((((v >> 4) * NKS + (h0 >> 5)) * 64 + (v & 15) + 16 * ((h0 >> 3) & 3)) * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (fl_lds_void*)((b ? wb1 : wb0) + hq * kFlQB + (n & 15) * 1024),
+                                                16, src, 0, 0, 0);
+    }
+  };
+  dma(0, 0);
+  // X fragments of row tile r (all K), resident for the launch
+  bf16x8 xa[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) xa[ks] = ld8(a.X + (size_t)(m0 + r * 16 + lr) * H + ks * 32 + 8 * lq);
+  const float inv = a.inv_count[0];
+  if (tid < FROWS) {
+    ys[tid] = a.labels[m0 + tid];
+    mrow[tid] = -INFINITY;
+  }
+  // (no global load may follow a DMA inside the chunk loop: waiting for its value would drain the DMA)
+  float bvs[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) bvs[c] = a.b[c * kFlVC + vt * 16 + lr];
+  dma(1, 1);   // last in the prologue: the first chunk's wait (vmcnt(8)) leaves exactly it in flight
+  float s_run = 0.f;   // thread tid < 32: running sum of exp of row tid
+  f32x4 lg[NCH], U[2][4];
+  zero_acc(U);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int b = c & 1;
+    const unsigned char* wb = b ? wb1 : wb0;
+    // B1: chunk c in LDS (own pieces: vmcnt -- chunk c + 1's 8 pieces may stay in flight; all: barrier)
+    if (c == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    STAMP();
+    if (c >= 1 && c + 1 < NCH) dma(c + 1, (c + 1) & 1);   // into chunk c - 1's buffer, read by all waves by now
+    // logits tile: rows 16 r + (lane & 15) x vocab columns 64 c + 16 vt + ..., K = H
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    {
+      const int vr = vt * 16 + lr, sw = fl_swz(vr);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int ch = ((ks & 3) * 4 + lq) ^ sw;
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(wb + (ks >> 2) * kFlQB + vr * 256 + ch * 16);
+        acc = mfma16(xa[ks], bfr, acc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += bvs[c];
+    lg[c] = acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float m = max16(acc[i]);
+      if (lr == 0) red[vt * 32 + r * 16 + lq * 4 + i] = m;
+    }
+    lds_barrier();   // B2: the chunk's per-tile row maxima
+    STAMP();
+    const float* mo = mrow + (c & 1) * 32;
+    float* mn_out = mrow + ((c + 1) & 1) * 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i;
+      const float mc = fmaxf(fmaxf(red[row], red[32 + row]), fmaxf(red[64 + row], red[96 + row]));
+      const float mn = fmaxf(mo[row], mc);
+      const float e = __expf(acc[i] - mn);
+      et[row * kFlELD + vt * 16 + lr] = f2bf(e);
+      const float se = sum16(e);
+      if (lr == 0) red[128 + vt * 32 + row] = se;
+    }
+    if (tid < FROWS) {
+      const float mc = fmaxf(fmaxf(red[tid], red[32 + tid]), fmaxf(red[64 + tid], red[96 + tid]));
+      const float mn = fmaxf(mo[tid], mc);
+      alpha[tid] = __expf(mo[tid] - mn);   // 0 on the first chunk (m = -inf)
+      mn_out[tid] = mn;
+    }
+    lds_barrier();   // B3: e tile, alpha, the chunk's row sums
+    STAMP();
+    if (tid < FROWS) s_run = alpha[tid] * s_run + ((red[128 + tid] + red[160 + tid]) + (red[192 + tid] + red[224 + tid]));
+    // U = alpha U + e_c · W_c: wave w owns dH columns 64 w .. 64 w + 63
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float al = alpha[rt * 16 + lq * 4 + i];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) U[rt][nt][i] *= al;
+      }
+#pragma unroll
+    for (int ks2 = 0; ks2 < kFlVC / 32; ++ks2) {
+      bf16x8 ae[2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+        ae[rt] = *reinterpret_cast<const bf16x8*>(et + (rt * 16 + lr) * kFlELD + ks2 * 32 + 8 * lq);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        // B[k = v][n = h]: lane 4q + p of each 16-lane group addresses row 32 ks2 + 8 (lane >> 4) + q (+ 4),
+        // columns 64 w + 16 nt + 4 p .. +3; lane i of the group receives column i of the 4 rows
+        const int q = (lane & 15) >> 2, p = lane & 3;
+        const int hin = 64 * (w & 1) + 16 * nt + 4 * p, hq = w >> 1;
+        // (assembled as whole 64-bit halves: per-element bf16 inserts were miscompiled into
+        // duplicated halves)
+        typedef unsigned fl_u32x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned fl_u32x4 __attribute__((ext_vector_type(4)));
+        fl_u32x2 half[2];
+#pragma unroll
+        for (int hr = 0; hr < 2; ++hr) {
+          const int vr = ks2 * 32 + 8 * lq + 4 * hr + q;
+          const unsigned char* ad = wb + hq * kFlQB + vr * 256 + (((hin >> 3) ^ fl_swz(vr)) << 4) + 8 * ((hin >> 2) & 1);
+          half[hr] = __builtin_bit_cast(fl_u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((fl_lds_v4s*)(ad)));
+        }
+        const fl_u32x4 raw = {half[0].x, half[0].y, half[1].x, half[1].y};
+        const bf16x8 bt = __builtin_bit_cast(bf16x8, raw);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) U[rt][nt] = mfma16(ae[rt], bt, U[rt][nt]);
+      }
+    }
+  }
+  // ---- final row statistics; dl (for dW_fc), the loss, dy
+  // the label rows W_fc[y][.] at this lane's dy positions (rows 16 rt + 4 lq + i, columns 64 w + 16 nt +
+  // lane & 15), gathered from the FT copy (their latency under the dl pass): dy = scale (U / s - W_fc[y])
+  u16 wy[2][4][4];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = max(ys[rt * 16 + lq * 4 + i], 0);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int h = 64 * w + 16 * nt + lr;
+        wy[rt][i][nt] = a.Wf[((((v >> 4) * NKS + (h >> 5)) * 64 + (v & 15) + 16 * ((h >> 3) & 3)) * 8) + (h & 7)];
+      }
+    }
+  const float* mfin = mrow + (NCH & 1) * 32;
+  if (tid < FROWS) srow[tid] = s_run;
+  lds_barrier();
+  STAMP();
+  float* lab = red;   // [32] label logits (the partial arrays are free now)
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    u16 dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r * 16 + lq * 4 + i, col = c * kFlVC + vt * 16 + lr, y = ys[row];
+      const float x = lg[c][i];
+      if (col == y) lab[row] = x;
+      const float scale = y >= 0 ? inv : 0.f;
+      const float d = (__expf(x - mfin[row]) * __builtin_amdgcn_rcpf(srow[row]) - (col == y ? 1.f : 0.f)) * scale;
+      dv[i] = f2bf(d);
+    }
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 pv = {(unsigned)dv[0] | ((unsigned)dv[1] << 16), (unsigned)dv[2] | ((unsigned)dv[3] << 16)};
+    *reinterpret_cast<u32x2*>(a.dlT + (size_t)(c * kFlVC + vt * 16 + lr) * a.ldT + a.colT + m0 + r * 16 + lq * 4) = pv;
+  }
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rt * 16 + lq * 4 + i, y = ys[row];
+      const float scale = y >= 0 ? inv : 0.f, rs = __builtin_amdgcn_rcpf(srow[row]);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        a.dy[(size_t)(m0 + row) * H + 64 * w + 16 * nt + lr] = (U[rt][nt][i] * rs - bf2f(wy[rt][i][nt])) * scale;
+    }
+  lds_barrier();   // label logits
+  STAMP();
+  if (w == 0) {
+    float l = 0.f;
+    if (lane < FROWS) {
+      const int y = ys[lane];
+      l = y >= 0 ? (logf(srow[lane]) + mfin[lane] - lab[lane]) * inv : 0.f;
+    }
+    l = wave_sum(l);
+    if (lane == 0) a.loss_part[blockIdx.x] = l;
+  }
+  STAMP();
+}
+
+bool fc_xent_fl_ok(const FcXentArgs& a) {
+  return step_lds_variants().fc_flash && a.V == 256 && a.H == 512 && a.Wf && a.dy && !a.dl && a.M % FROWS == 0 &&
+         a.ldT % 4 == 0 && a.colT % 4 == 0;
+}
+
 template <int KB>
 __global__ void __launch_bounds__(512) fc_sample_kernel(FcSampleArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -668,6 +906,10 @@ static bool fc_xent_v256_ok(const FcXentArgs& a) {
 }
 
 void fc_xent(const FcXentArgs& a, hipStream_t s) {
+  if (fc_xent_fl_ok(a)) {
+    hipLaunchKernelGGL(fc_xent_fl_kernel, dim3(a.M / FROWS), dim3(512), 0, s, a);
+    return;
+  }
   if (fc_xent_v256_ok(a)) {
     const size_t shm = (size_t)FROWS * (a.H + kX2Pad) * 2 + (2 * 8 * 32 + 64) * 4 + 256 * 40 * 2 +
                        (size_t)FROWS * (256 + 8) * 2 + FROWS * 4;

@@ -837,17 +837,15 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_seq2_kernel(SeqFwd2Args a) {
     load_gi0(s + 1, gin);
     if (do0) {
       L0.HSf[((size_t)(s + 1) * Bp + b) * H + j] = h0v;
-      if (L0.sr) {
-        const size_t so = ((size_t)s * Bp + b) * H + j;
-        L0.sr[so] = r0; L0.sz[so] = z0; L0.sn[so] = n0; L0.sghn[so] = ghn0;
-      }
+      const size_t so = ((size_t)s * Bp + b) * H + j;
+      if (L0.s16) st_save16(L0.s16 + so * 4, r0, z0, n0, ghn0);
+      else if (L0.sr) { L0.sr[so] = r0; L0.sz[so] = z0; L0.sn[so] = n0; L0.sghn[so] = ghn0; }
     }
     if (do1) {
       L1.HSf[((size_t)s * Bp + b) * H + j] = h1v;
-      if (L1.sr) {
-        const size_t so = ((size_t)(s - 1) * Bp + b) * H + j;
-        L1.sr[so] = r1; L1.sz[so] = z1; L1.sn[so] = n1; L1.sghn[so] = ghn1;
-      }
+      const size_t so = ((size_t)(s - 1) * Bp + b) * H + j;
+      if (L1.s16) st_save16(L1.s16 + so * 4, r1, z1, n1, ghn1);
+      else if (L1.sr) { L1.sr[so] = r1; L1.sz[so] = z1; L1.sn[so] = n1; L1.sghn[so] = ghn1; }
     }
   }
 }
@@ -1130,6 +1128,7 @@ bool gru_fwd_seq_supported(int H, int Bp) {
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
+  if (a.s16) throw std::runtime_error("gru_fwd_seq: packed bf16 saves are the wavefront's (gru_fwd_seq2) only");
   if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
@@ -1213,6 +1212,7 @@ bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
 }
 
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
+  if (a.s16) throw std::runtime_error("gru_bwd_seq: packed bf16 saves are read by the 16-row / large-H kernels only");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
 #define X(HH, NK, NW, NP)                                                              \

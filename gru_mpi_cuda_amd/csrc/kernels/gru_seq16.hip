@@ -70,7 +70,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
   int svid = 0;
   auto load_saves = [&](int t) {
     const size_t o = ((size_t)t * Bp + b) * H + j;
-    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[0] = a.dy[o];
+    if (a.s16) ld_save16_raw(a.s16 + o * 4, sv[1], sv[2]);   // unpacked at use
+    else { sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o]; }
     sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
     if constexpr (NTP > 0) svid = a.ids[(size_t)t * Bp + b];
   };
@@ -100,7 +102,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq16_kernel(SeqBwdArgs a) {
       }
     }
     const int idc = svid;
-    const float dy = sv[0], sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4], hprev = sv[5];
+    float sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4];
+    if (a.s16) unpack_save16(sv[1], sv[2], sr, sz, sn, sghn);
+    const float dy = sv[0], hprev = sv[5];
     if (t > 0) load_saves(t - 1);
 #pragma unroll
     for (int u = 0; u < 2; ++u)

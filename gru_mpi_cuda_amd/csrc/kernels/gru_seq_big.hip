@@ -148,8 +148,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       for (int e = 0; e < 4; ++e) {
         const size_t o = (size_t)t * Bp * H + item_off(pp, e);
         pre[pp][e][0] = a.dy[o];
-        pre[pp][e][1] = a.sr[o]; pre[pp][e][2] = a.sz[o]; pre[pp][e][3] = a.sn[o];
-        pre[pp][e][4] = a.HSf[o]; pre[pp][e][5] = a.sghn[o];   // HSf + t*Bp*H = h_{t-1}
+        if (a.s16) ld_save16_raw(a.s16 + o * 4, pre[pp][e][1], pre[pp][e][2]);   // unpacked at use
+        else { pre[pp][e][1] = a.sr[o]; pre[pp][e][2] = a.sz[o]; pre[pp][e][3] = a.sn[o]; pre[pp][e][5] = a.sghn[o]; }
+        pre[pp][e][4] = a.HSf[o];   // HSf + t*Bp*H = h_{t-1}
       }
     float ps[2][4];    // dh = (dy + carry) + partial sum: the step kernel's rounding order
 #pragma unroll
@@ -256,8 +257,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
       for (int e = 0; e < 4; ++e) {
         const int rq = ii * 16 + lq * 4 + e;
         const float dh = (pre[pp][e][0] + carry[pp][e]) + ps[pp][e];
-        const float r = pre[pp][e][1], z = pre[pp][e][2], n = pre[pp][e][3];
-        const float hp = pre[pp][e][4], ghn = pre[pp][e][5];
+        float r = pre[pp][e][1], z = pre[pp][e][2], n = pre[pp][e][3], ghn = pre[pp][e][5];
+        if (a.s16) unpack_save16(pre[pp][e][1], pre[pp][e][2], r, z, n, ghn);
+        const float hp = pre[pp][e][4];
         const float dn = dh * (1.f - z);
         const float dz = dh * (hp - n);
         const float dan = dn * (1.f - n * n);
@@ -348,8 +350,8 @@ bool gru_bwd_seq_big_supported(int H, int Bp) {
 long gru_bwd_seq_big_part_floats(int H, int Bp) { return 2L * Bp * H * kBS; }
 
 void gru_bwd_seq_big(const SeqBwdArgs& a, hipStream_t s) {
-  if (!gru_bwd_seq_big_supported(a.H, a.Bp) || !a.xbuf || !a.cnt || !a.part || !a.dy || !a.sr || !a.sz ||
-      !a.sn || !a.sghn || !a.HSf || !a.WhhT || a.ldG < a.T * a.Bp)
+  if (!gru_bwd_seq_big_supported(a.H, a.Bp) || !a.xbuf || !a.cnt || !a.part || !a.dy || ((!a.sr || !a.sz ||
+      !a.sn || !a.sghn) && !a.s16) || !a.HSf || !a.WhhT || a.ldG < a.T * a.Bp)
     throw std::runtime_error("gru_bwd_seq_big: unsupported shape or incomplete arguments");
   // only min(T, xring) slots of the exchange are addressed when a ring is active
   const size_t slots = a.xring >= 2 && a.xring < a.T ? (size_t)a.xring : (size_t)a.T;

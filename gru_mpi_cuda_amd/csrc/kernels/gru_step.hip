@@ -237,6 +237,7 @@ static bool use_lds(int algo, int H, int Bp, bool fused, int Kin, int ldT, int c
 
 void gru_fwd_step(const FwdStepArgs& a, hipStream_t s) {
   if (use_lds(a.algo, a.H, a.Bp, a.x_bf != nullptr, a.Kin, a.ldT, a.colT)) { gru_fwd_step_lds(a, s); return; }
+  if (a.s16) throw std::runtime_error("gru_fwd_step: packed bf16 saves need the LDS-staged step kernels");
   const int nks = a.H / 32;
   int ks, kb;
   pick_split(nks, ks, kb);

@@ -192,7 +192,8 @@ __global__ void __launch_bounds__(256, NS == 2 ? 2 : 1) gru_fwd_step_lds_kernel(
       a.h_f[o] = h;
       const u16 hb = f2bf(h);
       a.h_bf[o] = hb;
-      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+      if (a.s16) st_save16(a.s16 + o * 4, r, z, n, ghn);
+      else if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
       st[rr * 32 + wn * 16 + lr] = hb;
     }
   if (a.hT) {
@@ -342,7 +343,8 @@ __global__ void __launch_bounds__(256, 2) gru_fwd_step_lds64_kernel(FwdStepArgs 
       a.h_f[o] = h;
       const u16 hb = f2bf(h);
       a.h_bf[o] = hb;
-      if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+      if (a.s16) st_save16(a.s16 + o * 4, r, z, n, ghn);
+      else if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
       st[rr * 32 + wn * 16 + lr] = hb;
     }
   if (a.hT) {
@@ -486,7 +488,8 @@ __global__ void __launch_bounds__(512, 1) gru_fwd_step_big_kernel(FwdStepArgs a)
         a.h_f[o] = h;
         const u16 hb = f2bf(h);
         a.h_bf[o] = hb;
-        if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
+        if (a.s16) st_save16(a.s16 + o * 4, r, z, n, ghn);
+      else if (a.sr) { a.sr[o] = r; a.sz[o] = z; a.sn[o] = n; a.sghn[o] = ghn; }
         st[rr * 64 + uu] = hb;
       }
     }

@@ -35,6 +35,8 @@ struct FwdStepArgs {
   u16* hT = nullptr;               // transposed copy: hT[j*ldT + colT + b]  (nullable)
   int ldT = 0, colT = 0;
   float* sr = nullptr; float* sz = nullptr; float* sn = nullptr; float* sghn = nullptr;  // saves (nullable)
+  u16* s16 = nullptr;              // packed bf16 saves [Bp][H][4] (r, z, n, gh_n) instead of sr..sghn
+                                   // (LDS-staged kernels only, common.h st_save16)
   int Bp = 0, H = 0;
   int algo = 0;                    // 0 auto, 1 register-direct tile, 2 LDS-staged big tile (gru_step_lds.hip)
 };
@@ -86,6 +88,11 @@ struct StepLdsVariants {
                          // slots instead of one per step (0); docs/DESIGN.md §3.1d
   int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
                          // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
+  int save16 = 1;        // layers whose forward AND backward kernels take them (LDS-staged step kernels or
+                         // the two-layer wavefront; the large-H or 16-row persistent backward): packed
+                         // bf16 (r, z, n, gh_n) saves instead of four fp32 arrays (SeqPlan::s16)
+  int fc_flash = 0;      // V = 256, H = 512 training FC head: fc_xent_fl (W_fc read once per block, online
+                         // softmax over 4 vocabulary chunks, fc.hip); 0: the 8-wave two-stream kernel
   int fwd_fc = 0;        // one-layer H = 512, V = 256: the FC head (fc_xent + dW_fc) as consumer
                          // workgroups inside the persistent forward launch (gru_fwd_seq_fc); 0: after it
 };
@@ -127,6 +134,7 @@ struct SeqFwdArgs {
   // caller's
   u16* HF = nullptr;
   float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H] (nullable)
+  u16* s16 = nullptr;              // packed bf16 saves [T][Bp][H][4] instead (two-layer wavefront only)
   const u16* Whh = nullptr; const float* bhh = nullptr;
   const float* P = nullptr; const int* ids = nullptr;   // layer 0: table + ids [T][Bp]
   const float* Gi = nullptr;                            // layers >= 1: [T][Bp][3H]
@@ -186,6 +194,7 @@ void gru_fwd_seq2(const SeqFwd2Args& a, hipStream_t s);
 struct SeqBwdArgs {
   const float* dy = nullptr;       // [T][Bp][H]
   const float *sr = nullptr, *sz = nullptr, *sn = nullptr, *sghn = nullptr;   // [T][Bp][H]
+  const u16* s16 = nullptr;        // packed bf16 saves [T][Bp][H][4] instead (16-row and large-H kernels)
   const float* HSf = nullptr;      // [T+1][Bp][H]
   const u16* HT = nullptr; int ldT = 0;     // h_{t-1} at column t*Bp + b (fused dW_hh)
   const u16* HF = nullptr;         // SeqFwdArgs::HF of the same layer: preferred over HT when set

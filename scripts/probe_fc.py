@@ -7,6 +7,8 @@ import torch
 from gru_mpi_cuda_amd.ops import load_ext
 
 C = load_ext()
+if "FLASH" in os.environ:   # StepLdsVariants.fc_flash: 1 fc_xent_fl, 0 the two-stream 8-wave kernel
+    C.set_step_lds_variants(dict(fc_flash=int(os.environ["FLASH"])))
 dev = torch.device("cuda", 0)
 M, H, V = int(os.environ.get("M", 8192)), int(os.environ.get("H", 512)), 256
 s = torch.cuda.current_stream().cuda_stream
@@ -44,7 +46,7 @@ logits = X.float() @ W.float().T + b
 ref_loss = torch.nn.functional.cross_entropy(logits, y.long()).item()
 p = torch.softmax(logits, -1)
 p[torch.arange(M), y.long()] -= 1
-ref_dy = (p / M).bfloat16().float() @ W.float()
+ref_dy = (p / M) @ W.float()
 err = (dy - ref_dy).abs().max().item()
 dbg = torch.zeros(32, device=dev, dtype=torch.int64)
 d["dbg"] = dbg.data_ptr()

@@ -898,7 +898,8 @@ def test_dwfc_in_embedding_launch_bitwise(layers, H, B):
 @pytest.mark.parametrize("B,T,xcd", [(256, 32, "1"), (256, 40, "1"), (256, 12, "1"), (128, 32, "1"), (256, 32, "0")])
 def test_fc_in_forward_matches_fc_xent(B, T, xcd, monkeypatch):
     """StepLdsVariants.fwd_fc: the FC head as consumer workgroups of the persistent forward launch
-    (gru_fwd_seq_fc) against fc_xent + the dW_fc K-slice GEMM after it (fwd_fc = 0).  The logits,
+    (gru_fwd_seq_fc) against the two-stream fc_xent + the dW_fc K-slice GEMM after it (fwd_fc = 0,
+    fc_flash = 0).  The logits,
     softmax-xent and dH run the same MFMA k order, so the loss and every gradient except dW_fc / db_fc
     are bitwise equal; dW_fc / db_fc sum the same products per row block instead of per K-slice.
     T = 40: consumers with two items; T = 12: consumers without items; B = 128: 4 row blocks whose
@@ -915,7 +916,7 @@ def test_fc_in_forward_matches_fc_xent(B, T, xcd, monkeypatch):
     out = []
     try:
         for v in (0, 1):
-            C.set_step_lds_variants(dict(fwd_fc=v))
+            C.set_step_lds_variants(dict(fwd_fc=v, fc_flash=0))   # the consumers' math is fc_xent's
             tr = HipTrainer(cfg, params=params)
             plan = tr.t.plan()
             assert ("fwd=persistent+fc" in plan) == (v == 1), plan
@@ -980,7 +981,8 @@ def test_bwd16_matches_32_row_backward():
     out = []
     try:
         for v in (1, 0):
-            C.set_step_lds_variants(dict(bwd16=v))
+            # fp32 saves on both sides (the 32-row kernel reads no packed bf16 saves)
+            C.set_step_lds_variants(dict(bwd16=v, save16=0))
             tr = HipTrainer(cfg, params=params)
             assert ("bwd0=persistent16" in tr.t.plan()) == (v == 1), tr.t.plan()
             tr.forward_backward(x, y)
@@ -996,6 +998,43 @@ def test_bwd16_matches_32_row_backward():
     for k in g32:
         e = rel(g16[k], g32[k])
         assert e < 1e-4, f"{k}: 16-row vs 32-row rel err {e:.2e}"
+
+
+@pytest.mark.parametrize("layers,B,H,E,T,plan", [
+    (2, 128, 1024, 256, 12, "bwd0=persistent16"),       # config-4 shard: wavefront fwd, 16-row bwd
+    (1, 512, 2048, 128, 6, "bwd0=persistent-big"),      # config 5: LDS-staged step fwd, large-H bwd
+])
+def test_packed_bf16_saves(layers, B, H, E, T, plan):
+    """StepLdsVariants.save16: (r, z, n, gh_n) saved as 4 packed bf16 per item (common.h st_save16)
+    where the layer's forward and backward kernels both take them.  The forward never reads its saves,
+    so the loss is bitwise the fp32-saves run's; the gradients differ by the bf16 rounding of the
+    saves (< 1 % relative) and both runs stay within the fp64 oracle's 4 %."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=B, seq=T, seed=31)
+    params = init_params(cfg)
+    x, y = NameStream(cfg.batch, cfg.seq, seed=32).next()
+    out = []
+    try:
+        for v in (0, 1):
+            C.set_step_lds_variants(dict(save16=v))
+            tr = HipTrainer(cfg, params=params)
+            assert plan in tr.t.plan(), tr.t.plan()
+            tr.forward_backward(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((tr.loss(), tr.grad_dict()))
+    finally:
+        C.set_step_lds_variants(saved)
+    (l0, g0), (l1, g1) = out
+    assert l0 == l1
+    p64 = {k: v.double() for k, v in params.items()}
+    ref_loss, ref_g = cpu_ref.manual_backward(p64, cfg, torch.from_numpy(x), torch.from_numpy(y))
+    for k in ref_g:
+        assert rel(g1[k], g0[k]) < 1e-2, k
+        assert rel(g1[k], ref_g[k]) < 0.04, k
 
 
 @pytest.mark.parametrize("layers,B,H,E,T,plan", [

@@ -276,12 +276,26 @@ def test_bwd_step_dgit_n_only(ext, H, Bp, algo, sk):
     test_bwd_step(ext, False, H, Bp, algo, sk, n_only=True)
 
 
-@pytest.mark.parametrize("mode", ["plain", "fused_dh", "dl_v256"])
+@pytest.mark.parametrize("mode", ["plain", "fused_dh", "fused_dh_2s", "dl_v256"])
 @pytest.mark.parametrize("H", [256, 320, 512, 1024])
 def test_fc_xent(ext, mode, H):
+    """fused_dh at H = 512 takes fc_xent_fl (W_fc read once, online softmax over vocabulary chunks,
+    dy = scale (sum_v bf16(e_v) W_v / s - W_y)): checked against the fp32 (softmax - onehot) · W_fc;
+    fused_dh_2s runs the same call on the 8-wave two-stream kernel (StepLdsVariants fc_flash = 0),
+    whose dy is exactly dl(bf16) · W_fc."""
     fused_dh = mode.startswith("fused_dh")
-    if mode == "dl_v256" and H % 512:
+    if mode in ("dl_v256", "fused_dh_2s") and H % 512:
         pytest.skip("the 8-wave kernel is for H in (512, 1024)")
+    saved = ext.step_lds_variants()
+    ext.set_step_lds_variants(dict(fc_flash=0 if mode == "fused_dh_2s" else 1))
+    try:
+        _fc_xent_case(ext, mode, H, fused_dh)
+    finally:
+        ext.set_step_lds_variants(saved)
+
+
+def _fc_xent_case(ext, mode, H, fused_dh):
+    flash = mode == "fused_dh" and H == 512
     M, V = 128, 256
     X = bf(rnd(M, H, seed=1))
     W = bf(rnd(V, H, scale=H ** -0.5, seed=2))
@@ -319,7 +333,9 @@ def test_fc_xent(ext, mode, H):
     torch.testing.assert_close(lp.sum(), loss, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(dl.float(), ref, atol=1e-4, rtol=1e-2)
     torch.testing.assert_close(dlT[:, M:].T, dl, atol=0, rtol=0)
-    if mode == "fused_dh":   # dH = dlogits(bf16) · W_fc, fp32 accumulate
+    if flash:   # dH from bf16 exp(logit - running max) products, normalised at the end
+        torch.testing.assert_close(dy, ref @ W.float(), atol=1e-5, rtol=1e-2)
+    elif fused_dh:   # dH = dlogits(bf16) · W_fc, fp32 accumulate
         torch.testing.assert_close(dy, dl.float() @ W.float(), atol=1e-5, rtol=1e-3)
 
 
