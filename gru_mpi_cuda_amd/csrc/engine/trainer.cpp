@@ -93,12 +93,12 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     q.nrb = q.rows16 ? B / 16 : B / 32;
     any_bwd |= q.bwd;
   }
-  // packed bf16 saves where the layer's forward (LDS-staged step kernels, or the two-layer wavefront)
-  // and backward (large-H or 16-row persistent) kernels both read / write them
+  // packed bf16 saves where the layer's forward (persistent, or the LDS-staged step kernels) and
+  // backward (any persistent kernel) both read / write them
   for (int l = 0; l < L; ++l) {
     SeqPlan& q = seq_[l];
-    const bool fwd16 = persist_fwd_ ? (fwd_wave_ && (l % 2 == 1 || l + 1 < L)) : gru_step_picks_lds(step_algo_, H, B);
-    q.s16 = step_lds_variants().save16 && d_.overlap == 0 && (q.big || q.rows16) && fwd16;
+    const bool fwd16 = persist_fwd_ || gru_step_picks_lds(step_algo_, H, B);
+    q.s16 = step_lds_variants().save16 && d_.overlap == 0 && (q.big || q.bwd) && fwd16;
   }
   splits_ = 8;
   size_t o_cnt = R((size_t)2 * L * seq_flag_words(H, B) * 4 + 64), o_err = R(64), o_x = R((size_t)T * B * 3 * H * 2);

@@ -156,7 +156,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     SeqFwdArgs a;
     a.HSb = y.HSb; a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = seq_[l].HF;
     a.xch = xbuf_;   // shared with the backward exchange: the kernels never overlap
-    if (y.s16) a.s16 = y.s16;   // (the wavefront only: SeqPlan::s16)
+    if (y.s16) a.s16 = y.s16;   // (SeqPlan::s16)
     else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
     a.Whh = y.Whh; a.bhh = P("bias_hh_l" + std::to_string(l));
     if (l == 0) { a.P = Ptab_; a.ids = ids_; }
@@ -286,7 +286,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     if (q.bwd) {
       SeqBwdArgs a;
       a.dy = y.dy;
-      if (q.s16) a.s16 = y.s16;   // (the 16-row kernel only: SeqPlan::s16)
+      if (q.s16) a.s16 = y.s16;   // (SeqPlan::s16)
       else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);

@@ -423,6 +423,7 @@ __global__ void __launch_bounds__(512, WPE) gru_fwd_seq_kernel(SeqFwdArgs a, Seq
   const rsrc_t rHSf = make_rsrc(a.HSf, sv_bytes + (unsigned)(Bp * H * 4));
   const rsrc_t rSr = make_rsrc(a.sr, a.sr ? sv_bytes : 0u), rSz = make_rsrc(a.sz, a.sz ? sv_bytes : 0u);
   const rsrc_t rSn = make_rsrc(a.sn, a.sn ? sv_bytes : 0u), rSg = make_rsrc(a.sghn, a.sghn ? sv_bytes : 0u);
+  const rsrc_t rS16 = make_rsrc(a.s16, a.s16 ? 2u * sv_bytes : 0u);   // < 4 GB: checked on the host
   const unsigned sv_lane = (unsigned)((b * H + j) * 4);
   stamp(a.dbg, T + 1, 0);   // prologue stamps in the (unused) step slot T + 1
   zero_next_flags(a.zero_next, a.zero_words);
@@ -551,7 +552,11 @@ __global__ void __launch_bounds__(512, WPE) gru_fwd_seq_kernel(SeqFwdArgs a, Seq
     load_gi(t + 1, gin);
     const int sstep = __builtin_amdgcn_readfirstlane(t * Bp * H * 4);   // uniform: no waterfall loop
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(h), rHSf, sv_lane, sstep + Bp * H * 4, 0);
-    if (a.sr) {
+    if (a.s16) {   // packed bf16 (r, z, n, gh_n): one 8-B store at twice the fp32 offsets
+      typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+      const u32x2_ pv = {(unsigned)f2bf(r) | ((unsigned)f2bf(z) << 16), (unsigned)f2bf(n) | ((unsigned)f2bf(gh[2]) << 16)};
+      __builtin_amdgcn_raw_buffer_store_b64(pv, rS16, sv_lane * 2u, sstep * 2, 0);
+    } else if (a.sr) {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rSr, sv_lane, sstep, 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rSz, sv_lane, sstep, 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(n), rSn, sv_lane, sstep, 0);
@@ -912,7 +917,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
   __shared__ __attribute__((aligned(16))) int idsL[NTP > 0 ? 32 : 1];
   auto load_saves = [&](int t) {
     const size_t o = ((size_t)t * Bp + b) * H + j;
-    sv[0] = a.dy[o]; sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o];
+    sv[0] = a.dy[o];
+    if (a.s16) ld_save16_raw(a.s16 + o * 4, sv[1], sv[2]);   // unpacked at use
+    else { sv[1] = a.sr[o]; sv[2] = a.sz[o]; sv[3] = a.sn[o]; sv[4] = a.sghn[o]; }
     sv[5] = a.HSf[o];   // HS[t] = h_{t-1}
     if constexpr (NTP > 0) svid = a.ids[(size_t)t * Bp + b];   // this thread's row id (fused dP)
   };
@@ -956,8 +963,10 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_kernel(SeqBwdArgs a) {
       }
     }
     const int idc = svid;
-    const float dy = sv[0], sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4], hprev = sv[5];
+    float sr = sv[1], sz = sv[2], sn = sv[3], sghn = sv[4];
+    const float dy = sv[0], hprev = sv[5];
     if (t > 0) load_saves(t - 1);
+    if (a.s16) unpack_save16(sr, sz, sr, sz, sn, sghn);
     // operands of the fused weight-gradient MFMAs (independent of other workgroups): issued after
     // the hand-off so the poll above does not wait behind them; first used after the publish
     bf16x8 hB[NTW > 0 ? NTW : 1];
@@ -1128,8 +1137,7 @@ bool gru_fwd_seq_supported(int H, int Bp) {
 }
 
 void gru_fwd_seq(const SeqFwdArgs& a, hipStream_t s) {
-  if (a.s16) throw std::runtime_error("gru_fwd_seq: packed bf16 saves are the wavefront's (gru_fwd_seq2) only");
-  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
+  if ((size_t)(a.T + 1) * a.Bp * a.H * (a.s16 ? 8 : 4) >= (1ull << 31))
     throw std::runtime_error("gru_fwd_seq: saves exceed the 2 GB buffer-offset range");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const int rs = fwd_rs(a.H);
@@ -1157,7 +1165,7 @@ void gru_fwd_seq_fc(const SeqFwdArgs& a, const SeqFcArgs& f, hipStream_t s) {
   if (a.H != 512 || f.V != 256 || !a.HF || !f.Wf || !f.WTf || !f.dlF || !f.dy || !f.dW || !f.db || !f.loss_part ||
       !f.labels || !f.inv_count || !f.b)
     throw std::runtime_error("gru_fwd_seq_fc: needs H = 512, V = 256, the HF copy and every FC buffer");
-  if ((size_t)(a.T + 1) * a.Bp * a.H * 4 >= (1ull << 31))
+  if ((size_t)(a.T + 1) * a.Bp * a.H * (a.s16 ? 8 : 4) >= (1ull << 31))
     throw std::runtime_error("gru_fwd_seq_fc: saves exceed the 2 GB buffer-offset range");
   const int nrb = a.Bp / 32;
   dim3 grid((a.H / 16) * nrb + kFcCons * nrb), block(512);
@@ -1212,7 +1220,6 @@ bool gru_bwd_seq_supported(int H, int Bp, bool fuse_w, bool fuse_p) {
 }
 
 void gru_bwd_seq(const SeqBwdArgs& a, hipStream_t s) {
-  if (a.s16) throw std::runtime_error("gru_bwd_seq: packed bf16 saves are read by the 16-row / large-H kernels only");
   dim3 grid((a.H / 16) * (a.Bp / 32)), block(512);
   const bool fw = a.dWhh_part != nullptr, fp = a.dP_part != nullptr;
 #define X(HH, NK, NW, NP)                                                              \

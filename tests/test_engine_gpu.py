@@ -1001,6 +1001,7 @@ def test_bwd16_matches_32_row_backward():
 
 
 @pytest.mark.parametrize("layers,B,H,E,T,plan", [
+    (1, 256, 512, 512, 32, "bwd0=persistent+dWhh+dP"),  # headline: 32-row persistent fwd / bwd
     (2, 128, 1024, 256, 12, "bwd0=persistent16"),       # config-4 shard: wavefront fwd, 16-row bwd
     (1, 512, 2048, 128, 6, "bwd0=persistent-big"),      # config 5: LDS-staged step fwd, large-H bwd
 ])
