@@ -74,8 +74,10 @@ def main() -> int:
     ap.add_argument("--dp-pipeline", type=int, choices=[-1, 0, 1], default=None,
                     help="one-layer data-parallel tail: -1 auto (= one collective; the pipelined form measured "
                          "slower), 0 one collective, 1 pipelined")
-    ap.add_argument("--shard-optim", action="store_true",
-                    help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
+    ap.add_argument("--shard-optim", type=int, nargs="?", const=1, default=-1, choices=[-1, 0, 1, 2],
+                    help="sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather of the fp32 "
+                         "masters (1) or of the bf16 working copies (2)); -1 (default): the plan of "
+                         "bench/cost_model.py for this preset and world size (1 GPU: replicated)")
     ap.add_argument("--min-warmup", type=int, default=300,
                     help="untimed steps before the timed region are at least this many: W from --warmup plus "
                          "max(0, N - W) extra, reported as extra_warmup_steps (a fresh box runs its first "
@@ -126,10 +128,19 @@ def main() -> int:
         cfg = cfg.replace(overlap=True)
     if args.bucket_mb:
         cfg = cfg.replace(bucket_mb=args.bucket_mb)
-    if args.shard_optim:
-        cfg = cfg.replace(shard_optim=True)
+    dp_plan = "replicated"
+    if (args.shard_optim == -1 or args.dp_pipeline is None) and world > 1:
+        # the world-aware plan from measured 1-GPU costs + the xGMI collective model
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+        from cost_model import plan as _dp_plan
+        dp_plan = _dp_plan(args.preset, world)
+    shard = args.shard_optim if args.shard_optim != -1 else {"zero1_fp32": 1, "zero1_bf16": 2}.get(dp_plan, 0)
+    if shard:
+        cfg = cfg.replace(shard_optim=int(shard))
     if args.dp_pipeline is not None:
         cfg = cfg.replace(dp_pipeline=args.dp_pipeline)
+    elif dp_plan == "pipelined":
+        cfg = cfg.replace(dp_pipeline=1)
 
     stream = NameStream(per_gpu, cfg.seq, cfg.sos, cfg.eos, seed=1000 + ctx.rank, max_len=cfg.max_len)
     pool = [stream.next() for _ in range(8)]
@@ -169,7 +180,7 @@ def main() -> int:
 
     extra = max(0, args.min_warmup - args.warmup) if ctx.device.type == "cuda" else 0   # GPU clock ramp only
     if args.impl != "hip":
-        G = 1
+        G, lead = 1, 0
     single = step
 
     def run(i0, n):
@@ -215,7 +226,7 @@ def main() -> int:
                        "global_batch": cfg.batch, "seq_len": cfg.seq,
                        "parallelism": f"dp{world}", "impl": args.impl,
                        "optimizer": cfg.optimizer, "time_chunks": cfg.time_chunks,
-                       "overlap": cfg.overlap, "plan": plan, "shard_optim": cfg.shard_optim,
+                       "overlap": cfg.overlap, "plan": plan, "shard_optim": int(cfg.shard_optim), "dp_plan": dp_plan,
                        "dp_pipeline": (int(tr.t.dp_tail_recorded()) if args.impl == "hip" and hasattr(tr, "t") else 0),
                        "collectives": (len(tr.t.allreduce_log()) if args.impl == "hip" and comm is not None
                                        and hasattr(tr, "t") else 0)},

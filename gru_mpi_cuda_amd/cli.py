@@ -32,8 +32,9 @@ def _add_model_args(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--optimizer", choices=["adam", "sgd"], default=None)
     ap.add_argument("--lr-sched", dest="lr_sched", choices=["const", "cosine", "linear"], default=None,
                     help="learning-rate decay after --warmup-steps, down to --lr-min at --total-steps")
-    ap.add_argument("--shard-optim", dest="shard_optim", action="store_const", const=True, default=None,
-                    help="data-parallel: sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather)")
+    ap.add_argument("--shard-optim", dest="shard_optim", type=int, nargs="?", const=1, default=None, choices=[0, 1, 2],
+                    help="data-parallel: sharded optimiser step (reduce-scatter, Adam on 1/world, all-gather of "
+                         "the fp32 masters (1) or of the bf16 working copies (2))")
     ap.add_argument("--carry-hidden", dest="carry_hidden", action="store_const", const=True, default=None,
                     help="truncated BPTT: carry each step's final hidden state into the next step")
 

@@ -53,8 +53,11 @@ class GRUConfig:
                                 # leaves the gradient.
     # ---- distributed -------------------------------------------------------------
     bucket_mb: float = 8.0      # gradient all-reduce bucket size (MiB of fp32)
-    shard_optim: bool = False   # data-parallel ZeRO-1 step: reduce-scatter the gradient, Adam on the
-                                # owned 1/world slice, all-gather the fp32 masters (Trainer::set_shard_optim)
+    shard_optim: int = 0        # data-parallel ZeRO-1 step: reduce-scatter the gradient, Adam on the
+                                # owned 1/world slice, then all-gather (Trainer::set_shard_optim):
+                                # 1 (or True) the fp32 masters; 2 the bf16 working copies (half the
+                                # bytes; every bf16 layout re-derived locally, fp32 biases exchanged
+                                # exactly, other ranks' fp32 master slices gathered only for checkpoints)
     dp_pipeline: int = -1       # one-layer data-parallel step: the bucketed, pipelined tail (two
                                 # collectives on a comm stream beside the dW_fc / embedding GEMMs and
                                 # a split Adam; Trainer::record_dp_tail_l1).  1 on; 0 and -1 (auto) one

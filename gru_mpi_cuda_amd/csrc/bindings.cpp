@@ -130,6 +130,8 @@ PYBIND11_MODULE(_C, m) {
       .def("dp_pipeline", &Trainer::dp_pipeline)
       .def("dp_tail_recorded", &Trainer::dp_tail_recorded)
       .def("shard_optim", &Trainer::shard_optim)
+      .def("shard_mode", &Trainer::shard_mode)
+      .def("gather_params", [](Trainer& t, uintptr_t s) { t.gather_params(S(s)); })
       .def("shard_chunk", &Trainer::shard_chunk)
       .def("gather_opt_state", [](Trainer& t, uintptr_t s) { t.gather_opt_state(S(s)); })
       .def("inject_error", &Trainer::inject_error)

@@ -70,6 +70,13 @@ void RcclComm::reduce_scatter_avg_f32(const float* send, float* recv, long n, hi
 void RcclComm::allgather_u16(const unsigned short* send, unsigned short* recv, long n, hipStream_t s) {
   RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclBfloat16, C(live()), s));
 }
+void RcclComm::allgather_u16_sum_u32(const unsigned short* send, unsigned short* recv, long n, unsigned* pack,
+                                     long np, hipStream_t s) {
+  RCCL_CHECK(ncclGroupStart());
+  if (n > 0) RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclBfloat16, C(live()), s));
+  if (np > 0) RCCL_CHECK(ncclAllReduce(pack, pack, (size_t)np, ncclUint32, ncclSum, C(live()), s));
+  RCCL_CHECK(ncclGroupEnd());
+}
 void RcclComm::allgather_f32(const float* send, float* recv, long n, hipStream_t s) {
   RCCL_CHECK(ncclAllGather(send, recv, (size_t)n, ncclFloat32, C(live()), s));
 }

@@ -31,6 +31,11 @@ class RcclComm {
   // recv[world*n] = concat over ranks of send[n]; bf16 payload moved as 16-bit words
   void allgather_u16(const unsigned short* send, unsigned short* recv, long n, hipStream_t s);
   void allgather_f32(const float* send, float* recv, long n, hipStream_t s);
+  // sharded optimiser with bf16 working copies: the owned bf16 slices all-gathered and, in the same
+  // group launch, a 32-bit integer sum over `pack` (each rank contributes its own entries, zeros
+  // elsewhere: the sum is an exact bitwise exchange of the fp32 values kernels read directly)
+  void allgather_u16_sum_u32(const unsigned short* send, unsigned short* recv, long n, unsigned* pack, long np,
+                             hipStream_t s);
   // MPI_Scatterv / MPI_Gatherv as grouped point-to-point transfers (one group launch): rank r's
   // slice is [displ[r], displ[r] + count[r]) elements of the root's buffer.  Scatter: the root sends
   // every other rank its slice into that rank's recv (the root's own slice stays where it is);

@@ -218,6 +218,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
 }
 
 Trainer::~Trainer() {
+  if (pbf_) (void)hipFree(pbf_);
+  if (bpack_) (void)hipFree(bpack_);
   for (auto& g : g_fb_) g.reset();
   for (auto& g : g_step_) g.reset();
   for (auto& g : g_group_) g.reset();
@@ -542,17 +544,37 @@ OptimArgs Trainer::optim_args() const {
   return a;
 }
 
-void Trainer::set_shard_optim(bool on) {
+void Trainer::set_shard_optim(int mode) {
+  const bool on = mode != 0;
+  if (mode < 0 || mode > 2) throw std::runtime_error("set_shard_optim: mode 0 (off), 1 (fp32 gather) or 2 (bf16 gather)");
   if (on && !comm_) throw std::runtime_error("set_shard_optim: needs a communicator (call set_comm first)");
   if (on && o_.clip > 0.f)
     throw std::runtime_error("set_shard_optim: gradient clipping needs the global norm; not supported sharded");
   if (on && nflat_ % 4) throw std::runtime_error("set_shard_optim: flat parameter count must be a multiple of 4");
   shard_opt_ = on;
+  shard_mode_ = mode;
   if (on) {
     const int W = comm_->world();
     shard_chunk_ = nflat_ / (4L * W) * 4;
     if ((long)W * shard_chunk_ > 0 && shard_chunk_ > (1L << 30))
       throw std::runtime_error("set_shard_optim: shard too large for one optimiser job");
+  }
+  if (mode == 2) {
+    if (d_.V % 64 || d_.E % 64 || d_.H % 64)
+      throw std::runtime_error("set_shard_optim(2): the bf16 re-layout needs V, E, H % 64 == 0");
+    branges_ = FlatRanges{};
+    auto addr = [&](const std::string& k, int n) {
+      if (branges_.cnt >= 16) throw std::runtime_error("set_shard_optim(2): too many bias tensors");
+      branges_.off[branges_.cnt] = off_.at(k);
+      branges_.n[branges_.cnt++] = n;
+    };
+    for (int l = 0; l < d_.L; ++l) {
+      addr("bias_ih_l" + std::to_string(l), 3 * d_.H);
+      addr("bias_hh_l" + std::to_string(l), 3 * d_.H);
+    }
+    addr("fc.bias", d_.V);
+    if (!pbf_) HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&pbf_), (size_t)nflat_ * 2));
+    if (!bpack_) HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&bpack_), (size_t)branges_.total() * 4));
   }
   g_step_[0].reset();
   g_step_[1].reset();
@@ -575,12 +597,50 @@ void Trainer::record_sharded_opt(hipStream_t s) {
   // the fused optimiser launch's flat path (same update code as the replicated step), no casts:
   // the bf16 copies are refreshed from the gathered masters below
   OptCastJobs j;
+  if (shard_mode_ == 2) {
+    // mode 2: the owned slice's (and the tail's) bf16 working copy straight from Adam's registers;
+    // all-gather those (half the bytes of the fp32 masters) with the owned fp32 biases packed beside
+    // them, then re-derive every bf16 layout locally
+    if (c > 0) j.add((long)r * c, 0, (int)c, pbf_ + (long)r * c, nullptr);
+    if (tail > 0) j.add((long)W * c, 0, (int)tail, pbf_ + (long)W * c, nullptr);
+    if (j.n) adam_cast_multi(optim_args(), j, s);
+    const long nb = branges_.total();
+    flat_pack_u32(params_, bpack_, branges_, (long)r * c, (long)(r + 1) * c, (long)W * c, 0, s);
+    comm_->allgather_u16_sum_u32(pbf_ + (long)r * c, pbf_, c, bpack_, nb, s);   // one group launch
+    flat_pack_u32(params_, bpack_, branges_, 0, 0, (long)W * c, 1, s);
+    refresh_from_bf16(s);
+    HIP_LAUNCH_CHECK();
+    return;
+  }
   if (c > 0) j.add((long)r * c, 0, (int)c, nullptr, nullptr);
   if (tail > 0) j.add((long)W * c, 0, (int)tail, nullptr, nullptr);   // every rank: the same tail
   if (j.n) adam_cast_multi(optim_args(), j, s);
   if (c > 0 && W > 1) comm_->allgather_f32(params_ + (long)r * c, params_, c, s);   // in place
   refresh_weights(s);
   HIP_LAUNCH_CHECK();
+}
+
+void Trainer::refresh_from_bf16(hipStream_t s) {
+  // the refresh_weights layouts, from the gathered flat bf16 working copy (bitwise what the casts of
+  // the fp32 masters give: rounding is per element)
+  const int V = d_.V, E = d_.E, H = d_.H;
+  auto B16 = [&](const std::string& k) { return pbf_ + off_.at(k); };
+  CastJobs j;
+  j.add16(B16("embedding"), V, E, Emb, EmbT);
+  for (int l = 0; l < d_.L; ++l) {
+    const std::string k = std::to_string(l);
+    j.add16(B16("weight_hh_l" + k), 3 * H, H, Ls_[l].Whh, Ls_[l].WhhT);
+    j.add16(B16("weight_ih_l" + k), 3 * H, in_dim(l), Ls_[l].Wih, Ls_[l].WihT);
+  }
+  j.add16(B16("fc.weight"), V, H, Wfc, WfcT, WfcF, WfcTF);
+  cast_multi(j, s);
+  HIP_LAUNCH_CHECK();
+}
+
+void Trainer::gather_params(hipStream_t s) {
+  if (shard_mode_ != 2 || !comm_ || comm_->world() == 1 || shard_chunk_ == 0) return;
+  const long c = shard_chunk_;
+  comm_->allgather_f32(params_ + (long)comm_->rank() * c, params_, c, s);   // in place
 }
 
 void Trainer::gather_opt_state(hipStream_t s) {

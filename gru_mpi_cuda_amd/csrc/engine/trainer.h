@@ -155,10 +155,18 @@ class Trainer {
   long min_bucket_ = 0, ar_ready_ = 0, ar_launched_ = 0;
   bool ar_busy_ = false, dP_inplace_ = false;
   std::vector<std::pair<long, long>> ar_log_;   // (offset, floats) of every recorded collective
-  // sharded optimiser (set_shard_optim)
+  // sharded optimiser (set_shard_optim): mode 1 all-gathers the fp32 masters, mode 2 the bf16 working
+  // copies (flat mirror pbf_; the fp32 biases ride along as an exact integer-sum exchange, bpack_) and
+  // re-derives every bf16 layout locally -- the fp32 masters of other ranks' slices then go stale on this
+  // rank (gather_params() for checkpoints)
   bool shard_opt_ = false;
+  int shard_mode_ = 0;
   long shard_chunk_ = 0;
+  u16* pbf_ = nullptr;
+  unsigned* bpack_ = nullptr;
+  FlatRanges branges_;
   void record_sharded_opt(hipStream_t s);
+  void refresh_from_bf16(hipStream_t s);
   OptimArgs optim_args() const;
  public:
   void set_batch_device(const int* x, const int* y, int B, hipStream_t s);
@@ -177,8 +185,11 @@ class Trainer {
   // of 4; the < 4*world-float tail is all-reduced), runs Adam on the owned slice of the masters and
   // moments, all-gathers the updated masters in place and refreshes the bf16 MFMA copies.  Moments
   // outside the owned slice go stale: gather_opt_state() all-gathers them (checkpoints).
-  void set_shard_optim(bool on);
+  void set_shard_optim(int mode);   // 0 off, 1 fp32 masters gathered, 2 bf16 working copies gathered
   bool shard_optim() const { return shard_opt_; }
+  int shard_mode() const { return shard_mode_; }
+  // mode 2: all-gather the fp32 masters (every rank's slice current again; checkpoints, state_dict)
+  void gather_params(hipStream_t s);
   long shard_chunk() const { return shard_chunk_; }
   void gather_opt_state(hipStream_t s);
   void step(hipStream_t s);      // whole training step as one graph replay

@@ -460,16 +460,23 @@ int reduce_slabs_blocks(SlabJobs& j);   // fills j.blk_start, returns the launch
 DEV_HOST_INLINE long ft_offset(int r, int k, int K) {
   return ((long)((r >> 4) * (K >> 5) + (k >> 5)) * 64 + (r & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
 }
-struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; u16* dstF = nullptr; u16* dstTF = nullptr; };
+// src16 (instead of src): a bf16 source -- the layouts re-derived from gathered bf16 working copies
+// (sharded optimiser, Trainer::record_sharded_opt mode 2); bf16 -> fp32 -> bf16 is exact
+struct CastJob { const float* src; u16* dst; u16* dstT; int R, C; u16* dstF = nullptr; u16* dstTF = nullptr;
+                 const u16* src16 = nullptr; };
 struct CastJobs { CastJob job[24]; int blk_start[25]; int n = 0;
   void add(const float* s, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
-    job[n++] = CastJob{s, d, dT, R, C, dF, dTF}; } };
+    job[n++] = CastJob{s, d, dT, R, C, dF, dTF}; }
+  void add16(const u16* s, int R, int C, u16* d, u16* dT, u16* dF = nullptr, u16* dTF = nullptr) {
+    job[n++] = CastJob{nullptr, d, dT, R, C, dF, dTF, s}; } };
 void cast_multi(CastJobs& j, hipStream_t s);
 // Fused optimiser + weight refresh, one launch over every parameter tensor: Adam/SGD on the fp32
 // master slice [off, off+R*C) of the flat buffers, then (matrix jobs) its bf16 copy and/or bf16
 // transpose.  Matrix jobs need R % 64 == 0 and C % 64 == 0; R == 0 marks a flat (bias) job of C
 // elements, C % 4 == 0.
 // dstF / dstTF (nullable): FT-layout copies of the matrix / its transpose (see ft_offset)
+// Flat job with dst: the updated values' bf16 also go to dst[i - off] (the flat bf16 working copy of
+// the sharded optimiser's mode 2)
 // gsl (nullable): the job's gradient is the fixed-order sum of nsl slabs gsl[s * R*C + i] (split-K /
 // per-row-block partials), summed here instead of by a separate reduce launch; the sum is also
 // written to the gradient buffer (it stays observable).
@@ -481,6 +488,12 @@ struct OptCastJobs { OptCastJob job[32]; int blk_start[33]; int n = 0;
 void adam_cast_multi(const OptimArgs& a, OptCastJobs& j, hipStream_t s);
 
 void fill_f32(float* p, long n, float v, hipStream_t s);
+// Exact exchange of the fp32 entries of up to 16 flat ranges (the biases, which kernels read in fp32)
+// between ranks of a sharded optimiser: pack (unpack = 0): pack[k] = bits of p[f] if f is in the
+// owned chunk [lo, hi), else 0; unpack (1): p[f] = bits of pack[k] for f < tail (the replicated tail,
+// updated identically on every rank, is left alone).  k enumerates the ranges in order.
+struct FlatRanges { long off[16]; int n[16]; int cnt = 0; __host__ __device__ long total() const { long t = 0; for (int i = 0; i < cnt; ++i) t += n[i]; return t; } };
+void flat_pack_u32(float* p, unsigned* pack, const FlatRanges& r, long lo, long hi, long tail, int unpack, hipStream_t s);
 // placement census: out[b] = HW_REG_XCC_ID of the CU that ran block b
 void xcc_census(unsigned* out, int nblocks, int threads, hipStream_t s);
 // fault injection for watchdog tests: one wave busy-waits `us` microseconds (capped at 5 s)

@@ -133,7 +133,7 @@ __global__ void cast_multi_kernel(CastJobs j) {
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int y = ty; y < th; y += 4) {
     const int r = r0 + y, c = c0 + tx;
-    const float v = (r < J.R && c < J.C) ? J.src[(size_t)r * J.C + c] : 0.f;
+    const float v = (r < J.R && c < J.C) ? (J.src16 ? bf2f(J.src16[(size_t)r * J.C + c]) : J.src[(size_t)r * J.C + c]) : 0.f;
     tile[y][tx] = v;
     if (J.dst && r < J.R && c < J.C) J.dst[(size_t)r * J.C + c] = f2bf(v);
   }
@@ -174,6 +174,26 @@ void cast_multi(CastJobs& j, hipStream_t s) {
   }
   j.blk_start[j.n] = tot;
   hipLaunchKernelGGL(cast_multi_kernel, dim3(tot), dim3(256), 0, s, j);
+}
+
+__global__ void flat_pack_kernel(float* p, unsigned* pack, FlatRanges r, long lo, long hi, long tail, int unpack) {
+  const long tot = r.total();
+  for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < tot; k += (long)gridDim.x * blockDim.x) {
+    long base = 0, f = -1;
+    for (int i = 0; i < r.cnt; ++i) {
+      if (k < base + r.n[i]) { f = r.off[i] + (k - base); break; }
+      base += r.n[i];
+    }
+    if (f < 0) continue;
+    if (!unpack) pack[k] = (f >= lo && f < hi) ? __float_as_uint(p[f]) : 0u;
+    else if (f < tail) p[f] = __uint_as_float(pack[k]);
+  }
+}
+void flat_pack_u32(float* p, unsigned* pack, const FlatRanges& r, long lo, long hi, long tail, int unpack, hipStream_t s) {
+  const long tot = r.total();
+  if (tot <= 0) return;
+  const int blocks = (int)std::min<long>((tot + 255) / 256, 256);
+  hipLaunchKernelGGL(flat_pack_kernel, dim3(blocks), dim3(256), 0, s, p, pack, r, lo, hi, tail, unpack);
 }
 
 __global__ void adam_kernel(OptimArgs a) {

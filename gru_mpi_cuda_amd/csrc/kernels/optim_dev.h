@@ -182,7 +182,12 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
   if (J.R == 0) {   // flat job: 1024 elements per block
     const long i4 = (J.off >> 2) + (long)t * 256 + threadIdx.x;
     if ((long)t * 1024 + threadIdx.x * 4 < J.C) {
-      if constexpr (!DSC1) {
+      if (J.dst) {   // + the flat bf16 working copy (sharded optimiser, mode 2)
+        const float4 p = adam4<GSC1>(a, J, co, i4);
+        typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+        const u32x2_ b = {(unsigned)f2bf(p.x) | ((unsigned)f2bf(p.y) << 16), (unsigned)f2bf(p.z) | ((unsigned)f2bf(p.w) << 16)};
+        *reinterpret_cast<u32x2_*>(J.dst + (i4 * 4 - J.off)) = b;
+      } else if constexpr (!DSC1) {
         adam4<GSC1>(a, J, co, i4);
       } else {
         float4 p = reinterpret_cast<float4*>(a.p)[i4];

@@ -77,7 +77,7 @@ class HipTrainer:
             self.t.set_comm(self.comm, [(a, b - a) for a, b in self.buckets],
                             max(1024, int(cfg.bucket_mb * (1 << 20) / 4)))
             if cfg.shard_optim:
-                self.t.set_shard_optim(True)
+                self.t.set_shard_optim(int(cfg.shard_optim))
             self.t.set_dp_pipeline(int(cfg.dp_pipeline))
         self.t.refresh_weights(self._stream())
         self._one_graph = True
@@ -204,6 +204,8 @@ class HipTrainer:
                 "allreduce_ms_standalone": e0.elapsed_time(e1)}
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
+        if self.t.shard_mode() == 2:   # other ranks' fp32 master slices are only current after a gather
+            self.t.gather_params(self._stream())
         torch.cuda.synchronize(self.dev)
         return self._unpad({k: v.cpu() for k, v in from_flat(self.icfg, self.params).items()})
 
@@ -235,7 +237,7 @@ class HipTrainer:
 
 class CpuTrainer:
     def __init__(self, cfg: GRUConfig, ctx: Optional[DistCtx] = None,
-                 params: Optional[Dict[str, torch.Tensor]] = None, dtype=torch.float32):
+                 params: Optional[Dict[str, torch.Tensor]] = None, dtype=torch.float32, bf16_weights: bool = False):
         self.cfg = cfg
         self.ctx = ctx or DistCtx()
         if cfg.batch % self.ctx.world:
@@ -251,6 +253,10 @@ class CpuTrainer:
             import torch.distributed as dist
             dist.broadcast(self.flat_p, 0)
         self.shard = None
+        # bf16 working copies (cfg.shard_optim == 2, or bf16_weights=True for its replicated reference):
+        # the forward / backward use bf16-rounded weight matrices and fp32 biases, as the device step does
+        self.bf16 = bool(bf16_weights) or int(cfg.shard_optim) == 2
+        self.flat_bf = None
         if cfg.shard_optim and self.ctx.world > 1:
             # ZeRO-1 twin of Trainer::set_shard_optim: rank r owns flat floats [r*c, (r+1)*c) with c a
             # multiple of 4; the tail past world*c is updated by every rank
@@ -260,6 +266,10 @@ class CpuTrainer:
             c = n // (4 * W) * 4
             self.shard = (c, {"own": slice(r * c, (r + 1) * c), "tail": slice(W * c, n)})
             self.opt = cpu_ref.Adam(cfg, {k: self.flat_p[sl] for k, sl in self.shard[1].items()})
+            if int(cfg.shard_optim) == 2:   # the gathered flat bf16 working copy (Trainer::pbf_)
+                self.flat_bf = self.flat_p.to(torch.bfloat16)
+                self._bias_ranges = [(s.offset, s.offset + int(np.prod(s.shape))) for s in self.layout.segments
+                                     if "bias" in s.name]
         else:
             self.opt = cpu_ref.Adam(cfg, self.params)
         self.buckets = _bucket_list(cfg, self.layout.total)
@@ -270,9 +280,19 @@ class CpuTrainer:
     def reset_state(self) -> None:
         self._state = None
 
+    def compute_params(self) -> Dict[str, torch.Tensor]:
+        """The weights the step computes with: fp32 masters, or (bf16 working copies) the weight
+        matrices rounded to bf16 -- from the gathered flat bf16 copy when the optimiser is sharded
+        (other ranks' fp32 master slices are stale there) -- and the fp32 biases."""
+        if not self.bf16:
+            return self.params
+        src = self.layout.views(self.flat_bf.float()) if self.flat_bf is not None else None
+        return {k: (v if v.dim() == 1 else (src[k] if src is not None else v.to(torch.bfloat16).float()))
+                for k, v in self.params.items()}
+
     def forward_backward(self, x: np.ndarray, y: np.ndarray) -> None:
         out = [] if self.cfg.carry_hidden else None
-        loss, grads = cpu_ref.manual_backward(self.params, self.cfg, torch.from_numpy(np.asarray(x)),
+        loss, grads = cpu_ref.manual_backward(self.compute_params(), self.cfg, torch.from_numpy(np.asarray(x)),
                                               torch.from_numpy(np.asarray(y)), h0=self._state,
                                               state_out=out)
         if out is not None:
@@ -330,6 +350,23 @@ class CpuTrainer:
         import torch.distributed as dist
         c, sl = self.shard
         self.opt.step({k: self.flat_p[v] for k, v in sl.items()}, {k: self.flat_g[v] for k, v in sl.items()})
+        if self.flat_bf is not None:
+            # twin of record_sharded_opt mode 2: the owned slice's and the tail's bf16 copies, an
+            # all-gather of the bf16 slices, and the owned fp32 biases as an integer-sum exchange
+            W, r = self.ctx.world, self.ctx.rank
+            self.flat_bf[sl["own"]] = self.flat_p[sl["own"]].to(torch.bfloat16)
+            self.flat_bf[sl["tail"]] = self.flat_p[sl["tail"]].to(torch.bfloat16)
+            if c:
+                parts = list(self.flat_bf[:W * c].view(W, c).unbind(0))
+                dist.all_gather(parts, self.flat_bf[sl["own"]].clone())
+            idx = torch.cat([torch.arange(a, b) for a, b in self._bias_ranges])
+            bits = self.flat_p[idx].view(torch.int32).clone()
+            own = (idx >= r * c) & (idx < (r + 1) * c)
+            pack = torch.where(own, bits, torch.zeros_like(bits))
+            dist.all_reduce(pack, op=dist.ReduceOp.SUM)
+            keep = idx < W * c
+            self.flat_p[idx[keep]] = pack[keep].view(torch.float32)
+            return
         if c:
             parts = list(self.flat_p[:self.ctx.world * c].view(self.ctx.world, c).unbind(0))
             dist.all_gather(parts, self.flat_p[sl["own"]].clone())
@@ -342,7 +379,18 @@ class CpuTrainer:
     def loss(self) -> float:
         return self._loss
 
+    def gather_params(self) -> None:
+        """Twin of Trainer::gather_params: with bf16 working copies gathered (shard_optim 2) the fp32
+        master slices other ranks own are stale here until this all-gather."""
+        if self.flat_bf is None or not self.shard[0]:
+            return
+        import torch.distributed as dist
+        c, sl = self.shard
+        parts = list(self.flat_p[:self.ctx.world * c].view(self.ctx.world, c).unbind(0))
+        dist.all_gather(parts, self.flat_p[sl["own"]].clone())
+
     def state_dict(self) -> Dict[str, torch.Tensor]:
+        self.gather_params()
         return {k: v.detach().clone() for k, v in self.params.items()}
 
     def grad_dict(self) -> Dict[str, torch.Tensor]:

@@ -71,9 +71,11 @@ def test_bench_sharded_optimizer_world2():
     args = [sys.executable, "bench.py", "--gpus", "2", "--preset", "cpu_tiny", "--steps", "3", "--warmup", "1"]
     a = _lines(args, 2, env=env)
     b = _lines(args + ["--shard-optim"], 2, env=env)
-    assert b["config"]["shard_optim"] is True and a["config"]["shard_optim"] is False
+    assert b["config"]["shard_optim"] == 1 and a["config"]["shard_optim"] == 0
     assert a["final_loss"] == b["final_loss"]
     assert b["extra_warmup_steps"] == 0     # the GPU clock-ramp warm-up only runs on GPUs
+    c = _lines(args + ["--shard-optim", "2"], 2, env=env)   # bf16 working copies gathered
+    assert c["config"]["shard_optim"] == 2 and abs(c["final_loss"] - a["final_loss"]) < 0.05 * a["final_loss"]
 
 
 def test_bench_rejects_world_mismatch():

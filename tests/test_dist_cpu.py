@@ -191,6 +191,55 @@ def test_sharded_optimizer_equals_replicated(tmp_path, world):
             assert torch.equal(ref[k], got[k]), (r, k)
 
 
+def _shard_bf16_worker(rank, world, port, outdir, steps, mode):
+    """mode 'rep': replicated step computing with bf16-rounded weight matrices (the device's working
+    copies); 'zero2': ZeRO-1 with the bf16 working copies gathered (cfg.shard_optim = 2)."""
+    _env(rank, world, port)
+    from gru_mpi_cuda_amd.parallel import dist as gdist
+    from gru_mpi_cuda_amd.engine.trainer import CpuTrainer
+    ctx = gdist.init(use_gpu=False)
+    cfg = GRUConfig(vocab=256, embed=12, hidden=20, layers=2, batch=16, seq=5, lr=1e-2,
+                    shard_optim=2 if mode == "zero2" else 0)
+    tr = CpuTrainer(cfg, ctx, params=init_params(cfg, seed=1), bf16_weights=True)
+    ds = NameStream(cfg.batch, cfg.seq, seed=5)
+    per = cfg.batch // world
+    for _ in range(steps):
+        x, y = ds.next()
+        tr.step(x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per])
+    cp = tr.compute_params()
+    torch.save({"compute": {k: v.clone() for k, v in cp.items()}, "masters": tr.state_dict(), "loss": tr.loss()},
+               os.path.join(outdir, f"b{mode}_{world}_r{rank}.pt"))
+    gdist.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_bf16_gather_equals_replicated(tmp_path, world):
+    """ZeRO-1 with the bf16 working copies gathered (shard_optim = 2; CPU twin of Trainer::record_sharded_opt
+    mode 2: Adam on the owned slice, its bf16 copy all-gathered, the owned fp32 biases exchanged as an
+    integer sum) against the replicated step on bf16 working copies: after 3 steps every rank holds
+    bitwise the same bf16 weights, fp32 biases and (after gather_params) fp32 masters."""
+    ctx = mp.get_context("spawn")
+    for mode in ("rep", "zero2"):
+        port = _free_port()
+        procs = [ctx.Process(target=_shard_bf16_worker, args=(r, world, port, str(tmp_path), 3, mode))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(240)
+            assert p.exitcode == 0
+    ref0 = torch.load(tmp_path / f"brep_{world}_r0.pt", weights_only=True)
+    for r in range(world):
+        ref = torch.load(tmp_path / f"brep_{world}_r{r}.pt", weights_only=True)
+        got = torch.load(tmp_path / f"bzero2_{world}_r{r}.pt", weights_only=True)
+        assert got["loss"] == ref["loss"]   # (the loss is the rank's own shard of the batch)
+        for k in ref0["compute"]:           # every rank: the same weights
+            assert torch.equal(ref0["compute"][k], ref["compute"][k]), (r, k)
+        for part in ("compute", "masters"):
+            for k in ref[part]:
+                assert torch.equal(ref[part][k], got[part][k]), (r, part, k)
+
+
 def test_shard_and_buckets():
     from gru_mpi_cuda_amd.parallel.dist import shard, bucket_bounds
     for n in (0, 1, 7, 37, 64):

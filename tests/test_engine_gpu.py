@@ -401,23 +401,26 @@ def test_single_graph_step_with_rccl_world1(layers, E, H, bucket_mb, n_coll):
     torch.testing.assert_close(a.params, b.params, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("layers,E,H,opt", [(1, 512, 512, "adam"), (2, 128, 256, "adam"), (1, 256, 256, "sgd")])
-def test_sharded_optimizer_step_world1(layers, E, H, opt):
+def test_sharded_optimizer_step_world1(layers, E, H, opt, mode):
     """ZeRO-1 step (Trainer::set_shard_optim) on a 1-rank communicator: reduce-scatter (a copy),
     Adam on the owned slice (= everything, through the fused launch's flat path), in-place
     all-gather skipped, bf16 refresh -- must equal the no-comm step (same slab-sum order, same
     update formula; allowed one-ulp-level drift where the compiler contracts the matrix and flat
-    update paths differently), and gather_opt_state must leave the moments intact."""
+    update paths differently), and gather_opt_state must leave the moments intact.  mode 2 gathers the
+    bf16 working copies instead (flat bf16 mirror, biases exchanged as an integer sum, every layout
+    re-derived by the bf16-source cast)."""
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer
     from gru_mpi_cuda_amd.ops import load_ext
     C = load_ext()
     cfg = GRUConfig(vocab=256, embed=E, hidden=H, layers=layers, batch=64, seq=8, seed=3, optimizer=opt,
-                    shard_optim=True)
+                    shard_optim=mode)
     x, y = NameStream(cfg.batch, cfg.seq, seed=4).next()
     comm = C.RcclComm(C.RcclComm.unique_id(), 0, 1)
     a = HipTrainer(cfg, params=init_params(cfg), comm=comm)
-    b = HipTrainer(cfg.replace(shard_optim=False), params=init_params(cfg))
-    assert a.t.shard_optim() and a.t.shard_chunk() == a.layout.total // 4 * 4
+    b = HipTrainer(cfg.replace(shard_optim=0), params=init_params(cfg))
+    assert a.t.shard_optim() and a.t.shard_mode() == mode and a.t.shard_chunk() == a.layout.total // 4 * 4
     for _ in range(3):
         a.step(x, y)
         b.step(x, y)

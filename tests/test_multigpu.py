@@ -166,10 +166,12 @@ def test_dp_two_layer_flush_path_equals_one_gpu(tmp_path):
 
 
 @needs2
-def test_dp_sharded_optimizer_equals_one_gpu(tmp_path):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_dp_sharded_optimizer_equals_one_gpu(tmp_path, mode):
     """ZeRO-1 step at world 2 (reduce-scatter, SGD on the owned half, all-gather of the fp32
-    masters) equals one GPU on the whole batch."""
-    _compare_dp(tmp_path, 2, dict(H512_CFG, shard_optim=True), 2e-4)
+    masters (1) or of the bf16 working copies with the fp32 biases exchanged (2)) equals one GPU on
+    the whole batch."""
+    _compare_dp(tmp_path, 2, dict(H512_CFG, shard_optim=mode), 2e-4)
 
 
 ADAM_CFG = dict(H512_CFG, optimizer="adam", lr=1e-3)
