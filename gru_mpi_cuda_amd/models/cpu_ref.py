@@ -201,8 +201,16 @@ class Adam:
 def sample_inverse_cdf(prob: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     """The reference's ``random_select`` (namegensf.cu:322-333): first i with an fp32
     running sum ``psum > r`` in index order, else n-1.  prob [N, V], r [N]."""
-    # sequential prefix on CPU: fp32 like the reference, or fp64 for the exact-math oracle
-    cs = torch.cumsum(prob if prob.dtype == torch.float64 else prob.to(torch.float32), dim=-1)
+    # sequential prefix on CPU: fp32 like the reference, or fp64 for the exact-math oracle.  An explicit
+    # loop over the vocabulary (vectorised over the names): torch.cumsum does not promise the strictly
+    # left-to-right fp32 rounding of the reference's loop (a hypothesis case: 0.25 + 8.2e-9 + 8.2e-9
+    # stays 0.25 sequentially but not in cumsum)
+    p = prob if prob.dtype == torch.float64 else prob.to(torch.float32)
+    cs = torch.empty_like(p)
+    acc = torch.zeros_like(p[..., 0])
+    for i in range(p.shape[-1]):
+        acc = acc + p[..., i]
+        cs[..., i] = acc
     hit = cs > r.unsqueeze(-1)
     idx = hit.to(torch.int64).argmax(-1)
     return torch.where(hit.any(-1), idx, torch.full_like(idx, prob.shape[-1] - 1))
