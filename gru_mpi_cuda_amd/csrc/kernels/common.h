@@ -33,6 +33,15 @@ DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 }
 
 DEV bf16x8 ld8(const u16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+// acc + sum of the 8 bf16 of v: four v_dot2c_f32_bf16 against (1, 1) -- a quarter of the VALU
+// issue of eight converts + adds, which beside the MFMAs slowed gemm256's row-sum workgroups 8 %
+DEV float add_sum8(const bf16x8& v, float acc) {
+  const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{v[2 * i], v[2 * i + 1]}, one, acc, false);
+  return acc;
+}
 
 DEV bf16x8 zero8() {
   bf16x8 z;

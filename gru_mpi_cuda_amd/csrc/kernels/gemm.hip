@@ -155,7 +155,7 @@ bool gemm_library_wanted(const GemmArgs& a) {
   // with the bias row sum the library pays a second pass over A (5.5 TB/s): worth it only where
   // the LDS kernel's split-K slabs get big -- dW_hh at H = 2048 (6144 x 2048: 1.90 -> 1.25 + 0.15 ms);
   // at H = 1024 (3072 x 1024, K = 65536) the two GEMMs tie and the row sum is pure loss
-  // (profiles/r1_blaslt_ab.jsonl).  GK_BLASLT_MIN_GFLOP=0 lifts this too (tests).
+  // (profiles/r1_blaslt_ab.jsonl).  GK_BLASLT=all lifts this too (tests).
   if (a.rowsumA && (double)a.M * a.N < 8e6 && blaslt_min_gflop() > 0) return false;
   return true;
 }

@@ -39,16 +39,6 @@ DEV int xcd_remap256(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-// acc + sum of the 8 bf16 of v: four v_dot2c_f32_bf16 against (1, 1) -- a quarter of the VALU
-// issue of eight converts + adds, which beside the MFMAs slowed the row-sum waves' workgroups 8 %
-DEV float add_sum8(const bf16x8& v, float acc) {
-  const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_fdot2_f32_bf16(bf16x2_t{v[2 * i], v[2 * i + 1]}, one, acc, false);
-  return acc;
-}
-
 // RS: also the row sums of A (the bias gradient of a weight-gradient product) into
 // rowsumA[split][M], from the A fragments already in registers -- by the waves of the first column
 // tile that read each row (wave column 0 of tile column 0), instead of a second pass over A
@@ -522,8 +512,8 @@ __global__ void __launch_bounds__(512, 1) gemm256p_kernel(GemmArgs a, int ntn, i
 // (profiles/r4_gemm256_ring.jsonl); removed.  Twice the barriers per MFMA cost more than the deeper
 // prefetch gained.)
 
-// Which form (GK_GEMM256_MFMA=16 / 32 forces one; read per launch so tests and benches switch it
-// in-process).  Default: 32x32x16 only for short K-slices (<= 256), where it measured faster --
+// Which form (gemm_variants().mfma = 16 / 32 forces one; read per launch so tests and benches switch
+// it in-process).  Default: 32x32x16 only for short K-slices (<= 256), where it measured faster --
 // h2048 dH 65536 x 2048 x 256: 438 vs 360 TF -- and 16x16x32 elsewhere (sq8192 1284 vs 1203 TF,
 // h2048 dW_hh 4-way split 1139 vs 1073 TF; profiles/r3_gemm256_m32.jsonl)
 GemmVariants& gemm_variants() {
@@ -535,8 +525,8 @@ static int gemm256_mfma(int kper) {
   if (m == 16 || m == 32) return m;
   return kper <= 256 ? 32 : 16;
 }
-// The phased, staggered pipeline (gemm256p_kernel) for the 16x16x32 form: GK_GEMM256_PHASED=1
-// always, =0 never; unset: the split-K / row-sum weight-gradient products, the 192-row shapes and
+// The phased, staggered pipeline (gemm256p_kernel) for the 16x16x32 form: gemm_variants().phased = 1
+// always, = 0 never; unset: the split-K / row-sum weight-gradient products, the 192-row shapes and
 // K-slices >= 4096, gemm256_kernel (one vmcnt(0) + barrier per k-tile) for the shorter unsplit plain
 // products.  In microbenchmarks the staggered kernel led there too (h1024 Gi 795 vs 755 TF, h2048
 // logits 770 vs 758, profiles/r5_gemm_plain_shapes_ab.jsonl), but in the h2048 step the logits GEMM

@@ -374,7 +374,7 @@ struct GemmArgs {
                                    // 3 one-shot 64x64 (gemm_small), 4 hipBLASLt (+ row-sum kernel),
                                    // 5 LDS-staged 256x256 (gemm256.hip)
 };
-// algo 0 sends plain (no one-hot, no bias, unsplit) products of >= GK_BLASLT_MIN_GFLOP to hipBLASLt
+// algo 0 sends plain (no one-hot, no bias, unsplit) products of >= blaslt_min_gflop() to hipBLASLt
 bool gemm_library_ok(const GemmArgs& a);
 bool gemm_library_wanted(const GemmArgs& a);
 // the product on hipBLASLt (+ the row-sum pass when rowsumA): false, with nothing launched, when the

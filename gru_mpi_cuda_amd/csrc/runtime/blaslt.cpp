@@ -3,6 +3,7 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -107,18 +108,19 @@ void blaslt_init(bool force) {
   init_locked(s);
 }
 
-// GK_BLASLT=1 sends the plain (non-weight-gradient) GEMMs gemm_library_wanted() picks to the
-// library; off by default (the hand-written gemm256 takes them).  Separately, GK_WGRAD_GEMM=lib
+// GK_BLASLT=1 sends the plain (non-weight-gradient) GEMMs gemm_library_wanted() picks of >= 60 GFLOP
+// to the library, GK_BLASLT=all every eligible one; off by default (the hand-written gemm256 takes
+// them).  Separately, GK_WGRAD_GEMM=lib
 // routes the largest weight-gradient products (>= 8 M outputs and >= 60 GFLOP: dW_hh at H = 2048) to
 // the library (trainer_seq.cpp wgrad_engine); by default gemm256 takes those too.
 bool blaslt_enabled() {
   const char* e = std::getenv("GK_BLASLT");
-  return e && e[0] == '1';
+  return e && (e[0] == '1' || std::strcmp(e, "all") == 0);
 }
 
 double blaslt_min_gflop() {
-  const char* e = std::getenv("GK_BLASLT_MIN_GFLOP");
-  return e ? std::atof(e) : 60.0;
+  const char* e = std::getenv("GK_BLASLT");
+  return e && std::strcmp(e, "all") == 0 ? 0.0 : 60.0;
 }
 
 bool blaslt_gemm_nt(const u16* A, int lda, const u16* B, int ldb, float* C, int ldc, int M, int N, int K,

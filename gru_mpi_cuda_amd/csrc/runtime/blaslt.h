@@ -14,9 +14,9 @@ using u16 = unsigned short;
 // force: create the handle and workspace even when GK_BLASLT is off (a caller that routes some of its
 // own products to the library, e.g. the trainer's weight-gradient engine)
 void blaslt_init(bool force = false);
-// Smallest GEMM (2*M*N*K, in GFLOP) routed to the library under algo 0; env GK_BLASLT_MIN_GFLOP,
-// default 60.  The library is OFF by default (gemm256 took the weight gradients in round 2);
-// GK_BLASLT=1 enables it.
+// Smallest GEMM (2*M*N*K, in GFLOP) routed to the library under algo 0: 60, or 0 with GK_BLASLT=all.
+// The library is OFF by default (gemm256 took the weight gradients in round 2); GK_BLASLT=1 / all
+// enables it.
 double blaslt_min_gflop();
 bool blaslt_enabled();
 // C[M][N] (ldc) = A[M][K] (lda) . B[N][K]^T (ldb), fp32 out, fp32 accumulation (C += with

@@ -83,9 +83,8 @@ def test_trainer_grads_lds_step_kernels(monkeypatch, layers, B, H, blaslt):
     monkeypatch.setenv("GK_PERSIST", "0")
     monkeypatch.setenv("GK_STEP_ALGO", "2")
     if blaslt == "all":
-        monkeypatch.setenv("GK_BLASLT", "1")
+        monkeypatch.setenv("GK_BLASLT", "all")
         monkeypatch.setenv("GK_WGRAD_GEMM", "lib")
-        monkeypatch.setenv("GK_BLASLT_MIN_GFLOP", "0")
     cfg = GRUConfig(vocab=256, embed=128, hidden=H, layers=layers, batch=B, seq=6 if H < 2048 else 4,
                     time_chunks=2, seed=5)
     params = init_params(cfg)
@@ -680,9 +679,8 @@ def test_trainer_odd_shapes_match_cpu(layers, V, E, H, B, T):
 def test_trainer_grads_library_gemms(monkeypatch, sched):
     """Every eligible GEMM on hipBLASLt (threshold 0), incl. the overlapped schedule whose two
     streams run library GEMMs concurrently (one workspace per stream)."""
-    monkeypatch.setenv("GK_BLASLT", "1")
+    monkeypatch.setenv("GK_BLASLT", "all")
     monkeypatch.setenv("GK_WGRAD_GEMM", "lib")
-    monkeypatch.setenv("GK_BLASLT_MIN_GFLOP", "0")
     test_trainer_grads_match_cpu(monkeypatch, sched, 2, 128, 128, 4, 96)
 
 
