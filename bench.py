@@ -92,7 +92,8 @@ def main() -> int:
                          "the timed region's synchronize is cheap, then groups).  Reported as graph_steps "
                          "and lead_single_steps.")
     ap.add_argument("--variant", action="append", default=[], metavar="KEY=INT",
-                    help="kernel / step-plan variant (StepLdsVariants field, kernels.h), for A/B runs; repeatable")
+                    help="kernel / step-plan variant (StepLdsVariants field, kernels.h; gemm.KEY: a GemmVariants "
+                         "field), for A/B runs; repeatable")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launch mode: wall-clock limit of the whole N-rank job in s")
     args = ap.parse_args()
@@ -149,7 +150,13 @@ def main() -> int:
         from gru_mpi_cuda_amd.engine.trainer import make_trainer
         if args.variant and ctx.device.type == "cuda":
             from gru_mpi_cuda_amd.ops import load_ext
-            load_ext().set_step_lds_variants({k: int(v) for k, v in (x.split("=", 1) for x in args.variant)})
+            kv = [x.split("=", 1) for x in args.variant]   # "gemm.KEY=INT": a GemmVariants field
+            step = {k: int(v) for k, v in kv if not k.startswith("gemm.")}
+            gemm = {k[5:]: int(v) for k, v in kv if k.startswith("gemm.")}
+            if step:
+                load_ext().set_step_lds_variants(step)
+            if gemm:
+                load_ext().set_gemm_variants(gemm)
         from gru_mpi_cuda_amd.parallel.rccl import make_comm
         comm = make_comm(ctx) if ctx.device.type == "cuda" else None
         if comm is None and args.rccl_self and ctx.device.type == "cuda":

@@ -27,7 +27,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 KERNELS = ["kernels/gru_step.hip", "kernels/gru_seq.hip", "kernels/fc.hip", "kernels/gemm.hip",
            "kernels/gemm_lds.hip", "kernels/gemm_small.hip", "kernels/gru_step_lds.hip", "kernels/misc.hip",
            "kernels/gen_f32.hip", "kernels/gemm256.hip", "kernels/gen_persist.hip", "kernels/gru_seq_big.hip",
-           "kernels/gru_seq16.hip"]
+           "kernels/gru_seq16.hip", "kernels/onehot.hip"]
 ENGINE = ["runtime/blaslt.cpp", "engine/trainer.cpp", "engine/trainer_seq.cpp", "engine/generator.cpp", "comm/rccl_comm.cpp",
           "comm/watchdog.cpp", "comm/bootstrap.cpp", "data/name_loader.cpp"]
 PYBIND = ["bindings.cpp"]

@@ -281,7 +281,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_variants", []() {
     const GemmVariants& v = gemm_variants();
     py::dict d;
-    d["mfma"] = v.mfma; d["phased"] = v.phased; d["sched"] = v.sched; d["groupm"] = v.groupm;
+    d["mfma"] = v.mfma; d["phased"] = v.phased; d["sched"] = v.sched; d["groupm"] = v.groupm; d["onehot"] = v.onehot;
     return d;
   });
   m.def("set_gemm_variants", [](py::dict d) {
@@ -293,6 +293,7 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "phased") v.phased = x;
       else if (k == "sched") v.sched = x;
       else if (k == "groupm") v.groupm = x;
+      else if (k == "onehot") v.onehot = x;
       else throw std::runtime_error("set_gemm_variants: unknown field " + k);
     }
   });

@@ -358,6 +358,11 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
         p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)tok;
         if (dgiT_share_) { p.B = y.dghT; p.B2 = y.dgiT; p.b2_row = H3 - H; }
         p.C = slab_w_; p.ldc = H3; p.M = V; p.N = H3; p.K = (int)tok; p.splits = sp;
+        {   // the streaming one-hot kernel (G read once) picks its own K-slices (<= the slab's splits_)
+          GemmArgs q = p;
+          q.splits = std::min(splits_, onehot_dp_splits(H3, (int)tok));
+          if (gemm_variants().onehot && onehot_dp_ok(q)) { p = q; sp = q.splits; }
+        }
         gemm_nt(p, s);
         float* dPd = dp ? dP_target() : dP_;
         reduce_slabs(slab_w_, sp, (long)V * H3, dPd, s);

@@ -191,6 +191,11 @@ void gemm_nt(const GemmArgs& a, hipStream_t s) {
     gemm256(a, s);
     return;
   }
+  // one-hot dP over the whole vocabulary (V = 256): the streaming kernel reads G once
+  if ((a.algo == 0 || a.algo == 2) && a.onehot_ids && gemm_variants().onehot && onehot_dp_ok(a)) {
+    onehot_dp(a, s);
+    return;
+  }
   // latency-bound regime (fewer than one 128 x 128 workgroup per CU): the one-shot small kernel
   if (a.algo == 0 && gemm_small_kblocks(a) &&
       (a.M % 128 || a.N % 128 || (a.M / 128) * (a.N / 128) * a.splits < 256)) {

@@ -106,6 +106,8 @@ struct GemmVariants {
   int phased = -1;  // 1 / 0: always / never the staggered phased pipeline; -1: by shape
   int sched = -1;   // staggered pipeline staging schedule 0 / 1; -1: by k-tiles per workgroup
   int groupm = 4;   // grouped raster run length (tile-rows)
+  int onehot = 1;   // one-hot dP products with V = 256 on the streaming kernel (onehot.hip), 1: 128-column x
+                    // 64-token k-tiles, 2: 64 x 128, 3: 32 x 256; 0: the one-hot gemm_lds kernel
 };
 GemmVariants& gemm_variants();
 // LDS-staged large-H step kernels: H % 64 == 0, Bp % 128 == 0, no fused input projection
@@ -382,6 +384,10 @@ bool gemm_library_wanted(const GemmArgs& a);
 bool gemm_library(const GemmArgs& a, hipStream_t s);
 void gemm_nt(const GemmArgs& a, hipStream_t s);
 bool gemm_lds_ok(const GemmArgs& a);
+// dP = onehot(ids)^T · G^T with V = 256 (onehot.hip): G streamed once, all-zero one-hot tiles skipped
+bool onehot_dp_ok(const GemmArgs& a);
+int onehot_dp_splits(int N, int K);   // its K-slice count for an N-column product (about 384 workgroups)
+void onehot_dp(const GemmArgs& a, hipStream_t s);
 bool gemm256_ok(const GemmArgs& a);
 // rows of A per gemm256 tile for (M, N, splits): 256 or 192 (the phased kernel), 0 = no fit
 int gemm256_tile_rows(int M, int N, int K, int splits);

@@ -72,20 +72,74 @@ def test_gemm_library(ext, M, N, K, lda_pad, accumulate):
     torch.testing.assert_close(rs, A.float().sum(1), atol=1e-3 * K ** 0.5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("stream", [0, 1])
 @pytest.mark.parametrize("N,K,splits,algo", [(192, 512, 1, 1), (384, 1024, 1, 2), (256, 2048, 4, 2)])
-def test_gemm_onehot(ext, N, K, splits, algo):
-    """algo 2: the one-hot A tile is synthesised into the swizzled LDS image of the LDS GEMM."""
+def test_gemm_onehot(ext, N, K, splits, algo, stream):
+    """algo 2: the one-hot A tile synthesised into the swizzled LDS image of the LDS GEMM (stream = 0)
+    or, N % 128 == 0, the streaming one-hot kernel (onehot.hip, GemmVariants.onehot = 1)."""
     V = 256
     ids = torch.randint(0, V, (K,), device=DEV, dtype=torch.int32)
     ids[:64] = 7                                                   # a heavy bucket
     B = bf(rnd(N, K, seed=5))
-    C = torch.zeros(splits, V, N, device=DEV)
-    ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=V, N=N, K=K,
-                     splits=splits, algo=algo), S())
-    torch.cuda.synchronize()
+    C = torch.full((splits, V, N), float("nan"), device=DEV)
+    saved = ext.gemm_variants()
+    try:
+        ext.set_gemm_variants(dict(onehot=stream))
+        ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B.data_ptr(), ldb=K, C=C.data_ptr(), ldc=N, M=V, N=N, K=K,
+                         splits=splits, algo=algo), S())
+        torch.cuda.synchronize()
+    finally:
+        ext.set_gemm_variants(saved)
     oh = torch.nn.functional.one_hot(ids.long(), V).float()      # [K][V]
     ref = oh.T @ B.float().T
     torch.testing.assert_close(C.sum(0), ref, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("geo", [1, 2, 3])
+@pytest.mark.parametrize("K,splits,dist", [(65536, 8, "names"), (16384, 2, "uniform"), (8192, 16, "names"),
+                                          (4096, 1, "invalid"), (24576, 4, "one")])
+def test_onehot_dp_stream(ext, K, splits, dist, geo):
+    """The streaming one-hot kernel at its real shape family (N = 3H, B2 = the n-gate rows, 8192-deep
+    K-slices) against the fp32 product: char-like ids (a few 16-row vocabulary tiles active: most
+    waves skip most k-tiles), uniform ids (every tile active), ids outside [0, 256) that must match
+    nothing, and a single id.  Bitwise equal to the one-hot gemm_lds product per slab: the same MFMA
+    chains over the same exact one-hot x bf16 products, in the same k order (skipped tiles add zeros)."""
+    V, H = 256, 512
+    N = 3 * H
+    g = torch.Generator(device="cpu").manual_seed(K + splits)
+    if dist == "names":
+        ids = torch.randint(97, 123, (K,), generator=g, dtype=torch.int32)
+        ids[::17] = 0                                               # end-of-name / padding id
+    elif dist == "uniform":
+        ids = torch.randint(0, V, (K,), generator=g, dtype=torch.int32)
+    elif dist == "invalid":
+        ids = torch.randint(-300, 600, (K,), generator=g, dtype=torch.int32)
+    else:
+        ids = torch.full((K,), 101, dtype=torch.int32)
+    ids = ids.to(DEV)
+    B = bf(rnd(N, K, seed=7))
+    B2 = bf(rnd(N, K, seed=8))
+    B2[:2 * H] = float("nan")
+    B1 = B.clone()
+    B1[2 * H:] = float("nan")
+    merged = torch.cat([B[:2 * H], B2[2 * H:]])
+    out = []
+    saved = ext.gemm_variants()
+    try:
+        for stream in (geo, 0):   # GemmVariants.onehot: the streaming kernel's tile geometry, 0 = gemm_lds
+            ext.set_gemm_variants(dict(onehot=stream))
+            C = torch.full((splits, V, N), float("nan"), device=DEV)
+            ext.gemm_nt(dict(onehot_ids=ids.data_ptr(), B=B1.data_ptr(), B2=B2.data_ptr(), b2_row=2 * H, ldb=K,
+                             C=C.data_ptr(), ldc=N, M=V, N=N, K=K, splits=splits, algo=2), S())
+            torch.cuda.synchronize()
+            out.append(C)
+    finally:
+        ext.set_gemm_variants(saved)
+    valid = (ids >= 0) & (ids < V)
+    oh = torch.nn.functional.one_hot(torch.where(valid, ids, 0).long(), V).float() * valid[:, None].float()
+    ref = (oh.T @ merged.float().T)
+    torch.testing.assert_close(out[0].sum(0), ref, atol=1e-3, rtol=1e-4)
+    assert torch.equal(out[0], out[1])
 
 
 def _gates_ref(gi, gh, hp):
