@@ -243,10 +243,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T: split-K into dedicated slabs whose
     // reduce joins the multi-tensor reduce after the backward sweep (one launch fewer)
-    // few output tiles (V x H): split K until ~256 workgroups fill the chip
+    // few output tiles (V x H): split K until one round of workgroups fills the chip at two per CU
+    // (h2048, 2 x 16 tiles over 65536 tokens: 8 / 16 / 32 / 64 K-slices 138 / 107 / 122 / 129 us
+    // standalone, profiles/r6_gemm_dwfc.jsonl; 256 workgroups, the old bound, left half the slots idle)
     const int tiles = std::max(1, (V / 128) * (H / 128));
     int sp = 1;
-    while (sp * 2 <= kFcSplitsMax && tiles * sp < 256 && tok % (sp * 2) == 0 && (tok / (sp * 2)) % 128 == 0)
+    while (sp * 2 <= kFcSplitsMax && tiles * sp < 512 && tok % (sp * 2) == 0 && (tok / (sp * 2)) % 128 == 0)
       sp *= 2;
     GemmArgs w;
     w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;

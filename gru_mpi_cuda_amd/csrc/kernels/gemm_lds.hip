@@ -28,13 +28,6 @@ DEV int xcd_remap2(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-DEV float sum8f(const bf16x8& v) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s += (float)v[i];
-  return s;
-}
-
 // OH: one-hot A (dP = onehot(ids)^T · B, the embedding-table gradient): A[m][k] = (ids[k] == m) is
 // synthesised into the same swizzled LDS image the LDS-DMA would have written, from char ids
 // prefetched one k-tile ahead -- no A operand in memory at all.
@@ -138,7 +131,7 @@ DEV void gemm_lds_body(const GemmArgs& a, int id, int ntn, int ntm, int kper, u1
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       if (do_rs) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) rs[t] += sum8f(af[t]);
+        for (int t = 0; t < 4; ++t) rs[t] = add_sum8(af[t], rs[t]);   // four v_dot2 (common.h)
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

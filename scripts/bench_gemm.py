@@ -23,6 +23,7 @@ SHAPES = [  # (name, M, N, K, splits)
     ("h2048.dW_hh", 6144, 2048, 65536, 8),
     ("h2048.dH", 65536, 2048, 256, 1),
     ("h2048.logits", 65536, 256, 2048, 1),
+    ("h2048.dW_fc", 256, 2048, 65536, 32),
     ("h1024.dX", 8192, 1024, 3072, 1),
     ("sq4096", 4096, 4096, 4096, 1),
     ("sq8192", 8192, 8192, 8192, 1),
@@ -57,6 +58,8 @@ for name, M, N, K, sp in SHAPES:
     row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp}
     ref = (A.float() @ B.float().T) if M * N * K <= 2 ** 41 else None
     variants = [(1, sp), (2, sp), (4, 1)] + [(5, k) for k in (1, 2, 4, 8) if K % (64 * k) == 0 and (k == 1 or K >= 4096)]
+    # the 128 x 128 kernel at other split-K depths (GEMM_SPLITS2=8,16,..)
+    variants += [(2, int(k)) for k in os.environ.get("GEMM_SPLITS2", "").split(",") if k and int(k) != sp]
     # algo 3: the one-shot small GEMM at the K-slices it takes (h512 step products)
     variants += [(3, k) for k in (1, 2, 4, 6, 8, 16) if K % k == 0 and (K // k) in (128, 192, 256, 512, 1024, 1536, 2048)]
     # algo "5m": the 256 x 256 kernel on v_mfma_f32_32x32x16_bf16 (GemmVariants mfma = 32); "5o": the
@@ -79,7 +82,7 @@ for name, M, N, K, sp in SHAPES:
         if algo == "5r":
             rs = torch.empty(ks, M, device=dev)
             d["rowsumA"] = rs.data_ptr()
-        tag = f"algo{algo}" + (f"s{ks}" if algo_arg in (3, 5) else "")
+        tag = f"algo{algo}" + (f"s{ks}" if algo_arg in (3, 5) or (algo_arg == 2 and ks != sp) else "")
         if tag in row or f"{tag}_us" in row:
             tag += "b"   # a repeated variant (order check)
         try:
