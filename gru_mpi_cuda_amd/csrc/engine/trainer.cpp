@@ -212,6 +212,8 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   const char* ng = std::getenv("GK_NO_GRAPH");
   if (ng && ng[0] == '1') use_graph_ = false;
   overlap_ = d_.overlap != 0;
+  dy_in_bwd_ = fc_split_ && !overlap_ && !seq_.empty() && seq_.back().big && seq_.back().s16 && d_.V == 256 &&
+               step_lds_variants().big_dy;
   fc_in_fwd_ = persist_fwd_ && !fwd_wave_ && d_.L == 1 && !overlap_ && !fc_split_ && !seq_.empty() &&
                seq_[0].bwd && seq_[0].fuse_w && seq_[0].HF && step_lds_variants().fwd_fc &&
                Bp_ / 32 <= kFcSplitsMax && gru_fwd_seq_fc_supported(d_.H, Bp_, d_.V);

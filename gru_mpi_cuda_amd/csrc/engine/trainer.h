@@ -244,6 +244,7 @@ class Trainer {
   // one-layer H = 512, V = 256: the FC head runs as consumer workgroups of the persistent forward
   // (gru_fwd_seq_fc): no fc_xent launch, no dW_fc GEMM; decided per trainer (StepLdsVariants::fwd_fc)
   bool fc_in_fwd_ = false;
+  bool dy_in_bwd_ = false;     // the top layer's large-H backward computes dy = dl · W_fc itself (big_dy)
   bool fwd_wave_ = false;      // layer pairs (0,1), (2,3).. forward as one wavefront launch (gru_fwd_seq2)
   float* bpart_ = nullptr;     // split-K partial tiles of the persistent large-H backward
   int step_algo_ = 0;          // per-step kernel choice (GK_STEP_ALGO: 0 auto, 1 register tile, 2 LDS tile)

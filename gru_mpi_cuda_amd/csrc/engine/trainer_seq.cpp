@@ -226,10 +226,12 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       lg.M = (int)tok; lg.N = V; lg.K = H;
       gemm_nt(lg, s);
       softmax_xent(logits_, f, s);
-      GemmArgs g;   // dy_top = dlogits · W_fc
-      g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
-      g.M = (int)tok; g.N = H; g.K = V;
-      gemm_nt(g, s);
+      if (!dy_in_bwd_) {   // (else the top layer's large-H backward forms dy from dl itself)
+        GemmArgs g;   // dy_top = dlogits · W_fc
+        g.A = dl_; g.lda = V; g.B = WfcT; g.ldb = V; g.C = top.dy; g.ldc = H;
+        g.M = (int)tok; g.N = H; g.K = V;
+        gemm_nt(g, s);
+      }
     } else if (V % 128 == 0 && H % (16 * (V / 64)) == 0) {
       // dy_top = dlogits · W_fc fused into the softmax-xent kernel (dlogits never leave LDS)
       f.dl = nullptr; f.WT = WfcT; f.dy = top.dy; f.Wf = WfcF; f.WTf = WfcTF;
@@ -311,6 +313,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)tok; a.dgi = y.dgi;
       a.dgiT_n_only = l == 0 && dgiT_share_;
       a.dbhh_part = q.dbhh_part; a.dbih_part = l == 0 ? q.dbih_part : nullptr;   // (l > 0: from the dW_ih GEMM)
+      if (dy_in_bwd_ && l == L - 1) { a.dl = dl_; a.WfcT = WfcT; a.V = V; a.dy = nullptr; }
       a.cnt = cnt_ + (size_t)(L + l) * fw; a.err = err_;
       a.T = T; a.Bp = B; a.H = H;
       a.xring = step_lds_variants().bwd_xring;
@@ -565,6 +568,7 @@ std::string Trainer::plan() const {
          (seq_[l].bwd ? (seq_[l].rows16 ? "persistent16" : "persistent") : seq_[l].big ? "persistent-big" : "per-step");
     if (seq_[l].fuse_w) p += "+dWhh";
     if (seq_[l].fuse_p) p += "+dP";
+    if (dy_in_bwd_ && l + 1 == seq_.size()) p += "+dy";
   }
   bool any_step = !persist_fwd_;
   for (const SeqPlan& q : seq_) any_step |= !q.bwd;

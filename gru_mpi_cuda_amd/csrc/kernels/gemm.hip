@@ -172,7 +172,8 @@ bool gemm_library(const GemmArgs& a, hipStream_t s) {
 }
 
 void gemm_nt(const GemmArgs& a, hipStream_t s) {
-  if (a.B2 && !gemm_lds_ok(a)) throw std::runtime_error("gemm_nt: a split B operand (B2) needs the one-hot LDS kernel");
+  if (a.B2 && !gemm_lds_ok(a) && !(gemm_variants().onehot && onehot_dp_ok(a)))
+    throw std::runtime_error("gemm_nt: a split B operand (B2) needs a one-hot LDS / streaming kernel");
   // large plain products: hipBLASLt (bf16 in, fp32 out), when it has an algorithm for the shape
   if (gemm_library_wanted(a) && gemm_library(a, s)) return;
   if (a.algo == 4) throw std::runtime_error("gemm_nt: library GEMM requested but not available for this shape");

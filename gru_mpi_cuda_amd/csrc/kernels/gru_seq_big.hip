@@ -10,6 +10,7 @@
 // A second try on the 64-row step kernel's tile -- two workgroups per CU, 512 co-resident, the same
 // k order and epilogue -- was correct and slower still: h2048 9.37-9.40 vs 8.77-8.81 ms, h1024_l2 x
 // 1024 equal, profiles/r4_h2048_h1024_fwd64_ab.jsonl; removed.)
+#include <algorithm>
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -43,6 +44,13 @@ template <int N> DEV void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N)
 //     loads behind the acquire) and W_hh^T (plain, its first ring slots issued
 //     before the wait) through a 4-deep LDS ring; the fp32 partial tile goes out write-through (parity-double-buffered), one
 //     flag per (tile, split), and the S partners wait for each other;
+//   * fused dy (SeqBwdArgs::dl, the top layer): dy_t = dl_t . W_fc is not read from memory; each split
+//     adds vocabulary quarter `split` (64 deep) of it to its partial tile, from one extra k-tile
+//     (A = dl_t rows, B = W_fc^T rows) staged in ring slot 3 at the top of the step (waves 1-7 wait
+//     for it while wave 0 polls) and multiplied under the latency of the first exchange k-tiles.  This removes the dH GEMM
+//     (65536 x 2048 x 256 at config 5: 173 us) and its 537 MB fp32 dy, written once and read back by
+//     this kernel.  At t = T - 1 (no exchange yet) the splits still trade partials: the partial flags
+//     count ep + 1;
 //   * the epilogue runs on row quarter `split` of the tile: partials summed in split order (the same
 //     sum whoever runs it), the gate gradients, carry = z * dh kept in REGISTERS across steps (the
 //     same thread owns the same elements every step), dGh_t staged row-major in LDS and published as
@@ -58,6 +66,9 @@ constexpr int kRowPad = 136;                // row-major staging pitch (u16): 27
 DEV int big_bwd_ntu(int H) { return H / 128; }
 }  // namespace
 
+// FDY: the fused dy (SeqBwdArgs::dl), compile-time and only with the packed bf16 saves (s16): the
+// register file is full, and dy / the four fp32 save slots of the epilogue prefetch pay for its staging
+template <bool FDY>
 __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   // ONE __shared__ object (ring + bias accumulators): see the forward
   __shared__ __attribute__((aligned(16))) u16 lds_all[kBNS * 256 * 64 + 2 * 4 * 128 * 2];
@@ -83,6 +94,9 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
   // the row tile, each of which published it after its own step-(t+1) reads of dGh_{t+2}: the slot
   // being rewritten (t + 2 for xr = 2) has no reader left.
   const int xr = a.xring >= 2 ? a.xring : T;
+  // (fused dy: dl [T * Bp][256] and W_fc^T [H][256] bf16)
+  const rsrc_g rL = mk_rsrc(a.dl, FDY ? (unsigned)((size_t)T * Bp * 256 * 2) : 0u);
+  const rsrc_g rF = mk_rsrc(a.WfcT, FDY ? (unsigned)((size_t)H * 256 * 2) : 0u);
   const rsrc_g rP = mk_rsrc(a.part, (unsigned)((size_t)2 * 64 * kBS * kPiece * 16));
   unsigned* const gflag = a.cnt;
   unsigned* const pflag = a.cnt + 4096;
@@ -147,8 +161,8 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const size_t o = (size_t)t * Bp * H + item_off(pp, e);
-        pre[pp][e][0] = a.dy[o];
-        if (a.s16) ld_save16_raw(a.s16 + o * 4, pre[pp][e][1], pre[pp][e][2]);   // unpacked at use
+        pre[pp][e][0] = FDY ? 0.f : a.dy[o];
+        if (FDY || a.s16) ld_save16_raw(a.s16 + o * 4, pre[pp][e][1], pre[pp][e][2]);   // unpacked at use
         else { pre[pp][e][1] = a.sr[o]; pre[pp][e][2] = a.sz[o]; pre[pp][e][3] = a.sn[o]; pre[pp][e][5] = a.sghn[o]; }
         pre[pp][e][4] = a.HSf[o];   // HSf + t*Bp*H = h_{t-1}
       }
@@ -158,42 +172,15 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) ps[pp][e] = 0.f;
     __syncthreads();   // the previous step's LDS staging reads are done before the ring refills
-    const bool kloop = t < T - 1;
-    if (kloop) {
+    const bool xloop = t < T - 1;          // dGh_{t+1} . W_hh (nothing to exchange at the last step)
+    constexpr bool fdy = FDY;              // + this split's quarter of dl_t . W_fc
+    if (xloop || fdy) {
       f32x4 acc[4][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // W_hh^T rows of the first ring slots do not depend on the exchange: waves 4-7 put them in flight
-      // before the wait (each wave's vmcnt counts only its own pieces, so the ring's waits still hold)
-      if (w >= 4) {
-#pragma unroll
-        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
-      }
-      // dGh_{t+1}: column block cb of this slice (gate cb / ntu, unit tile cb % ntu) x 4 row quarters
-      if (w == 0) {
-        spin_until(gflag, 4 * ncb, 16, ep, [&](int l) {
-          const int cb = split * ncb + (l >> 2);
-          return (rt * ntu + cb % ntu) * kBS + (l & 3);
-        });
-        // plain A loads behind one wave's agent acquire, shared in the XCD's L2 (sc1 loads instead --
-        // one fetch per workgroup from the memory side -- measured equal, r4_h2048_big_acq_ab.jsonl;
-        // that switch was removed in round 5)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      if (w < 4) {
-#pragma unroll
-        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
-      }
-      for (int kt = 0; kt < nk; ++kt) {
-        const int ahead = min(kBNS - 2, nk - 1 - kt);
-        if (ahead >= 2) vmwait<8>(); else if (ahead == 1) vmwait<4>(); else vmwait<0>();
-        lds_barrier();
-        if (kt + kBNS - 1 < nk) stage((kt + kBNS - 1) % kBNS, kt + kBNS - 1, t);
-        const u16* LA = lds[kt % kBNS];
+      auto mma_tile = [&](const u16* LA) {
         const u16* LB = LA + 128 * 64;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -214,6 +201,63 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
         }
+      };
+      if constexpr (FDY) {
+        // the dy k-tile into ring slot 3 (first refilled at k-tile 3, after this tile's MFMAs):
+        // A = dl_t rows b0.. x vocabulary quarter `split` (waves 0-3), B = W_fc^T rows j0.. (waves 4-7)
+        // buffer loads: the lane part is one of two offsets (row srow, swizzled chunk for even / odd q),
+        // everything else a scalar offset -- the 64-bit addresses, and then 4 lane offsets, spilled
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+        const unsigned lo[2] = {(unsigned)((srow * 256 + (sslot ^ ((srow >> 1) & 7)) * 8) * 2),
+                                (unsigned)((srow * 256 + (sslot ^ ((4 + (srow >> 1)) & 7)) * 8) * 2)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          lds_void_g* dst = (lds_void_g*)(&lds[kBNS - 1][(4 * w + q) * 8 * 64]);
+          const int rowq = ((4 * wu + q) * 8) & 127;   // first tile row of this piece
+          if (wu < 4)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rL, dst, 16, lo[q & 1], ((t * Bp + b0 + rowq) * 256 + split * 64) * 2, 0, 0);
+          else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rF, dst, 16, lo[q & 1], ((j0 + rowq) * 256 + split * 64) * 2, 0, 0);
+        }
+      }
+      // W_hh^T rows of the first ring slots do not depend on the exchange: waves 4-7 put them in flight
+      // before the wait (each wave's vmcnt counts only its own pieces, so the ring's waits still hold)
+      if (xloop && w >= 4) {
+#pragma unroll
+        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
+      }
+      // dGh_{t+1}: column block cb of this slice (gate cb / ntu, unit tile cb % ntu) x 4 row quarters
+      if (xloop && w == 0) {
+        spin_until(gflag, 4 * ncb, 16, ep, [&](int l) {
+          const int cb = split * ncb + (l >> 2);
+          return (rt * ntu + cb % ntu) * kBS + (l & 3);
+        });
+        // plain A loads behind one wave's agent acquire, shared in the XCD's L2 (sc1 loads instead --
+        // one fetch per workgroup from the memory side -- measured equal, r4_h2048_big_acq_ab.jsonl;
+        // that switch was removed in round 5)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if constexpr (FDY) {
+        // the dy tile's share of each wave has landed -- waves 1-7 wait while wave 0 polls (waves 4-7
+        // keep their 3 W_hh^T slots, issued behind it, in flight)
+        if (xloop && w >= 4) vmwait<12>(); else vmwait<0>();
+      }
+      if (xloop || FDY) __syncthreads();   // the flags are seen (xloop) and the dy tile is published (FDY)
+      if (xloop && w < 4) {
+#pragma unroll
+        for (int s2 = 0; s2 < kBNS - 1; ++s2) stage(s2, s2, t);
+      }
+      // the dy tile's MFMAs under the latency of the first exchange k-tiles just issued
+      if constexpr (FDY) mma_tile(lds[kBNS - 1]);
+      if (xloop) {
+        for (int kt = 0; kt < nk; ++kt) {
+          const int ahead = min(kBNS - 2, nk - 1 - kt);
+          if (ahead >= 2) vmwait<8>(); else if (ahead == 1) vmwait<4>(); else vmwait<0>();
+          lds_barrier();   // (at kt = 0 also: every wave is done with the dy tile in slot 3)
+          if (kt + kBNS - 1 < nk) stage((kt + kBNS - 1) % kBNS, kt + kBNS - 1, t);
+          mma_tile(lds[kt % kBNS]);
+        }
       }
       // this split's partial tile, write-through; drain; one flag; wait for the S partners
       const size_t pbase = ((size_t)(ep & 1) * 64 + tile) * kBS * kPiece;
@@ -226,10 +270,11 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      // (partial flags count ep + 1: with the fused dy the partners also trade at t = T - 1, ep = 0)
       if (tid == 0)
-        __hip_atomic_store(pflag + (size_t)(tile * kBS + split) * 16, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pflag + (size_t)(tile * kBS + split) * 16, ep + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w == 0)
-        spin_until(pflag, kBS, 16, ep, [&](int l) { return tile * kBS + l; });
+        spin_until(pflag, kBS, 16, ep + 1, [&](int l) { return tile * kBS + l; });
       __syncthreads();
       // partial sums of the epilogue items, split order 0..S-1
 #pragma unroll
@@ -258,7 +303,7 @@ __global__ void __launch_bounds__(512, 1) gru_bwd_seq_big_kernel(SeqBwdArgs a) {
         const int rq = ii * 16 + lq * 4 + e;
         const float dh = (pre[pp][e][0] + carry[pp][e]) + ps[pp][e];
         float r = pre[pp][e][1], z = pre[pp][e][2], n = pre[pp][e][3], ghn = pre[pp][e][5];
-        if (a.s16) unpack_save16(pre[pp][e][1], pre[pp][e][2], r, z, n, ghn);
+        if (FDY || a.s16) unpack_save16(pre[pp][e][1], pre[pp][e][2], r, z, n, ghn);
         const float hp = pre[pp][e][4];
         const float dn = dh * (1.f - z);
         const float dz = dh * (hp - n);
@@ -343,21 +388,28 @@ bool gru_bwd_seq_big_supported(int H, int Bp) {
   int dev = 0, ncu = 0, per = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gru_bwd_seq_big_kernel, 512, 0) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gru_bwd_seq_big_kernel<false>, 512, 0) != hipSuccess) return false;
+  int per2 = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, gru_bwd_seq_big_kernel<true>, 512, 0) != hipSuccess) return false;
+  per = std::min(per, per2);
   return ncu * per >= 256;
 }
 
 long gru_bwd_seq_big_part_floats(int H, int Bp) { return 2L * Bp * H * kBS; }
 
 void gru_bwd_seq_big(const SeqBwdArgs& a, hipStream_t s) {
-  if (!gru_bwd_seq_big_supported(a.H, a.Bp) || !a.xbuf || !a.cnt || !a.part || !a.dy || ((!a.sr || !a.sz ||
+  if (!gru_bwd_seq_big_supported(a.H, a.Bp) || !a.xbuf || !a.cnt || !a.part || (!a.dy && !a.dl) || ((!a.sr || !a.sz ||
       !a.sn || !a.sghn) && !a.s16) || !a.HSf || !a.WhhT || a.ldG < a.T * a.Bp)
     throw std::runtime_error("gru_bwd_seq_big: unsupported shape or incomplete arguments");
+  if (a.dl && (!a.WfcT || a.V != 64 * kBS || !a.s16))
+    throw std::runtime_error("gru_bwd_seq_big: the fused dy needs W_fc^T, V = 256 and the packed saves");
   // only min(T, xring) slots of the exchange are addressed when a ring is active
   const size_t slots = a.xring >= 2 && a.xring < a.T ? (size_t)a.xring : (size_t)a.T;
   if (slots * a.Bp * 3 * a.H * 2 >= (1ull << 32))
     throw std::runtime_error("gru_bwd_seq_big: exchange exceeds the 4 GB buffer range");
-  hipLaunchKernelGGL(gru_bwd_seq_big_kernel, dim3(256), dim3(512), 0, s, a);
+  if ((size_t)a.T * a.Bp * 256 * 2 >= (1ull << 31)) throw std::runtime_error("gru_bwd_seq_big: dl exceeds the buffer range");
+  if (a.dl) hipLaunchKernelGGL(gru_bwd_seq_big_kernel<true>, dim3(256), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(gru_bwd_seq_big_kernel<false>, dim3(256), dim3(512), 0, s, a);
 }
 
 }  // namespace gk

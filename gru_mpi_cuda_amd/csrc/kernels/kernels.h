@@ -95,6 +95,8 @@ struct StepLdsVariants {
                          // softmax over 4 vocabulary chunks, fc.hip); 0: the 8-wave two-stream kernel
   int fwd_fc = 0;        // one-layer H = 512, V = 256: the FC head (fc_xent + dW_fc) as consumer
                          // workgroups inside the persistent forward launch (gru_fwd_seq_fc); 0: after it
+  int big_dy = 1;        // top layer on the persistent large-H backward, V = 256: dy = dl · W_fc inside it
+                         // (SeqBwdArgs::dl) instead of the dH GEMM + an fp32 dy in memory
 };
 // (Round 5 removed the measured-equal / marginal switches fwd_ns, fwd8, fwd64 = 2, fwd64_fused,
 // fwd64_all, bwd_sk_pf, bwd_sk_map and big_acq with the code only they reached; docs/DESIGN.md §7.)
@@ -219,6 +221,11 @@ struct SeqBwdArgs {
   float* part = nullptr;           // large-H kernel: split-K partial tiles (gru_bwd_seq_big_part_floats)
                                    // (one fetch per XCD, shared in its L2) instead of sc1 loads
   int dgiT_n_only = 0;             // large-H kernel: dGi^T gets only the n-gate rows (r / z = dGh^T's)
+  // large-H kernel, top layer: dy = dl · W_fc computed inside (one extra 64-deep k-tile per K-slice,
+  // run while the exchange flags are awaited) instead of read from `dy`: dl [T*Bp][V] bf16 row-major
+  // (softmax_xent's), W_fc^T [H][V] bf16, V = 4 x 64
+  const u16* dl = nullptr;
+  const u16* WfcT = nullptr;
   int xring = 0;                   // step / 16-row kernels: exchange slots reused every xring steps
                                    // (>= 2; 0 = one per step; StepLdsVariants::bwd_xring)
   int T = 0, Bp = 0, H = 0;

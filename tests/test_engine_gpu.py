@@ -140,6 +140,48 @@ def test_trainer_grads_big_persistent_backward(layers, B, H, E):
         assert e < 1e-2, f"{k}: persistent vs per-step rel err {e:.5f}"
 
 
+@pytest.mark.parametrize("T", [4, 1])
+def test_big_backward_fused_dy(T):
+    """StepLdsVariants.big_dy: the top layer's large-H backward forms dy = dl · W_fc itself (one extra
+    64-deep k-tile per K-slice, the partners trading partials from the last step on) instead of the dH
+    GEMM writing an fp32 dy: loss bitwise, gradients within rounding of the dH-GEMM schedule, over a
+    forward_backward and two Adam steps (and against the fp64 oracle in
+    test_trainer_grads_big_persistent_backward, which runs the fused form).  T = 1: only the step
+    without an exchange."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    saved = C.step_lds_variants()
+    cfg = GRUConfig(vocab=256, embed=128, hidden=2048, layers=1, batch=512, seq=T, seed=21)
+    params = init_params(cfg)
+    ds = NameStream(cfg.batch, T, seed=22)
+    batches = [ds.next() for _ in range(3)]
+    out = []
+    try:
+        for v in (0, 1):
+            C.set_step_lds_variants(dict(big_dy=v))
+            tr = HipTrainer(cfg, params=params)
+            plan = tr.t.plan()
+            assert "persistent-big" in plan and ("+dy" in plan) == (v == 1), plan
+            tr.forward_backward(*batches[0])
+            g = {k: t.clone() for k, t in tr.grad_dict().items()}
+            loss = tr.loss()
+            for x, y in batches[1:]:
+                tr.step(x, y)
+            torch.cuda.synchronize()
+            assert tr.t.read_error() == 0
+            out.append((g, loss, tr.params.clone(), tr.loss()))
+    finally:
+        C.set_step_lds_variants(saved)
+    (g0, l0, p0, s0), (g1, l1, p1, s1) = out
+    assert l0 == l1
+    # dh differs in the last fp32 bits (dy summed with the partials in another order); the gate
+    # gradients are stored in bf16, so a few of them round the other way (1.2e-4 measured on dW_ih0)
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-3, k
+    assert rel(p1, p0) < 1e-3 and abs(s1 - s0) < 1e-4 * abs(s0)
+
+
 def test_trainer_adam_step_and_learning():
     from gru_mpi_cuda_amd.engine.trainer import HipTrainer, CpuTrainer
     cfg = GRUConfig(vocab=256, embed=128, hidden=128, layers=1, batch=64, seq=16, time_chunks=2, lr=3e-3, seed=1)
