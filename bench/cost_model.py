@@ -46,11 +46,12 @@ MEASURED = {
                  adam_us=14.1, coll1_us={"replicated": 7.0, "zero1_fp32": 8.6, "zero1_bf16": 9.0, "pipelined": 14.0},
                  hideable_us={"pipelined": 10.6}),
     # config-4 shard (L = 2, H = 1024, 128 sequences / GPU) and config 5 (H = 2048, 512 / GPU): 1-GPU step
-    # without a communicator (r6 packed saves) + the 1-rank collective node estimated as at h512 per MB
-    "h1024_l2": dict(layers=2, params=13_119_744, grad_mb=52.5, step_ms={"replicated": 1.32},
-                     adam_us=74.5, coll1_us={"replicated": 7.0 + 52.5 / 5.25 * 1.0}, hideable_us={}),
-    "h2048": dict(layers=1, params=26_226_944, grad_mb=104.9, step_ms={"replicated": 8.43},
-                  adam_us=161.5, coll1_us={"replicated": 7.0 + 104.9 / 5.25 * 1.0}, hideable_us={}),
+    # without a communicator (round-6 final tree, profiles/r6_final_benches.jsonl; Adam from the final
+    # traces) + the 1-rank collective node estimated as at h512 per MB
+    "h1024_l2": dict(layers=2, params=13_119_744, grad_mb=52.5, step_ms={"replicated": 1.3225},
+                     adam_us=75.2, coll1_us={"replicated": 7.0 + 52.5 / 5.25 * 1.0}, hideable_us={}),
+    "h2048": dict(layers=1, params=26_226_944, grad_mb=104.9, step_ms={"replicated": 7.92},
+                  adam_us=155.6, coll1_us={"replicated": 7.0 + 104.9 / 5.25 * 1.0}, hideable_us={}),
 }
 RELAYOUT_US_PER_MPARAM = 12.1 / 1.838336     # cast_multi from the bf16 mirror (h512 trace)
 REFRESH_US_PER_MPARAM = 12.6 / 1.838336      # cast_multi from the fp32 masters (h512 trace)
