@@ -93,7 +93,7 @@ void colsum(const float* in, int R, int C, float* out, hipStream_t s) {
 // tiny kernels, each paying the ~1.6 us graph-node floor).  Blocks are dealt to jobs by a
 // prefix sum over their block counts.
 __global__ void __launch_bounds__(256) reduce_multi_kernel(SlabJobs j) {
-  __shared__ u16 tile[16][72];   // 144-B rows: the transposed reads (one column, 8 rows) spread over banks
+  __shared__ __attribute__((aligned(16))) u16 tile[16][kRedTileP];   // optim_dev.h: conflict-free column reads
   reduce_multi_body(j, blockIdx.x, tile);
 }
 int reduce_slabs_blocks(SlabJobs& j) {

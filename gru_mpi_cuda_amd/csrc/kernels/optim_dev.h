@@ -172,10 +172,13 @@ DEV void adam4x4(const OptimArgs& a, const OptCastJob& J, const AdamCoef& k, lon
 // gtile (nullable): the tile's fp32 gradient already in LDS ([64][68], this tile's 64 x 64 block);
 // it is also written to the gradient buffer (observable) unless store_g is false (the buffer
 // holds something still being read, e.g. the all-reduced dP in the W_ih0 slot), and J.gsl is ignored
-// bf16 staging tile pitch: 66 u16 = 33 dwords (odd), so the column reads of the transposed copies --
-// 8 lanes 8 rows apart, 8 columns -- land in distinct banks (68: 2-way); rows are then only 4-B
-// aligned, so the tile is written and read in 4-B pieces
+// bf16 staging tile pitch: 66 u16 = 33 dwords (odd), and element (r, c) sits at column c ^ adam_sw(r)
+// (rows 32..63 swap 4-column groups): a 32-lane half of the transposed copies' column reads covers 8
+// row segments x 4 columns, and with the pitch alone segments s and s + 4 met in one bank (2-way, 38 %
+// LDS conflicts in r5_h512_pmc_summary_final.txt); rows are only 4-B aligned, so the tile is written
+// and read in 4-B pieces (the swizzle moves aligned 4-column groups, so pairs stay in one dword)
 constexpr int kAdamTileP = 66;
+DEV int adam_sw(int r) { return (r & 32) >> 3; }
 template <bool GSC1, bool DSC1>
 DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const AdamCoef& co, u16 (*tile)[kAdamTileP],
                         const float (*gtile)[68] = nullptr, bool store_g = true) {
@@ -228,7 +231,7 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
       else *reinterpret_cast<uint2*>(J.dst + (size_t)r * J.C + c) = w;
     }
     if (!J.dstT && !J.dstF && !J.dstTF) continue;
-    unsigned* tw = reinterpret_cast<unsigned*>(&tile[ty + 16 * q][4 * tx]);
+    unsigned* tw = reinterpret_cast<unsigned*>(&tile[ty + 16 * q][(4 * tx) ^ adam_sw(ty + 16 * q)]);
     tw[0] = w.x;
     tw[1] = w.y;
   }
@@ -241,7 +244,7 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
       const int col = piece >> 3, seg = piece & 7;
       u16 v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col];
+      for (int e = 0; e < 8; ++e) v[e] = tile[seg * 8 + e][col ^ adam_sw(seg * 8 + e)];
       *reinterpret_cast<uint4*>(J.dstT + (size_t)(c0 + col) * J.R + r0 + seg * 8) = *reinterpret_cast<const uint4*>(v);
     }
   }
@@ -252,23 +255,27 @@ DEV void adam_cast_unit(const OptimArgs& a, const OptCastJob& J, int t, const Ad
     const int fl = pc & 63, fr = (pc >> 6) & 3, fk = pc >> 8;   // lane, 16-row tile, 32-k step
     const int rr = fr * 16 + (fl & 15), kk = fk * 32 + 8 * (fl >> 4);
     u16 v[8];
-    if (J.dstF) {   // 8 consecutive u16 of one row: four 4-B reads
-      const unsigned* tr = reinterpret_cast<const unsigned*>(&tile[rr][kk]);
-      const uint4 v4 = make_uint4(tr[0], tr[1], tr[2], tr[3]);
+    if (J.dstF) {   // 8 consecutive u16 of one row: four 4-B reads (column pairs kk + 2i at (kk + 2i) ^ sw)
+      const int sw = adam_sw(rr);
+      const unsigned* tr = reinterpret_cast<const unsigned*>(&tile[rr][0]);
+      const uint4 v4 = make_uint4(tr[(kk ^ sw) >> 1], tr[((kk + 2) ^ sw) >> 1], tr[((kk + 4) ^ sw) >> 1], tr[((kk + 6) ^ sw) >> 1]);
       *reinterpret_cast<uint4*>(J.dstF + ft_offset(r0 + rr, c0 + kk, J.C)) = v4;
     }
     if (J.dstTF) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = tile[kk + e][rr];
+      for (int e = 0; e < 8; ++e) v[e] = tile[kk + e][rr ^ adam_sw(kk + e)];
       *reinterpret_cast<uint4*>(J.dstTF + ft_offset(c0 + rr, r0 + kk, J.R)) = *reinterpret_cast<const uint4*>(v);
     }
   }
 }
 
 // One block's share of a multi-tensor slab reduction (reduce_slabs_multi): block b of the prefix sum
-// over the jobs' block counts; tile: 16 x 72 u16 of LDS for the transposed bf16 copies.  Blocks past
-// the last job do nothing.
-DEV void reduce_multi_body(const SlabJobs& j, int b, u16 (*tile)[72]) {
+// over the jobs' block counts; tile: 16 x kRedTileP u16 of LDS for the transposed bf16 copies.  Blocks
+// past the last job do nothing.
+// pitch 66 u16 = 33 dwords: the column reads' two 8-row segments land in different banks (72, 36
+// dwords, put them in one: 2-way, 40 % LDS conflicts in r5_h512_pmc_summary_final.txt)
+constexpr int kRedTileP = 66;
+DEV void reduce_multi_body(const SlabJobs& j, int b, u16 (*tile)[kRedTileP]) {
   if (b >= j.blk_start[j.n]) return;
   int k = 0;
   while (k + 1 < j.n && b >= j.blk_start[k + 1]) ++k;
@@ -288,7 +295,9 @@ DEV void reduce_multi_body(const SlabJobs& j, int b, u16 (*tile)[72]) {
     w.y = (unsigned)f2bf(acc.z) | ((unsigned)f2bf(acc.w) << 16);
     if (J.bf) *reinterpret_cast<uint2*>(J.bf + o) = w;
     if (!J.bfT) return;
-    *reinterpret_cast<uint2*>(&tile[ty][4 * tx]) = w;
+    unsigned* tw = reinterpret_cast<unsigned*>(&tile[ty][4 * tx]);   // (4-B aligned rows, see kRedTileP)
+    tw[0] = w.x;
+    tw[1] = w.y;
     __syncthreads();
     if (threadIdx.x < 128) {   // 64 columns x 2 pieces of 8 rows (16 B)
       const int col = threadIdx.x >> 1, seg = threadIdx.x & 1;
