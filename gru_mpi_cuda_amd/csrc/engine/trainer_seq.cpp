@@ -69,6 +69,9 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
     w.C = sp == 1 ? dst : slab_w_; w.ldc = N;
     if (rowsum_dst) w.rowsumA = sp == 1 ? rowsum_dst : rs_w_;   // bias gradient fused (row sums of A)
     if (sp && sp <= splits_ && gemm256_ok(w)) {
+      // (slabs of their own summed inside the Adam launch instead of this reduce measured equal in the
+      // config-4 shard: the three 11-us reduces gone, Adam 75 -> 103 us, step 1.3139 vs 1.3132 ms in
+      // the trace, profiles/r6_c4_wgrad_defer_step_summary.txt; not kept)
       w.algo = 5;
       gemm_nt(w, s);
       if (sp > 1) {
@@ -119,9 +122,9 @@ void Trainer::wgrad_gemm(const u16* A, int lda, const u16* Bm, int ldb, int M, i
 }
 
 void Trainer::slab_job(SlabJobs& j, const float* src, int splits, long n, float* dst) {
-  // deep split-K slabs (the dW_fc GEMM's 32) stay with the reduce kernel: summed inside the Adam
-  // launch they serialise 32 loads per element on its few tile blocks
-  constexpr int max_splits = 8;
+  // deep split-K slabs (32) stay with the reduce kernel: summed inside the Adam launch they serialise
+  // 32 loads per element on its few tile blocks (16: two batches of 8 in flight)
+  constexpr int max_splits = 16;
   SlabJobs& t = (defer_slabs_ && splits <= max_splits) ? deferred_ : j;
   if (t.n >= 24) throw std::runtime_error("slab job list full");
   t.add(src, splits, n, dst);
@@ -245,13 +248,15 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     // dW_fc = dlogits^T · H_top, db_fc = row sums of dlogits^T: split-K into dedicated slabs whose
     // reduce joins the multi-tensor reduce after the backward sweep (one launch fewer)
-    // few output tiles (V x H): split K until one round of workgroups fills the chip at two per CU
-    // (h2048, 2 x 16 tiles over 65536 tokens: 8 / 16 / 32 / 64 K-slices 138 / 107 / 122 / 129 us
-    // standalone, profiles/r6_gemm_dwfc.jsonl; 256 workgroups, the old bound, left half the slots idle)
+    // few output tiles (V x H): split K until ~256 workgroups fill the chip
     const int tiles = std::max(1, (V / 128) * (H / 128));
     int sp = 1;
-    while (sp * 2 <= kFcSplitsMax && tiles * sp < 512 && tok % (sp * 2) == 0 && (tok / (sp * 2)) % 128 == 0)
+    while (sp * 2 <= kFcSplitsMax && tiles * sp < 256 && tok % (sp * 2) == 0 && (tok / (sp * 2)) % 128 == 0)
       sp *= 2;
+    // ... and at deep K (>= 4096 per slice after that) one more, for a whole round at two per CU (h2048,
+    // 2 x 16 tiles over 65536 tokens: 8 / 16 / 32 / 64 K-slices 138 / 107 / 122 / 129 us standalone,
+    // profiles/r6_gemm_dwfc.jsonl)
+    if (sp * 2 <= kFcSplitsMax && tiles * sp < 512 && tok % (sp * 2) == 0 && tok / (sp * 2) >= 4096) sp *= 2;
     GemmArgs w;
     w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;
     w.C = slab_fc2_; w.ldc = H; w.rowsumA = rs_fc2_;
@@ -260,8 +265,11 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // latency per workgroup and half the slabs of the 32-way 128 x 128 split
     // 1024: 8 slabs, summed inside the Adam launch (0.2362 -> 0.2338 ms at h512,
     // profiles/r1_fc_kslice_ab.jsonl; 512 measured equal to 128x128 split-K, r1_small_gemm_ab.jsonl)
+    // (only while its 64 x 64 tiles x K-slices fit one round at one workgroup per CU: at H = 1024 the
+    // 512 workgroups took 22.4 us in the config-4 shard, the 128^2 kernel 14.5 at 16 K-slices standalone,
+    // profiles/r6_gemm_c4_shapes.jsonl)
     constexpr int kslice = 1024;
-    if (kslice > 0 && tok % kslice == 0 && tok / kslice <= kFcSplitsMax) {
+    if (kslice > 0 && tok % kslice == 0 && tok / kslice <= kFcSplitsMax && (V / 64) * (H / 64) * (tok / kslice) <= 256) {
       GemmArgs ws = w;
       ws.splits = (int)(tok / kslice); ws.algo = 3;
       if (gemm_small_kblocks(ws)) { w = ws; sp = ws.splits; }
