@@ -350,7 +350,9 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
         if (col == y) lab[row] = x;
         const float d = (__expf(x - mx[r][i]) * rs - (col == y ? 1.f : 0.f)) * scale;
         const u16 db = f2bf(d);
-        st[col * 40 + row] = db;
+        // dl^T staging: row r of column col at r ^ 2 ((col >> 3) & 1) -- with the plain index, columns
+        // col and col + 8 of a 32-lane write half met in one bank (40-u16 pitch: 20 dwords, period 8)
+        st[col * 40 + (row ^ (((col >> 3) & 1) << 1))] = db;
         dlr[row * LDR + col] = db;
       }
     }
@@ -364,11 +366,13 @@ __global__ void __launch_bounds__(512, 1) fc_xent_v256_kernel(FcXentArgs a) {
     for (int ww = 0; ww < NW; ++ww) sum += red[NW * 32 + ww * 32 + row];
     lrow[row] = (y >= 0) ? (logf(sum) + m - lab[row]) * inv : 0.f;
   }
-  // dl^T: each column's 32 rows are 64 contiguous bytes -> four 16-B stores
+  // dl^T: each column's 32 rows are 64 contiguous bytes -> four 16-B stores (rows XOR 2 undone by
+  // swapping the dword pairs)
   for (int q = tid; q < V * 4; q += 512) {
     const int col = q >> 2, seg = q & 3;
-    *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) =
-        *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
+    uint4 v = *reinterpret_cast<const uint4*>(st + col * 40 + seg * 8);
+    if ((col >> 3) & 1) v = make_uint4(v.y, v.x, v.w, v.z);
+    *reinterpret_cast<uint4*>(a.dlT + (size_t)col * a.ldT + a.colT + m0 + seg * 8) = v;
   }
   STAMP();
   if constexpr (!DH) {   // row-major dl: 32 rows x 512 B, whole 16-B pieces
