@@ -84,8 +84,9 @@ struct StepLdsVariants {
   int bwd_big = 1;       // large H x large batch: the persistent split-K backward (0: T step kernels)
   int bwd16 = 1;         // persistent backward on 16-row blocks where 32-row blocks are not XCD-local
                          // (H = 1024, Bp = 128: the config-4 shard)
-  int bwd_xring = 4;     // persistent backward (32- and 16-row): dGh exchange as a ring of this many
-                         // slots instead of one per step (0); docs/DESIGN.md §3.1d
+  int bwd_xring = 2;     // persistent backward (32- and 16-row, large-H): dGh exchange as a ring of this
+                         // many slots instead of one per step (0); docs/DESIGN.md §3.1d.  2 since round 6:
+                         // headline -0.6 us, config-4 shard -7 us against 4 (profiles/r6_bxr2_*.jsonl)
   int fwd_xring = 4;     // one-layer persistent forward: the same for the h exchange (the two-layer
                          // wavefront keeps one slot per step: measured equal, r4_fwd_xring_ab.jsonl)
   int save16 = 1;        // layers whose forward AND backward kernels take them (LDS-staged step kernels or

@@ -872,7 +872,7 @@ def test_bench_shape_matches_oracle_and_cpu_adam():
     batches = [ds.next() for _ in range(20)]
     from gru_mpi_cuda_amd.ops import load_ext
     v = load_ext().step_lds_variants()
-    assert v["bwd_xring"] == 4 and v["fwd_xring"] == 4, v   # the plan this test describes
+    assert v["bwd_xring"] == 2 and v["fwd_xring"] == 4, v   # the plan this test describes
     tr = HipTrainer(cfg, params=params)
     plan = tr.t.plan()
     assert plan.startswith("fwd=persistent") and "bwd0=persistent+dWhh+dP" in plan, plan
