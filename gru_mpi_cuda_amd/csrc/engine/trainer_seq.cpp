@@ -556,8 +556,11 @@ void Trainer::record_emb_tail(hipStream_t s, const float* dP_fp32) {
   if (fc_held_on_) gemm_nt(fc_held_, s);
   fc_held_on_ = false;
   const GemmArgs both[2] = {g, e};
-  if (gemm_lds_ok(g) && gemm_lds_ok(e)) {
-    gemm_lds_group(both, 2, s);   // one launch for both small products
+  // one launch for both products while they fit one round of 128^2 workgroups at two per CU; past that
+  // (h2048: 768 + 256 tiles) each on its own launch
+  const long wg = (long)(g.M / 128) * (g.N / 128) * g.splits + (long)(e.M / 128) * (e.N / 128) * e.splits;
+  if (gemm_lds_ok(g) && gemm_lds_ok(e) && wg <= 512) {
+    gemm_lds_group(both, 2, s);
   } else {
     gemm_nt(g, s);
     gemm_nt(e, s);
