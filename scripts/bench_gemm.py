@@ -26,6 +26,7 @@ SHAPES = [  # (name, M, N, K, splits)
     ("h2048.dW_fc", 256, 2048, 65536, 32),
     ("h1024.dW_fc", 256, 1024, 8192, 8),
     ("h2048.dW_ih0", 6144, 2048, 256, 1),
+    ("h2048.P", 256, 6144, 2048, 1),
     ("h2048.dEmb", 256, 2048, 6144, 8),
     ("h1024.dW_hh", 3072, 1024, 8192, 4),
     ("h1024.dX", 8192, 1024, 3072, 1),
