@@ -851,6 +851,43 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(const float* __restri
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, V = a.V, per = V / 64;
   const int m0 = blockIdx.x * 32;
   const float inv = a.inv_count[0];
+  // V = 256 (4 logits per lane): one 16-B load per row, all 8 rows of the wave issued up front (one
+  // memory latency per block instead of one per row), 8-B dl stores
+  if (per == 4) {
+    float4 xv[8];
+    int yv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = m0 + w + 4 * k;
+      xv[k] = *reinterpret_cast<const float4*>(logits + (size_t)row * V + lane * 4);
+      yv[k] = a.labels[row];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int rr = w + 4 * k, row = m0 + rr, y = yv[k];
+      const float x[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+      const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+      float ex[4], se = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { ex[e] = __expf(x[e] - mx); se += ex[e]; }
+      se = wave_sum(se);
+      const float rs = 1.f / se, scale = (y >= 0) ? inv : 0.f;
+      float ly = 0.f;
+      u16 d[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = lane * 4 + e;
+        if (col == y) ly = x[e];
+        d[e] = f2bf((ex[e] * rs - (col == y ? 1.f : 0.f)) * scale);
+        st[col][rr] = d[e];
+      }
+      if (a.dl)
+        *reinterpret_cast<uint2*>(a.dl + (size_t)row * V + lane * 4) =
+            make_uint2((unsigned)d[0] | ((unsigned)d[1] << 16), (unsigned)d[2] | ((unsigned)d[3] << 16));
+      ly = wave_sum(ly);   // only the label's lane contributes
+      if (lane == 0) nll[rr] = (y >= 0) ? (logf(se) + mx - ly) * inv : 0.f;
+    }
+  } else
   for (int rr = w; rr < 32; rr += 4) {
     const int row = m0 + rr, y = a.labels[row];
     const float* L = logits + (size_t)row * V + lane * per;
