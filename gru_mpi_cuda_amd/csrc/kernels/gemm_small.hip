@@ -242,6 +242,11 @@ void gemm_small_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
   const int nkb = small_blocks(a, &nch);
   if (!nkb || a.rowsumA) throw std::runtime_error("gemm_small_with_prep: unsupported shape");
   const int ntn = a.N / 64, ntm = a.M / 64, nprep = prep_batch_blocks(p.T, p.Bp);
+  // past one round of workgroups at one per CU (the 128 KiB 8-block image): 4-block chunks, two per CU
+  // (config 5's 256 x 6144 table, 384 tiles: 41.5 -> 29.9 us, step 7.938-7.963 -> 7.920-7.928 ms,
+  // profiles/r6_prep4_c5_ab.jsonl); the same k order, so the same table
+  int nkb2 = nkb;
+  if (nkb == 8 && ntn * ntm * a.splits > 256) { nkb2 = 4; nch *= 2; }
   const dim3 grid(ntn * ntm * a.splits + nprep), block(256);
   const bool bias = a.bias && a.splits == 1;
 #define GP_CASE(N)                                                                                        \
@@ -249,7 +254,7 @@ void gemm_small_with_prep(const GemmArgs& a, const PrepJob& p, hipStream_t s) {
     if (bias) hipLaunchKernelGGL((gemm_small_prep_kernel<N, true>), grid, block, 0, s, a, ntn, ntm, p, nprep, nch); \
     else hipLaunchKernelGGL((gemm_small_prep_kernel<N, false>), grid, block, 0, s, a, ntn, ntm, p, nprep, nch);     \
     return;
-  switch (nkb) { GP_CASE(2) GP_CASE(3) GP_CASE(4) GP_CASE(8) default: break; }
+  switch (nkb2) { GP_CASE(2) GP_CASE(3) GP_CASE(4) GP_CASE(8) default: break; }
 #undef GP_CASE
 }
 
