@@ -257,7 +257,7 @@ PYBIND11_MODULE(_C, m) {
     const StepLdsVariants& v = step_lds_variants();
     py::dict d;
     d["fwd64"] = v.fwd64; d["bwd_sk_min_h"] = v.bwd_sk_min_h; d["dwfc_group"] = v.dwfc_group;
-    d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring; d["fwd_fc"] = v.fwd_fc; d["fc_flash"] = v.fc_flash; d["save16"] = v.save16; d["big_dy"] = v.big_dy;
+    d["bwd_big"] = v.bwd_big; d["bwd16"] = v.bwd16; d["bwd_xring"] = v.bwd_xring; d["fwd_xring"] = v.fwd_xring; d["fwd_fc"] = v.fwd_fc; d["fc_flash"] = v.fc_flash; d["save16"] = v.save16; d["big_dy"] = v.big_dy; d["ld_pad"] = v.ld_pad;
     return d;
   });
   m.def("set_step_lds_variants", [](py::dict d) {
@@ -275,6 +275,7 @@ PYBIND11_MODULE(_C, m) {
       else if (k == "fwd_fc") v.fwd_fc = x;
       else if (k == "fc_flash") v.fc_flash = x;
       else if (k == "big_dy") v.big_dy = x;
+      else if (k == "ld_pad") v.ld_pad = x;
       else if (k == "save16") v.save16 = x;
       else throw std::runtime_error("set_step_lds_variants: unknown field " + k);
     }

@@ -24,6 +24,13 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   Tc_ = d_.T / C_;
   const int V = d_.V, E = d_.E, H = d_.H, T = d_.T, L = d_.L, B = Bp_;
   const size_t tok = (size_t)T * B;
+  // leading dimension of the token-major transposed operands (dGh^T / dGi^T, dl^T): rows 64 KiB or
+  // more apart (tok = T * B, usually a power of two) get 64 elements of padding -- config 5 (128 KiB
+  // rows): one-hot dP 226 -> 198 us, dW_hh 1224 -> 1187, backward 3191 -> 3148, step 8.005-8.049 ->
+  // 7.966-7.974 ms; at the headline's 16 KiB rows it measured 1-2 us slower, so those stay dense
+  // (profiles/r6_ldpad_*.jsonl, r6_ldpad_traces.txt)
+  const int pad = step_lds_variants().ld_pad;
+  ldG_ = (long)tok + (pad >= 0 ? pad : tok >= 32768 ? 64 : 0);
 
   // ---- size the arena
   struct Pend { size_t off; };
@@ -35,7 +42,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
   size_t o_np = R(256 * 4), o_gs = R(16), o_step = R(16);
   size_t o_Emb = R((size_t)V * E * 2), o_EmbT = R((size_t)V * E * 2), o_Wfc = R((size_t)V * H * 2), o_WfcT = R((size_t)V * H * 2);
   size_t o_WfcF = R((size_t)V * H * 2), o_WfcTF = R((size_t)V * H * 2);
-  size_t o_dl = R(tok * V * 2), o_dlT = R(tok * V * 2), o_dPb = R((size_t)V * 3 * H * 2), o_dPTb = R((size_t)V * 3 * H * 2);
+  size_t o_dl = R(tok * V * 2), o_dlT = R((size_t)ldG_ * V * 2), o_dPb = R((size_t)V * 3 * H * 2), o_dPTb = R((size_t)V * 3 * H * 2);
   // fp32 logits of the GEMM + row-softmax FC path (shapes the fused 8-wave kernel does not cover)
   fc_split_ = !fc_xent_fused_ok(V, H, (int)tok) && tok % 128 == 0 && V % 128 == 0 && V <= 512 && H % 64 == 0 &&
               H >= 128;
@@ -52,7 +59,7 @@ Trainer::Trainer(const Dims& d, const OptCfg& o, float* params, float* grads, fl
     x.c0 = R((size_t)B * H * 4); x.c1 = R((size_t)B * H * 4);
     x.HSb = R((tok + B) * H * 2); x.HT = R((tok + B) * H * 2);
     x.g0 = R((size_t)B * 3 * H * 2); x.g1 = R((size_t)B * 3 * H * 2);
-    x.dghT = R(tok * 3 * H * 2); x.dgiT = R(tok * 3 * H * 2);
+    x.dghT = R((size_t)ldG_ * 3 * H * 2); x.dgiT = R((size_t)ldG_ * 3 * H * 2);
     x.dgi = l > 0 ? R(tok * 3 * H * 2) : 0;
     x.Whh = R((size_t)3 * H * H * 2); x.WhhT = R((size_t)3 * H * H * 2);
     x.Wih = R((size_t)3 * H * K * 2); x.WihT = R((size_t)3 * H * K * 2);
@@ -387,7 +394,7 @@ void Trainer::bwd_step(int l, int t, hipStream_t s) {
   a.hprev = y.HSf + so;
   a.carry_out = y.carry[t & 1];
   a.dgh = y.dgh[t & 1];
-  a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = T * B; a.colT = t * B;
+  a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldT = (int)ldG_; a.colT = t * B;
   a.dgi = y.dgi ? y.dgi + (size_t)t * B * 3 * H : nullptr;
   a.dgiT_n_only = l == 0 && dgiT_share_;
   a.Bp = B; a.H = H; a.algo = step_algo_;
@@ -441,7 +448,7 @@ void Trainer::record_fb(hipStream_t s0) {
         FcXentArgs f;
         f.X = y.HSb + (t0 + B) * H; f.W = Wfc; f.b = P("fc.bias");
         f.labels = labels_ + t0; f.inv_count = inv_count_;
-        f.dl = dl_ + t0 * V; f.dlT = dlT_; f.ldT = T * B; f.colT = (int)t0;
+        f.dl = dl_ + t0 * V; f.dlT = dlT_; f.ldT = (int)ldG_; f.colT = (int)t0;
         f.loss_part = loss_part_ + t0 / 32;
         f.M = Tc * B; f.H = H; f.V = V;
         fc_xent(f, s1);
@@ -450,7 +457,7 @@ void Trainer::record_fb(hipStream_t s0) {
         g.C = y.dy + t0 * H; g.ldc = H; g.M = Tc * B; g.N = H; g.K = V;
         gemm_nt(g, s1);
         GemmArgs w;   // dW_fc slab c (+ db_fc as row sums of dlogits^T)
-        w.A = dlT_ + t0; w.lda = T * B; w.B = y.HT + t0 + B; w.ldb = (T + 1) * B;
+        w.A = dlT_ + t0; w.lda = (int)ldG_; w.B = y.HT + t0 + B; w.ldb = (T + 1) * B;
         w.C = slab_fc_ + (size_t)c * V * H; w.ldc = H; w.rowsumA = rs_fc_ + (size_t)c * V;
         w.M = V; w.N = H; w.K = Tc * B;
         gemm_nt(w, s1);
@@ -470,19 +477,19 @@ void Trainer::record_fb(hipStream_t s0) {
       edge(s0, s1);
       const size_t t0 = (size_t)c * Tc * B;
       GemmArgs w;   // dW_hh slab c = dGh^T · h_{t-1}, db_hh = row sums of dGh^T
-      w.A = y.dghT + t0; w.lda = T * B; w.B = y.HT + t0; w.ldb = (T + 1) * B;
+      w.A = y.dghT + t0; w.lda = (int)ldG_; w.B = y.HT + t0; w.ldb = (T + 1) * B;
       w.C = y.slab_hh + (size_t)c * H3 * H; w.ldc = H; w.rowsumA = y.rs_hh + (size_t)c * H3;
       w.M = H3; w.N = H; w.K = Tc * B;
       gemm_nt(w, s1);
       if (l == 0) {
         GemmArgs p;   // dP slab c = onehot(x)^T · dGi   ([V][3H]; gives dEmb, dW_ih0, db_ih0)
-        p.onehot_ids = ids_ + t0; p.B = y.dgiT + t0; p.ldb = T * B;
+        p.onehot_ids = ids_ + t0; p.B = y.dgiT + t0; p.ldb = (int)ldG_;
         if (dgiT_share_) { p.B = y.dghT + t0; p.B2 = y.dgiT + t0; p.b2_row = 2 * H; }
         p.C = slab_P_ + (size_t)c * V * H3; p.ldc = H3; p.M = V; p.N = H3; p.K = Tc * B;
         gemm_nt(p, s1);
       } else {
         GemmArgs wi;  // dW_ih slab c = dGi^T · h_below
-        wi.A = y.dgiT + t0; wi.lda = T * B; wi.B = Ls_[l - 1].HT + t0 + B; wi.ldb = (T + 1) * B;
+        wi.A = y.dgiT + t0; wi.lda = (int)ldG_; wi.B = Ls_[l - 1].HT + t0 + B; wi.ldb = (T + 1) * B;
         wi.C = y.slab_ih + (size_t)c * H3 * K; wi.ldc = K; wi.rowsumA = y.rs_ih + (size_t)c * H3;
         wi.M = H3; wi.N = K; wi.K = Tc * B;
         gemm_nt(wi, s1);

@@ -267,6 +267,7 @@ class Trainer {
   GemmArgs fc_held_;
   bool fc_held_on_ = false;
   int nloss_ = 0;                // loss partials of the recorded step (fc_xent blocks)
+  long ldG_ = 0;   // leading dimension of dGh^T / dGi^T / dl^T (tokens + padding)
   static constexpr int kFcSplitsMax = 32;   // dW_fc: only (V/128)(H/128) output tiles -> deep split-K
  public:
   bool uses_persistent() const { return persist_fwd_ || (!seq_.empty() && seq_[0].bwd); }

@@ -219,7 +219,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     FcXentArgs f;
     f.X = top.HSb + (size_t)B * H; f.W = Wfc; f.b = P("fc.bias");
     f.labels = labels_; f.inv_count = inv_count_;
-    f.dl = dl_; f.dlT = dlT_; f.ldT = (int)tok; f.colT = 0;
+    f.dl = dl_; f.dlT = dlT_; f.ldT = (int)ldG_; f.colT = 0;
     f.loss_part = loss_part_; f.M = (int)tok; f.H = H; f.V = V;
     if (fc_split_) {
       // large H: logits and dH as LDS GEMMs around a row-wise softmax-xent (the fused FC kernel
@@ -258,7 +258,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     // profiles/r6_gemm_dwfc.jsonl)
     if (sp * 2 <= kFcSplitsMax && tiles * sp < 512 && tok % (sp * 2) == 0 && tok / (sp * 2) >= 4096) sp *= 2;
     GemmArgs w;
-    w.A = dlT_; w.lda = (int)tok; w.B = top.HT + B; w.ldb = (T + 1) * B;
+    w.A = dlT_; w.lda = (int)ldG_; w.B = top.HT + B; w.ldb = (T + 1) * B;
     w.C = slab_fc2_; w.ldc = H; w.rowsumA = rs_fc2_;
     w.M = V; w.N = H; w.K = (int)tok; w.splits = sp;
     // one-shot small GEMM over 512-deep K-slices when that fits the slab budget: one memory
@@ -302,7 +302,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
       a.HSf = y.HSf; a.HT = y.HT; a.ldT = (T + 1) * B; a.HF = q.HF; a.WhhT = y.WhhT; a.xbuf = xbuf_;
       const bool need_T = !q.fuse_w || (l == 0 ? !q.fuse_p : true);
-      a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)tok;
+      a.dghT = need_T ? y.dghT : nullptr; a.dgiT = need_T ? y.dgiT : nullptr; a.ldG = (int)ldG_;
       a.dgi = y.dgi;
       a.dWhh_part = q.dWhh_part; a.dbhh_part = q.dbhh_part; a.dbih_part = q.dbih_part;
       if (q.fuse_p) { a.ids = ids_; a.dP_part = dP_part_; a.V = V; }
@@ -318,7 +318,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
       if (q.s16) a.s16 = y.s16;
       else { a.sr = y.sr; a.sz = y.sz; a.sn = y.sn; a.sghn = y.sghn; }
       a.WhhT = y.WhhT; a.xbuf = xbuf_; a.part = bpart_;
-      a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)tok; a.dgi = y.dgi;
+      a.dghT = y.dghT; a.dgiT = y.dgiT; a.ldG = (int)ldG_; a.dgi = y.dgi;
       a.dgiT_n_only = l == 0 && dgiT_share_;
       a.dbhh_part = q.dbhh_part; a.dbih_part = l == 0 ? q.dbih_part : nullptr;   // (l > 0: from the dW_ih GEMM)
       if (dy_in_bwd_ && l == L - 1) { a.dl = dl_; a.WfcT = WfcT; a.V = V; a.dy = nullptr; }
@@ -361,14 +361,14 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     }
     if (j.n) reduce_slabs_multi(j, s);
     if (!q.fuse_w)
-      wgrad_gemm(y.dghT, (int)tok, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
+      wgrad_gemm(y.dghT, (int)ldG_, y.HT, (T + 1) * B, H3, H, (int)tok, G("weight_hh_l" + k),
                  (q.bwd || q.big) ? nullptr : G("bias_hh_l" + k), s);
     if (l == 0) {
       if (!q.fuse_p) {
         GemmArgs p;   // dP = onehot(x)^T · dGi, split-K then reduce
         int sp = splits_;
         while (sp > 1 && (tok % sp || (tok / sp) % 128)) sp >>= 1;
-        p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)tok;
+        p.onehot_ids = ids_; p.B = y.dgiT; p.ldb = (int)ldG_;
         if (dgiT_share_) { p.B = y.dghT; p.B2 = y.dgiT; p.b2_row = H3 - H; }
         p.C = slab_w_; p.ldc = H3; p.M = V; p.N = H3; p.K = (int)tok; p.splits = sp;
         {   // the streaming one-hot kernel (G read once) picks its own K-slices (<= the slab's splits_)
@@ -406,7 +406,7 @@ void Trainer::record_fb_seq(hipStream_t s, bool dp) {
     } else {
       const int K = in_dim(l);
       // dW_ih = dGi^T · h_below, db_ih = row sums of dGi^T
-      wgrad_gemm(y.dgiT, (int)tok, Ls_[l - 1].HT + B, (T + 1) * B, H3, K, (int)tok, G("weight_ih_l" + k),
+      wgrad_gemm(y.dgiT, (int)ldG_, Ls_[l - 1].HT + B, (T + 1) * B, H3, K, (int)tok, G("weight_ih_l" + k),
                  G("bias_ih_l" + k), s);
       if (dp) {
         ar_ready_ = group_end(l);   // FC (if l is the top layer) + this layer's four gradients

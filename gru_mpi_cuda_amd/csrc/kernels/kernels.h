@@ -98,6 +98,8 @@ struct StepLdsVariants {
                          // workgroups inside the persistent forward launch (gru_fwd_seq_fc); 0: after it
   int big_dy = 1;        // top layer on the persistent large-H backward, V = 256: dy = dl · W_fc inside it
                          // (SeqBwdArgs::dl) instead of the dH GEMM + an fp32 dy in memory
+  int ld_pad = -1;       // padding of the dGh^T / dGi^T / dl^T leading dimension: -1 = 64 elements where
+                         // its rows would be >= 64 KiB apart (trainer.cpp), else this many (tests)
 };
 // (Round 5 removed the measured-equal / marginal switches fwd_ns, fwd8, fwd64 = 2, fwd64_fused,
 // fwd64_all, bwd_sk_pf, bwd_sk_map and big_acq with the code only they reached; docs/DESIGN.md §7.)

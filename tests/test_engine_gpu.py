@@ -416,6 +416,33 @@ def test_dp_pipelined_tail_world1(E, H, group):
     assert d.max().item() <= 2 * cfg.lr * 2 * group + 1e-6 and (d > 1e-6).float().mean().item() < 1e-3
 
 
+@pytest.mark.parametrize("layers,H,batch,seq", [(1, 512, 256, 32), (2, 1024, 128, 16), (1, 2048, 512, 8)])
+def test_padded_transposed_leading_dim_bitwise(layers, H, batch, seq):
+    """dGh^T / dGi^T / dl^T with a padded leading dimension (StepLdsVariants.ld_pad; by default 64
+    elements once their rows are >= 64 KiB apart, config 5): the persistent backward kernels (32-row,
+    16-row, large-H) write them and the weight-gradient, one-hot dP and dW_fc products read them at
+    that pitch -- bit for bit the dense layout's step (the same k order everywhere)."""
+    from gru_mpi_cuda_amd.engine.trainer import HipTrainer
+    from gru_mpi_cuda_amd.ops import load_ext
+    C = load_ext()
+    cfg = GRUConfig(vocab=256, embed=512, hidden=H, layers=layers, batch=batch, seq=seq, seed=3)
+    ds = NameStream(cfg.batch, cfg.seq, seed=4)
+    batches = [ds.next() for _ in range(2)]
+    saved = C.step_lds_variants()
+    out = []
+    try:
+        for pad in (0, 64):
+            C.set_step_lds_variants(dict(ld_pad=pad))
+            tr = HipTrainer(cfg, params=init_params(cfg))
+            for x, y in batches:
+                tr.step(x, y)
+            torch.cuda.synchronize()
+            out.append((tr.params.clone(), tr.loss()))
+    finally:
+        C.set_step_lds_variants(saved)
+    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
+
+
 @pytest.mark.parametrize("layers,E,H,bucket_mb,n_coll", [
     (1, 256, 256, 8.0, 1), (2, 128, 256, 0.25, 3), (1, 512, 512, 1.0, 1),
     (2, 512, 256, 0.25, 2), (2, 512, 256, 64.0, 1)])
